@@ -1,0 +1,41 @@
+"""BinaryNet on MNIST-shaped data — the reference example
+(examples/larq_experiment.py) expressed with zookeeper_amd.
+
+    python examples/larq_experiment.py BinaryNetMnist epochs=0
+    python examples/larq_experiment.py BinaryNetMnist epochs=1 steps_per_epoch=20 batch_size=64
+
+TFDS MNIST is not available offline, so the dataset is the synthetic
+MNIST-shaped component (swap in ``HFDataset`` / ``NumpyDataset`` for real data).
+"""
+
+from typing import Sequence, Tuple
+
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from zookeeper_amd import ComponentField, Field, cli, task
+from zookeeper_amd.data import PadCropAndFlip, SyntheticMNIST
+from zookeeper_amd.models import BinaryNet
+from zookeeper_amd.train import Adam, TrainingExperiment
+
+
+@task
+class BinaryNetMnist(TrainingExperiment):
+    dataset = ComponentField(SyntheticMNIST)
+    input_shape: Tuple[int, int, int] = Field((28, 28, 1))
+    preprocessing = ComponentField(PadCropAndFlip, pad_size=32)
+    model = ComponentField(BinaryNet)
+
+    epochs = Field(100)
+    batch_size = Field(128)
+    learning_rate: float = Field(5e-3)
+    optimizer = ComponentField(Adam)
+
+    loss = Field("sparse_categorical_crossentropy")
+    metrics: Sequence[str] = Field(lambda: ["accuracy"])
+
+
+if __name__ == "__main__":
+    cli()

@@ -304,6 +304,22 @@ def _collect_fields(cls: type) -> Dict[str, Field]:
     return fields
 
 
+def _resolve_string_annotations(cls: type, fields: Dict[str, Field]) -> None:
+    """Resolve PEP 563 (``from __future__ import annotations``) string
+    annotations against the defining module, when possible.  Unresolvable
+    names (e.g. classes local to a function) stay strings and are then not
+    type-checked."""
+    import sys
+
+    module_ns = vars(sys.modules.get(cls.__module__, object())) if cls.__module__ else {}
+    for f in fields.values():
+        if isinstance(f.type, str):
+            try:
+                f.type = eval(f.type, dict(module_ns), dict(vars(cls)))  # noqa: S307
+            except Exception:
+                pass
+
+
 def component(cls: Type) -> Type:
     """Turn a class into a component (see the module docstring)."""
     if not inspect.isclass(cls):
@@ -320,6 +336,7 @@ def component(cls: Type) -> Type:
     _validate_post_configure(cls)
 
     fields = _collect_fields(cls)
+    _resolve_string_annotations(cls, fields)
     if not fields:
         utils.warn(f"Component {cls.__name__} has no defined fields.")
 

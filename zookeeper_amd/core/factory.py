@@ -95,6 +95,12 @@ def factory(cls: Type) -> Type:
         raise TypeError(_BUILD_RETURN_ERROR)
 
     ret = sig.return_annotation
+    if isinstance(ret, str):
+        # PEP 563 string annotation: resolve in the defining module.
+        try:
+            ret = eval(ret, getattr(cls.build, "__globals__", {}), dict(vars(cls)))  # noqa: S307
+        except Exception:
+            pass
     cls.__component_factory_return_type__ = ret
     cls.__component_factory_value__ = utils.missing
     cls.build = _memoised_build(cls, cls.build)

@@ -1,0 +1,493 @@
+"""Dataset components.
+
+Parity with the reference's TF adapters (zookeeper/tf/dataset.py):
+
+* ``Dataset`` ABC: ``train(decoders=None) -> (source, num_examples)`` is
+  abstract, ``validation``/``test`` raise ``ValueError`` unless overridden
+  (:11-46);
+* ``base_splits``: composite split specs (``"train+validation"``) → base
+  splits so example counts can be summed (:49-66); TFDS slice syntax
+  (``"train[:10%]"``) is understood too;
+* ``TFDSDataset`` → :class:`HFDataset` (TFDS/TF are not part of this stack;
+  the HuggingFace ``datasets`` library plays the same role: a named dataset
+  with splits, cached under ``data_dir``, optional download, automatic
+  ``num_classes`` from the ``label`` / ``labels.feature`` / ``objects.label``
+  features — :69-166);
+* ``MultiTFDSDataset`` → :class:`MultiDataset` (:169-255), with the
+  reference's empty-dict bug fixed (an empty validation mapping raises
+  instead of returning ``(None, 0)``).
+
+Instead of a ``tf.data.Dataset`` a split is a *map-style source*: ``len()``
+plus ``get_batch(indices) -> {"image": uint8[B,H,W,C], "label": int64[B]}``.
+Sources are consumed by :class:`zookeeper_amd.data.loader.DeviceLoader`,
+which assembles batches in pinned host memory and streams them to the GPU.
+
+New for the MI355X benchmarks: synthetic datasets of ImageNet / CIFAR-10 /
+MNIST shape (random uint8 images, uniform labels, deterministic per index) —
+there is no network access for real data on the GPU boxes.
+"""
+
+from __future__ import annotations
+
+import abc
+import os
+import re
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from zookeeper_amd.core import utils
+from zookeeper_amd.core.field import Field
+
+Batch = Dict[str, np.ndarray]
+
+
+# --------------------------------------------------------------------------- #
+# Sources
+# --------------------------------------------------------------------------- #
+
+
+class Source(abc.ABC):
+    """Map-style collection of examples (features dict per index)."""
+
+    @abc.abstractmethod
+    def __len__(self) -> int: ...
+
+    @abc.abstractmethod
+    def get_batch(self, indices: np.ndarray) -> Batch: ...
+
+    @property
+    def image_shape(self) -> Optional[Tuple[int, ...]]:
+        return None
+
+
+class ArraySource(Source):
+    """Examples held in (possibly memory-mapped) numpy arrays."""
+
+    def __init__(self, images: np.ndarray, labels: np.ndarray):
+        if len(images) != len(labels):
+            raise ValueError("images and labels must have the same length")
+        self.images, self.labels = images, labels
+
+    def __len__(self) -> int:
+        return len(self.labels)
+
+    def get_batch(self, indices: np.ndarray) -> Batch:
+        idx = np.asarray(indices)
+        return {"image": self.images[idx], "label": self.labels[idx].astype(np.int64)}
+
+    @property
+    def image_shape(self):
+        return tuple(self.images.shape[1:])
+
+
+class ConcatSource(Source):
+    """Concatenation of sources in order (``MultiDataset`` splits)."""
+
+    def __init__(self, sources: Sequence[Source]):
+        self.sources = list(sources)
+        self.offsets = np.cumsum([0] + [len(s) for s in self.sources])
+
+    def __len__(self) -> int:
+        return int(self.offsets[-1])
+
+    def get_batch(self, indices: np.ndarray) -> Batch:
+        idx = np.asarray(indices)
+        which = np.searchsorted(self.offsets, idx, side="right") - 1
+        parts: List[Tuple[np.ndarray, Batch]] = []
+        for s in np.unique(which):
+            sel = np.nonzero(which == s)[0]
+            parts.append((sel, self.sources[s].get_batch(idx[sel] - self.offsets[s])))
+        out: Batch = {}
+        for key in parts[0][1]:
+            first = parts[0][1][key]
+            buf = np.empty((len(idx),) + first.shape[1:], dtype=first.dtype)
+            for sel, b in parts:
+                buf[sel] = b[key]
+            out[key] = buf
+        return out
+
+    @property
+    def image_shape(self):
+        return self.sources[0].image_shape if self.sources else None
+
+
+def _mix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser (vectorised), used for per-index determinism."""
+    x = x.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+    return x
+
+
+class SyntheticSource(Source):
+    """Random uint8 images + uniform labels, a deterministic function of
+    ``(seed, index)`` so every rank / epoch sees the same example for an index.
+
+    To keep host cost bounded for ImageNet-sized images, pixel data is drawn
+    from a pool of ``pool`` pre-generated images (selected per index); labels
+    are independent per index.
+    """
+
+    def __init__(self, num_examples: int, image_shape: Tuple[int, int, int],
+                 num_classes: int, seed: int = 0, pool: int = 64):
+        self.num_examples, self.num_classes, self.seed = num_examples, num_classes, seed
+        self._shape = tuple(image_shape)
+        rng = np.random.default_rng(seed)
+        self.pool = rng.integers(0, 256, size=(min(pool, num_examples),) + self._shape,
+                                 dtype=np.uint8)
+
+    def __len__(self) -> int:
+        return self.num_examples
+
+    def labels_for(self, idx: np.ndarray) -> np.ndarray:
+        h = _mix64(idx.astype(np.uint64) + np.uint64(self.seed) * np.uint64(0x9E3779B97F4A7C15))
+        return (h % np.uint64(self.num_classes)).astype(np.int64)
+
+    def get_batch(self, indices: np.ndarray) -> Batch:
+        idx = np.asarray(indices, dtype=np.int64)
+        if idx.size and (idx.min() < 0 or idx.max() >= self.num_examples):
+            raise IndexError("synthetic index out of range")
+        pick = _mix64(idx.astype(np.uint64) ^ np.uint64(0xA5A5A5A5)) % np.uint64(len(self.pool))
+        return {"image": self.pool[pick.astype(np.int64)], "label": self.labels_for(idx)}
+
+    @property
+    def image_shape(self):
+        return self._shape
+
+
+# --------------------------------------------------------------------------- #
+# Split helpers
+# --------------------------------------------------------------------------- #
+
+_SLICE = re.compile(r"^(?P<name>[\w-]+)(\[(?P<lo>-?\d*%?):(?P<hi>-?\d*%?)\])?$")
+
+
+def base_splits(split: str) -> List[str]:
+    """``"train+validation"`` → ``["train", "validation"]``."""
+    if "+" in split:
+        return [s for part in split.split("+") for s in base_splits(part)]
+    return [split.strip()]
+
+
+def _bound(token: str, n: int, default: int) -> int:
+    if token == "":
+        return default
+    if token.endswith("%"):
+        v = int(round(int(token[:-1]) * n / 100))
+    else:
+        v = int(token)
+    if v < 0:
+        v += n
+    return max(0, min(n, v))
+
+
+def slice_range(split: str, n: int) -> Tuple[str, int, int]:
+    """Parse ``name[lo:hi]`` (absolute or percent bounds) against size ``n``."""
+    m = _SLICE.match(split.strip())
+    if not m:
+        raise ValueError(f"Invalid split specification '{split}'.")
+    if m.group("lo") is None:
+        return m.group("name"), 0, n
+    return m.group("name"), _bound(m.group("lo"), n, 0), _bound(m.group("hi"), n, n)
+
+
+class _SubsetSource(Source):
+    def __init__(self, inner: Source, lo: int, hi: int):
+        self.inner, self.lo, self.hi = inner, lo, hi
+
+    def __len__(self) -> int:
+        return self.hi - self.lo
+
+    def get_batch(self, indices: np.ndarray) -> Batch:
+        return self.inner.get_batch(np.asarray(indices) + self.lo)
+
+    @property
+    def image_shape(self):
+        return self.inner.image_shape
+
+
+# --------------------------------------------------------------------------- #
+# Dataset components
+# --------------------------------------------------------------------------- #
+
+
+class Dataset(abc.ABC):
+    """A dataset with a mandatory training split and optional validation /
+    test splits.  Subclass, add ``Field``s and decorate with ``@component``."""
+
+    @abc.abstractmethod
+    def train(self, decoders=None) -> Tuple[Source, int]:
+        """Return ``(source, num_examples)`` of the training split."""
+        raise NotImplementedError
+
+    def validation(self, decoders=None) -> Tuple[Source, int]:
+        raise ValueError(
+            f"Dataset '{self.__class__.__name__}' is not configured with validation data."
+        )
+
+    def test(self, decoders=None) -> Tuple[Source, int]:
+        raise ValueError(f"Dataset '{self.__class__.__name__}' is not configured with test data.")
+
+
+class SplitDataset(Dataset):
+    """Shared logic for datasets addressed by split strings."""
+
+    train_split: str = Field()
+    validation_split: Optional[str] = Field(None)
+    test_split: Optional[str] = Field(None)
+
+    def load(self, split: str, decoders=None, shuffle: bool = False) -> Source:
+        parts = []
+        for base in base_splits(split):
+            name, lo, hi = slice_range(base, self.split_size(slice_range(base, 1)[0]))
+            src = self.load_base_split(name, decoders)
+            parts.append(src if (lo, hi) == (0, len(src)) else _SubsetSource(src, lo, hi))
+        return parts[0] if len(parts) == 1 else ConcatSource(parts)
+
+    def num_examples(self, split: str) -> int:
+        total = 0
+        for base in base_splits(split):
+            name = slice_range(base, 1)[0]
+            _, lo, hi = slice_range(base, self.split_size(name))
+            total += hi - lo
+        return total
+
+    def split_size(self, name: str) -> int:
+        return len(self.load_base_split(name, None))
+
+    def load_base_split(self, name: str, decoders) -> Source:
+        raise NotImplementedError
+
+    def _split(self, split: Optional[str], what: str, decoders, shuffle: bool):
+        if split is None:
+            raise ValueError(
+                f"Dataset {self.__class__.__name__} is not configured with a {what} split."
+            )
+        return self.load(split, decoders=decoders, shuffle=shuffle), self.num_examples(split)
+
+    def train(self, decoders=None):
+        return self._split(self.train_split, "train", decoders, True)
+
+    def validation(self, decoders=None):
+        return self._split(self.validation_split, "validation", decoders, False)
+
+    def test(self, decoders=None):
+        return self._split(self.test_split, "test", decoders, False)
+
+
+class SyntheticDataset(SplitDataset):
+    """Random images of a fixed shape (no download, no disk).  Splits are
+    ``train`` / ``validation`` / ``test`` with the configured sizes."""
+
+    image_shape: Tuple[int, int, int] = Field()
+    num_classes: int = Field()
+    num_train_examples: int = Field()
+    num_validation_examples: int = Field(0)
+    num_test_examples: int = Field(0)
+    seed: int = Field(0)
+    train_split: str = Field("train")
+    validation_split: Optional[str] = Field("validation")
+    test_split: Optional[str] = Field(None)
+
+    def split_size(self, name: str) -> int:
+        sizes = {
+            "train": self.num_train_examples,
+            "validation": self.num_validation_examples,
+            "test": self.num_test_examples,
+        }
+        if name not in sizes:
+            raise ValueError(f"Unknown synthetic split '{name}'.")
+        return sizes[name]
+
+    def load_base_split(self, name: str, decoders) -> Source:
+        n = self.split_size(name)
+        salt = {"train": 0, "validation": 1, "test": 2}[name]
+        return SyntheticSource(n, self.image_shape, self.num_classes, seed=self.seed * 3 + salt)
+
+
+class HFDataset(SplitDataset):
+    """A HuggingFace ``datasets`` dataset (the TFDS role of the reference).
+
+    ``name`` is a hub name or a local path; with ``data_dir`` pointing at a
+    ``save_to_disk`` directory the data is read fully offline.  ``download``
+    mirrors TFDS' flag: when False, a missing dataset raises with a hint.
+    """
+
+    name: str = Field()
+    data_dir: Optional[str] = Field(None)
+    download: bool = Field(False)
+    image_key: str = Field("image")
+    label_key: str = Field("label")
+
+    def _load_hf(self, split: Optional[str] = None):
+        import datasets as hf
+
+        try:
+            if self.data_dir is not None and os.path.isdir(os.path.join(self.data_dir, self.name)):
+                ds = hf.load_from_disk(os.path.join(self.data_dir, self.name))
+                return ds[split] if split is not None else ds
+            mode = None if self.download else "reuse_cache_if_exists"
+            return hf.load_dataset(self.name, split=split, cache_dir=self.data_dir,
+                                   download_mode=mode)
+        except Exception:
+            if not self.download:
+                utils.warn(
+                    f"Field 'download' of component {self.__class__.__name__} is False. "
+                    "If the dataset is not available locally, set 'download' to True to "
+                    "download and prepare it automatically."
+                )
+            raise
+
+    @property
+    def info(self):
+        if "_info" not in self.__dict__:
+            self.__dict__["_info"] = self._load_hf()
+        return self.__dict__["_info"]
+
+    @property
+    def num_classes(self) -> int:
+        try:
+            ds = self.info
+            features = ds[next(iter(ds))].features if hasattr(ds, "keys") else ds.features
+            if "label" in features and hasattr(features["label"], "num_classes"):
+                return features["label"].num_classes
+            if "labels" in features and hasattr(features["labels"], "feature"):
+                return features["labels"].feature.num_classes
+            if "objects" in features and "label" in features["objects"]:
+                obj = features["objects"]
+                inner = obj.feature if hasattr(obj, "feature") else obj
+                return inner["label"].num_classes
+        except Exception:
+            pass
+        raise ValueError("Unable to determine the number of classes automatically.")
+
+    def split_size(self, name: str) -> int:
+        return len(self._load_hf(name))
+
+    def load_base_split(self, name: str, decoders) -> Source:
+        return _HFSource(self._load_hf(name), self.image_key, self.label_key, decoders)
+
+
+class _HFSource(Source):
+    def __init__(self, ds, image_key: str, label_key: str, decoders=None):
+        self.ds, self.image_key, self.label_key = ds, image_key, label_key
+        self.decoders = decoders or {}
+
+    def __len__(self) -> int:
+        return len(self.ds)
+
+    def get_batch(self, indices: np.ndarray) -> Batch:
+        rows = self.ds[np.asarray(indices).tolist()]
+        decode = self.decoders.get(self.image_key, _to_uint8_hwc)
+        images = np.stack([decode(im) for im in rows[self.image_key]])
+        return {"image": images, "label": np.asarray(rows[self.label_key], dtype=np.int64)}
+
+
+def _to_uint8_hwc(im: Any) -> np.ndarray:
+    a = np.asarray(im, dtype=np.uint8)
+    return a[..., None] if a.ndim == 2 else a
+
+
+class ImageFolderDataset(SplitDataset):
+    """``root/<split>/<class_name>/<image files>`` decoded with PIL and resized
+    to ``image_size`` (H, W)."""
+
+    root: str = Field()
+    image_size: Tuple[int, int] = Field((224, 224))
+    train_split: str = Field("train")
+    validation_split: Optional[str] = Field("val")
+
+    def _classes(self) -> List[str]:
+        d = os.path.join(self.root, self.train_split.split("[")[0].split("+")[0])
+        return sorted(e for e in os.listdir(d) if os.path.isdir(os.path.join(d, e)))
+
+    @property
+    def num_classes(self) -> int:
+        return len(self._classes())
+
+    def load_base_split(self, name: str, decoders) -> Source:
+        classes = {c: i for i, c in enumerate(self._classes())}
+        files, labels = [], []
+        base = os.path.join(self.root, name)
+        for c in sorted(os.listdir(base)):
+            for f in sorted(os.listdir(os.path.join(base, c))):
+                files.append(os.path.join(base, c, f))
+                labels.append(classes[c])
+        return _FileSource(files, np.asarray(labels, dtype=np.int64), tuple(self.image_size))
+
+
+class _FileSource(Source):
+    def __init__(self, files: List[str], labels: np.ndarray, size: Tuple[int, int]):
+        self.files, self.labels, self.size = files, labels, size
+
+    def __len__(self) -> int:
+        return len(self.files)
+
+    def get_batch(self, indices: np.ndarray) -> Batch:
+        from PIL import Image
+
+        out = []
+        for i in np.asarray(indices):
+            with Image.open(self.files[i]) as im:
+                im = im.convert("RGB").resize((self.size[1], self.size[0]))
+                out.append(np.asarray(im, dtype=np.uint8))
+        return {"image": np.stack(out), "label": self.labels[np.asarray(indices)]}
+
+    @property
+    def image_shape(self):
+        return (self.size[0], self.size[1], 3)
+
+
+class NumpyDataset(SplitDataset):
+    """Splits stored as ``<root>/<split>.npz`` with ``image`` (uint8 NHWC) and
+    ``label`` arrays (loaded memory-mapped via ``np.load(mmap_mode='r')``)."""
+
+    root: str = Field()
+
+    def load_base_split(self, name: str, decoders) -> Source:
+        path = os.path.join(self.root, f"{name}.npz")
+        with np.load(path) as z:
+            images, labels = z["image"], z["label"]
+        return ArraySource(images, labels)
+
+    @property
+    def num_classes(self) -> int:
+        src = self.load_base_split(base_splits(self.train_split)[0].split("[")[0], None)
+        return int(np.max(src.labels)) + 1
+
+
+class MultiDataset(Dataset):
+    """Concatenation of several named datasets per split (parity with
+    ``MultiTFDSDataset``, zookeeper/tf/dataset.py:169-255).  The split fields
+    map dataset *component names* to split strings; ``datasets`` supplies the
+    named member datasets."""
+
+    datasets: Dict[str, Any] = Field()
+    train_split: Dict[str, str] = Field()
+    validation_split: Dict[str, str] = Field(lambda: {})
+    test_split: Dict[str, str] = Field(lambda: {})
+
+    def num_examples(self, splits: Dict[str, str]) -> int:
+        return sum(self.datasets[n].num_examples(s) for n, s in splits.items())
+
+    def load(self, splits: Dict[str, str], decoders=None, shuffle: bool = False) -> Source:
+        return ConcatSource([self.datasets[n].load(s, decoders, shuffle) for n, s in splits.items()])
+
+    def _split(self, splits, what, decoders, shuffle):
+        if not splits:
+            raise ValueError(
+                f"Dataset {self.__class__.__name__} is not configured with a {what} split."
+            )
+        return self.load(splits, decoders, shuffle), self.num_examples(splits)
+
+    def train(self, decoders=None):
+        return self._split(self.train_split, "train", decoders, True)
+
+    def validation(self, decoders=None):
+        return self._split(self.validation_split, "validation", decoders, False)
+
+    def test(self, decoders=None):
+        return self._split(self.test_split, "test", decoders, False)

@@ -1,0 +1,154 @@
+"""Binary ResNet "E" family (BinaryResNetE18 and deeper variants).
+
+Architecture as published in Larq-Zoo (Bethge et al., "Back to Simplicity:
+How to Train Accurate BNNs from Scratch?", 2019) — not part of the reference
+repo, which only ships BinaryNet; see SURVEY §2.4:
+
+* float stem for ImageNet-size inputs: 7×7/2 conv (he_normal) → BN → ReLU →
+  3×3/2 max-pool (``same``) → BN; for inputs < 50 px a 3×3 conv instead;
+* ``2·layers`` residual blocks per stage, each ONE binary 3×3 conv
+  (``ste_sign`` inputs and kernels, ``weight_clip``, ``same`` padding with
+  zeros) → BN, plus its own shortcut; a stage transition strides the conv by
+  2 and the shortcut is AvgPool 2×2/2 → float 1×1 conv → BN;
+* ReLU → global average pool → float Dense(num_classes) (→ softmax in loss).
+
+``num_layers`` 18 → stages of (2, 2, 2, 2) original blocks ×2 = 16 binary
+convs at 64/128/256/512 channels.
+
+Execution: the ``hip`` backend runs each binary block as ONE fused autograd
+op (:func:`zookeeper_amd.ops.binary_block`): bit-packing of the input signs
+and STE mask, XNOR-popcount implicit-GEMM conv with the BN statistics fused
+into its epilogue, BN-apply + residual add, and a matching fused backward on
+MFMA.  The ``torch`` backend is the pure-PyTorch oracle used by the tests.
+"""
+
+from __future__ import annotations
+
+from typing import Sequence
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from zookeeper_amd.core import Field, factory
+from zookeeper_amd.models.base import ModelFactory
+from zookeeper_amd.nn.layers import (
+    AvgPool2d,
+    BatchNorm,
+    GlobalAvgPool,
+    MaxPool2d,
+    QuantConv2d,
+    glorot_normal_,
+)
+
+_SPECS = {
+    18: ((2, 2, 2, 2), (64, 128, 256, 512)),
+    34: ((3, 4, 6, 3), (64, 128, 256, 512)),
+    50: ((3, 4, 6, 3), (256, 512, 1024, 2048)),
+    101: ((3, 4, 23, 3), (256, 512, 1024, 2048)),
+    152: ((3, 8, 36, 3), (256, 512, 1024, 2048)),
+}
+
+
+class BinaryResBlock(nn.Module):
+    """``out = BN(bconv(sign(x))) + shortcut(x)``."""
+
+    def __init__(self, cin: int, cout: int, stride: int, momentum: float = 0.9,
+                 eps: float = 1e-5, backend: str = "torch", pad_value: float = 0.0):
+        super().__init__()
+        self.cin, self.cout, self.stride, self.backend = cin, cout, stride, backend
+        self.conv = QuantConv2d(cin, cout, 3, stride, "same", "ste_sign", "ste_sign",
+                                "weight_clip", pad_values=pad_value)
+        self.bn = BatchNorm(cout, momentum=momentum, eps=eps)
+        self.downsample = None
+        if cin != cout:
+            self.downsample = nn.Sequential(
+                AvgPool2d(2, 2),
+                QuantConv2d(cin, cout, 1, 1, "valid"),
+                BatchNorm(cout, momentum=momentum, eps=eps),
+            )
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        residual = self.downsample(x) if self.downsample is not None else x
+        if self.backend == "hip" and x.is_cuda:
+            from zookeeper_amd import ops
+
+            return ops.binary_block(x, residual, self.conv, self.bn)
+        return self.bn(self.conv(x)) + residual
+
+
+class BinaryResNetE(nn.Module):
+    def __init__(self, input_shape, num_classes: int, num_layers: int = 18,
+                 initial_filters: int = 64, backend: str = "torch"):
+        super().__init__()
+        h, w, c = input_shape
+        blocks, filters = _SPECS[num_layers]
+        if initial_filters != 64 and num_layers < 50:
+            filters = tuple(initial_filters * 2**i for i in range(4))
+        stem = []
+        if h < 50:
+            stem.append(QuantConv2d(c, initial_filters, 3, 1, "same", kernel_initializer="he_normal"))
+        else:
+            stem += [
+                QuantConv2d(c, initial_filters, 7, 2, "same", kernel_initializer="he_normal"),
+                BatchNorm(initial_filters, momentum=0.9, eps=1e-5),
+                nn.ReLU(),
+                MaxPool2d(3, 2, "same"),
+                BatchNorm(initial_filters, momentum=0.9, eps=1e-5),
+            ]
+        self.stem = nn.Sequential(*stem)
+        body = []
+        cin = initial_filters
+        for stage, (n, f) in enumerate(zip(blocks, filters)):
+            # Each original 2-conv block becomes two single-conv blocks with
+            # their own shortcuts ("E" = extra shortcuts).
+            for i in range(2 * n):
+                stride = 1 if stage == 0 or i != 0 else 2
+                body.append(BinaryResBlock(cin, f, stride, backend=backend))
+                cin = f
+        self.body = nn.Sequential(*body)
+        self.pool = GlobalAvgPool()
+        self.fc = nn.Linear(cin, num_classes)
+        glorot_normal_(self.fc.weight)
+        nn.init.zeros_(self.fc.bias)
+        self.input_shape, self.num_classes = tuple(input_shape), num_classes
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.stem(x)
+        x = self.body(x)
+        x = self.pool(F.relu(x)).float()
+        return F.linear(x, self.fc.weight, self.fc.bias)
+
+    def set_backend(self, backend: str) -> "BinaryResNetE":
+        for m in self.modules():
+            if isinstance(m, BinaryResBlock):
+                m.backend = backend
+        return self
+
+
+@factory
+class BinaryResNetE18(ModelFactory):
+    """``@factory`` for BinaryResNet-E (default depth 18)."""
+
+    num_layers: int = Field(18)
+    initial_filters: int = Field(64)
+
+    def build(self) -> nn.Module:
+        return BinaryResNetE(self.input_shape, self.num_classes, self.num_layers,
+                             self.initial_filters, backend=self.resolved_backend())
+
+
+def stage_shapes(input_shape: Sequence[int], num_layers: int = 18):
+    """(H, W, C_in, C_out, stride) of every binary conv — used by benchmarks."""
+    h = input_shape[0]
+    blocks, filters = _SPECS[num_layers]
+    size = (h + 1) // 2
+    size = (size + 1) // 2 if h >= 50 else h
+    out, cin = [], 64
+    for stage, (n, f) in enumerate(zip(blocks, filters)):
+        for i in range(2 * n):
+            stride = 1 if stage == 0 or i != 0 else 2
+            out.append((size, size, cin, f, stride))
+            size = (size + stride - 1) // stride
+            cin = f
+    return out

@@ -1,0 +1,80 @@
+"""Float ResNet-50 (v1.5: stride on the 3×3 conv), bf16 on MFMA.
+
+North-star config 2 of BASELINE.json ("ResNet-50 float bf16 ImageNet-shape on
+1 MI355X").  Layers are NHWC (channels_last) throughout; BN momentum 0.9,
+eps 1e-5; the last BN of every bottleneck starts at γ = 0.
+"""
+
+from __future__ import annotations
+
+from typing import Sequence
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from zookeeper_amd.core import Field, factory
+from zookeeper_amd.models.base import ModelFactory
+from zookeeper_amd.nn.layers import BatchNorm, GlobalAvgPool, MaxPool2d, QuantConv2d, glorot_normal_
+
+
+class Bottleneck(nn.Module):
+    def __init__(self, cin: int, width: int, stride: int):
+        super().__init__()
+        cout = width * 4
+        self.conv1 = QuantConv2d(cin, width, 1, 1, "valid", kernel_initializer="he_normal")
+        self.bn1 = BatchNorm(width, 0.9, 1e-5)
+        self.conv2 = QuantConv2d(width, width, 3, stride, "same", kernel_initializer="he_normal")
+        self.bn2 = BatchNorm(width, 0.9, 1e-5)
+        self.conv3 = QuantConv2d(width, cout, 1, 1, "valid", kernel_initializer="he_normal")
+        self.bn3 = BatchNorm(cout, 0.9, 1e-5)
+        nn.init.zeros_(self.bn3.weight)
+        self.down = None
+        if stride != 1 or cin != cout:
+            self.down = nn.Sequential(
+                QuantConv2d(cin, cout, 1, stride, "valid", kernel_initializer="he_normal"),
+                BatchNorm(cout, 0.9, 1e-5),
+            )
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        idt = self.down(x) if self.down is not None else x
+        y = F.relu(self.bn1(self.conv1(x)))
+        y = F.relu(self.bn2(self.conv2(y)))
+        y = self.bn3(self.conv3(y))
+        return F.relu(y + idt)
+
+
+class ResNetModule(nn.Module):
+    def __init__(self, input_shape, num_classes: int, blocks: Sequence[int] = (3, 4, 6, 3)):
+        super().__init__()
+        c = input_shape[2]
+        self.stem = nn.Sequential(
+            QuantConv2d(c, 64, 7, 2, "same", kernel_initializer="he_normal"),
+            BatchNorm(64, 0.9, 1e-5),
+            nn.ReLU(),
+            MaxPool2d(3, 2, "same"),
+        )
+        layers, cin = [], 64
+        for stage, n in enumerate(blocks):
+            width = 64 * 2**stage
+            for i in range(n):
+                layers.append(Bottleneck(cin, width, 2 if (i == 0 and stage > 0) else 1))
+                cin = width * 4
+        self.body = nn.Sequential(*layers)
+        self.pool = GlobalAvgPool()
+        self.fc = nn.Linear(cin, num_classes)
+        glorot_normal_(self.fc.weight)
+        nn.init.zeros_(self.fc.bias)
+        self.input_shape, self.num_classes = tuple(input_shape), num_classes
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.pool(self.body(self.stem(x))).float()
+        return F.linear(x, self.fc.weight, self.fc.bias)
+
+
+@factory
+class ResNet50(ModelFactory):
+    blocks: Sequence[int] = Field((3, 4, 6, 3))
+
+    def build(self) -> nn.Module:
+        return ResNetModule(self.input_shape, self.num_classes, self.blocks)

@@ -1,0 +1,260 @@
+"""Layers with Keras/Larq semantics on NHWC (``channels_last``) tensors.
+
+Reference usage: the BinaryNet example builds ``lq.layers.QuantConv2D`` /
+``QuantDense`` + ``BatchNormalization(scale=False)`` stacks
+(examples/larq_experiment.py:59-103).  These modules reproduce those layer
+semantics in PyTorch:
+
+* ``padding="same"`` follows TensorFlow: the total padding
+  ``max((out-1)*s + k - in, 0)`` is split ``total//2`` before and the rest
+  after (asymmetric for even inputs with stride 2);
+* quantized layers binarise inputs/kernels with the named quantizer and apply
+  ``kernel_constraint`` (``weight_clip``) after each optimizer step;
+* ``BatchNorm`` uses Keras' momentum convention
+  (``moving = momentum*moving + (1-momentum)*batch``) and ``scale``/``center``
+  switches (``scale=False`` ⇒ no γ).
+
+Weights are stored ``[out, in, kh, kw]`` in ``channels_last`` memory format,
+i.e. physically OHWI — the layout the HIP implicit-GEMM kernels consume.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple, Union
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from zookeeper_amd.nn.quantizers import CONSTRAINTS, Quantizer, get_quantizer
+
+IntPair = Union[int, Tuple[int, int]]
+
+
+def _pair(v: IntPair) -> Tuple[int, int]:
+    return (v, v) if isinstance(v, int) else tuple(v)  # type: ignore[return-value]
+
+
+def same_padding(size: int, kernel: int, stride: int, dilation: int = 1) -> Tuple[int, int]:
+    """TensorFlow ``SAME`` padding (before, after) for one spatial dim."""
+    eff = (kernel - 1) * dilation + 1
+    out = math.ceil(size / stride)
+    total = max((out - 1) * stride + eff - size, 0)
+    return total // 2, total - total // 2
+
+
+def conv_out_size(size: int, kernel: int, stride: int, padding: str) -> int:
+    if padding == "same":
+        return math.ceil(size / stride)
+    return (size - kernel) // stride + 1
+
+
+def pad_same_nhwc(x: torch.Tensor, kernel: Tuple[int, int], stride: Tuple[int, int],
+                  value: float = 0.0) -> torch.Tensor:
+    """Pad an NCHW-shaped (channels_last-strided) tensor TF-``SAME`` style."""
+    ph = same_padding(x.shape[2], kernel[0], stride[0])
+    pw = same_padding(x.shape[3], kernel[1], stride[1])
+    if ph == (0, 0) and pw == (0, 0):
+        return x
+    return F.pad(x, (pw[0], pw[1], ph[0], ph[1]), value=value)
+
+
+def glorot_normal_(w: torch.Tensor) -> torch.Tensor:
+    """Keras ``glorot_normal`` (truncated normal, std = sqrt(2/(fan_in+fan_out)))."""
+    receptive = w[0][0].numel() if w.dim() > 2 else 1
+    fan_in, fan_out = w.shape[1] * receptive, w.shape[0] * receptive
+    std = math.sqrt(2.0 / (fan_in + fan_out)) / 0.87962566103423978
+    with torch.no_grad():
+        return nn.init.trunc_normal_(w, 0.0, std, -2 * std, 2 * std)
+
+
+def he_normal_(w: torch.Tensor) -> torch.Tensor:
+    receptive = w[0][0].numel() if w.dim() > 2 else 1
+    fan_in = w.shape[1] * receptive
+    std = math.sqrt(2.0 / fan_in) / 0.87962566103423978
+    with torch.no_grad():
+        return nn.init.trunc_normal_(w, 0.0, std, -2 * std, 2 * std)
+
+
+INITIALIZERS = {"glorot_normal": glorot_normal_, "he_normal": he_normal_}
+
+
+class QuantConv2d(nn.Module):
+    """2-D convolution with optional input/kernel quantizers (Larq
+    ``QuantConv2D`` semantics).  With both quantizers ``None`` this is a plain
+    float convolution."""
+
+    def __init__(
+        self,
+        in_channels: int,
+        out_channels: int,
+        kernel_size: IntPair,
+        stride: IntPair = 1,
+        padding: str = "valid",
+        input_quantizer: Quantizer = None,
+        kernel_quantizer: Quantizer = None,
+        kernel_constraint: Optional[str] = None,
+        use_bias: bool = False,
+        groups: int = 1,
+        pad_values: float = 0.0,
+        kernel_initializer: str = "glorot_normal",
+    ):
+        super().__init__()
+        if padding not in ("same", "valid"):
+            raise ValueError(f"padding must be 'same' or 'valid', got {padding!r}")
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.kernel_size, self.stride = _pair(kernel_size), _pair(stride)
+        self.padding, self.groups, self.pad_values = padding, groups, pad_values
+        self.input_quantizer_name = input_quantizer if isinstance(input_quantizer, str) else None
+        self.kernel_quantizer_name = kernel_quantizer if isinstance(kernel_quantizer, str) else None
+        self.input_quantizer = get_quantizer(input_quantizer)
+        self.kernel_quantizer = get_quantizer(kernel_quantizer)
+        self.kernel_constraint = kernel_constraint
+        w = torch.empty(out_channels, in_channels // groups, *self.kernel_size)
+        INITIALIZERS[kernel_initializer](w)
+        self.weight = nn.Parameter(w.contiguous(memory_format=torch.channels_last))
+        self.bias = nn.Parameter(torch.zeros(out_channels)) if use_bias else None
+
+    def extra_repr(self) -> str:
+        return (
+            f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, "
+            f"stride={self.stride}, padding={self.padding!r}, "
+            f"input_quantizer={self.input_quantizer_name}, "
+            f"kernel_quantizer={self.kernel_quantizer_name}"
+        )
+
+    def quantized_weight(self) -> torch.Tensor:
+        w = self.weight
+        return self.kernel_quantizer(w) if self.kernel_quantizer is not None else w
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.input_quantizer is not None:
+            x = self.input_quantizer(x)
+        if self.padding == "same":
+            x = pad_same_nhwc(x, self.kernel_size, self.stride, self.pad_values)
+        w = self.quantized_weight().to(x.dtype)
+        b = self.bias.to(x.dtype) if self.bias is not None else None
+        return F.conv2d(x, w, b, self.stride, 0, 1, self.groups)
+
+    def apply_constraints(self) -> None:
+        if self.kernel_constraint is not None:
+            CONSTRAINTS[self.kernel_constraint](self.weight)
+
+
+class QuantDense(nn.Module):
+    """Fully-connected layer with optional quantizers (Larq ``QuantDense``)."""
+
+    def __init__(
+        self,
+        in_features: int,
+        out_features: int,
+        input_quantizer: Quantizer = None,
+        kernel_quantizer: Quantizer = None,
+        kernel_constraint: Optional[str] = None,
+        use_bias: bool = False,
+        kernel_initializer: str = "glorot_normal",
+    ):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.input_quantizer = get_quantizer(input_quantizer)
+        self.kernel_quantizer = get_quantizer(kernel_quantizer)
+        self.kernel_constraint = kernel_constraint
+        w = torch.empty(out_features, in_features)
+        INITIALIZERS[kernel_initializer](w)
+        self.weight = nn.Parameter(w)
+        self.bias = nn.Parameter(torch.zeros(out_features)) if use_bias else None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.input_quantizer is not None:
+            x = self.input_quantizer(x)
+        w = self.weight
+        if self.kernel_quantizer is not None:
+            w = self.kernel_quantizer(w)
+        b = self.bias.to(x.dtype) if self.bias is not None else None
+        return F.linear(x, w.to(x.dtype), b)
+
+    def apply_constraints(self) -> None:
+        if self.kernel_constraint is not None:
+            CONSTRAINTS[self.kernel_constraint](self.weight)
+
+
+class BatchNorm(nn.Module):
+    """Batch normalisation over the channel dim with Keras conventions.
+
+    ``momentum`` is Keras' (0.99 default ⇒ torch momentum 0.01); ``scale=False``
+    drops γ, ``center=False`` drops β.  Works on ``[N, C]`` and NCHW-shaped
+    (channels_last) tensors; statistics are computed in fp32.
+    """
+
+    def __init__(self, num_features: int, momentum: float = 0.99, eps: float = 1e-3,
+                 scale: bool = True, center: bool = True):
+        super().__init__()
+        self.num_features, self.momentum, self.eps = num_features, momentum, eps
+        self.weight = nn.Parameter(torch.ones(num_features)) if scale else None
+        self.bias = nn.Parameter(torch.zeros(num_features)) if center else None
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.ones(num_features))
+
+    def extra_repr(self) -> str:
+        return (f"{self.num_features}, momentum={self.momentum}, eps={self.eps}, "
+                f"scale={self.weight is not None}, center={self.bias is not None}")
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        w = self.weight
+        b = self.bias
+        if x.dtype != torch.float32:
+            # Compute in fp32 (the oracle path); HIP kernels fuse this.
+            y = F.batch_norm(x.float(), self.running_mean, self.running_var, w, b,
+                             self.training, 1.0 - self.momentum, self.eps)
+            return y.to(x.dtype)
+        return F.batch_norm(x, self.running_mean, self.running_var, w, b, self.training,
+                            1.0 - self.momentum, self.eps)
+
+
+class MaxPool2d(nn.Module):
+    """Max pooling with TF ``same``/``valid`` padding semantics."""
+
+    def __init__(self, pool_size: IntPair = 2, stride: Optional[IntPair] = None,
+                 padding: str = "valid"):
+        super().__init__()
+        self.pool_size = _pair(pool_size)
+        self.stride = _pair(stride if stride is not None else pool_size)
+        self.padding = padding
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.padding == "same":
+            x = pad_same_nhwc(x, self.pool_size, self.stride, float("-inf"))
+        return F.max_pool2d(x, self.pool_size, self.stride)
+
+
+class AvgPool2d(nn.Module):
+    """Average pooling (``valid`` padding, the only form the model zoo uses)."""
+
+    def __init__(self, pool_size: IntPair = 2, stride: Optional[IntPair] = None):
+        super().__init__()
+        self.pool_size = _pair(pool_size)
+        self.stride = _pair(stride if stride is not None else pool_size)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return F.avg_pool2d(x, self.pool_size, self.stride)
+
+
+class GlobalAvgPool(nn.Module):
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return x.mean(dim=(2, 3))
+
+
+class Flatten(nn.Module):
+    """Flatten in NHWC order (Keras ``Flatten`` on channels-last tensors)."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+
+
+def apply_constraints(model: nn.Module) -> None:
+    """Apply every layer's kernel constraint (call after the optimizer step)."""
+    for m in model.modules():
+        fn = getattr(m, "apply_constraints", None)
+        if fn is not None and m is not model:
+            fn()

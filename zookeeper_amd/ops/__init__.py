@@ -1,0 +1,11 @@
+"""Custom operators backed by the hand-written gfx950 HIP kernels.
+
+Every op has a pure-PyTorch reference implementation (the *oracle*) used on
+CPU and by the numerics tests; on a GPU the HIP kernels are the only path
+(no silent fallback — see ``_native``).
+"""
+
+from zookeeper_amd.ops._native import available, load_error
+from zookeeper_amd.ops.elementwise import chunk_table, fused_optimizer_step, normalize_flip
+
+__all__ = ["available", "chunk_table", "fused_optimizer_step", "load_error", "normalize_flip"]

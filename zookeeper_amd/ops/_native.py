@@ -1,0 +1,107 @@
+"""Loader for the in-tree native library ``zookeeper_amd/_zkamd.so``.
+
+The library holds the hand-written HIP kernels for gfx950 and the C++ runtime
+pieces (pinned host ring / gather pool).  It exports a plain C ABI — every
+entry point takes raw device pointers, sizes and a ``hipStream_t`` — and is
+bound with ``ctypes``.  The library links against ``libamdhip64.so.7``; torch
+is imported first so the process shares torch's already-loaded HIP runtime
+(same SONAME) and kernels launch on torch's current stream.
+
+Build: ``python -m zookeeper_amd.csrc.build`` (or ``__graft_entry__.build()``).
+
+If a GPU is present but the library is missing or fails to load, ``lib()``
+raises: GPU code paths never fall back silently.  Set ``ZK_NATIVE=0`` to
+force the pure-PyTorch path deliberately.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+import torch
+
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_HERE, "_zkamd.so")
+
+_lib: Optional[ctypes.CDLL] = None
+_load_error: Optional[str] = None
+_tried = False
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    from zookeeper_amd.ops import _signatures
+
+    for name, (restype, argtypes) in _signatures.SIGNATURES.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.restype = restype
+        fn.argtypes = argtypes
+
+
+def _load() -> None:
+    global _lib, _load_error, _tried
+    if _tried:
+        return
+    _tried = True
+    if os.environ.get("ZK_NATIVE", "1") == "0":
+        _load_error = "disabled by ZK_NATIVE=0"
+        return
+    if not os.path.exists(LIB_PATH):
+        _load_error = f"{LIB_PATH} not built (run `python -m zookeeper_amd.csrc.build`)"
+        return
+    try:
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        _declare(lib)
+        _lib = lib
+    except OSError as e:
+        _load_error = str(e)
+
+
+def available() -> bool:
+    """True if the native library is loaded (GPU kernels need a GPU too)."""
+    _load()
+    return _lib is not None
+
+
+def load_error() -> Optional[str]:
+    _load()
+    return _load_error
+
+
+def lib() -> ctypes.CDLL:
+    _load()
+    if _lib is None:
+        raise RuntimeError(f"zookeeper_amd native library unavailable: {_load_error}")
+    return _lib
+
+
+def stream_ptr(device: Optional[torch.device] = None) -> int:
+    """Raw ``hipStream_t`` of torch's current stream."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t: torch.Tensor) -> int:
+    return t.data_ptr()
+
+
+def check(code: int, what: str = "kernel") -> None:
+    if code != 0:
+        raise RuntimeError(f"{what} failed with hipError {code}")
+
+
+def gather_rows(src: np.ndarray, idx: np.ndarray, dst: torch.Tensor, threads: int = 8) -> None:
+    """Native multi-threaded row gather ``dst[i] = src[idx[i]]`` (host memory)."""
+    l = lib()
+    src = np.ascontiguousarray(src) if not src.flags.c_contiguous else src
+    idx64 = np.ascontiguousarray(idx, dtype=np.int64)
+    row_bytes = int(np.prod(src.shape[1:])) * src.itemsize
+    rc = l.zk_gather_rows(
+        src.ctypes.data, ctypes.c_int64(row_bytes), idx64.ctypes.data,
+        ctypes.c_int64(len(idx64)), ctypes.c_void_p(dst.data_ptr()), ctypes.c_int(threads),
+    )
+    if rc != 0:
+        raise RuntimeError(f"zk_gather_rows failed with code {rc}")

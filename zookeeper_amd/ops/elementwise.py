@@ -1,0 +1,69 @@
+"""Memory-bound fused ops: input normalisation and the fused optimizer."""
+
+from __future__ import annotations
+
+import ctypes
+import itertools
+from typing import Sequence
+
+import torch
+
+from zookeeper_amd.ops._native import check, lib, stream_ptr
+
+_flip_seed = itertools.count(1)
+
+
+def normalize_flip(image: torch.Tensor, mean: Sequence[float], std: Sequence[float],
+                   flip: bool, seed: int = None) -> torch.Tensor:
+    """uint8 ``[B,H,W,3]`` → bf16 ``[B,H,W,3]`` normalised, optionally with a
+    per-image random horizontal flip (one kernel)."""
+    if image.dtype != torch.uint8 or image.dim() != 4 or image.shape[3] != 3:
+        raise ValueError("normalize_flip expects uint8 [B,H,W,3]")
+    if not image.is_contiguous():
+        image = image.contiguous()
+    B, H, W, _ = image.shape
+    if W % 4:
+        raise ValueError("normalize_flip needs W % 4 == 0")
+    out = torch.empty((B, H, W, 3), dtype=torch.bfloat16, device=image.device)
+    m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    s = (ctypes.c_float * 3)(*[float(v) for v in std])
+    seed = next(_flip_seed) if seed is None else seed
+    check(lib().zk_normalize_flip_c3(image.data_ptr(), out.data_ptr(), B, H, W, m, s,
+                                     int(bool(flip)), seed, stream_ptr(image.device)),
+          "zk_normalize_flip_c3")
+    return out
+
+
+CHUNK = 16384
+
+
+def chunk_table(flat) -> torch.Tensor:
+    """Split every parameter of a FlatParams into ≤CHUNK-element chunks:
+    rows of ``[offset, numel, clip_bits, decay]`` (int64)."""
+    import struct
+
+    rows = []
+    for s in flat.slots:
+        clip_bits = struct.unpack("<i", struct.pack("<f", s.clip))[0]
+        for lo in range(0, s.numel, CHUNK):
+            rows.append([s.offset + lo, min(CHUNK, s.numel - lo), clip_bits, int(s.decay)])
+    return torch.tensor(rows, dtype=torch.int64)
+
+
+def fused_optimizer_step(opt, lr: float) -> None:
+    """One launch: Adam/SGD + decay + 1/world grad scaling + weight_clip."""
+    flat, sp = opt.flat, opt.spec
+    if getattr(opt, "_chunks", None) is None:
+        opt._chunks = chunk_table(flat).to(flat.data.device)
+    ch = opt._chunks
+    st = stream_ptr(flat.data.device)
+    if sp.kind == "adam":
+        t = opt.step_count
+        check(lib().zk_adam_step(flat.data.data_ptr(), flat.grad.data_ptr(), opt.m.data_ptr(),
+                                 opt.v.data_ptr(), ch.data_ptr(), ch.shape[0], lr, sp.beta_1,
+                                 sp.beta_2, sp.epsilon, sp.weight_decay, 1 - sp.beta_1**t,
+                                 1 - sp.beta_2**t, opt.grad_scale, st), "zk_adam_step")
+    else:
+        check(lib().zk_sgd_step(flat.data.data_ptr(), flat.grad.data_ptr(), opt.m.data_ptr(),
+                                ch.data_ptr(), ch.shape[0], lr, sp.momentum, sp.weight_decay,
+                                opt.grad_scale, int(sp.nesterov), st), "zk_sgd_step")
