@@ -58,8 +58,12 @@ def test_fused_optimizer_matches_torch_path(ops, kind):
         flat = FlatParams(m)
         opt = spec.create(flat, grad_scale=0.5)
         g = torch.Generator(device="cuda").manual_seed(1)
+        pad = torch.ones(flat.total, dtype=torch.bool, device="cuda")
+        for sl in flat.slots:
+            pad[sl.offset:sl.offset + sl.numel] = False
         for _ in range(3):
             flat.grad.copy_(torch.randn(flat.total, device="cuda", generator=g))
+            flat.grad[pad] = 0  # alignment padding never carries gradient
             if native:
                 opt.step()
             else:
@@ -67,5 +71,3 @@ def test_fused_optimizer_matches_torch_path(ops, kind):
                 opt._step_torch(spec.lr_at(opt.step_count - 1))
         results.append(flat.data.clone())
     torch.testing.assert_close(results[0], results[1], atol=1e-5, rtol=1e-5)
-    # weight_clip applied to the binary kernel
-    assert results[0].abs().max() <= 1.0 + 1e-6 or True

@@ -1,0 +1,393 @@
+// Binary convolution on bit-packed operands for gfx950 (MI355X).
+//
+// Forward of a Larq-style QuantConv2D with ste_sign input and kernel
+// quantizers, as an implicit GEMM
+//      M = B*Ho*Wo output pixels,  N = Cout,  K = kh*kw*Cin  (bits)
+// on packed words (bit i of word w = sign bit of channel 32w+i, 1 = +1):
+//      y[m,n] = sum_valid_taps  sum_words (32 - 2*popc(a ^ b))
+// i.e. the ±1 dot product computed with v_xor_b32 + v_bcnt_u32_b32 (popcount
+// with accumulate) on LDS-staged bit tiles.  No ±1 tensor is ever
+// materialised; operands are 16x (vs bf16) / 32x (vs fp32) smaller.
+//
+// Padding.  Larq's default pads the *quantized* input with 0 (not ±1).  The
+// main loop stays branch-free: padded taps load a = 0, which adds popc(b) =
+// P[n][t] to the xor-popcount sum; the epilogue removes it using the
+// per-(channel, tap) popcounts P of the packed kernel and the per-pixel count
+// of valid taps:
+//      y = 32*CW*nvalid - 2*S + 2*sum_{t invalid} P[n][t].
+// With pad_value = +1 (QuickNet) padded words are all-ones and every tap is
+// valid: y = 32*CW*T - 2*S.
+//
+// Epilogue fusions: optional ReLU (QuickNet applies it before BN), exact
+// int16 output (|y| <= 9*Cin fits), and the BatchNorm batch statistics
+// sum(y) and sum(y^2) as exact int64 atomics (deterministic, no fp rounding).
+//
+// Tiling (v1): 256 threads = 4 waves, tile 128 pixels x 64 channels, each
+// thread an 8x4 register micro-tile of int32 accumulators; one K-step = one
+// kernel tap (all CW = Cin/32 words), A and B tap tiles staged through LDS
+// ([word][pixel] / [word][channel] so a thread reads its 8 pixels and 4
+// channels with 2 + 1 ds_read_b128), next tap prefetched into registers
+// while the current one is consumed.
+#include "../common.h"
+
+namespace {
+
+constexpr int BM = 128;
+constexpr int BN = 64;
+constexpr int NT = 256;
+
+// --------------------------------------------------------------------------
+// sign / STE-mask packing of activations: x bf16 [P][C] -> bits, mask [P][C/32]
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sign_pack_kernel(const uint16_t* __restrict__ x,
+                                                        uint32_t* __restrict__ bits,
+                                                        uint32_t* __restrict__ mask,
+                                                        long long nwords, float clip) {
+  for (long long w = blockIdx.x * (long long)blockDim.x + threadIdx.x; w < nwords;
+       w += (long long)gridDim.x * blockDim.x) {
+    const uint4* src = reinterpret_cast<const uint4*>(x + 32 * w);
+    uint32_t b = 0, mk = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint4 v = src[q];
+      uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const float f = zk::bf16_to_f32((uint16_t)(u[h] >> (16 * s)));
+          const int i = q * 8 + h * 2 + s;
+          b |= (uint32_t)(f >= 0.f) << i;
+          mk |= (uint32_t)(fabsf(f) <= clip) << i;
+        }
+      }
+    }
+    bits[w] = b;
+    if (mask) mask[w] = mk;
+  }
+}
+
+// --------------------------------------------------------------------------
+// Kernel packing: w fp32 [Cout][T][Cin] (OHWI) -> wbits [Cout][T][CW],
+// wpop [Cout][T] (popcount per tap), wsign bf16 ±1 [Cout][T][Cin] (optional)
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restrict__ w,
+                                                          uint32_t* __restrict__ wbits,
+                                                          int* __restrict__ wpop,
+                                                          uint16_t* __restrict__ wsign,
+                                                          int CoutT, int Cin) {
+  const int ct = blockIdx.x * blockDim.x + threadIdx.x;  // (co, t)
+  if (ct >= CoutT) return;
+  const int CW = Cin >> 5;
+  const float* src = w + (long long)ct * Cin;
+  int pop = 0;
+  for (int wd = 0; wd < CW; ++wd) {
+    uint32_t b = 0;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) {
+      const float f = src[wd * 32 + i];
+      b |= (uint32_t)(f >= 0.f) << i;
+      if (wsign) wsign[(long long)ct * Cin + wd * 32 + i] = f >= 0.f ? 0x3F80 : 0xBF80;
+    }
+    wbits[(long long)ct * CW + wd] = b;
+    pop += __popc(b);
+  }
+  wpop[ct] = pop;
+}
+
+// --------------------------------------------------------------------------
+// XNOR-popcount implicit-GEMM forward
+// --------------------------------------------------------------------------
+struct ConvGeom {
+  int B, H, W, Ho, Wo, Cout, kh, kw, stride, pad_t, pad_l;
+  long long P;  // B*Ho*Wo
+};
+
+template <int CW>
+__global__ __launch_bounds__(NT) void bconv_fwd_kernel(const uint32_t* __restrict__ xbits,
+                                                       const uint32_t* __restrict__ wbits,
+                                                       const int* __restrict__ wpop,
+                                                       int16_t* __restrict__ y,
+                                                       unsigned long long* __restrict__ stats,
+                                                       ConvGeom g, int pad_ones, int relu) {
+  static_assert(CW >= 1 && CW <= 32, "CW");
+  constexpr int A_WORDS = BM * CW;              // words of one A tap tile
+  constexpr int A_PER = (A_WORDS + NT - 1) / NT;  // per thread
+  constexpr int B_WORDS = BN * CW;
+  constexpr int B_PER = (B_WORDS + NT - 1) / NT;
+
+  __shared__ uint32_t As[CW][BM];
+  __shared__ uint32_t Bs[CW][BN];
+  __shared__ int red[2][4][BN];
+
+  const int tid = threadIdx.x;
+  const int tn = tid & 15;       // 4 channels each
+  const int tm = tid >> 4;       // 8 pixels each
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int T = g.kh * g.kw;
+
+  // Loader assignment: fixed (pixel, word) pairs per thread across taps.
+  int ld_pix[A_PER], ld_wd[A_PER], ld_b[A_PER], ld_hi[A_PER], ld_wi[A_PER];
+#pragma unroll
+  for (int j = 0; j < A_PER; ++j) {
+    const int i = tid + j * NT;
+    ld_pix[j] = i / CW;
+    ld_wd[j] = i % CW;
+    const long long m = m0 + ld_pix[j];
+    if (i < A_WORDS && m < g.P) {
+      const int wo = (int)(m % g.Wo);
+      const long long r = m / g.Wo;
+      const int ho = (int)(r % g.Ho);
+      ld_b[j] = (int)(r / g.Ho);
+      ld_hi[j] = ho * g.stride - g.pad_t;
+      ld_wi[j] = wo * g.stride - g.pad_l;
+    } else {
+      ld_b[j] = -1;
+      ld_hi[j] = ld_wi[j] = 0;
+    }
+  }
+
+  uint32_t ra[A_PER], rb[B_PER];
+  auto load_tap = [&](int t) {
+    const int th = t / g.kw, tw = t % g.kw;
+#pragma unroll
+    for (int j = 0; j < A_PER; ++j) {
+      uint32_t v = 0;
+      if (ld_b[j] >= 0) {
+        const int hi = ld_hi[j] + th, wi = ld_wi[j] + tw;
+        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+          v = xbits[(((long long)ld_b[j] * g.H + hi) * g.W + wi) * CW + ld_wd[j]];
+        else
+          v = pad_ones ? 0xFFFFFFFFu : 0u;
+      }
+      ra[j] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < B_PER; ++j) {
+      const int i = tid + j * NT;
+      uint32_t v = 0;
+      if (i < B_WORDS) {
+        const int n = n0 + i / CW;
+        if (n < g.Cout) v = wbits[((long long)n * T + t) * CW + (i % CW)];
+      }
+      rb[j] = v;
+    }
+  };
+  auto store_tap = [&]() {
+#pragma unroll
+    for (int j = 0; j < A_PER; ++j) {
+      const int i = tid + j * NT;
+      if (i < A_WORDS) As[ld_wd[j]][ld_pix[j]] = ra[j];
+    }
+#pragma unroll
+    for (int j = 0; j < B_PER; ++j) {
+      const int i = tid + j * NT;
+      if (i < B_WORDS) Bs[i % CW][i / CW] = rb[j];
+    }
+  };
+
+  int acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0;
+
+  load_tap(0);
+  for (int t = 0; t < T; ++t) {
+    __syncthreads();  // previous tap fully consumed
+    store_tap();
+    __syncthreads();
+    if (t + 1 < T) load_tap(t + 1);  // prefetch next tap under the compute
+#pragma unroll
+    for (int k = 0; k < CW; ++k) {
+      const uint4 a0 = *reinterpret_cast<const uint4*>(&As[k][tm * 8]);
+      const uint4 a1 = *reinterpret_cast<const uint4*>(&As[k][tm * 8 + 4]);
+      const uint4 bq = *reinterpret_cast<const uint4*>(&Bs[k][tn * 4]);
+      const uint32_t a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const uint32_t b[4] = {bq.x, bq.y, bq.z, bq.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += __popc(a[i] ^ b[j]);
+    }
+  }
+
+  // ---- epilogue: padding correction, ReLU, int16 store, BN statistics ----
+  int s1[4] = {0, 0, 0, 0};
+  long long s2[4] = {0, 0, 0, 0};
+  const int nbase = n0 + tn * 4;
+  int pop[4][9];
+  const bool need_corr = !pad_ones;
+  if (need_corr) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      for (int t = 0; t < T && t < 9; ++t)
+        pop[j][t] = (nbase + j < g.Cout) ? wpop[(nbase + j) * T + t] : 0;
+  }
+  const int full = 32 * CW * T;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long long m = m0 + tm * 8 + i;
+    if (m >= g.P) continue;
+    int corr[4] = {0, 0, 0, 0};
+    int kmax = full;
+    if (need_corr) {
+      const int wo = (int)(m % g.Wo);
+      const int ho = (int)((m / g.Wo) % g.Ho);
+      const int hi0 = ho * g.stride - g.pad_t, wi0 = wo * g.stride - g.pad_l;
+      int nvalid = 0;
+      for (int t = 0; t < T; ++t) {
+        const int hi = hi0 + t / g.kw, wi = wi0 + t % g.kw;
+        const bool ok = hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+        nvalid += ok;
+        if (!ok) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) corr[j] += pop[j][t < 9 ? t : 8];
+        }
+      }
+      kmax = 32 * CW * nvalid;
+    }
+    int16_t out[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int v = kmax - 2 * acc[i][j] + 2 * corr[j];
+      if (relu) v = v > 0 ? v : 0;
+      out[j] = (int16_t)v;
+      s1[j] += v;
+      s2[j] += (long long)v * v;
+    }
+    if (nbase + 3 < g.Cout) {
+      uint2 pk;
+      pk.x = (uint32_t)(uint16_t)out[0] | ((uint32_t)(uint16_t)out[1] << 16);
+      pk.y = (uint32_t)(uint16_t)out[2] | ((uint32_t)(uint16_t)out[3] << 16);
+      *reinterpret_cast<uint2*>(y + m * g.Cout + nbase) = pk;
+    } else {
+      for (int j = 0; j < 4; ++j)
+        if (nbase + j < g.Cout) y[m * g.Cout + nbase + j] = out[j];
+    }
+  }
+  // Reduce the statistics over the 16 threads sharing `tn`: lanes tn+16q
+  // within a wave (shuffles), then the 4 waves through LDS.
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int a = s1[j];
+    long long b = s2[j];
+    a += __shfl_xor(a, 16, 64);
+    a += __shfl_xor(a, 32, 64);
+    b += __shfl_xor(b, 16, 64);
+    b += __shfl_xor(b, 32, 64);
+    s1[j] = a;
+    s2[j] = b;
+  }
+  __shared__ long long red2[4][BN];
+  const int wave = tid >> 6, lane = tid & 63;
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[0][wave][lane * 4 + j] = s1[j];
+      red2[wave][lane * 4 + j] = s2[j];
+    }
+  }
+  __syncthreads();
+  if (tid < BN && n0 + tid < g.Cout) {
+    long long a = 0, b = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      a += red[0][w][tid];
+      b += red2[w][tid];
+    }
+    atomicAdd(stats + n0 + tid, (unsigned long long)a);
+    atomicAdd(stats + g.Cout + n0 + tid, (unsigned long long)b);
+  }
+}
+
+// --------------------------------------------------------------------------
+// Bits -> bf16 ±1 (for library GEMM operands), optional +1 padding handled
+// by the caller.
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void unpack_sign_kernel(const uint32_t* __restrict__ bits,
+                                                          uint16_t* __restrict__ out,
+                                                          long long nwords) {
+  for (long long w = blockIdx.x * (long long)blockDim.x + threadIdx.x; w < nwords;
+       w += (long long)gridDim.x * blockDim.x) {
+    const uint32_t b = bits[w];
+    uint4* dst = reinterpret_cast<uint4*>(out + 32 * w);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t v[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int i = q * 8 + h * 2;
+        const uint32_t lo = ((b >> i) & 1) ? 0x3F80u : 0xBF80u;
+        const uint32_t hi = ((b >> (i + 1)) & 1) ? 0x3F80u : 0xBF80u;
+        v[h] = lo | (hi << 16);
+      }
+      dst[q] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+int grid_for(long long work, int per_block = 256, int cap = 16384) {
+  long long b = (work + per_block - 1) / per_block;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+ZK_EXPORT int zk_sign_pack(const void* x, void* bits, void* mask, long long nwords, float clip,
+                           hipStream_t stream) {
+  hipLaunchKernelGGL(sign_pack_kernel, dim3(grid_for(nwords)), dim3(256), 0, stream,
+                     (const uint16_t*)x, (uint32_t*)bits, (uint32_t*)mask, nwords, clip);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_weight_pack(const void* w, void* wbits, void* wpop, void* wsign, int Cout,
+                             int T, int Cin, hipStream_t stream) {
+  if (Cin % 32) return (int)hipErrorInvalidValue;
+  const int n = Cout * T;
+  hipLaunchKernelGGL(weight_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, stream,
+                     (const float*)w, (uint32_t*)wbits, (int*)wpop, (uint16_t*)wsign, n, Cin);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_unpack_sign(const void* bits, void* out, long long nwords, hipStream_t stream) {
+  hipLaunchKernelGGL(unpack_sign_kernel, dim3(grid_for(nwords)), dim3(256), 0, stream,
+                     (const uint32_t*)bits, (uint16_t*)out, nwords);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// stats must be zeroed by the caller ([2][Cout] int64).
+ZK_EXPORT int zk_bconv_fwd(const void* xbits, const void* wbits, const void* wpop, void* y,
+                           void* stats, int B, int H, int W, int Cin, int Cout, int kh, int kw,
+                           int stride, int pad_t, int pad_l, int Ho, int Wo, int pad_ones,
+                           int relu, hipStream_t stream) {
+  if (Cin % 32 || kh * kw > 9) return (int)hipErrorInvalidValue;
+  ConvGeom g{B, H, W, Ho, Wo, Cout, kh, kw, stride, pad_t, pad_l, (long long)B * Ho * Wo};
+  dim3 grid((unsigned)((g.P + BM - 1) / BM), (unsigned)((Cout + BN - 1) / BN));
+  const int CW = Cin / 32;
+#define ZK_BCONV_CASE(cw)                                                                   \
+  case cw:                                                                                  \
+    hipLaunchKernelGGL(bconv_fwd_kernel<cw>, grid, dim3(NT), 0, stream,                      \
+                       (const uint32_t*)xbits, (const uint32_t*)wbits, (const int*)wpop,     \
+                       (int16_t*)y, (unsigned long long*)stats, g, pad_ones, relu);          \
+    break;
+  switch (CW) {
+    ZK_BCONV_CASE(1)
+    ZK_BCONV_CASE(2)
+    ZK_BCONV_CASE(4)
+    ZK_BCONV_CASE(8)
+    ZK_BCONV_CASE(16)
+    ZK_BCONV_CASE(32)
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+#undef ZK_BCONV_CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
