@@ -1,0 +1,135 @@
+"""Fused binary residual block (XNOR-popcount conv + BN + STE) vs the
+pure-PyTorch oracle: forward output, BN running statistics and all
+gradients.  The oracle runs in fp32 on the same ±1 semantics."""
+
+import copy
+
+import pytest
+import torch
+
+from zookeeper_amd.models.binary_resnet import BinaryResBlock
+from zookeeper_amd.models.quicknet import QuickNetBlock
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from zookeeper_amd import ops
+
+    assert ops.available(), ops.load_error()
+
+
+def _run(block, x, backend, g):
+    block = block.train()
+    block.backend = backend
+    xx = x.detach().clone().requires_grad_(True)
+    if backend == "torch":
+        # fp32 oracle
+        blk = copy.deepcopy(block).float()
+        out = blk(xx.float())
+        out.backward(g.float())
+        return out.float(), xx.grad.float(), blk
+    out = block(xx)
+    out.backward(g)
+    return out.float(), xx.grad.float(), block
+
+
+CASES = [
+    # (cin, cout, stride, H)  — E18 shapes (reduced batch)
+    (64, 64, 1, 14),
+    (64, 128, 2, 14),
+    (128, 128, 1, 7),
+    (256, 512, 2, 8),
+]
+
+
+@pytest.mark.parametrize("cin,cout,stride,hw", CASES)
+def test_binary_res_block_matches_oracle(cin, cout, stride, hw):
+    _setup()
+    torch.manual_seed(0)
+    blk = BinaryResBlock(cin, cout, stride).cuda()
+    with torch.no_grad():
+        blk.bn.weight.uniform_(0.5, 1.5)
+        blk.bn.bias.uniform_(-0.5, 0.5)
+        blk.conv.weight.uniform_(-1, 1)
+    x = (torch.randn(4, cin, hw, hw, device="cuda") * 1.5).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    ho = (hw + stride - 1) // stride
+    g = torch.randn(4, cout, ho, ho, device="cuda").to(torch.bfloat16)
+    g = g.contiguous(memory_format=torch.channels_last)
+
+    ref_blk = copy.deepcopy(blk)
+    out_h, dx_h, b_h = _run(blk, x, "hip", g)
+    out_r, dx_r, b_r = _run(ref_blk, x, "torch", g)
+
+    torch.testing.assert_close(out_h, out_r, atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(b_h.bn.running_mean, b_r.bn.running_mean, atol=1e-3, rtol=1e-4)
+    torch.testing.assert_close(b_h.bn.running_var, b_r.bn.running_var, atol=1e-2, rtol=1e-3)
+    # gradients: bf16 GEMMs vs fp32 oracle
+    scale = dx_r.abs().max().item()
+    assert (dx_h - dx_r).abs().max().item() <= 3e-2 * scale + 1e-3
+    for name in ("conv.weight", "bn.weight", "bn.bias"):
+        gh = dict(b_h.named_parameters())[name].grad.float()
+        gr = dict(b_r.named_parameters())[name].grad.float()
+        err = (gh - gr).abs().max().item()
+        assert err <= 3e-2 * gr.abs().max().item() + 1e-3, f"{name}: {err}"
+
+
+def test_quicknet_block_matches_oracle():
+    _setup()
+    torch.manual_seed(1)
+    blk = QuickNetBlock(64).cuda()
+    with torch.no_grad():
+        blk.conv.weight.uniform_(-1.25, 1.25)
+    x = (torch.randn(2, 64, 10, 10, device="cuda")).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    g = torch.randn(2, 64, 10, 10, device="cuda").to(torch.bfloat16)
+    g = g.contiguous(memory_format=torch.channels_last)
+    ref = copy.deepcopy(blk)
+    out_h, dx_h, b_h = _run(blk, x, "hip", g)
+    out_r, dx_r, b_r = _run(ref, x, "torch", g)
+    torch.testing.assert_close(out_h, out_r, atol=5e-2, rtol=2e-2)
+    scale = dx_r.abs().max().item()
+    assert (dx_h - dx_r).abs().max().item() <= 3e-2 * scale + 1e-3
+
+
+def test_bconv_forward_exact_integers():
+    """The raw XNOR conv output must equal the ±1 convolution exactly."""
+    _setup()
+    from zookeeper_amd.nn.layers import pad_same_nhwc
+    from zookeeper_amd.nn.quantizers import sign_pm1
+    from zookeeper_amd.ops._native import lib, stream_ptr
+    import torch.nn.functional as F
+
+    torch.manual_seed(3)
+    for (cin, cout, stride, hw, pad_ones) in [(32, 64, 1, 9, 0), (64, 128, 2, 12, 0),
+                                              (128, 64, 1, 5, 1), (512, 64, 1, 3, 0)]:
+        B = 3
+        x = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
+        w = torch.randn(cout, 3, 3, cin, device="cuda")
+        L = lib()
+        st = stream_ptr()
+        nwords = x.numel() // 32
+        bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
+        L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), None, nwords, 1.0, st)
+        wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
+        wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
+        L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), None, cout, 9, cin, st)
+        from zookeeper_amd.nn.layers import same_padding
+        pt, pb = same_padding(hw, 3, stride)
+        ho = (hw + pt + pb - 3) // stride + 1
+        y = torch.empty(B, ho, ho, cout, dtype=torch.int16, device="cuda")
+        stats = torch.zeros(2, cout, dtype=torch.int64, device="cuda")
+        rc = L.zk_bconv_fwd(bits.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), y.data_ptr(),
+                            stats.data_ptr(), B, hw, hw, cin, cout, 3, 3, stride, pt, pt, ho, ho,
+                            pad_ones, 0, st)
+        assert rc == 0
+        xs = sign_pm1(x.float()).permute(0, 3, 1, 2)
+        xs = pad_same_nhwc(xs, (3, 3), (stride, stride), 1.0 if pad_ones else 0.0)
+        ws = sign_pm1(w).permute(0, 3, 1, 2)
+        ref = F.conv2d(xs.double(), ws.double(), stride=stride).permute(0, 2, 3, 1)
+        assert torch.equal(y.double(), ref), (cin, cout, stride, hw, pad_ones)
+        assert torch.equal(stats[0].double(), ref.sum(dim=(0, 1, 2)))
+        assert torch.equal(stats[1].double(), (ref * ref).sum(dim=(0, 1, 2)))

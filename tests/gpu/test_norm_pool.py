@@ -1,0 +1,95 @@
+"""bf16 NHWC BatchNorm(+ReLU) and pooling HIP kernels vs fp32 PyTorch."""
+
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from zookeeper_amd.nn.layers import AvgPool2d, BatchNorm, MaxPool2d
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from zookeeper_amd import ops
+
+    assert ops.available(), ops.load_error()
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("C,relu,affine", [(64, False, True), (128, True, True),
+                                           (512, False, False), (2048, True, True)])
+def test_batchnorm_train(C, relu, affine):
+    torch.manual_seed(0)
+    bn = BatchNorm(C, momentum=0.9, eps=1e-5, scale=affine, center=affine,
+                   activation="relu" if relu else None).cuda()
+    if affine:
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.5, 0.5)
+    x = _cl(torch.randn(4, C, 6, 5, device="cuda") * 2 + 0.5).to(torch.bfloat16)
+    g = _cl(torch.randn(4, C, 6, 5, device="cuda")).to(torch.bfloat16)
+    ref = copy.deepcopy(bn).float()
+    xh = x.clone().requires_grad_(True)
+    yh = bn(xh)
+    yh.backward(g)
+    xr = x.float().clone().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(g.float())
+    torch.testing.assert_close(yh.float(), yr, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(xh.grad.float(), xr.grad, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, atol=1e-4, rtol=1e-3)
+    torch.testing.assert_close(bn.running_var, ref.running_var, atol=1e-3, rtol=1e-3)
+    if affine:
+        torch.testing.assert_close(bn.weight.grad, ref.weight.grad, atol=5e-2, rtol=2e-2)
+        torch.testing.assert_close(bn.bias.grad, ref.bias.grad, atol=5e-2, rtol=2e-2)
+
+
+def test_batchnorm_eval_uses_running_stats():
+    bn = BatchNorm(32, momentum=0.9, eps=1e-5).cuda()
+    with torch.no_grad():
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.5, 2)
+    bn.eval()
+    x = _cl(torch.randn(2, 32, 4, 4, device="cuda")).to(torch.bfloat16)
+    y = bn(x).float()
+    ref = F.batch_norm(x.float(), bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, 1e-5)
+    torch.testing.assert_close(y, ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("k,s,padding,hw", [(3, 2, "same", 112), (3, 2, "same", 9),
+                                            (2, 2, "valid", 8), (2, 1, "valid", 7)])
+def test_maxpool(k, s, padding, hw):
+    torch.manual_seed(1)
+    x = _cl(torch.randn(2, 64, hw, hw, device="cuda")).to(torch.bfloat16)
+    mp = MaxPool2d(k, s, padding)
+    xh = x.clone().requires_grad_(True)
+    yh = mp(xh)
+    xr = x.float().clone().requires_grad_(True)
+    yr = MaxPool2d(k, s, padding)(xr)
+    torch.testing.assert_close(yh.float(), yr, atol=0, rtol=0)
+    g = torch.randn_like(yr)
+    yh.backward(g.to(torch.bfloat16))
+    yr.backward(g.to(torch.bfloat16).float())
+    torch.testing.assert_close(xh.grad.float(), xr.grad, atol=2e-2, rtol=1e-2)
+
+
+def test_avgpool2():
+    torch.manual_seed(2)
+    x = _cl(torch.randn(2, 128, 14, 14, device="cuda")).to(torch.bfloat16)
+    xh = x.clone().requires_grad_(True)
+    yh = AvgPool2d(2, 2)(xh)
+    xr = x.float().clone().requires_grad_(True)
+    yr = F.avg_pool2d(xr, 2, 2)
+    torch.testing.assert_close(yh.float(), yr, atol=2e-2, rtol=1e-2)
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    yh.backward(g)
+    yr.backward(g.float())
+    torch.testing.assert_close(xh.grad.float(), xr.grad, atol=1e-2, rtol=1e-2)

@@ -1,0 +1,315 @@
+// BatchNorm pieces fused around the binary convolution (gfx950).
+//
+// Training-mode BN over NHWC [P][C] tensors (P = B*H*W):
+//   forward   stats come exact (int64 sums of the int16 conv output, from the
+//             conv epilogue) -> bn_finalize (per-channel scale/shift, running
+//             statistics update with Bessel's correction, saved mean/rstd)
+//             -> bn_apply: out = scale[c]*y + shift[c] (+ residual), bf16.
+//   backward  bn_bwd_reduce: sum(g), sum(g*yhat) per channel
+//             -> bn_bwd_dx: dy = gamma*rstd*(g - mean(g) - yhat*mean(g*yhat))
+//                (times 1{y>0} when a ReLU sits between conv and BN)
+//             -> optional STE + residual: dx = dgrad * 1{|x|<=clip} + dres.
+// All kernels are HBM-bound; every thread moves 16 B per tensor per access
+// (8 channels), vectorised, with grid-stride loops.
+#include "../common.h"
+
+namespace {
+
+__global__ void bn_finalize_kernel(const unsigned long long* __restrict__ stats, int C,
+                                   double P, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float eps, float momentum,
+                                   float* __restrict__ running_mean,
+                                   float* __restrict__ running_var, float* __restrict__ scale,
+                                   float* __restrict__ shift, float* __restrict__ mean_out,
+                                   float* __restrict__ rstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double s1 = (double)(long long)stats[c];
+  const double s2 = (double)(long long)stats[C + c];
+  const double mean = s1 / P;
+  double var = s2 / P - mean * mean;
+  if (var < 0) var = 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  scale[c] = g * rstd;
+  shift[c] = b - (float)mean * g * rstd;
+  mean_out[c] = (float)mean;
+  rstd_out[c] = rstd;
+  if (running_mean) {
+    const double unbiased = P > 1 ? var * P / (P - 1) : var;
+    // Keras convention: moving = momentum * moving + (1 - momentum) * batch.
+    running_mean[c] = momentum * running_mean[c] + (1.f - momentum) * (float)mean;
+    running_var[c] = momentum * running_var[c] + (1.f - momentum) * (float)unbiased;
+  }
+}
+
+// y int16 [P][C] -> out bf16 = scale*y + shift (+ residual bf16).
+// Each thread owns one group of 8 channels (coefficients in registers) and
+// walks rows; CG = C/8 threads cover a row.
+template <int CG>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const int16_t* __restrict__ y,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const uint16_t* __restrict__ res,
+                                                       uint16_t* __restrict__ out,
+                                                       long long P) {
+  constexpr int C = CG * 8;
+  constexpr int RB = 256 / CG;
+  const int cg = threadIdx.x % CG;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = scale[cg * 8 + k];
+    sh[k] = shift[cg * 8 + k];
+  }
+  for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
+       r += (long long)gridDim.x * RB) {
+    const long long i = (r * C) / 8 + cg;
+    const uint4 yv = reinterpret_cast<const uint4*>(y)[i];
+    const int16_t* yy = reinterpret_cast<const int16_t*>(&yv);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = sc[k] * (float)yy[k] + sh[k];
+    if (res) {
+      const uint4 rv = reinterpret_cast<const uint4*>(res)[i];
+      const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o[2 * k] += zk::bf16_to_f32((uint16_t)(rr[k] & 0xffff));
+        o[2 * k + 1] += zk::bf16_to_f32((uint16_t)(rr[k] >> 16));
+      }
+    }
+    reinterpret_cast<uint4*>(out)[i] =
+        make_uint4(zk::pack_bf16x2(o[0], o[1]), zk::pack_bf16x2(o[2], o[3]),
+                   zk::pack_bf16x2(o[4], o[5]), zk::pack_bf16x2(o[6], o[7]));
+  }
+}
+
+// sums[0][c] += sum g ; sums[1][c] += sum g*yhat  (g bf16, y int16)
+template <int CG>  // channel groups of 8 per row = C / 8
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g,
+                                                            const int16_t* __restrict__ y,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            float* __restrict__ sums,
+                                                            long long P) {
+  constexpr int C = CG * 8;
+  constexpr int RB = 256 / CG;  // rows per block iteration
+  const int cg = threadIdx.x % CG;
+  const int r0 = threadIdx.x / CG;
+  float mu[8], rs[8], sg[8], sgy[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mu[k] = mean[cg * 8 + k];
+    rs[k] = rstd[cg * 8 + k];
+    sg[k] = 0.f;
+    sgy[k] = 0.f;
+  }
+  for (long long r = (long long)blockIdx.x * RB + r0; r < P; r += (long long)gridDim.x * RB) {
+    const long long off = r * C + cg * 8;
+    const uint4 gv = *reinterpret_cast<const uint4*>(g + off);
+    const uint4 yv = *reinterpret_cast<const uint4*>(y + off);
+    const uint32_t gg[4] = {gv.x, gv.y, gv.z, gv.w};
+    const int16_t* yy = reinterpret_cast<const int16_t*>(&yv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float gk = zk::bf16_to_f32((uint16_t)(gg[k >> 1] >> (16 * (k & 1))));
+      sg[k] += gk;
+      sgy[k] += gk * ((float)yy[k] - mu[k]) * rs[k];
+    }
+  }
+  __shared__ float red[2][256][9];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[0][threadIdx.x][k] = sg[k];
+    red[1][threadIdx.x][k] = sgy[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int gcg = c / 8, k = c % 8;
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < RB; ++rr) {
+      a += red[0][rr * CG + gcg][k];
+      b += red[1][rr * CG + gcg][k];
+    }
+    atomicAdd(sums + c, a);
+    atomicAdd(sums + C + c, b);
+  }
+}
+
+// dy = k1[c]*g - k2[c] - k3[c]*(y - mean[c])   [times 1{y>0} if relu]
+// with k1 = gamma*rstd, k2 = k1*mean(g), k3 = k1*rstd*mean(g*yhat)
+template <int CG>
+__global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint16_t* __restrict__ g,
+                                                        const int16_t* __restrict__ y,
+                                                        const float* __restrict__ coef,
+                                                        uint16_t* __restrict__ dy, long long P,
+                                                        int relu) {
+  constexpr int C = CG * 8;
+  constexpr int RB = 256 / CG;
+  const int cg = threadIdx.x % CG;
+  float k1[8], k0[8], k3[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = cg * 8 + k;
+    k1[k] = coef[c];
+    k3[k] = coef[2 * C + c];
+    // fold the mean term: dy = k1*g + (k3*mu - k2) - k3*y
+    k0[k] = k3[k] * coef[3 * C + c] - coef[C + c];
+  }
+  for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
+       r += (long long)gridDim.x * RB) {
+    const long long i = (r * C) / 8 + cg;
+    const uint4 gv = reinterpret_cast<const uint4*>(g)[i];
+    const uint4 yv = reinterpret_cast<const uint4*>(y)[i];
+    const uint32_t gg[4] = {gv.x, gv.y, gv.z, gv.w};
+    const int16_t* yy = reinterpret_cast<const int16_t*>(&yv);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float gk = zk::bf16_to_f32((uint16_t)(gg[k >> 1] >> (16 * (k & 1))));
+      float v = k1[k] * gk + k0[k] - k3[k] * (float)yy[k];
+      if (relu && yy[k] <= 0) v = 0.f;
+      o[k] = v;
+    }
+    reinterpret_cast<uint4*>(dy)[i] =
+        make_uint4(zk::pack_bf16x2(o[0], o[1]), zk::pack_bf16x2(o[2], o[3]),
+                   zk::pack_bf16x2(o[4], o[5]), zk::pack_bf16x2(o[6], o[7]));
+  }
+}
+
+// dx = dgrad * bit(mask) (+ dres), all [P][C]; mask packed [P][C/32]
+__global__ __launch_bounds__(256) void ste_combine_kernel(const uint16_t* __restrict__ dgrad,
+                                                          const uint32_t* __restrict__ mask,
+                                                          const uint16_t* __restrict__ dres,
+                                                          uint16_t* __restrict__ dx,
+                                                          long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    const uint32_t mw = mask[i >> 2];  // 8 channels = one quarter of a word
+    const int sh = (int)(i & 3) * 8;
+    const uint4 dv = reinterpret_cast<const uint4*>(dgrad)[i];
+    uint32_t d[4] = {dv.x, dv.y, dv.z, dv.w};
+    uint32_t r[4] = {0, 0, 0, 0};
+    if (dres) {
+      const uint4 rv = reinterpret_cast<const uint4*>(dres)[i];
+      r[0] = rv.x; r[1] = rv.y; r[2] = rv.z; r[3] = rv.w;
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float lo = ((mw >> (sh + 2 * k)) & 1) ? zk::bf16_to_f32((uint16_t)(d[k] & 0xffff)) : 0.f;
+      float hi = ((mw >> (sh + 2 * k + 1)) & 1) ? zk::bf16_to_f32((uint16_t)(d[k] >> 16)) : 0.f;
+      if (dres) {
+        lo += zk::bf16_to_f32((uint16_t)(r[k] & 0xffff));
+        hi += zk::bf16_to_f32((uint16_t)(r[k] >> 16));
+      }
+      o[k] = zk::pack_bf16x2(lo, hi);
+    }
+    reinterpret_cast<uint4*>(dx)[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+int grid_for(long long work, int cap = 4096) {
+  long long b = (work + 255) / 256;
+  if (b > cap) b = cap;
+  return b < 1 ? 1 : (int)b;
+}
+
+}  // namespace
+
+ZK_EXPORT int zk_bn_finalize(const void* stats, int C, double P, const void* gamma,
+                             const void* beta, float eps, float momentum, void* running_mean,
+                             void* running_var, void* scale, void* shift, void* mean,
+                             void* rstd, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream,
+                     (const unsigned long long*)stats, C, P, (const float*)gamma,
+                     (const float*)beta, eps, momentum, (float*)running_mean,
+                     (float*)running_var, (float*)scale, (float*)shift, (float*)mean,
+                     (float*)rstd);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+#define ZK_CG_SWITCH(C, MACRO) \
+  switch ((C) / 8) {            \
+    MACRO(4)                    \
+    MACRO(8)                    \
+    MACRO(16)                   \
+    MACRO(32)                   \
+    MACRO(64)                   \
+    default:                    \
+      return (int)hipErrorInvalidValue; \
+  }
+
+static int rows_grid(long long P, int C) {
+  const long long rb = 256 / (C / 8);
+  long long b = (P + rb - 1) / rb;
+  if (b > 4096) b = 4096;
+  return b < 1 ? 1 : (int)b;
+}
+
+ZK_EXPORT int zk_bn_apply(const void* y, const void* scale, const void* shift, const void* res,
+                          void* out, long long P, int C, hipStream_t stream) {
+  if (C % 32) return (int)hipErrorInvalidValue;
+#define ZK_APPLY_CASE(cg)                                                                   \
+  case cg:                                                                                  \
+    hipLaunchKernelGGL(bn_apply_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, stream,    \
+                       (const int16_t*)y, (const float*)scale, (const float*)shift,         \
+                       (const uint16_t*)res, (uint16_t*)out, P);                            \
+    break;
+  ZK_CG_SWITCH(C, ZK_APPLY_CASE)
+#undef ZK_APPLY_CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_bn_bwd_reduce(const void* g, const void* y, const void* mean, const void* rstd,
+                               void* sums, long long P, int C, hipStream_t stream) {
+  const int blocks = 1024;
+#define ZK_RED_CASE(cg)                                                                   \
+  case cg:                                                                                \
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<cg>, dim3(blocks), dim3(256), 0, stream,      \
+                       (const uint16_t*)g, (const int16_t*)y, (const float*)mean,         \
+                       (const float*)rstd, (float*)sums, P);                              \
+    break;
+  switch (C / 8) {
+    ZK_RED_CASE(4)
+    ZK_RED_CASE(8)
+    ZK_RED_CASE(16)
+    ZK_RED_CASE(32)
+    ZK_RED_CASE(64)
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+#undef ZK_RED_CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_bn_bwd_dx(const void* g, const void* y, const void* coef, void* dy, long long P,
+                           int C, int relu, hipStream_t stream) {
+  if (C % 32) return (int)hipErrorInvalidValue;
+#define ZK_DX_CASE(cg)                                                                      \
+  case cg:                                                                                  \
+    hipLaunchKernelGGL(bn_bwd_dx_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, stream,   \
+                       (const uint16_t*)g, (const int16_t*)y, (const float*)coef,           \
+                       (uint16_t*)dy, P, relu);                                             \
+    break;
+  ZK_CG_SWITCH(C, ZK_DX_CASE)
+#undef ZK_DX_CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_ste_combine(const void* dgrad, const void* mask, const void* dres, void* dx,
+                             long long n_elems, hipStream_t stream) {
+  if (n_elems % 32) return (int)hipErrorInvalidValue;
+  const long long n8 = n_elems / 8;
+  hipLaunchKernelGGL(ste_combine_kernel, dim3(grid_for(n8)), dim3(256), 0, stream,
+                     (const uint16_t*)dgrad, (const uint32_t*)mask, (const uint16_t*)dres,
+                     (uint16_t*)dx, n8);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}

@@ -69,30 +69,42 @@ __global__ __launch_bounds__(256) void sign_pack_kernel(const uint16_t* __restri
 
 // --------------------------------------------------------------------------
 // Kernel packing: w fp32 [Cout][T][Cin] (OHWI) -> wbits [Cout][T][CW],
-// wpop [Cout][T] (popcount per tap), wsign bf16 ±1 [Cout][T][Cin] (optional)
+// wpop [Cout][T] (popcount per tap; zeroed by the caller), wsign bf16 ±1
+// [Cout][T][Cin] (optional).  One thread per packed word (8 float4 loads).
 // --------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restrict__ w,
                                                           uint32_t* __restrict__ wbits,
                                                           int* __restrict__ wpop,
                                                           uint16_t* __restrict__ wsign,
-                                                          int CoutT, int Cin) {
-  const int ct = blockIdx.x * blockDim.x + threadIdx.x;  // (co, t)
-  if (ct >= CoutT) return;
-  const int CW = Cin >> 5;
-  const float* src = w + (long long)ct * Cin;
-  int pop = 0;
-  for (int wd = 0; wd < CW; ++wd) {
-    uint32_t b = 0;
-#pragma unroll 8
-    for (int i = 0; i < 32; ++i) {
-      const float f = src[wd * 32 + i];
-      b |= (uint32_t)(f >= 0.f) << i;
-      if (wsign) wsign[(long long)ct * Cin + wd * 32 + i] = f >= 0.f ? 0x3F80 : 0xBF80;
-    }
-    wbits[(long long)ct * CW + wd] = b;
-    pop += __popc(b);
+                                                          long long nwords, int CW) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= nwords) return;
+  const float4* src = reinterpret_cast<const float4*>(w + 32 * i);
+  uint32_t b = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 v = src[q];
+    b |= (uint32_t)(v.x >= 0.f) << (4 * q);
+    b |= (uint32_t)(v.y >= 0.f) << (4 * q + 1);
+    b |= (uint32_t)(v.z >= 0.f) << (4 * q + 2);
+    b |= (uint32_t)(v.w >= 0.f) << (4 * q + 3);
   }
-  wpop[ct] = pop;
+  wbits[i] = b;
+  atomicAdd(wpop + i / CW, __popc(b));
+  if (wsign) {
+    uint4* dst = reinterpret_cast<uint4*>(wsign + 32 * i);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t v[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int k = q * 8 + h * 2;
+        v[h] = (((b >> k) & 1) ? 0x3F80u : 0xBF80u) |
+               ((((b >> (k + 1)) & 1) ? 0x3F80u : 0xBF80u) << 16);
+      }
+      dst[q] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -103,87 +115,101 @@ struct ConvGeom {
   long long P;  // B*Ho*Wo
 };
 
+// TPS taps per K-stage (KS = TPS*CW words staged at once): few, large stages
+// amortise the barrier and global-load latency when Cin is small.
 template <int CW>
-__global__ __launch_bounds__(NT) void bconv_fwd_kernel(const uint32_t* __restrict__ xbits,
+struct StageCfg {
+  static constexpr int TPS = (CW <= 2) ? 9 : (16 / CW > 0 ? 16 / CW : 1);
+  static constexpr int KS = TPS * CW;
+};
+
+template <int CW>
+__global__ __launch_bounds__(NT, 3) void bconv_fwd_kernel(const uint32_t* __restrict__ xbits,
                                                        const uint32_t* __restrict__ wbits,
                                                        const int* __restrict__ wpop,
                                                        int16_t* __restrict__ y,
                                                        unsigned long long* __restrict__ stats,
                                                        ConvGeom g, int pad_ones, int relu) {
-  static_assert(CW >= 1 && CW <= 32, "CW");
-  constexpr int A_WORDS = BM * CW;              // words of one A tap tile
-  constexpr int A_PER = (A_WORDS + NT - 1) / NT;  // per thread
-  constexpr int B_WORDS = BN * CW;
+  constexpr int TPS = StageCfg<CW>::TPS;
+  constexpr int KS = StageCfg<CW>::KS;
+  constexpr int A_WORDS = BM * KS;
+  constexpr int A_PER = (A_WORDS + NT - 1) / NT;
+  constexpr int B_WORDS = BN * KS;
   constexpr int B_PER = (B_WORDS + NT - 1) / NT;
 
-  __shared__ uint32_t As[CW][BM];
-  __shared__ uint32_t Bs[CW][BN];
-  __shared__ int red[2][4][BN];
+  __shared__ uint32_t As[KS][BM];
+  __shared__ uint32_t Bs[KS][BN];
+  __shared__ int pix_b[BM], pix_h[BM], pix_w[BM];
+  __shared__ int red1[4][BN];
+  __shared__ long long red2[4][BN];
 
   const int tid = threadIdx.x;
-  const int tn = tid & 15;       // 4 channels each
-  const int tm = tid >> 4;       // 8 pixels each
+  const int tn = tid & 15;  // 4 channels each
+  const int tm = tid >> 4;  // 8 pixels each
   const long long m0 = (long long)blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
   const int T = g.kh * g.kw;
+  const int nstages = (T + TPS - 1) / TPS;
 
-  // Loader assignment: fixed (pixel, word) pairs per thread across taps.
-  int ld_pix[A_PER], ld_wd[A_PER], ld_b[A_PER], ld_hi[A_PER], ld_wi[A_PER];
-#pragma unroll
-  for (int j = 0; j < A_PER; ++j) {
-    const int i = tid + j * NT;
-    ld_pix[j] = i / CW;
-    ld_wd[j] = i % CW;
-    const long long m = m0 + ld_pix[j];
-    if (i < A_WORDS && m < g.P) {
+  if (tid < BM) {
+    const long long m = m0 + tid;
+    if (m < g.P) {
       const int wo = (int)(m % g.Wo);
       const long long r = m / g.Wo;
-      const int ho = (int)(r % g.Ho);
-      ld_b[j] = (int)(r / g.Ho);
-      ld_hi[j] = ho * g.stride - g.pad_t;
-      ld_wi[j] = wo * g.stride - g.pad_l;
+      pix_b[tid] = (int)(r / g.Ho);
+      pix_h[tid] = (int)(r % g.Ho) * g.stride - g.pad_t;
+      pix_w[tid] = wo * g.stride - g.pad_l;
     } else {
-      ld_b[j] = -1;
-      ld_hi[j] = ld_wi[j] = 0;
+      pix_b[tid] = -1;
+      pix_h[tid] = pix_w[tid] = 0;
     }
   }
+  __syncthreads();
 
+  // Loader mapping: word i of a stage tile -> (pixel = i % BM, k = i / BM), so
+  // each thread always loads the same pixel (its coordinates stay in 3
+  // registers) and consecutive lanes write consecutive LDS words.
+  static_assert(NT % BM == 0 && NT % BN == 0, "loader mapping");
   uint32_t ra[A_PER], rb[B_PER];
-  auto load_tap = [&](int t) {
-    const int th = t / g.kw, tw = t % g.kw;
+  const uint32_t pad_word = pad_ones ? 0xFFFFFFFFu : 0u;
+  const int my_pix = tid % BM;
+  const int my_b = pix_b[my_pix], my_h = pix_h[my_pix], my_w = pix_w[my_pix];
+  const int my_n = tid % BN;
+  auto load_stage = [&](int s) {
+    const int t0 = s * TPS;
 #pragma unroll
     for (int j = 0; j < A_PER; ++j) {
+      const int k = tid / BM + j * (NT / BM);
       uint32_t v = 0;
-      if (ld_b[j] >= 0) {
-        const int hi = ld_hi[j] + th, wi = ld_wi[j] + tw;
-        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
-          v = xbits[(((long long)ld_b[j] * g.H + hi) * g.W + wi) * CW + ld_wd[j]];
-        else
-          v = pad_ones ? 0xFFFFFFFFu : 0u;
+      const int t = t0 + k / CW;
+      if (k < KS && my_b >= 0 && t < T) {
+        const int hi = my_h + t / g.kw, wi = my_w + t % g.kw;
+        v = (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+                ? xbits[(((long long)my_b * g.H + hi) * g.W + wi) * CW + (k % CW)]
+                : pad_word;
       }
       ra[j] = v;
     }
 #pragma unroll
     for (int j = 0; j < B_PER; ++j) {
-      const int i = tid + j * NT;
+      const int k = tid / BN + j * (NT / BN);
+      const int t = t0 + k / CW;
       uint32_t v = 0;
-      if (i < B_WORDS) {
-        const int n = n0 + i / CW;
-        if (n < g.Cout) v = wbits[((long long)n * T + t) * CW + (i % CW)];
-      }
+      if (k < KS && n0 + my_n < g.Cout && t < T)
+        v = wbits[((long long)(n0 + my_n) * T + t) * CW + (k % CW)];
       rb[j] = v;
     }
   };
-  auto store_tap = [&]() {
+  auto store_stage = [&]() {
 #pragma unroll
     for (int j = 0; j < A_PER; ++j) {
-      const int i = tid + j * NT;
-      if (i < A_WORDS) As[ld_wd[j]][ld_pix[j]] = ra[j];
+      const int k = tid / BM + j * (NT / BM);
+      if (k < KS) As[k][my_pix] = ra[j];
     }
 #pragma unroll
     for (int j = 0; j < B_PER; ++j) {
-      const int i = tid + j * NT;
-      if (i < B_WORDS) Bs[i % CW][i / CW] = rb[j];
+      const int k = tid / BN + j * (NT / BN);
+      if (k < KS) Bs[k][my_n] = rb[j];
     }
   };
 
@@ -193,14 +219,14 @@ __global__ __launch_bounds__(NT) void bconv_fwd_kernel(const uint32_t* __restric
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = 0;
 
-  load_tap(0);
-  for (int t = 0; t < T; ++t) {
-    __syncthreads();  // previous tap fully consumed
-    store_tap();
+  load_stage(0);
+  for (int s = 0; s < nstages; ++s) {
+    if (s) __syncthreads();  // previous stage fully consumed
+    store_stage();
     __syncthreads();
-    if (t + 1 < T) load_tap(t + 1);  // prefetch next tap under the compute
-#pragma unroll
-    for (int k = 0; k < CW; ++k) {
+    if (s + 1 < nstages) load_stage(s + 1);  // prefetch under the compute
+    const int kwords = min(TPS, T - s * TPS) * CW;
+    for (int k = 0; k < kwords; ++k) {
       const uint4 a0 = *reinterpret_cast<const uint4*>(&As[k][tm * 8]);
       const uint4 a1 = *reinterpret_cast<const uint4*>(&As[k][tm * 8 + 4]);
       const uint4 bq = *reinterpret_cast<const uint4*>(&Bs[k][tn * 4]);
@@ -217,36 +243,31 @@ __global__ __launch_bounds__(NT) void bconv_fwd_kernel(const uint32_t* __restric
   int s1[4] = {0, 0, 0, 0};
   long long s2[4] = {0, 0, 0, 0};
   const int nbase = n0 + tn * 4;
-  int pop[4][9];
-  const bool need_corr = !pad_ones;
-  if (need_corr) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      for (int t = 0; t < T && t < 9; ++t)
-        pop[j][t] = (nbase + j < g.Cout) ? wpop[(nbase + j) * T + t] : 0;
-  }
   const int full = 32 * CW * T;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const long long m = m0 + tm * 8 + i;
+    const int pix = tm * 8 + i;
+    const long long m = m0 + pix;
     if (m >= g.P) continue;
     int corr[4] = {0, 0, 0, 0};
     int kmax = full;
-    if (need_corr) {
-      const int wo = (int)(m % g.Wo);
-      const int ho = (int)((m / g.Wo) % g.Ho);
-      const int hi0 = ho * g.stride - g.pad_t, wi0 = wo * g.stride - g.pad_l;
-      int nvalid = 0;
-      for (int t = 0; t < T; ++t) {
-        const int hi = hi0 + t / g.kw, wi = wi0 + t % g.kw;
-        const bool ok = hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
-        nvalid += ok;
-        if (!ok) {
+    if (!pad_ones) {
+      const int hi0 = pix_h[pix], wi0 = pix_w[pix];
+      // Fast path: interior pixel, every tap valid.
+      if (hi0 < 0 || wi0 < 0 || hi0 + g.kh > g.H || wi0 + g.kw > g.W) {
+        int nvalid = 0;
+        for (int t = 0; t < T; ++t) {
+          const int hi = hi0 + t / g.kw, wi = wi0 + t % g.kw;
+          if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W) {
+            ++nvalid;
+          } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) corr[j] += pop[j][t < 9 ? t : 8];
+            for (int j = 0; j < 4; ++j)
+              corr[j] += (nbase + j < g.Cout) ? wpop[(nbase + j) * T + t] : 0;
+          }
         }
+        kmax = 32 * CW * nvalid;
       }
-      kmax = 32 * CW * nvalid;
     }
     int16_t out[4];
 #pragma unroll
@@ -267,25 +288,20 @@ __global__ __launch_bounds__(NT) void bconv_fwd_kernel(const uint32_t* __restric
         if (nbase + j < g.Cout) y[m * g.Cout + nbase + j] = out[j];
     }
   }
-  // Reduce the statistics over the 16 threads sharing `tn`: lanes tn+16q
-  // within a wave (shuffles), then the 4 waves through LDS.
+  // Statistics: reduce over the 16 threads sharing `tn` (lanes tn+16q of a
+  // wave via shuffles, then the 4 waves through LDS), one atomic per channel.
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    int a = s1[j];
-    long long b = s2[j];
-    a += __shfl_xor(a, 16, 64);
-    a += __shfl_xor(a, 32, 64);
-    b += __shfl_xor(b, 16, 64);
-    b += __shfl_xor(b, 32, 64);
-    s1[j] = a;
-    s2[j] = b;
+    s1[j] += __shfl_xor(s1[j], 16, 64);
+    s1[j] += __shfl_xor(s1[j], 32, 64);
+    s2[j] += __shfl_xor(s2[j], 16, 64);
+    s2[j] += __shfl_xor(s2[j], 32, 64);
   }
-  __shared__ long long red2[4][BN];
   const int wave = tid >> 6, lane = tid & 63;
   if (lane < 16) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      red[0][wave][lane * 4 + j] = s1[j];
+      red1[wave][lane * 4 + j] = s1[j];
       red2[wave][lane * 4 + j] = s2[j];
     }
   }
@@ -294,7 +310,7 @@ __global__ __launch_bounds__(NT) void bconv_fwd_kernel(const uint32_t* __restric
     long long a = 0, b = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      a += red[0][w][tid];
+      a += red1[w][tid];
       b += red2[w][tid];
     }
     atomicAdd(stats + n0 + tid, (unsigned long long)a);
@@ -348,9 +364,11 @@ ZK_EXPORT int zk_sign_pack(const void* x, void* bits, void* mask, long long nwor
 ZK_EXPORT int zk_weight_pack(const void* w, void* wbits, void* wpop, void* wsign, int Cout,
                              int T, int Cin, hipStream_t stream) {
   if (Cin % 32) return (int)hipErrorInvalidValue;
-  const int n = Cout * T;
-  hipLaunchKernelGGL(weight_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, stream,
-                     (const float*)w, (uint32_t*)wbits, (int*)wpop, (uint16_t*)wsign, n, Cin);
+  const long long nwords = (long long)Cout * T * (Cin / 32);
+  hipMemsetAsync(wpop, 0, sizeof(int) * (size_t)Cout * T, stream);
+  hipLaunchKernelGGL(weight_pack_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0,
+                     stream, (const float*)w, (uint32_t*)wbits, (int*)wpop, (uint16_t*)wsign,
+                     nwords, Cin / 32);
   ZK_CHECK_LAUNCH();
   return 0;
 }

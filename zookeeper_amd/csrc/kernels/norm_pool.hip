@@ -1,0 +1,486 @@
+// BatchNorm (+ReLU) on bf16 NHWC activations and NHWC pooling, gfx950.
+//
+// Used for the float parts of the binary networks (stem, downsample
+// shortcuts, transitions) and for the float ResNet: everything here is
+// HBM-bound, 16 B per thread per access, channel-group-per-thread layout so
+// per-channel coefficients stay in registers.
+//
+//   bn_stats_bf16     sum x, sum x^2 per channel (fp32 per thread, fp64 atomics)
+//   bn_finalize_f64   scale/shift/mean/rstd + running statistics (Keras momentum)
+//   bn_apply_bf16     y = scale*x + shift (+ReLU)
+//   bn_bwd_reduce_bf16  sum g', sum g'*xhat   (g' = g * 1{y>0} when ReLU fused)
+//   bn_bwd_dx_bf16    dx = k1*g' - k2 - k3*(x - mean)
+//   maxpool_fwd/bwd   k x k / stride, TF 'same' (-inf) padding, argmax tap saved
+//   avgpool2_fwd/bwd  2x2 / 2 'valid'
+#include "../common.h"
+
+namespace {
+
+__device__ __forceinline__ void load8_bf16(const uint16_t* p, float (&v)[8]) {
+  const uint4 q = *reinterpret_cast<const uint4*>(p);
+  const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = zk::bf16_to_f32((uint16_t)(u[k] & 0xffff));
+    v[2 * k + 1] = zk::bf16_to_f32((uint16_t)(u[k] >> 16));
+  }
+}
+
+__device__ __forceinline__ void store8_bf16(uint16_t* p, const float (&v)[8]) {
+  *reinterpret_cast<uint4*>(p) =
+      make_uint4(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
+                 zk::pack_bf16x2(v[4], v[5]), zk::pack_bf16x2(v[6], v[7]));
+}
+
+template <int CG>
+__global__ __launch_bounds__(256) void bn_stats_bf16_kernel(const uint16_t* __restrict__ x,
+                                                            double* __restrict__ sums,
+                                                            long long P) {
+  constexpr int C = CG * 8;
+  constexpr int RB = 256 / CG;
+  const int cg = threadIdx.x % CG;
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
+       r += (long long)gridDim.x * RB) {
+    float v[8];
+    load8_bf16(x + r * C + cg * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s1[k] += v[k];
+      s2[k] += v[k] * v[k];
+    }
+  }
+  __shared__ float red[2][256][9];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[0][threadIdx.x][k] = s1[k];
+    red[1][threadIdx.x][k] = s2[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double a = 0, b = 0;
+    for (int rr = 0; rr < RB; ++rr) {
+      a += red[0][rr * CG + c / 8][c % 8];
+      b += red[1][rr * CG + c / 8][c % 8];
+    }
+    atomicAdd(sums + c, a);
+    atomicAdd(sums + C + c, b);
+  }
+}
+
+__global__ void bn_finalize_f64_kernel(const double* __restrict__ sums, int C, double P,
+                                       const float* __restrict__ gamma,
+                                       const float* __restrict__ beta, float eps, float momentum,
+                                       float* __restrict__ rmean, float* __restrict__ rvar,
+                                       float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double mean = sums[c] / P;
+  double var = sums[C + c] / P - mean * mean;
+  if (var < 0) var = 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  coef[c] = g * rstd;                          // scale
+  coef[C + c] = b - (float)mean * g * rstd;    // shift
+  coef[2 * C + c] = (float)mean;
+  coef[3 * C + c] = rstd;
+  if (rmean) {
+    const double unbiased = P > 1 ? var * P / (P - 1) : var;
+    rmean[c] = momentum * rmean[c] + (1.f - momentum) * (float)mean;
+    rvar[c] = momentum * rvar[c] + (1.f - momentum) * (float)unbiased;
+  }
+}
+
+template <int CG>
+__global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __restrict__ x,
+                                                            const float* __restrict__ coef,
+                                                            uint16_t* __restrict__ y, long long P,
+                                                            int relu) {
+  constexpr int C = CG * 8;
+  constexpr int RB = 256 / CG;
+  const int cg = threadIdx.x % CG;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = coef[cg * 8 + k];
+    sh[k] = coef[C + cg * 8 + k];
+  }
+  for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
+       r += (long long)gridDim.x * RB) {
+    float v[8];
+    load8_bf16(x + r * C + cg * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] = sc[k] * v[k] + sh[k];
+      if (relu) v[k] = fmaxf(v[k], 0.f);
+    }
+    store8_bf16(y + r * C + cg * 8, v);
+  }
+}
+
+template <int CG>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
+    const uint16_t* __restrict__ g, const uint16_t* __restrict__ x,
+    const uint16_t* __restrict__ y, const float* __restrict__ coef, float* __restrict__ sums,
+    long long P) {
+  constexpr int C = CG * 8;
+  constexpr int RB = 256 / CG;
+  const int cg = threadIdx.x % CG;
+  float mu[8], rs[8], sg[8], sgx[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mu[k] = coef[2 * C + cg * 8 + k];
+    rs[k] = coef[3 * C + cg * 8 + k];
+    sg[k] = sgx[k] = 0.f;
+  }
+  for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
+       r += (long long)gridDim.x * RB) {
+    float gv[8], xv[8];
+    load8_bf16(g + r * C + cg * 8, gv);
+    load8_bf16(x + r * C + cg * 8, xv);
+    if (y) {  // fused ReLU: gradient only where the output was positive
+      float yv[8];
+      load8_bf16(y + r * C + cg * 8, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sg[k] += gv[k];
+      sgx[k] += gv[k] * (xv[k] - mu[k]) * rs[k];
+    }
+  }
+  __shared__ float red[2][256][9];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[0][threadIdx.x][k] = sg[k];
+    red[1][threadIdx.x][k] = sgx[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < RB; ++rr) {
+      a += red[0][rr * CG + c / 8][c % 8];
+      b += red[1][rr * CG + c / 8][c % 8];
+    }
+    atomicAdd(sums + c, a);
+    atomicAdd(sums + C + c, b);
+  }
+}
+
+// bcoef: [k1, k0, k3] x C with dx = k1*g' + k0 - k3*x
+template <int CG>
+__global__ __launch_bounds__(256) void bn_bwd_dx_bf16_kernel(
+    const uint16_t* __restrict__ g, const uint16_t* __restrict__ x,
+    const uint16_t* __restrict__ y, const float* __restrict__ bcoef, uint16_t* __restrict__ dx,
+    long long P) {
+  constexpr int C = CG * 8;
+  constexpr int RB = 256 / CG;
+  const int cg = threadIdx.x % CG;
+  float k1[8], k0[8], k3[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    k1[k] = bcoef[cg * 8 + k];
+    k0[k] = bcoef[C + cg * 8 + k];
+    k3[k] = bcoef[2 * C + cg * 8 + k];
+  }
+  for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
+       r += (long long)gridDim.x * RB) {
+    float gv[8], xv[8], o[8];
+    load8_bf16(g + r * C + cg * 8, gv);
+    load8_bf16(x + r * C + cg * 8, xv);
+    if (y) {
+      float yv[8];
+      load8_bf16(y + r * C + cg * 8, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = k1[k] * gv[k] + k0[k] - k3[k] * xv[k];
+    store8_bf16(dx + r * C + cg * 8, o);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Max pooling (NHWC bf16), window k, stride s, TF padding (pt, pl) with -inf.
+// One thread = 8 channels of one output pixel; argmax tap (uint8) saved.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x,
+                                                          uint16_t* __restrict__ y,
+                                                          uint8_t* __restrict__ arg, int B,
+                                                          int H, int W, int C, int Ho, int Wo,
+                                                          int k, int s, int pt, int pl) {
+  const int CG = C / 8;
+  const long long total = (long long)B * Ho * Wo * CG;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % CG);
+    const long long pix = i / CG;
+    const int wo = (int)(pix % Wo);
+    const int ho = (int)((pix / Wo) % Ho);
+    const int b = (int)(pix / ((long long)Wo * Ho));
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      best[q] = -INFINITY;
+      bi[q] = 0;
+    }
+    for (int dh = 0; dh < k; ++dh) {
+      const int hi = ho * s - pt + dh;
+      if (hi < 0 || hi >= H) continue;
+      for (int dw = 0; dw < k; ++dw) {
+        const int wi = wo * s - pl + dw;
+        if (wi < 0 || wi >= W) continue;
+        float v[8];
+        load8_bf16(x + (((long long)b * H + hi) * W + wi) * C + cg * 8, v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (v[q] > best[q]) {
+            best[q] = v[q];
+            bi[q] = (uint8_t)(dh * k + dw);
+          }
+      }
+    }
+    store8_bf16(y + pix * C + cg * 8, best);
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *reinterpret_cast<uint2*>(arg + pix * C + cg * 8) = packed;
+  }
+}
+
+// Gather form (deterministic, no atomics): each input pixel sums the
+// gradients of the output windows whose argmax it was.
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                          const uint8_t* __restrict__ arg,
+                                                          uint16_t* __restrict__ dx, int B,
+                                                          int H, int W, int C, int Ho, int Wo,
+                                                          int k, int s, int pt, int pl) {
+  const int CG = C / 8;
+  const long long total = (long long)B * H * W * CG;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % CG);
+    const long long pix = i / CG;
+    const int wi = (int)(pix % W);
+    const int hi = (int)((pix / W) % H);
+    const int b = (int)(pix / ((long long)W * H));
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // outputs whose window covers (hi, wi): ho*s - pt <= hi <= ho*s - pt + k - 1
+    const int ho_lo = max(0, (hi + pt - k + s) / s), ho_hi = min(Ho - 1, (hi + pt) / s);
+    const int wo_lo = max(0, (wi + pl - k + s) / s), wo_hi = min(Wo - 1, (wi + pl) / s);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      const int dh = hi - (ho * s - pt);
+      if (dh < 0 || dh >= k) continue;
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        const int dw = wi - (wo * s - pl);
+        if (dw < 0 || dw >= k) continue;
+        const long long o = (((long long)b * Ho + ho) * Wo + wo) * C + cg * 8;
+        const uint2 a = *reinterpret_cast<const uint2*>(arg + o);
+        const uint8_t* ab = reinterpret_cast<const uint8_t*>(&a);
+        float g[8];
+        load8_bf16(dy + o, g);
+        const uint8_t tap = (uint8_t)(dh * k + dw);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (ab[q] == tap) acc[q] += g[q];
+      }
+    }
+    store8_bf16(dx + pix * C + cg * 8, acc);
+  }
+}
+
+// 2x2 / stride 2 'valid' average pooling.
+__global__ __launch_bounds__(256) void avgpool2_fwd_kernel(const uint16_t* __restrict__ x,
+                                                           uint16_t* __restrict__ y, int B,
+                                                           int H, int W, int C, int Ho, int Wo) {
+  const int CG = C / 8;
+  const long long total = (long long)B * Ho * Wo * CG;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % CG);
+    const long long pix = i / CG;
+    const int wo = (int)(pix % Wo);
+    const int ho = (int)((pix / Wo) % Ho);
+    const int b = (int)(pix / ((long long)Wo * Ho));
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      float v[8];
+      load8_bf16(x + (((long long)b * H + 2 * ho + (d >> 1)) * W + 2 * wo + (d & 1)) * C + cg * 8,
+                 v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += v[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] *= 0.25f;
+    store8_bf16(y + pix * C + cg * 8, acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void avgpool2_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                           uint16_t* __restrict__ dx, int B,
+                                                           int H, int W, int C, int Ho, int Wo) {
+  const int CG = C / 8;
+  const long long total = (long long)B * H * W * CG;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % CG);
+    const long long pix = i / CG;
+    const int wi = (int)(pix % W);
+    const int hi = (int)((pix / W) % H);
+    const int b = (int)(pix / ((long long)W * H));
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if ((hi >> 1) < Ho && (wi >> 1) < Wo) {
+      load8_bf16(dy + (((long long)b * Ho + (hi >> 1)) * Wo + (wi >> 1)) * C + cg * 8, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] *= 0.25f;
+    }
+    store8_bf16(dx + pix * C + cg * 8, v);
+  }
+}
+
+int rows_grid(long long P, int C) {
+  const long long rb = 256 / (C / 8);
+  long long b = (P + rb - 1) / rb;
+  if (b > 2048) b = 2048;
+  return b < 1 ? 1 : (int)b;
+}
+
+int flat_grid(long long work) {
+  long long b = (work + 255) / 256;
+  if (b > 16384) b = 16384;
+  return b < 1 ? 1 : (int)b;
+}
+
+}  // namespace
+
+#define ZK_CG_CASES(C, BODY) \
+  switch ((C) / 8) {         \
+    BODY(1)                  \
+    BODY(2)                  \
+    BODY(4)                  \
+    BODY(8)                  \
+    BODY(16)                 \
+    BODY(32)                 \
+    BODY(64)                 \
+    BODY(128)                \
+    BODY(256)                \
+    default:                 \
+      return (int)hipErrorInvalidValue; \
+  }
+
+// sums: [2][C] fp64, zeroed by the caller.
+ZK_EXPORT int zk_bn_stats_bf16(const void* x, void* sums, long long P, int C, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+#define CASE(cg)                                                                           \
+  case cg:                                                                                 \
+    hipLaunchKernelGGL(bn_stats_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,  \
+                       (const uint16_t*)x, (double*)sums, P);                              \
+    break;
+  ZK_CG_CASES(C, CASE)
+#undef CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// coef out: [4][C] = scale, shift, mean, rstd
+ZK_EXPORT int zk_bn_finalize_f64(const void* sums, int C, double P, const void* gamma,
+                                 const void* beta, float eps, float momentum, void* rmean,
+                                 void* rvar, void* coef, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
+                     (const double*)sums, C, P, (const float*)gamma, (const float*)beta, eps,
+                     momentum, (float*)rmean, (float*)rvar, (float*)coef);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_bn_apply_bf16(const void* x, const void* coef, void* y, long long P, int C,
+                               int relu, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+#define CASE(cg)                                                                           \
+  case cg:                                                                                 \
+    hipLaunchKernelGGL(bn_apply_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,  \
+                       (const uint16_t*)x, (const float*)coef, (uint16_t*)y, P, relu);     \
+    break;
+  ZK_CG_CASES(C, CASE)
+#undef CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_bn_bwd_reduce_bf16(const void* g, const void* x, const void* y,
+                                    const void* coef, void* sums, long long P, int C,
+                                    hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+#define CASE(cg)                                                                              \
+  case cg:                                                                                    \
+    hipLaunchKernelGGL(bn_bwd_reduce_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st, \
+                       (const uint16_t*)g, (const uint16_t*)x, (const uint16_t*)y,            \
+                       (const float*)coef, (float*)sums, P);                                  \
+    break;
+  ZK_CG_CASES(C, CASE)
+#undef CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_bn_bwd_dx_bf16(const void* g, const void* x, const void* y, const void* bcoef,
+                                void* dx, long long P, int C, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+#define CASE(cg)                                                                             \
+  case cg:                                                                                   \
+    hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,   \
+                       (const uint16_t*)g, (const uint16_t*)x, (const uint16_t*)y,           \
+                       (const float*)bcoef, (uint16_t*)dx, P);                               \
+    break;
+  ZK_CG_CASES(C, CASE)
+#undef CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_maxpool_fwd(const void* x, void* y, void* arg, int B, int H, int W, int C,
+                             int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st) {
+  if (C % 8 || k * k > 255) return (int)hipErrorInvalidValue;
+  const long long work = (long long)B * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(flat_grid(work)), dim3(256), 0, st,
+                     (const uint16_t*)x, (uint16_t*)y, (uint8_t*)arg, B, H, W, C, Ho, Wo, k, s,
+                     pt, pl);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_maxpool_bwd(const void* dy, const void* arg, void* dx, int B, int H, int W,
+                             int C, int Ho, int Wo, int k, int s, int pt, int pl,
+                             hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const long long work = (long long)B * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(flat_grid(work)), dim3(256), 0, st,
+                     (const uint16_t*)dy, (const uint8_t*)arg, (uint16_t*)dx, B, H, W, C, Ho,
+                     Wo, k, s, pt, pl);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_avgpool2_fwd(const void* x, void* y, int B, int H, int W, int C, int Ho,
+                              int Wo, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const long long work = (long long)B * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(avgpool2_fwd_kernel, dim3(flat_grid(work)), dim3(256), 0, st,
+                     (const uint16_t*)x, (uint16_t*)y, B, H, W, C, Ho, Wo);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_avgpool2_bwd(const void* dy, void* dx, int B, int H, int W, int C, int Ho,
+                              int Wo, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const long long work = (long long)B * H * W * (C / 8);
+  hipLaunchKernelGGL(avgpool2_bwd_kernel, dim3(flat_grid(work)), dim3(256), 0, st,
+                     (const uint16_t*)dy, (uint16_t*)dx, B, H, W, C, Ho, Wo);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}

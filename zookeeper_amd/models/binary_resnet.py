@@ -91,8 +91,7 @@ class BinaryResNetE(nn.Module):
         else:
             stem += [
                 QuantConv2d(c, initial_filters, 7, 2, "same", kernel_initializer="he_normal"),
-                BatchNorm(initial_filters, momentum=0.9, eps=1e-5),
-                nn.ReLU(),
+                BatchNorm(initial_filters, momentum=0.9, eps=1e-5, activation="relu"),
                 MaxPool2d(3, 2, "same"),
                 BatchNorm(initial_filters, momentum=0.9, eps=1e-5),
             ]

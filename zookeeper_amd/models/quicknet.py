@@ -97,8 +97,7 @@ class QuickNetModule(nn.Module):
         f0 = section_filters[0]
         self.stem = nn.Sequential(
             QuantConv2d(c, f0 // 4, 3, 2, "same", kernel_initializer="he_normal"),
-            BatchNorm(f0 // 4, momentum=0.9, eps=1e-5),
-            nn.ReLU(),
+            BatchNorm(f0 // 4, momentum=0.9, eps=1e-5, activation="relu"),
             QuantConv2d(f0 // 4, f0 // 4, 3, 2, "same", groups=f0 // 4,
                         kernel_initializer="he_normal"),
             BatchNorm(f0 // 4, momentum=0.9, eps=1e-5),

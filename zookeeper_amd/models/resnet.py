@@ -23,9 +23,9 @@ class Bottleneck(nn.Module):
         super().__init__()
         cout = width * 4
         self.conv1 = QuantConv2d(cin, width, 1, 1, "valid", kernel_initializer="he_normal")
-        self.bn1 = BatchNorm(width, 0.9, 1e-5)
+        self.bn1 = BatchNorm(width, 0.9, 1e-5, activation="relu")
         self.conv2 = QuantConv2d(width, width, 3, stride, "same", kernel_initializer="he_normal")
-        self.bn2 = BatchNorm(width, 0.9, 1e-5)
+        self.bn2 = BatchNorm(width, 0.9, 1e-5, activation="relu")
         self.conv3 = QuantConv2d(width, cout, 1, 1, "valid", kernel_initializer="he_normal")
         self.bn3 = BatchNorm(cout, 0.9, 1e-5)
         nn.init.zeros_(self.bn3.weight)
@@ -38,8 +38,8 @@ class Bottleneck(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idt = self.down(x) if self.down is not None else x
-        y = F.relu(self.bn1(self.conv1(x)))
-        y = F.relu(self.bn2(self.conv2(y)))
+        y = self.bn1(self.conv1(x))
+        y = self.bn2(self.conv2(y))
         y = self.bn3(self.conv3(y))
         return F.relu(y + idt)
 
@@ -50,8 +50,7 @@ class ResNetModule(nn.Module):
         c = input_shape[2]
         self.stem = nn.Sequential(
             QuantConv2d(c, 64, 7, 2, "same", kernel_initializer="he_normal"),
-            BatchNorm(64, 0.9, 1e-5),
-            nn.ReLU(),
+            BatchNorm(64, 0.9, 1e-5, activation="relu"),
             MaxPool2d(3, 2, "same"),
         )
         layers, cin = [], 64

@@ -36,6 +36,15 @@ def _pair(v: IntPair) -> Tuple[int, int]:
     return (v, v) if isinstance(v, int) else tuple(v)  # type: ignore[return-value]
 
 
+def _use_native(x: torch.Tensor) -> bool:
+    """HIP kernels run for bf16 tensors on the GPU when the library is loaded."""
+    if not (x.is_cuda and x.dtype == torch.bfloat16):
+        return False
+    from zookeeper_amd import ops
+
+    return ops.available()
+
+
 def same_padding(size: int, kernel: int, stride: int, dilation: int = 1) -> Tuple[int, int]:
     """TensorFlow ``SAME`` padding (before, after) for one spatial dim."""
     eff = (kernel - 1) * dilation + 1
@@ -188,9 +197,12 @@ class BatchNorm(nn.Module):
     """
 
     def __init__(self, num_features: int, momentum: float = 0.99, eps: float = 1e-3,
-                 scale: bool = True, center: bool = True):
+                 scale: bool = True, center: bool = True, activation: Optional[str] = None):
         super().__init__()
+        if activation not in (None, "relu"):
+            raise ValueError("BatchNorm activation must be None or 'relu'")
         self.num_features, self.momentum, self.eps = num_features, momentum, eps
+        self.activation = activation
         self.weight = nn.Parameter(torch.ones(num_features)) if scale else None
         self.bias = nn.Parameter(torch.zeros(num_features)) if center else None
         self.register_buffer("running_mean", torch.zeros(num_features))
@@ -201,15 +213,23 @@ class BatchNorm(nn.Module):
                 f"scale={self.weight is not None}, center={self.bias is not None}")
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        relu = self.activation == "relu"
+        if _use_native(x):
+            from zookeeper_amd.ops import norm_pool
+
+            if norm_pool.supported(x):
+                return norm_pool.batch_norm(x, self, relu)
         w = self.weight
         b = self.bias
         if x.dtype != torch.float32:
-            # Compute in fp32 (the oracle path); HIP kernels fuse this.
+            # Oracle path: compute in fp32, return in the input dtype.
             y = F.batch_norm(x.float(), self.running_mean, self.running_var, w, b,
                              self.training, 1.0 - self.momentum, self.eps)
-            return y.to(x.dtype)
-        return F.batch_norm(x, self.running_mean, self.running_var, w, b, self.training,
-                            1.0 - self.momentum, self.eps)
+            y = y.to(x.dtype)
+        else:
+            y = F.batch_norm(x, self.running_mean, self.running_var, w, b, self.training,
+                             1.0 - self.momentum, self.eps)
+        return F.relu(y) if relu else y
 
 
 class MaxPool2d(nn.Module):
@@ -223,6 +243,11 @@ class MaxPool2d(nn.Module):
         self.padding = padding
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        k, s = self.pool_size, self.stride
+        if _use_native(x) and x.dim() == 4 and x.shape[1] % 8 == 0 and k[0] == k[1] and s[0] == s[1]:
+            from zookeeper_amd.ops import norm_pool
+
+            return norm_pool.max_pool(x, k[0], s[0], self.padding)
         if self.padding == "same":
             x = pad_same_nhwc(x, self.pool_size, self.stride, float("-inf"))
         return F.max_pool2d(x, self.pool_size, self.stride)
@@ -237,6 +262,11 @@ class AvgPool2d(nn.Module):
         self.stride = _pair(stride if stride is not None else pool_size)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if (_use_native(x) and x.dim() == 4 and x.shape[1] % 8 == 0
+                and self.pool_size == (2, 2) and self.stride == (2, 2)):
+            from zookeeper_amd.ops import norm_pool
+
+            return norm_pool.avg_pool2(x)
         return F.avg_pool2d(x, self.pool_size, self.stride)
 
 

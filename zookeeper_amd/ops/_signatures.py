@@ -19,6 +19,27 @@ SIGNATURES = {
     "zk_gather_rows": (I32, [P, I64, P, I64, P, I32]),
     # preprocessing
     "zk_normalize_flip_c3": (I32, [P, P, I32, I32, I32, FP, FP, I32, U64, P]),
+    # binary convolution
+    "zk_sign_pack": (I32, [P, P, P, I64, F32, P]),
+    "zk_weight_pack": (I32, [P, P, P, P, I32, I32, I32, P]),
+    "zk_unpack_sign": (I32, [P, P, I64, P]),
+    "zk_bconv_fwd": (I32, [P, P, P, P, P] + [I32] * 14 + [P]),
+    # batch norm
+    "zk_bn_finalize": (I32, [P, I32, C.c_double, P, P, F32, F32, P, P, P, P, P, P, P]),
+    "zk_bn_apply": (I32, [P, P, P, P, P, I64, I32, P]),
+    "zk_bn_bwd_reduce": (I32, [P, P, P, P, P, I64, I32, P]),
+    "zk_bn_bwd_dx": (I32, [P, P, P, P, I64, I32, I32, P]),
+    "zk_ste_combine": (I32, [P, P, P, P, I64, P]),
+    # batch norm (bf16) and pooling
+    "zk_bn_stats_bf16": (I32, [P, P, I64, I32, P]),
+    "zk_bn_finalize_f64": (I32, [P, I32, C.c_double, P, P, F32, F32, P, P, P, P]),
+    "zk_bn_apply_bf16": (I32, [P, P, P, I64, I32, I32, P]),
+    "zk_bn_bwd_reduce_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
+    "zk_bn_bwd_dx_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
+    "zk_maxpool_fwd": (I32, [P, P, P] + [I32] * 10 + [P]),
+    "zk_maxpool_bwd": (I32, [P, P, P] + [I32] * 10 + [P]),
+    "zk_avgpool2_fwd": (I32, [P, P] + [I32] * 6 + [P]),
+    "zk_avgpool2_bwd": (I32, [P, P] + [I32] * 6 + [P]),
     # optimizers
     "zk_adam_step": (I32, [P, P, P, P, P, I32, F32, F32, F32, F32, F32, F32, F32, F32, P]),
     "zk_sgd_step": (I32, [P, P, P, P, I32, F32, F32, F32, F32, I32, P]),

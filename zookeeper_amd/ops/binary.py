@@ -1,0 +1,186 @@
+"""Fused binary residual block: ``out = BN(act(bconv(sign(x)))) + residual``.
+
+One autograd op per block (used by BinaryResNet-E and QuickNet on the
+``hip`` backend).  Forward kernels (``csrc/kernels/binary_conv.hip``,
+``batchnorm.hip``):
+
+1. ``zk_sign_pack``   x bf16 → sign bits + STE mask bits (|x| ≤ clip), 1 bit each;
+2. ``zk_weight_pack`` latent fp32 kernel → sign bits, per-tap popcounts, ±1 bf16;
+3. ``zk_bconv_fwd``   XNOR-popcount implicit GEMM on LDS bit tiles → exact
+   int16 output (+ optional ReLU) and exact int64 BN statistics;
+4. ``zk_bn_finalize`` per-channel scale/shift, running statistics (Keras
+   momentum, Bessel-corrected variance);
+5. ``zk_bn_apply``    out = scale·y + shift + residual, bf16.
+
+Backward: ``zk_bn_bwd_reduce`` (Σg, Σg·ŷ) → ``zk_bn_bwd_dx`` (dy, ReLU mask)
+→ data and weight gradients of the ±1 convolution as bf16 GEMMs
+(dy ⊛ sign(W)ᵀ and sign(x)ᵀ ⊛ dy, exact ±1 operands in bf16) →
+``zk_ste_combine`` (STE mask of the input + residual gradient, one pass).
+
+Saved for backward: 2 bits per input element (sign, STE mask), the int16
+conv output and per-channel vectors — no bf16 copy of the input.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from zookeeper_amd.nn.layers import same_padding
+from zookeeper_amd.ops._native import check, lib, stream_ptr
+
+
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    """NCHW-shaped tensor → contiguous NHWC storage (no copy if channels_last)."""
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+class _BinaryBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, gamma, beta, bn, meta):
+        (stride, act_relu, clip, pad_ones, identity) = meta
+        B, Cin, H, W = x.shape
+        Cout, _, kh, kw = weight.shape
+        T = kh * kw
+        pt, pb = same_padding(H, kh, stride)
+        pl, pr = same_padding(W, kw, stride)
+        Ho, Wo = (H + pt + pb - kh) // stride + 1, (W + pl + pr - kw) // stride + 1
+        dev = x.device
+        st = stream_ptr(dev)
+        L = lib()
+
+        xn = _nhwc(x)
+        nwords = B * H * W * Cin // 32
+        bits = torch.empty(nwords, dtype=torch.int32, device=dev)
+        mask = torch.empty(nwords, dtype=torch.int32, device=dev)
+        check(L.zk_sign_pack(xn.data_ptr(), bits.data_ptr(), mask.data_ptr(), nwords, clip, st),
+              "zk_sign_pack")
+
+        w_ohwi = weight.permute(0, 2, 3, 1).contiguous()  # no copy for channels_last
+        wbits = torch.empty(Cout * T * Cin // 32, dtype=torch.int32, device=dev)
+        wpop = torch.empty(Cout * T, dtype=torch.int32, device=dev)
+        wsign = torch.empty((Cout, kh, kw, Cin), dtype=torch.bfloat16, device=dev)
+        check(L.zk_weight_pack(w_ohwi.data_ptr(), wbits.data_ptr(), wpop.data_ptr(),
+                               wsign.data_ptr(), Cout, T, Cin, st), "zk_weight_pack")
+
+        P = B * Ho * Wo
+        y = torch.empty((B, Ho, Wo, Cout), dtype=torch.int16, device=dev)
+        stats = torch.zeros((2, Cout), dtype=torch.int64, device=dev)
+        check(L.zk_bconv_fwd(bits.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), y.data_ptr(),
+                             stats.data_ptr(), B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho,
+                             Wo, int(pad_ones), int(act_relu), st), "zk_bconv_fwd")
+
+        scale = torch.empty(Cout, dtype=torch.float32, device=dev)
+        shift = torch.empty_like(scale)
+        mean = torch.empty_like(scale)
+        rstd = torch.empty_like(scale)
+        gp = gamma.data_ptr() if gamma is not None else None
+        bp = beta.data_ptr() if beta is not None else None
+        if bn.training:
+            check(L.zk_bn_finalize(stats.data_ptr(), Cout, float(P), gp, bp, bn.eps, bn.momentum,
+                                   bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+                                   scale.data_ptr(), shift.data_ptr(), mean.data_ptr(),
+                                   rstd.data_ptr(), st), "zk_bn_finalize")
+        else:
+            rstd.copy_(torch.rsqrt(bn.running_var + bn.eps))
+            mean.copy_(bn.running_mean)
+            g_ = gamma if gamma is not None else torch.ones_like(rstd)
+            b_ = beta if beta is not None else torch.zeros_like(rstd)
+            scale.copy_(g_ * rstd)
+            shift.copy_(b_ - mean * scale)
+
+        res = xn if identity else (_nhwc(residual) if residual is not None else None)
+        out = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=dev)
+        check(L.zk_bn_apply(y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                            res.data_ptr() if res is not None else None, out.data_ptr(), P,
+                            Cout, st), "zk_bn_apply")
+
+        ctx.save_for_backward(bits, mask, wsign, y, mean, rstd, gamma, weight)
+        ctx.geom = (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo)
+        ctx.meta = meta
+        ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
+        ctx.has_residual = residual is not None and not identity
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dout):
+        bits, mask, wsign, y, mean, rstd, gamma, weight = ctx.saved_tensors
+        (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
+        (_, act_relu, clip, pad_ones, identity) = ctx.meta
+        dev = dout.device
+        st = stream_ptr(dev)
+        L = lib()
+        P = B * Ho * Wo
+
+        g = _nhwc(dout.to(torch.bfloat16))
+        sums = torch.zeros((2, Cout), dtype=torch.float32, device=dev)
+        check(L.zk_bn_bwd_reduce(g.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                 sums.data_ptr(), P, Cout, st), "zk_bn_bwd_reduce")
+        gam = gamma.detach() if gamma is not None else torch.ones_like(rstd)
+        k1 = gam * rstd
+        coef = torch.stack([k1, k1 * sums[0] / P, k1 * rstd * sums[1] / P, mean]).contiguous()
+        dy = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=dev)
+        check(L.zk_bn_bwd_dx(g.data_ptr(), y.data_ptr(), coef.data_ptr(), dy.data_ptr(), P,
+                             Cout, int(act_relu), st), "zk_bn_bwd_dx")
+
+        # ±1 operands as bf16 for the data/weight-gradient GEMMs.
+        xs = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
+        check(L.zk_unpack_sign(bits.data_ptr(), xs.data_ptr(), bits.numel(), st),
+              "zk_unpack_sign")
+        xs_nchw = xs.permute(0, 3, 1, 2)
+        w_nchw = wsign.permute(0, 3, 1, 2)
+        dy_nchw = dy.permute(0, 3, 1, 2)
+        symmetric = (pt == pb and pl == pr) and not pad_ones
+        if symmetric:
+            inp, pad = xs_nchw, (pt, pl)
+        else:
+            inp = torch.nn.functional.pad(xs_nchw, (pl, pr, pt, pb), value=1.0 if pad_ones else 0.0)
+            inp = inp.contiguous(memory_format=torch.channels_last)
+            pad = (0, 0)
+        need_dx = ctx.needs_input_grad[0]
+        dgrad, dw, _ = torch.ops.aten.convolution_backward(
+            dy_nchw, inp, w_nchw, None, (stride, stride), pad, (1, 1), False, (0, 0), 1,
+            (need_dx, True, False))
+
+        dx = None
+        if need_dx:
+            if not symmetric:
+                dgrad = dgrad[:, :, pt:pt + H, pl:pl + W]
+            dgn = _nhwc(dgrad)
+            dx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
+            dres = g if identity else None
+            check(L.zk_ste_combine(dgn.data_ptr(), mask.data_ptr(),
+                                   dres.data_ptr() if dres is not None else None, dx.data_ptr(),
+                                   dx.numel(), st), "zk_ste_combine")
+            dx = dx.permute(0, 3, 1, 2)
+        w = weight.detach()
+        dweight = dw.float() * (w.abs() <= clip).to(torch.float32)
+        dgamma = sums[1].clone() if ctx.has_gamma else None
+        dbeta = sums[0].clone() if ctx.has_beta else None
+        dres_out = dout if ctx.has_residual else None
+        return dx, dres_out, dweight, dgamma, dbeta, None, None
+
+
+def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
+                 act: Optional[str] = None, clip_value: float = 1.0,
+                 pad_value: float = 0.0) -> torch.Tensor:
+    """Run ``bn(act(conv(x))) + residual`` with the fused HIP kernels.
+
+    ``conv`` must be a binary ``QuantConv2d`` (ste_sign input and kernel,
+    ``same`` padding), ``bn`` a :class:`~zookeeper_amd.nn.BatchNorm`.
+    ``residual`` may be ``x`` itself (identity shortcut, fused into the
+    backward) or a separately computed tensor, or ``None``.
+    """
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    if x.shape[1] % 32 or conv.weight.shape[0] % 8:
+        raise ValueError("binary_block needs Cin % 32 == 0 and Cout % 8 == 0")
+    if conv.stride[0] != conv.stride[1]:
+        raise ValueError("binary_block needs a square stride")
+    identity = residual is x
+    if residual is not None and not identity and residual.dtype != torch.bfloat16:
+        residual = residual.to(torch.bfloat16)
+    meta = (conv.stride[0], act == "relu", float(clip_value), pad_value == 1.0, identity)
+    return _BinaryBlockFn.apply(x, None if identity else residual, conv.weight, bn.weight,
+                                bn.bias, bn, meta)

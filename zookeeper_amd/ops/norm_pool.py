@@ -1,0 +1,154 @@
+"""BatchNorm(+ReLU) and pooling on bf16 NHWC tensors (HIP kernels in
+``csrc/kernels/norm_pool.hip``), as autograd functions.
+
+Tensors are NCHW-*shaped* with ``channels_last`` strides (physically NHWC),
+the layout every model in the zoo uses.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from zookeeper_amd.nn.layers import same_padding
+from zookeeper_amd.ops._native import check, lib, stream_ptr
+
+
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    return t.permute(0, 2, 3, 1).contiguous() if t.dim() == 4 else t.contiguous()
+
+
+def _back(t: torch.Tensor, like_dim: int) -> torch.Tensor:
+    return t.permute(0, 3, 1, 2) if like_dim == 4 else t
+
+
+def supported(x: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() in (2, 4)
+            and x.shape[1] % 8 == 0 and x.shape[1] <= 2048)
+
+
+class _BatchNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, bn, relu):
+        dim = x.dim()
+        C = x.shape[1]
+        xn = _nhwc(x)
+        P = xn.numel() // C
+        dev = x.device
+        st = stream_ptr(dev)
+        L = lib()
+        coef = torch.empty((4, C), dtype=torch.float32, device=dev)
+        if bn.training:
+            sums = torch.zeros((2, C), dtype=torch.float64, device=dev)
+            check(L.zk_bn_stats_bf16(xn.data_ptr(), sums.data_ptr(), P, C, st), "zk_bn_stats_bf16")
+            check(L.zk_bn_finalize_f64(sums.data_ptr(), C, float(P),
+                                       gamma.data_ptr() if gamma is not None else None,
+                                       beta.data_ptr() if beta is not None else None,
+                                       bn.eps, bn.momentum, bn.running_mean.data_ptr(),
+                                       bn.running_var.data_ptr(), coef.data_ptr(), st),
+                  "zk_bn_finalize_f64")
+        else:
+            rstd = torch.rsqrt(bn.running_var + bn.eps)
+            g = gamma if gamma is not None else torch.ones_like(rstd)
+            b = beta if beta is not None else torch.zeros_like(rstd)
+            coef[0] = g * rstd
+            coef[1] = b - bn.running_mean * coef[0]
+            coef[2] = bn.running_mean
+            coef[3] = rstd
+        y = torch.empty_like(xn)
+        check(L.zk_bn_apply_bf16(xn.data_ptr(), coef.data_ptr(), y.data_ptr(), P, C, int(relu), st),
+              "zk_bn_apply_bf16")
+        ctx.save_for_backward(xn, y if relu else None, coef, gamma)
+        ctx.dim, ctx.P, ctx.C = dim, P, C
+        ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
+        return _back(y, dim)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xn, y, coef, gamma = ctx.saved_tensors
+        P, C = ctx.P, ctx.C
+        dev = dy.device
+        st = stream_ptr(dev)
+        L = lib()
+        g = _nhwc(dy.to(torch.bfloat16))
+        sums = torch.zeros((2, C), dtype=torch.float32, device=dev)
+        check(L.zk_bn_bwd_reduce_bf16(g.data_ptr(), xn.data_ptr(),
+                                      y.data_ptr() if y is not None else None,
+                                      coef.data_ptr(), sums.data_ptr(), P, C, st),
+              "zk_bn_bwd_reduce_bf16")
+        mean, rstd = coef[2], coef[3]
+        gam = gamma.detach() if gamma is not None else torch.ones_like(rstd)
+        k1 = gam * rstd
+        k3 = k1 * rstd * sums[1] / P
+        k0 = k3 * mean - k1 * sums[0] / P
+        bcoef = torch.stack([k1, k0, k3]).contiguous()
+        dx = torch.empty_like(g)
+        check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), xn.data_ptr(),
+                                  y.data_ptr() if y is not None else None, bcoef.data_ptr(),
+                                  dx.data_ptr(), P, C, st), "zk_bn_bwd_dx_bf16")
+        dgamma = sums[1].clone() if ctx.has_gamma else None
+        dbeta = sums[0].clone() if ctx.has_beta else None
+        return _back(dx, ctx.dim), dgamma, dbeta, None, None
+
+
+def batch_norm(x: torch.Tensor, bn, relu: bool = False) -> torch.Tensor:
+    return _BatchNormFn.apply(x, bn.weight, bn.bias, bn, relu)
+
+
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, padding):
+        B, C, H, W = x.shape
+        if padding == "same":
+            pt, pb = same_padding(H, k, s)
+            pl, pr = same_padding(W, k, s)
+        else:
+            pt = pb = pl = pr = 0
+        Ho, Wo = (H + pt + pb - k) // s + 1, (W + pl + pr - k) // s + 1
+        xn = _nhwc(x)
+        y = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=x.device)
+        arg = torch.empty((B, Ho, Wo, C), dtype=torch.uint8, device=x.device)
+        check(lib().zk_maxpool_fwd(xn.data_ptr(), y.data_ptr(), arg.data_ptr(), B, H, W, C, Ho,
+                                   Wo, k, s, pt, pl, stream_ptr(x.device)), "zk_maxpool_fwd")
+        ctx.save_for_backward(arg)
+        ctx.geom = (B, H, W, C, Ho, Wo, k, s, pt, pl)
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        B, H, W, C, Ho, Wo, k, s, pt, pl = ctx.geom
+        g = _nhwc(dy.to(torch.bfloat16))
+        dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
+        check(lib().zk_maxpool_bwd(g.data_ptr(), arg.data_ptr(), dx.data_ptr(), B, H, W, C, Ho,
+                                   Wo, k, s, pt, pl, stream_ptr(dy.device)), "zk_maxpool_bwd")
+        return dx.permute(0, 3, 1, 2), None, None, None
+
+
+def max_pool(x: torch.Tensor, k: int, s: int, padding: str = "valid") -> torch.Tensor:
+    return _MaxPoolFn.apply(x, k, s, padding)
+
+
+class _AvgPool2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        B, C, H, W = x.shape
+        Ho, Wo = H // 2, W // 2
+        xn = _nhwc(x)
+        y = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=x.device)
+        check(lib().zk_avgpool2_fwd(xn.data_ptr(), y.data_ptr(), B, H, W, C, Ho, Wo,
+                                    stream_ptr(x.device)), "zk_avgpool2_fwd")
+        ctx.geom = (B, H, W, C, Ho, Wo)
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, H, W, C, Ho, Wo = ctx.geom
+        g = _nhwc(dy.to(torch.bfloat16))
+        dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
+        check(lib().zk_avgpool2_bwd(g.data_ptr(), dx.data_ptr(), B, H, W, C, Ho, Wo,
+                                    stream_ptr(dy.device)), "zk_avgpool2_bwd")
+        return dx.permute(0, 3, 1, 2)
+
+
+def avg_pool2(x: torch.Tensor) -> torch.Tensor:
+    return _AvgPool2Fn.apply(x)
