@@ -1,0 +1,65 @@
+"""MFMA dgrad / wgrad kernels of the binary conv vs fp64 references (the ±1
+operand is exact; dy is bf16, so errors come only from fp32 accumulation)."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+@pytest.mark.parametrize("cin,cout,stride,hw,pad_ones", [
+    (64, 64, 1, 12, 0), (64, 128, 2, 12, 0), (128, 128, 1, 7, 1), (256, 512, 2, 8, 0),
+    (128, 64, 1, 9, 0)])
+def test_dgrad_wgrad(cin, cout, stride, hw, pad_ones):
+    from zookeeper_amd.nn.layers import pad_same_nhwc, same_padding
+    from zookeeper_amd.nn.quantizers import sign_pm1
+    from zookeeper_amd.ops._native import lib, stream_ptr
+
+    torch.manual_seed(0)
+    L, st = lib(), stream_ptr()
+    B = 3
+    x = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
+    w = torch.empty(cout, 3, 3, cin, device="cuda").uniform_(-1.2, 1.2)
+    pt, pb = same_padding(hw, 3, stride)
+    ho = (hw + pt + pb - 3) // stride + 1
+    dy = torch.randn(B, ho, ho, cout, device="cuda").to(torch.bfloat16)
+    nwords = x.numel() // 32
+    bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
+    mask = torch.empty(nwords, dtype=torch.int32, device="cuda")
+    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), nwords, 1.0, st) == 0
+    wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
+    wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
+    wt = torch.empty(9, cin, cout, dtype=torch.bfloat16, device="cuda")
+    assert L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(),
+                            cout, 9, cin, st) == 0
+    dres = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
+    dx = torch.empty(B, hw, hw, cin, dtype=torch.bfloat16, device="cuda")
+    assert L.zk_bconv_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(), dres.data_ptr(),
+                            dx.data_ptr(), B, hw, hw, cin, ho, ho, cout, 3, 3, stride, pt, pt,
+                            st) == 0
+    dw = torch.zeros(cout, 3, 3, cin, device="cuda")
+    assert L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w.data_ptr(), dw.data_ptr(), B, hw,
+                            hw, cin, ho, ho, cout, 3, 3, stride, pt, pt, pad_ones, 1.0, 1024,
+                            st) == 0
+    torch.cuda.synchronize()
+
+    # fp64 reference through autograd of the ±1 convolution
+    xs = sign_pm1(x.double()).permute(0, 3, 1, 2).requires_grad_(True)
+    ws = sign_pm1(w.double()).permute(0, 3, 1, 2).requires_grad_(True)
+    xp = pad_same_nhwc(xs, (3, 3), (stride, stride), 1.0 if pad_ones else 0.0)
+    out = F.conv2d(xp, ws, stride=stride)
+    out.backward(dy.double().permute(0, 3, 1, 2))
+    ste_x = (x.double().abs() <= 1.0)
+    ref_dx = xs.grad.permute(0, 2, 3, 1) * ste_x + dres.double()
+    ref_dw = ws.grad.permute(0, 2, 3, 1) * (w.double().abs() <= 1.0)
+    err_dx = (dx.double() - ref_dx).abs().max().item()
+    assert err_dx <= 1e-2 * ref_dx.abs().max().item() + 1e-2, err_dx
+    err_dw = (dw.double() - ref_dw).abs().max().item()
+    assert err_dw <= 1e-4 * ref_dw.abs().max().item() + 1e-3, err_dw

@@ -69,14 +69,16 @@ __global__ __launch_bounds__(256) void sign_pack_kernel(const uint16_t* __restri
 
 // --------------------------------------------------------------------------
 // Kernel packing: w fp32 [Cout][T][Cin] (OHWI) -> wbits [Cout][T][CW],
-// wpop [Cout][T] (popcount per tap; zeroed by the caller), wsign bf16 ±1
-// [Cout][T][Cin] (optional).  One thread per packed word (8 float4 loads).
+// wpop [Cout][T] (popcount per tap; zeroed by the caller), and (optional)
+// wt: the ±1 kernel as bf16, transposed to [T][Cin][Cout] for the dgrad
+// GEMM (K = Cout contiguous).  One thread per packed word (8 float4 loads).
 // --------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restrict__ w,
                                                           uint32_t* __restrict__ wbits,
                                                           int* __restrict__ wpop,
-                                                          uint16_t* __restrict__ wsign,
-                                                          long long nwords, int CW) {
+                                                          uint16_t* __restrict__ wt,
+                                                          long long nwords, int CW, int T,
+                                                          int Cout) {
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (i >= nwords) return;
   const float4* src = reinterpret_cast<const float4*>(w + 32 * i);
@@ -91,19 +93,14 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restric
   }
   wbits[i] = b;
   atomicAdd(wpop + i / CW, __popc(b));
-  if (wsign) {
-    uint4* dst = reinterpret_cast<uint4*>(wsign + 32 * i);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t v[4];
-#pragma unroll
-      for (int h = 0; h < 4; ++h) {
-        const int k = q * 8 + h * 2;
-        v[h] = (((b >> k) & 1) ? 0x3F80u : 0xBF80u) |
-               ((((b >> (k + 1)) & 1) ? 0x3F80u : 0xBF80u) << 16);
-      }
-      dst[q] = make_uint4(v[0], v[1], v[2], v[3]);
-    }
+  if (wt) {
+    const int wd = (int)(i % CW);
+    const long long ct = i / CW;
+    const int t = (int)(ct % T), co = (int)(ct / T);
+    const int Cin = CW * 32;
+    uint16_t* dst = wt + ((long long)t * Cin + wd * 32) * Cout + co;
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) dst[(long long)k * Cout] = ((b >> k) & 1) ? 0x3F80 : 0xBF80;
   }
 }
 
@@ -361,14 +358,14 @@ ZK_EXPORT int zk_sign_pack(const void* x, void* bits, void* mask, long long nwor
   return 0;
 }
 
-ZK_EXPORT int zk_weight_pack(const void* w, void* wbits, void* wpop, void* wsign, int Cout,
+ZK_EXPORT int zk_weight_pack(const void* w, void* wbits, void* wpop, void* wt, int Cout,
                              int T, int Cin, hipStream_t stream) {
   if (Cin % 32) return (int)hipErrorInvalidValue;
   const long long nwords = (long long)Cout * T * (Cin / 32);
   hipMemsetAsync(wpop, 0, sizeof(int) * (size_t)Cout * T, stream);
   hipLaunchKernelGGL(weight_pack_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0,
-                     stream, (const float*)w, (uint32_t*)wbits, (int*)wpop, (uint16_t*)wsign,
-                     nwords, Cin / 32);
+                     stream, (const float*)w, (uint32_t*)wbits, (int*)wpop, (uint16_t*)wt,
+                     nwords, Cin / 32, T, Cout);
   ZK_CHECK_LAUNCH();
   return 0;
 }

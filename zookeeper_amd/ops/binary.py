@@ -13,9 +13,10 @@ One autograd op per block (used by BinaryResNet-E and QuickNet on the
 5. ``zk_bn_apply``    out = scale·y + shift + residual, bf16.
 
 Backward: ``zk_bn_bwd_reduce`` (Σg, Σg·ŷ) → ``zk_bn_bwd_dx`` (dy, ReLU mask)
-→ data and weight gradients of the ±1 convolution as bf16 GEMMs
-(dy ⊛ sign(W)ᵀ and sign(x)ᵀ ⊛ dy, exact ±1 operands in bf16) →
-``zk_ste_combine`` (STE mask of the input + residual gradient, one pass).
+→ ``zk_bconv_dgrad`` (MFMA implicit GEMM dy ⊛ sign(W)ᵀ with the input STE
+mask and the identity-residual gradient fused into its epilogue) and
+``zk_bconv_wgrad`` (MFMA implicit GEMM reading the packed sign bits of x
+directly, kernel STE mask in the epilogue, split-K fp32 atomics).
 
 Saved for backward: 2 bits per input element (sign, STE mask), the int16
 conv output and per-channel vectors — no bf16 copy of the input.
@@ -60,9 +61,10 @@ class _BinaryBlockFn(torch.autograd.Function):
         w_ohwi = weight.permute(0, 2, 3, 1).contiguous()  # no copy for channels_last
         wbits = torch.empty(Cout * T * Cin // 32, dtype=torch.int32, device=dev)
         wpop = torch.empty(Cout * T, dtype=torch.int32, device=dev)
-        wsign = torch.empty((Cout, kh, kw, Cin), dtype=torch.bfloat16, device=dev)
+        # ±1 kernel transposed to [T][Cin][Cout] for the dgrad GEMM.
+        wt = torch.empty((T, Cin, Cout), dtype=torch.bfloat16, device=dev)
         check(L.zk_weight_pack(w_ohwi.data_ptr(), wbits.data_ptr(), wpop.data_ptr(),
-                               wsign.data_ptr(), Cout, T, Cin, st), "zk_weight_pack")
+                               wt.data_ptr(), Cout, T, Cin, st), "zk_weight_pack")
 
         P = B * Ho * Wo
         y = torch.empty((B, Ho, Wo, Cout), dtype=torch.int16, device=dev)
@@ -96,7 +98,7 @@ class _BinaryBlockFn(torch.autograd.Function):
                             res.data_ptr() if res is not None else None, out.data_ptr(), P,
                             Cout, st), "zk_bn_apply")
 
-        ctx.save_for_backward(bits, mask, wsign, y, mean, rstd, gamma, weight)
+        ctx.save_for_backward(bits, mask, wt, y, mean, rstd, gamma, w_ohwi)
         ctx.geom = (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo)
         ctx.meta = meta
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
@@ -105,7 +107,7 @@ class _BinaryBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        bits, mask, wsign, y, mean, rstd, gamma, weight = ctx.saved_tensors
+        bits, mask, wt, y, mean, rstd, gamma, w_ohwi = ctx.saved_tensors
         (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
         (_, act_relu, clip, pad_ones, identity) = ctx.meta
         dev = dout.device
@@ -124,42 +126,70 @@ class _BinaryBlockFn(torch.autograd.Function):
         check(L.zk_bn_bwd_dx(g.data_ptr(), y.data_ptr(), coef.data_ptr(), dy.data_ptr(), P,
                              Cout, int(act_relu), st), "zk_bn_bwd_dx")
 
-        # ±1 operands as bf16 for the data/weight-gradient GEMMs.
-        xs = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
-        check(L.zk_unpack_sign(bits.data_ptr(), xs.data_ptr(), bits.numel(), st),
-              "zk_unpack_sign")
-        xs_nchw = xs.permute(0, 3, 1, 2)
-        w_nchw = wsign.permute(0, 3, 1, 2)
-        dy_nchw = dy.permute(0, 3, 1, 2)
-        symmetric = (pt == pb and pl == pr) and not pad_ones
-        if symmetric:
-            inp, pad = xs_nchw, (pt, pl)
-        else:
-            inp = torch.nn.functional.pad(xs_nchw, (pl, pr, pt, pb), value=1.0 if pad_ones else 0.0)
-            inp = inp.contiguous(memory_format=torch.channels_last)
-            pad = (0, 0)
         need_dx = ctx.needs_input_grad[0]
-        dgrad, dw, _ = torch.ops.aten.convolution_backward(
-            dy_nchw, inp, w_nchw, None, (stride, stride), pad, (1, 1), False, (0, 0), 1,
-            (need_dx, True, False))
-
+        native = Cout % 64 == 0 and Cin % 64 == 0
         dx = None
-        if need_dx:
-            if not symmetric:
-                dgrad = dgrad[:, :, pt:pt + H, pl:pl + W]
-            dgn = _nhwc(dgrad)
-            dx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
-            dres = g if identity else None
-            check(L.zk_ste_combine(dgn.data_ptr(), mask.data_ptr(),
-                                   dres.data_ptr() if dres is not None else None, dx.data_ptr(),
-                                   dx.numel(), st), "zk_ste_combine")
-            dx = dx.permute(0, 3, 1, 2)
-        w = weight.detach()
-        dweight = dw.float() * (w.abs() <= clip).to(torch.float32)
-        dgamma = sums[1].clone() if ctx.has_gamma else None
-        dbeta = sums[0].clone() if ctx.has_beta else None
+        if native:
+            # MFMA implicit GEMMs; STE mask + residual gradient fused in dgrad.
+            if need_dx:
+                dx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
+                dres = g if identity else None
+                check(L.zk_bconv_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(),
+                                       dres.data_ptr() if dres is not None else None,
+                                       dx.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
+                                       stride, pt, pl, st), "zk_bconv_dgrad")
+                dx = dx.permute(0, 3, 1, 2)
+            dw = torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev)
+            check(L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w_ohwi.data_ptr(),
+                                   dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride,
+                                   pt, pl, int(pad_ones), clip, 1024, st), "zk_bconv_wgrad")
+            dweight = dw.permute(0, 3, 1, 2)
+        else:
+            dx, dweight = _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx)
+        dgamma = sums[1] if ctx.has_gamma else None
+        dbeta = sums[0] if ctx.has_beta else None
         dres_out = dout if ctx.has_residual else None
         return dx, dres_out, dweight, dgamma, dbeta, None, None
+
+
+def _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx):
+    """Fallback for channel counts the MFMA kernels do not tile (Cin or Cout
+    not a multiple of 64): bf16 library convolution backward on unpacked ±1
+    operands, then the fused STE/residual kernel."""
+    (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
+    (_, _, clip, pad_ones, identity) = ctx.meta
+    dev = dy.device
+    st = stream_ptr(dev)
+    L = lib()
+    xs = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
+    check(L.zk_unpack_sign(bits.data_ptr(), xs.data_ptr(), bits.numel(), st), "zk_unpack_sign")
+    xs_nchw = xs.permute(0, 3, 1, 2)
+    w_nchw = wt.permute(2, 1, 0).reshape(Cout, Cin, kh, kw).contiguous(
+        memory_format=torch.channels_last)
+    symmetric = (pt == pb and pl == pr) and not pad_ones
+    if symmetric:
+        inp, pad = xs_nchw, (pt, pl)
+    else:
+        inp = torch.nn.functional.pad(xs_nchw, (pl, pr, pt, pb), value=1.0 if pad_ones else 0.0)
+        inp = inp.contiguous(memory_format=torch.channels_last)
+        pad = (0, 0)
+    dgrad, dw, _ = torch.ops.aten.convolution_backward(
+        dy.permute(0, 3, 1, 2), inp, w_nchw, None, (stride, stride), pad, (1, 1), False,
+        (0, 0), 1, (need_dx, True, False))
+    dx = None
+    if need_dx:
+        if not symmetric:
+            dgrad = dgrad[:, :, pt:pt + H, pl:pl + W]
+        dgn = _nhwc(dgrad)
+        dx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
+        dres = g if identity else None
+        check(L.zk_ste_combine(dgn.data_ptr(), mask.data_ptr(),
+                               dres.data_ptr() if dres is not None else None, dx.data_ptr(),
+                               dx.numel(), st), "zk_ste_combine")
+        dx = dx.permute(0, 3, 1, 2)
+    w = w_ohwi.permute(0, 3, 1, 2)
+    dweight = dw.float() * (w.abs() <= clip).to(torch.float32)
+    return dx, dweight
 
 
 def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
