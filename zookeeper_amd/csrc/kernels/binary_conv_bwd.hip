@@ -237,7 +237,6 @@ __global__ __launch_bounds__(NT, 2) void bconv_wgrad_kernel(
   long long kend = kbeg + k_per_split;
   if (kend > P) kend = P;
   const int CW = g.Cin >> 5;
-  const uint32_t padw = pad_ones ? 0xFFFFFFFFu : 0u;
 
   uint4 ra[A_CH];
   uint32_t rb = 0;
@@ -259,16 +258,18 @@ __global__ __launch_bounds__(NT, 2) void bconv_wgrad_kernel(
       const long long p = k0 + kr;
       uint32_t v = 0;
       if (p < kend) {
-        rb_valid = 1;
         const int wo = (int)(p % g.Wo);
         const long long r = p / g.Wo;
         const int ho = (int)(r % g.Ho);
         const int b = (int)(r / g.Ho);
         const int hi = ho * g.s - g.pt + th, wi = wo * g.s - g.pl + tw;
-        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W) {
           v = xbits[(((long long)b * g.H + hi) * g.W + wi) * CW + (ci0 >> 5) + wd];
-        else
-          v = padw;
+          rb_valid = 1;
+        } else if (pad_ones) {
+          v = 0xFFFFFFFFu;  // +1 padding
+          rb_valid = 1;
+        }  // zero padding: the row contributes nothing (expanded as 0, not -1)
       }
       rb = v;
     }
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(NT, 2) void bconv_wgrad_kernel(
       const int kr = tid / (BN / 32), wd = tid % (BN / 32);
       uint16_t* dst = &Bs[kr * LDB + 32 * wd];
       // Expand 32 sign bits into 32 bf16 (+1 = 0x3F80, -1 = 0xBF80); rows past
-      // the split end are zero (no contribution).
+      // the split end and zero-padded taps are 0 (no contribution).
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         uint32_t v[4];
