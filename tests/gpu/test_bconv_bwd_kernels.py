@@ -43,11 +43,11 @@ def test_dgrad_wgrad(cin, cout, stride, hw, pad_ones):
     dx = torch.empty(B, hw, hw, cin, dtype=torch.bfloat16, device="cuda")
     assert L.zk_bconv_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(), dres.data_ptr(),
                             dx.data_ptr(), B, hw, hw, cin, ho, ho, cout, 3, 3, stride, pt, pt,
-                            st) == 0
+                            -1, st) == 0
     dw = torch.zeros(cout, 3, 3, cin, device="cuda")
     assert L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w.data_ptr(), dw.data_ptr(), B, hw,
                             hw, cin, ho, ho, cout, 3, 3, stride, pt, pt, pad_ones, 1.0, 1024,
-                            st) == 0
+                            -1, st) == 0
     torch.cuda.synchronize()
 
     # fp64 reference through autograd of the ±1 convolution

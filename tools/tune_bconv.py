@@ -1,0 +1,111 @@
+"""Time every tile variant of the binary-conv kernels on the BinaryResNet-E18
+layer shapes (MI355X) and print a table; also times the library (MIOpen)
+bf16 convolution backward on the same shapes for reference.
+
+    python tools/tune_bconv.py [--batch 256] [--reps 10] [--out FILE]
+"""
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from zookeeper_amd.models.binary_resnet import stage_shapes  # noqa: E402
+from zookeeper_amd.nn.layers import same_padding  # noqa: E402
+from zookeeper_amd.ops._native import lib, stream_ptr  # noqa: E402
+
+DG_VARIANTS = 8
+WG_VARIANTS = 8
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1000 / reps  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    L, st = lib(), stream_ptr()
+    B = args.batch
+    shapes = sorted(set(stage_shapes((224, 224, 3))))
+    results = []
+    for (H, W, cin, cout, s) in shapes:
+        pt, pb = same_padding(H, 3, s)
+        Ho = (H + pt + pb - 3) // s + 1
+        x = torch.randn(B, H, W, cin, device="cuda").to(torch.bfloat16)
+        w = torch.empty(cout, 3, 3, cin, device="cuda").uniform_(-1, 1)
+        dy = torch.randn(B, Ho, Ho, cout, device="cuda").to(torch.bfloat16)
+        nwords = x.numel() // 32
+        bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
+        mask = torch.empty_like(bits)
+        L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), nwords, 1.0, st)
+        wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
+        wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
+        wt = torch.empty(9, cin, cout, dtype=torch.bfloat16, device="cuda")
+        L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(), cout, 9,
+                         cin, st)
+        dx = torch.empty_like(x)
+        dw = torch.zeros(cout, 3, 3, cin, device="cuda")
+        y = torch.empty(B, Ho, Ho, cout, dtype=torch.int16, device="cuda")
+        stats = torch.zeros(2, cout, dtype=torch.int64, device="cuda")
+        flops = 2.0 * B * Ho * Ho * cout * 9 * cin
+        row = {"shape": [H, W, cin, cout, s], "gflop": flops / 1e9}
+        row["fwd_xnor_us"] = timeit(lambda: L.zk_bconv_fwd(
+            bits.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), y.data_ptr(), stats.data_ptr(),
+            B, H, W, cin, cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, st), args.reps)
+        for v in range(DG_VARIANTS):
+            rc = L.zk_bconv_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(), None,
+                                  dx.data_ptr(), B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, v, st)
+            if rc != 0:
+                row[f"dgrad_v{v}_us"] = None
+                torch.cuda.synchronize()
+                continue
+            row[f"dgrad_v{v}_us"] = timeit(lambda: L.zk_bconv_dgrad(
+                dy.data_ptr(), wt.data_ptr(), mask.data_ptr(), None, dx.data_ptr(), B, H, W, cin,
+                Ho, Ho, cout, 3, 3, s, pt, pt, v, st), args.reps)
+        for v in range(WG_VARIANTS):
+            for tb in (512, 1024, 2048):
+                rc = L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w.data_ptr(), dw.data_ptr(),
+                                      B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v, st)
+                if rc != 0:
+                    row[f"wgrad_v{v}_tb{tb}_us"] = None
+                    continue
+                row[f"wgrad_v{v}_tb{tb}_us"] = timeit(lambda: L.zk_bconv_wgrad(
+                    dy.data_ptr(), bits.data_ptr(), w.data_ptr(), dw.data_ptr(), B, H, W, cin, Ho,
+                    Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v, st), args.reps)
+        # library reference: bf16 conv backward on unpacked ±1 operands
+        xs = torch.where(x >= 0, 1.0, -1.0).to(torch.bfloat16).permute(0, 3, 1, 2)
+        wsn = torch.where(w >= 0, 1.0, -1.0).to(torch.bfloat16).permute(0, 3, 1, 2)
+        if s == 1:
+            row["miopen_bwd_us"] = timeit(lambda: torch.ops.aten.convolution_backward(
+                dy.permute(0, 3, 1, 2), xs, wsn, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
+                (True, True, False)), args.reps)
+        dgs = [row[k] for k in row if k.startswith("dgrad_v") and row[k]]
+        wgs = [row[k] for k in row if k.startswith("wgrad_v") and row[k]]
+        row["best_dgrad_tflops"] = flops / min(dgs) / 1e6
+        row["best_wgrad_tflops"] = flops / min(wgs) / 1e6
+        results.append(row)
+        print(json.dumps(row), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(results, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -9,17 +9,23 @@
 //   wgrad  dW[co, (t,ci)] = sum_{p=(b,ho,wo)} dY[p, co] * sign(x)[p shifted by t, ci]
 //          epilogue: * 1{|w| <= clip} (kernel STE), fp32 atomics (split-K)
 //
-// Both are implicit GEMMs on v_mfma_f32_32x32x16_bf16 with LDS-staged tiles:
-//   * dgrad: A = gathered dY rows (K = Cout contiguous), B = S^T stored
-//     [t][ci][co] (K contiguous) -> fragments are 16-B ds_read_b128 rows;
-//   * wgrad: K = pixels is the outer (strided) dimension of both operands,
-//     so tiles are staged [k][m] / [k][n] with coalesced 16-B loads and the
-//     MFMA fragments are read with the gfx950 transposing LDS read
-//     ds_read_b64_tr_b16.  The sign(x) operand is never materialised: the
-//     loader reads the packed sign bits (1 bit/element) and expands 32 of
-//     them to 32 bf16 ±1 values straight into LDS (16x less HBM traffic).
-// Tiles: 256 threads = 4 waves in a WM x WN grid, each wave TM x TN 32x32
-// MFMA tiles, BK = 32, register-prefetch double buffering.
+// Both are implicit GEMMs on v_mfma_f32_32x32x16_bf16, LDS-staged, BK = 64,
+// register-prefetch double buffering (global loads for stage k+1 are issued
+// before the MFMAs of stage k), 4 waves per workgroup.
+//
+//   * dgrad computes the TRANSPOSED product D[ci][pixel] = S^T . dY^T (A and
+//     B fragments swapped) so every lane owns one pixel and 4 consecutive
+//     channels per accumulator group: the fused epilogue (STE mask word,
+//     residual gradient, bf16 store) moves 8 B per access instead of 2 B.
+//     Operands are K-contiguous (dY rows: Cout; S^T stored [t][ci][co]) ->
+//     fragments are ds_read_b128 rows of 144-B padded LDS rows.
+//   * wgrad: K = pixels is the strided dimension of both operands, so tiles
+//     are staged [k][m] / [k][n] with coalesced 16-B loads and fragments are
+//     read with the gfx950 transposing LDS read ds_read_b64_tr_b16.  The
+//     sign(x) operand is never materialised: the loader reads the packed sign
+//     bits and expands 32 of them into 32 bf16 ±1 values in LDS.  N runs over
+//     (tap, ci) flattened and a 192-wide tile spans several taps when Cin is
+//     small, so the 64-channel stage still gets 3 MFMA tiles per wave.
 #include "../common.h"
 
 namespace {
@@ -30,11 +36,28 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int NT = 256;
-constexpr int BK = 32;
 
 struct Geom {
   int B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl;
 };
+
+// XCD-aware block mapping (speed only, never correctness).  Blocks are
+// dealt round-robin over the 8 XCDs, so blocks L and L+8 share an L2.  For a
+// gx x gy grid with gy | 8, give every XCD one fixed N-tile (`ny`) and a
+// contiguous share of the M-tiles: the B panel of that N-tile then stays
+// resident in that XCD's L2 instead of being re-fetched by all 8.
+__device__ __forceinline__ void xcd_remap_2d(int gx, int gy, int& mx, int& ny) {
+  const int L = blockIdx.x + gx * blockIdx.y;
+  if (gy <= 8 && (8 % gy) == 0 && ((long long)gx * gy) % 8 == 0) {
+    const int xcd = L & 7, k = L >> 3;
+    const int groups = 8 / gy;
+    ny = xcd % gy;
+    mx = (xcd / gy) + groups * k;
+  } else {
+    mx = blockIdx.x;
+    ny = blockIdx.y;
+  }
+}
 
 __device__ __forceinline__ f32x16 mfma32(const uint4& a, const uint4& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
@@ -42,19 +65,20 @@ __device__ __forceinline__ f32x16 mfma32(const uint4& a, const uint4& b, const f
 }
 
 // ===========================================================================
-// dgrad
+// dgrad:  tile BM pixels x BN input channels; waves WM x WN
 // ===========================================================================
-template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(NT, 2) void bconv_dgrad_kernel(
+template <int BM, int BN, int WM, int WN, int BK, int OCC>
+__global__ __launch_bounds__(NT, OCC) void bconv_dgrad_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ wt,
     const uint32_t* __restrict__ mask, const uint16_t* __restrict__ dres,
     uint16_t* __restrict__ dx, Geom g) {
   static_assert(WM * WN == 4, "4 waves");
-  constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
+  constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile (pixels x channels)
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  constexpr int LDK = BK + 8;                  // padded row (80 B): conflict-free b128 reads
-  constexpr int A_CH = BM * BK / 8 / NT;       // 16-B chunks per thread
-  constexpr int B_CH = BN * BK / 8 / NT;
+  constexpr int LDK = BK + 8;                  // 144-B rows
+  constexpr int CPR = BK / 8;                  // 16-B chunks per row
+  constexpr int A_CH = BM * CPR / NT;
+  constexpr int B_CH = BN * CPR / NT;
   static_assert(A_CH >= 1 && B_CH >= 1, "tile too small");
 
   __shared__ __attribute__((aligned(16))) uint16_t As[BM * LDK];
@@ -63,25 +87,37 @@ __global__ __launch_bounds__(NT, 2) void bconv_dgrad_kernel(
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int wm = wave / WN, wn = wave % WN;
-  const long long M = (long long)g.B * g.H * g.W;
-  const long long m0 = (long long)blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  const int T = g.kh * g.kw;
-  const int kchunks = g.Cout / BK;  // Cout % 32 == 0
+  int mtile, ntile;
+  xcd_remap_2d(gridDim.x, gridDim.y, mtile, ntile);
+  // Stride-s dgrad is split into s*s parity classes of input pixels
+  // (blockIdx.z); a class only receives the taps whose offset matches its
+  // parity, so no MFMA work is spent on structurally-zero taps.
+  const int s = g.s;
+  const int ph = blockIdx.z / s, pw = blockIdx.z % s;
+  const int Hc = (g.H - ph + s - 1) / s, Wc = (g.W - pw + s - 1) / s;
+  const long long M = (long long)g.B * Hc * Wc;  // pixels of this class
+  const long long m0 = (long long)mtile * BM;
+  if (m0 >= M) return;
+  const int n0 = ntile * BN;
+  const int kchunks = g.Cout / BK;
+  int th_list[3], tw_list[3], nth = 0, ntw = 0;
+  for (int k = 0; k < g.kh && nth < 3; ++k)
+    if ((ph + g.pt - k) % s == 0) th_list[nth++] = k;
+  for (int k = 0; k < g.kw && ntw < 3; ++k)
+    if ((pw + g.pl - k) % s == 0) tw_list[ntw++] = k;
+  const int T = nth * ntw;
 
-  // Loader: chunk i -> (row = i / 4, c8 = i % 4) (4 chunks of 8 bf16 per 32-wide row).
-  int a_row[A_CH], a_c8[A_CH], a_b[A_CH], a_h[A_CH], a_w[A_CH];
+  int a_b[A_CH], a_h[A_CH], a_w[A_CH];
 #pragma unroll
   for (int j = 0; j < A_CH; ++j) {
-    const int i = tid + j * NT;
-    a_row[j] = i >> 2;
-    a_c8[j] = i & 3;
-    const long long m = m0 + a_row[j];
+    const int row = (tid + j * NT) / CPR;
+    const long long m = m0 + row;
     if (m < M) {
-      a_w[j] = (int)(m % g.W);
-      const long long r = m / g.W;
-      a_h[j] = (int)(r % g.H);
-      a_b[j] = (int)(r / g.H);
+      const int jw = (int)(m % Wc);
+      const long long r = m / Wc;
+      a_h[j] = (int)(r % Hc) * s + ph;
+      a_w[j] = jw * s + pw;
+      a_b[j] = (int)(r / Hc);
     } else {
       a_b[j] = -1;
       a_h[j] = a_w[j] = 0;
@@ -89,19 +125,21 @@ __global__ __launch_bounds__(NT, 2) void bconv_dgrad_kernel(
   }
   uint4 ra[A_CH], rb[B_CH];
   auto load = [&](int kc) {
-    const int t = kc / kchunks;
+    const int ti = kc / kchunks;
     const int co0 = (kc % kchunks) * BK;
-    const int th = t / g.kw, tw = t % g.kw;
+    const int th = th_list[ti / ntw], tw = tw_list[ti % ntw];
+    const int t = th * g.kw + tw;
 #pragma unroll
     for (int j = 0; j < A_CH; ++j) {
+      const int c8 = (tid + j * NT) % CPR;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (a_b[j] >= 0) {
-        const int hn = a_h[j] + g.pt - th, wn_ = a_w[j] + g.pl - tw;
-        if (hn >= 0 && wn_ >= 0 && hn % g.s == 0 && wn_ % g.s == 0) {
-          const int ho = hn / g.s, wo = wn_ / g.s;
+        const int hn = a_h[j] + g.pt - th, wn_ = a_w[j] + g.pl - tw;  // divisible by s
+        if (hn >= 0 && wn_ >= 0) {
+          const int ho = hn / s, wo = wn_ / s;
           if (ho < g.Ho && wo < g.Wo)
             v = *reinterpret_cast<const uint4*>(
-                dy + (((long long)a_b[j] * g.Ho + ho) * g.Wo + wo) * g.Cout + co0 + 8 * a_c8[j]);
+                dy + (((long long)a_b[j] * g.Ho + ho) * g.Wo + wo) * g.Cout + co0 + 8 * c8);
         }
       }
       ra[j] = v;
@@ -109,22 +147,21 @@ __global__ __launch_bounds__(NT, 2) void bconv_dgrad_kernel(
 #pragma unroll
     for (int j = 0; j < B_CH; ++j) {
       const int i = tid + j * NT;
-      const int row = i >> 2, c8 = i & 3;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (n0 + row < g.Cin)
-        v = *reinterpret_cast<const uint4*>(wt + ((long long)t * g.Cin + n0 + row) * g.Cout +
-                                            co0 + 8 * c8);
-      rb[j] = v;
+      const int row = i / CPR, c8 = i % CPR;
+      rb[j] = *reinterpret_cast<const uint4*>(wt + ((long long)t * g.Cin + n0 + row) * g.Cout +
+                                              co0 + 8 * c8);
     }
   };
   auto store = [&]() {
 #pragma unroll
-    for (int j = 0; j < A_CH; ++j)
-      *reinterpret_cast<uint4*>(&As[a_row[j] * LDK + 8 * a_c8[j]]) = ra[j];
+    for (int j = 0; j < A_CH; ++j) {
+      const int i = tid + j * NT;
+      *reinterpret_cast<uint4*>(&As[(i / CPR) * LDK + 8 * (i % CPR)]) = ra[j];
+    }
 #pragma unroll
     for (int j = 0; j < B_CH; ++j) {
       const int i = tid + j * NT;
-      *reinterpret_cast<uint4*>(&Bs[(i >> 2) * LDK + 8 * (i & 3)]) = rb[j];
+      *reinterpret_cast<uint4*>(&Bs[(i / CPR) * LDK + 8 * (i % CPR)]) = rb[j];
     }
   };
 
@@ -138,7 +175,7 @@ __global__ __launch_bounds__(NT, 2) void bconv_dgrad_kernel(
 
   const int r32 = lane & 31, h = lane >> 5;
   const int nk = T * kchunks;
-  load(0);
+  if (nk > 0) load(0);
   for (int kc = 0; kc < nk; ++kc) {
     if (kc) __syncthreads();
     store();
@@ -155,40 +192,53 @@ __global__ __launch_bounds__(NT, 2) void bconv_dgrad_kernel(
       for (int b = 0; b < TN; ++b)
         bfr[b] = *reinterpret_cast<const uint4*>(
             &Bs[(wn * WTN + b * 32 + r32) * LDK + ks * 16 + 8 * h]);
+      // Transposed product: rows = channels (B), columns = pixels (A).
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < TN; ++b) acc[a][b] = mfma32(af[a], bfr[b], acc[a][b]);
+        for (int b = 0; b < TN; ++b) acc[a][b] = mfma32(bfr[b], af[a], acc[a][b]);
     }
   }
 
-  // Epilogue: STE mask + residual gradient, bf16 store.
+  // Epilogue: lane = pixel, 4 consecutive channels per register group.
   const int CW = g.Cin >> 5;
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
+    const long long mc = m0 + wm * WTM + a * 32 + r32;
+    if (mc >= M) continue;
+    const int jw = (int)(mc % Wc);
+    const long long rr = mc / Wc;
+    const long long m =
+        ((rr / Hc) * g.H + (long long)(rr % Hc) * s + ph) * g.W + (long long)jw * s + pw;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const long long m = m0 + row;
-      if (m >= M) continue;
+    for (int b = 0; b < TN; ++b) {
+      const int nb = n0 + wn * WTN + b * 32;  // 32-aligned: one mask word
+      const uint32_t mw = mask ? mask[m * CW + (nb >> 5)] : 0xFFFFFFFFu;
 #pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int n = n0 + wn * WTN + b * 32 + r32;
-        if (n >= g.Cin) continue;
-        float v = acc[a][b][r];
-        if (mask && !((mask[m * CW + (n >> 5)] >> (n & 31)) & 1u)) v = 0.f;
-        if (dres) v += zk::bf16_to_f32(dres[m * g.Cin + n]);
-        dx[m * g.Cin + n] = zk::f32_to_bf16(v);
+      for (int q = 0; q < 4; ++q) {
+        const int nl = 8 * q + 4 * h;  // channel offset within the 32-block
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[e] = ((mw >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
+        const long long off = m * g.Cin + nb + nl;
+        if (dres) {
+          const uint2 d = *reinterpret_cast<const uint2*>(dres + off);
+          v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
+          v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
+          v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
+          v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
+        }
+        *reinterpret_cast<uint2*>(dx + off) =
+            make_uint2(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]));
       }
     }
   }
 }
 
 // ===========================================================================
-// wgrad
+// wgrad:  tile BM output channels x BN (tap, ci) columns; K = pixels
 // ===========================================================================
-// Transposed fragment read: lane gets column (c0 + l&15) of rows k0..k0+3
-// from a [k][m] bf16 tile with row stride `ld` elements.
 __device__ __forceinline__ s16x4 tr_read(const uint16_t* base, int ld, int row, int col) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (__attribute__((address_space(3))) s16x4*)(base + row * ld + col));
@@ -196,7 +246,7 @@ __device__ __forceinline__ s16x4 tr_read(const uint16_t* base, int ld, int row, 
 
 // 32x32x16 operand (8 k-values of one row/column) from a [k][m] LDS tile:
 // lane l: group g = l>>4, i = l&15, q = i>>2, p = i&3; read s covers k rows
-// 8*(g>>1) + 4s + q, columns 16*(g&1) + 4p .. +3 (relative to the 32-col tile).
+// 8*(g>>1) + 4s + q, columns 16*(g&1) + 4p .. +3 of the 32-wide block.
 __device__ __forceinline__ uint4 tr_frag(const uint16_t* tile, int ld, int k0, int c0, int lane) {
   const int gq = lane >> 4, i = lane & 15;
   const int q = i >> 2, p = i & 3;
@@ -208,17 +258,18 @@ __device__ __forceinline__ uint4 tr_frag(const uint16_t* tile, int ld, int k0, i
   return __builtin_bit_cast(uint4, v);
 }
 
-template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(NT, 2) void bconv_wgrad_kernel(
+template <int BM, int BN, int WM, int WN, int BK, int OCC>
+__global__ __launch_bounds__(NT, OCC) void bconv_wgrad_kernel(
     const uint16_t* __restrict__ dy, const uint32_t* __restrict__ xbits,
     const float* __restrict__ w, float* __restrict__ dw, Geom g, int pad_ones, float clip,
     long long k_per_split) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  constexpr int LDA = BM + 8, LDB = BN + 8;      // padded rows
-  constexpr int A_CH = BK * BM / 8 / NT;         // 16-B chunks of dY per thread
-  constexpr int BWORDS = BK * (BN / 32);         // packed words of a B stage
+  constexpr int LDA = BM + 8, LDB = BN + 8;
+  constexpr int A_CH = BK * BM / 8 / NT;     // 16-B chunks of dY per thread
+  constexpr int WPR = BN / 32;               // packed words per B row
+  constexpr int B_W = (BK * WPR + NT - 1) / NT;
   static_assert(A_CH >= 1, "tile");
 
   __shared__ __attribute__((aligned(16))) uint16_t As[BK * LDA];
@@ -228,19 +279,43 @@ __global__ __launch_bounds__(NT, 2) void bconv_wgrad_kernel(
   const int wave = tid >> 6, lane = tid & 63;
   const int wm = wave / WN, wn = wave % WN;
   const long long P = (long long)g.B * g.Ho * g.Wo;
-  const int m0 = blockIdx.x * BM;                 // co
-  const int ntile_per_tap = g.Cin / BN;
-  const int t = blockIdx.y / ntile_per_tap;       // tap
-  const int ci0 = (blockIdx.y % ntile_per_tap) * BN;
-  const int th = t / g.kw, tw = t % g.kw;
-  const long long kbeg = (long long)blockIdx.z * k_per_split;
+  // XCD-aware mapping: all (co, n) tiles of one K-split run on one XCD, so
+  // the split's dY rows and sign bits are fetched into a single L2.
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  {
+    const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+    if (gz % 8 == 0) {
+      const long long L = blockIdx.x + (long long)gx * (blockIdx.y + (long long)gy * blockIdx.z);
+      const int xcd = (int)(L & 7);
+      const long long k = L >> 3;
+      const long long tiles = (long long)gx * gy;
+      bz = xcd + 8 * (int)(k / tiles);
+      const int tile = (int)(k % tiles);
+      bx = tile % gx;
+      by = tile / gx;
+    }
+  }
+  const int m0 = bx * BM;   // co
+  const int n0 = by * BN;   // flattened (t, ci)
+  const long long kbeg = (long long)bz * k_per_split;
   long long kend = kbeg + k_per_split;
   if (kend > P) kend = P;
   const int CW = g.Cin >> 5;
 
+  // Per-thread B word columns are fixed: word wd of the tile -> tap / word.
+  int b_tap[B_W], b_wrd[B_W];
+#pragma unroll
+  for (int j = 0; j < B_W; ++j) {
+    const int i = tid + j * NT;
+    const int wd = i % WPR;
+    const int n = n0 + 32 * wd;
+    b_tap[j] = n / g.Cin;
+    b_wrd[j] = (n % g.Cin) >> 5;
+  }
+
   uint4 ra[A_CH];
-  uint32_t rb = 0;
-  int rb_valid = 0;
+  uint32_t rb[B_W];
+  uint32_t rb_ok = 0;
   auto load = [&](long long k0) {
 #pragma unroll
     for (int j = 0; j < A_CH; ++j) {
@@ -248,30 +323,33 @@ __global__ __launch_bounds__(NT, 2) void bconv_wgrad_kernel(
       const int kr = i / (BM / 8), c8 = i % (BM / 8);
       const long long p = k0 + kr;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (p < kend && m0 + 8 * c8 < g.Cout)
-        v = *reinterpret_cast<const uint4*>(dy + p * g.Cout + m0 + 8 * c8);
+      if (p < kend) v = *reinterpret_cast<const uint4*>(dy + p * g.Cout + m0 + 8 * c8);
       ra[j] = v;
     }
-    rb_valid = 0;
-    if (tid < BWORDS) {
-      const int kr = tid / (BN / 32), wd = tid % (BN / 32);
-      const long long p = k0 + kr;
+    rb_ok = 0;
+#pragma unroll
+    for (int j = 0; j < B_W; ++j) {
+      const int i = tid + j * NT;
       uint32_t v = 0;
-      if (p < kend) {
-        const int wo = (int)(p % g.Wo);
-        const long long r = p / g.Wo;
-        const int ho = (int)(r % g.Ho);
-        const int b = (int)(r / g.Ho);
-        const int hi = ho * g.s - g.pt + th, wi = wo * g.s - g.pl + tw;
-        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W) {
-          v = xbits[(((long long)b * g.H + hi) * g.W + wi) * CW + (ci0 >> 5) + wd];
-          rb_valid = 1;
-        } else if (pad_ones) {
-          v = 0xFFFFFFFFu;  // +1 padding
-          rb_valid = 1;
-        }  // zero padding: the row contributes nothing (expanded as 0, not -1)
+      if (i < BK * WPR) {
+        const long long p = k0 + i / WPR;
+        if (p < kend) {
+          const int wo = (int)(p % g.Wo);
+          const long long r = p / g.Wo;
+          const int ho = (int)(r % g.Ho);
+          const int b = (int)(r / g.Ho);
+          const int t = b_tap[j];
+          const int hi = ho * g.s - g.pt + t / g.kw, wi = wo * g.s - g.pl + t % g.kw;
+          if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W) {
+            v = xbits[(((long long)b * g.H + hi) * g.W + wi) * CW + b_wrd[j]];
+            rb_ok |= 1u << j;
+          } else if (pad_ones) {
+            v = 0xFFFFFFFFu;
+            rb_ok |= 1u << j;
+          }  // zero padding: contributes 0 (not -1)
+        }
       }
-      rb = v;
+      rb[j] = v;
     }
   };
   auto store = [&]() {
@@ -281,19 +359,22 @@ __global__ __launch_bounds__(NT, 2) void bconv_wgrad_kernel(
       const int kr = i / (BM / 8), c8 = i % (BM / 8);
       *reinterpret_cast<uint4*>(&As[kr * LDA + 8 * c8]) = ra[j];
     }
-    if (tid < BWORDS) {
-      const int kr = tid / (BN / 32), wd = tid % (BN / 32);
+#pragma unroll
+    for (int j = 0; j < B_W; ++j) {
+      const int i = tid + j * NT;
+      if (i >= BK * WPR) continue;
+      const int kr = i / WPR, wd = i % WPR;
       uint16_t* dst = &Bs[kr * LDB + 32 * wd];
-      // Expand 32 sign bits into 32 bf16 (+1 = 0x3F80, -1 = 0xBF80); rows past
-      // the split end and zero-padded taps are 0 (no contribution).
+      const bool ok = (rb_ok >> j) & 1u;
+      const uint32_t bits = rb[j];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         uint32_t v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int k = q * 8 + e * 2;
-          const uint32_t lo = rb_valid ? (((rb >> k) & 1) ? 0x3F80u : 0xBF80u) : 0u;
-          const uint32_t hi = rb_valid ? (((rb >> (k + 1)) & 1) ? 0x3F80u : 0xBF80u) : 0u;
+          const uint32_t lo = ok ? (((bits >> k) & 1) ? 0x3F80u : 0xBF80u) : 0u;
+          const uint32_t hi = ok ? (((bits >> (k + 1)) & 1) ? 0x3F80u : 0xBF80u) : 0u;
           v[e] = lo | (hi << 16);
         }
         *reinterpret_cast<uint4*>(dst + 8 * q) = make_uint4(v[0], v[1], v[2], v[3]);
@@ -331,21 +412,21 @@ __global__ __launch_bounds__(NT, 2) void bconv_wgrad_kernel(
     }
   }
 
-  // Epilogue: kernel STE mask, split-K accumulation with fp32 atomics into
-  // dW [Cout][T][Cin] (OHWI, the channels_last layout of the latent kernel).
+  // Epilogue: kernel STE mask, split-K fp32 atomics into dW [Cout][T*Cin]
+  // (OHWI, the channels_last layout of the latent kernel); each
+  // wave-instruction adds 2 x 128 contiguous bytes.
   const int h = lane >> 5, r32 = lane & 31;
+  const int NTOT = g.kh * g.kw * g.Cin;
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (co >= g.Cout) continue;
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
-        const int ci = ci0 + wn * WTN + b * 32 + r32;
-        const long long idx = ((long long)co * (g.kh * g.kw) + t) * g.Cin + ci;
-        const float v = acc[a][b][r];
-        if (fabsf(w[idx]) <= clip) atomicAdd(dw + idx, v);
+        const int n = n0 + wn * WTN + b * 32 + r32;
+        const long long idx = (long long)co * NTOT + n;
+        if (fabsf(w[idx]) <= clip) atomicAdd(dw + idx, acc[a][b][r]);
       }
     }
   }
@@ -353,25 +434,92 @@ __global__ __launch_bounds__(NT, 2) void bconv_wgrad_kernel(
 
 }  // namespace
 
-// wt: ±1 bf16 [T][Cin][Cout]; mask/dres optional.  Requires Cout % 32 == 0,
-// Cin % 64 == 0.
+// ---------------------------------------------------------------------------
+// Host entry points.  `variant` selects a tile configuration (-1 = the
+// built-in heuristic, tuned on MI355X with tools/tune_bconv.py).
+// ---------------------------------------------------------------------------
+namespace {
+
+template <int BM, int BN, int WM, int WN, int BK, int OCC>
+int launch_dgrad(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
+                 const Geom& g, hipStream_t stream) {
+  if (g.Cout % BK || g.Cin % BN) return (int)hipErrorInvalidValue;
+  const long long Mc = (long long)g.B * ((g.H + g.s - 1) / g.s) * ((g.W + g.s - 1) / g.s);
+  hipLaunchKernelGGL((bconv_dgrad_kernel<BM, BN, WM, WN, BK, OCC>),
+                     dim3((unsigned)((Mc + BM - 1) / BM), g.Cin / BN, g.s * g.s), dim3(NT), 0,
+                     stream,
+                     (const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
+                     (const uint16_t*)dres, (uint16_t*)dx, g);
+  return 0;
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int OCC>
+int launch_wgrad(const void* dy, const void* xbits, const void* w, void* dw, const Geom& g,
+                 int pad_ones, float clip, int target_blocks, hipStream_t stream) {
+  const int NTOT = g.kh * g.kw * g.Cin;
+  if (g.Cout % BM || NTOT % BN) return (int)hipErrorInvalidValue;
+  const long long P = (long long)g.B * g.Ho * g.Wo;
+  const long long tiles = (long long)(g.Cout / BM) * (NTOT / BN);
+  long long splits = (target_blocks + tiles - 1) / tiles;
+  const long long max_splits = (P + 8 * BK - 1) / (8 * BK);  // >= 8 K-steps per split
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  long long kps = (P + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  splits = (P + kps - 1) / kps;
+  if (splits >= 8) splits = (splits + 7) / 8 * 8;  // XCD mapping wants gz % 8 == 0
+  hipLaunchKernelGGL((bconv_wgrad_kernel<BM, BN, WM, WN, BK, OCC>),
+                     dim3(g.Cout / BM, (unsigned)(NTOT / BN), (unsigned)splits), dim3(NT), 0,
+                     stream, (const uint16_t*)dy, (const uint32_t*)xbits, (const float*)w,
+                     (float*)dw, g, pad_ones, clip, kps);
+  return 0;
+}
+
+int dgrad_variant(int v, const void* dy, const void* wt, const void* mask, const void* dres,
+                  void* dx, const Geom& g, hipStream_t st) {
+  switch (v) {
+    case 0: return launch_dgrad<128, 128, 2, 2, 64, 2>(dy, wt, mask, dres, dx, g, st);
+    case 1: return launch_dgrad<256, 64, 4, 1, 64, 2>(dy, wt, mask, dres, dx, g, st);
+    case 2: return launch_dgrad<128, 64, 2, 2, 64, 3>(dy, wt, mask, dres, dx, g, st);
+    case 3: return launch_dgrad<64, 64, 2, 2, 64, 4>(dy, wt, mask, dres, dx, g, st);
+    case 4: return launch_dgrad<128, 64, 4, 1, 64, 3>(dy, wt, mask, dres, dx, g, st);
+    case 5: return launch_dgrad<128, 128, 2, 2, 32, 2>(dy, wt, mask, dres, dx, g, st);
+    case 6: return launch_dgrad<128, 64, 2, 2, 32, 4>(dy, wt, mask, dres, dx, g, st);
+    case 7: return launch_dgrad<64, 64, 2, 2, 32, 4>(dy, wt, mask, dres, dx, g, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+int wgrad_variant(int v, const void* dy, const void* xb, const void* w, void* dw, const Geom& g,
+                  int po, float clip, int tb, hipStream_t st) {
+  switch (v) {
+    case 0: return launch_wgrad<128, 192, 2, 2, 64, 2>(dy, xb, w, dw, g, po, clip, tb, st);
+    case 1: return launch_wgrad<64, 192, 2, 2, 64, 2>(dy, xb, w, dw, g, po, clip, tb, st);
+    case 2: return launch_wgrad<128, 64, 2, 2, 64, 3>(dy, xb, w, dw, g, po, clip, tb, st);
+    case 3: return launch_wgrad<64, 64, 2, 2, 64, 4>(dy, xb, w, dw, g, po, clip, tb, st);
+    case 4: return launch_wgrad<128, 192, 2, 2, 32, 2>(dy, xb, w, dw, g, po, clip, tb, st);
+    case 5: return launch_wgrad<64, 192, 2, 2, 32, 3>(dy, xb, w, dw, g, po, clip, tb, st);
+    case 6: return launch_wgrad<128, 64, 2, 2, 32, 4>(dy, xb, w, dw, g, po, clip, tb, st);
+    case 7: return launch_wgrad<64, 64, 2, 2, 32, 4>(dy, xb, w, dw, g, po, clip, tb, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+// wt: ±1 bf16 [T][Cin][Cout]; mask / dres optional.  Requires Cout % 64 == 0
+// and Cin % 64 == 0.
 ZK_EXPORT int zk_bconv_dgrad(const void* dy, const void* wt, const void* mask, const void* dres,
                              void* dx, int B, int H, int W, int Cin, int Ho, int Wo, int Cout,
-                             int kh, int kw, int stride, int pt, int pl, hipStream_t stream) {
-  if (Cout % BK || Cin % 64) return (int)hipErrorInvalidValue;
+                             int kh, int kw, int stride, int pt, int pl, int variant,
+                             hipStream_t stream) {
+  if (Cout % 64 || Cin % 64) return (int)hipErrorInvalidValue;
   Geom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
-  const long long M = (long long)B * H * W;
-  if (Cin % 128 == 0) {
-    dim3 grid((unsigned)((M + 127) / 128), Cin / 128);
-    hipLaunchKernelGGL((bconv_dgrad_kernel<128, 128, 2, 2>), grid, dim3(NT), 0, stream,
-                       (const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
-                       (const uint16_t*)dres, (uint16_t*)dx, g);
-  } else {
-    dim3 grid((unsigned)((M + 127) / 128), Cin / 64);
-    hipLaunchKernelGGL((bconv_dgrad_kernel<128, 64, 4, 1>), grid, dim3(NT), 0, stream,
-                       (const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
-                       (const uint16_t*)dres, (uint16_t*)dx, g);
-  }
+  // Tuned on MI355X (tools/tune_bconv.py, E18 shapes, batch 256): the
+  // 64x64 / BK=32 tile at 4 workgroups per CU wins every shape.
+  if (variant < 0) variant = 7;
+  const int rc = dgrad_variant(variant, dy, wt, mask, dres, dx, g, stream);
+  if (rc) return rc;
   ZK_CHECK_LAUNCH();
   return 0;
 }
@@ -381,35 +529,25 @@ ZK_EXPORT int zk_bconv_dgrad(const void* dy, const void* wt, const void* mask, c
 ZK_EXPORT int zk_bconv_wgrad(const void* dy, const void* xbits, const void* w, void* dw, int B,
                              int H, int W, int Cin, int Ho, int Wo, int Cout, int kh, int kw,
                              int stride, int pt, int pl, int pad_ones, float clip,
-                             int target_blocks, hipStream_t stream) {
+                             int target_blocks, int variant, hipStream_t stream) {
   if (Cout % 64 || Cin % 64) return (int)hipErrorInvalidValue;
   Geom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
-  const long long P = (long long)B * Ho * Wo;
-  const int T = kh * kw;
-  const int BMv = (Cout % 128 == 0) ? 128 : 64;
-  const int BNv = (Cin % 128 == 0) ? 128 : 64;
-  const long long tiles = (long long)(Cout / BMv) * T * (Cin / BNv);
-  long long splits = (target_blocks + tiles - 1) / tiles;
-  const long long max_splits = (P + 255) / 256;  // keep >= 256 pixels per split
-  if (splits > max_splits) splits = max_splits;
-  if (splits < 1) splits = 1;
-  long long kps = (P + splits - 1) / splits;
-  kps = (kps + BK - 1) / BK * BK;
-  splits = (P + kps - 1) / kps;
-  dim3 grid(Cout / BMv, (unsigned)(T * (Cin / BNv)), (unsigned)splits);
-#define ZK_WG(bm, bn, wm, wn)                                                                \
-  hipLaunchKernelGGL((bconv_wgrad_kernel<bm, bn, wm, wn>), grid, dim3(NT), 0, stream,         \
-                     (const uint16_t*)dy, (const uint32_t*)xbits, (const float*)w, (float*)dw, \
-                     g, pad_ones, clip, kps)
-  if (BMv == 128 && BNv == 128)
-    ZK_WG(128, 128, 2, 2);
-  else if (BMv == 128)
-    ZK_WG(128, 64, 4, 1);
-  else if (BNv == 128)
-    ZK_WG(64, 128, 1, 4);
-  else
-    ZK_WG(64, 64, 2, 2);
-#undef ZK_WG
+  const int NTOT = kh * kw * Cin;
+  if (variant < 0) {
+    // Tuned on MI355X (tools/tune_bconv.py): strided layers and the
+    // 64-channel stage prefer smaller tiles, deep layers the 128x192 tile.
+    if (NTOT % 192 != 0)
+      variant = 3;
+    else if (stride > 1)
+      variant = 3;
+    else if (Cout == 64)
+      variant = 5;
+    else
+      variant = (Cout >= 256) ? 4 : 0;
+  }
+  const int rc = wgrad_variant(variant, dy, xbits, w, dw, g, pad_ones, clip, target_blocks,
+                               stream);
+  if (rc) return rc;
   ZK_CHECK_LAUNCH();
   return 0;
 }

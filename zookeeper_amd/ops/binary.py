@@ -137,12 +137,12 @@ class _BinaryBlockFn(torch.autograd.Function):
                 check(L.zk_bconv_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(),
                                        dres.data_ptr() if dres is not None else None,
                                        dx.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
-                                       stride, pt, pl, st), "zk_bconv_dgrad")
+                                       stride, pt, pl, -1, st), "zk_bconv_dgrad")
                 dx = dx.permute(0, 3, 1, 2)
             dw = torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev)
             check(L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w_ohwi.data_ptr(),
                                    dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride,
-                                   pt, pl, int(pad_ones), clip, 1024, st), "zk_bconv_wgrad")
+                                   pt, pl, int(pad_ones), clip, 1024, -1, st), "zk_bconv_wgrad")
             dweight = dw.permute(0, 3, 1, 2)
         else:
             dx, dweight = _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx)
