@@ -1,0 +1,70 @@
+"""Worker for the multi-process data-parallel tests (gloo, CPU).
+
+Run as ``python tests/dp_worker.py <mode> <outdir>`` with the torch.distributed
+env contract set by the launcher under test."""
+
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+
+def make_model():
+    torch.manual_seed(1234)
+    from zookeeper_amd.nn import QuantDense
+
+    return nn.Sequential(
+        nn.Linear(12, 32), nn.Tanh(),
+        QuantDense(32, 16, "ste_sign", "ste_sign", "weight_clip"),
+        nn.Linear(16, 5),
+    )
+
+
+def data(global_batch=8, steps=3):
+    g = torch.Generator().manual_seed(7)
+    xs = torch.randn(steps, global_batch, 12, generator=g)
+    ys = torch.randint(0, 5, (steps, global_batch), generator=g)
+    return xs, ys
+
+
+def train(rank, world, bucket_mb):
+    from zookeeper_amd.core import configure
+    from zookeeper_amd.parallel import dist as zdist
+    from zookeeper_amd.train import Adam, Trainer
+
+    info = zdist.init("gloo") if world > 1 else zdist.DistInfo()
+    spec = Adam()
+    configure(spec, {"learning_rate": 0.01})
+    model = make_model()
+    if rank == 1:  # different init on rank 1: the broadcast must fix it
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_(1.0)
+    tr = Trainer(model, "sparse_categorical_crossentropy", spec, info, bucket_mb=bucket_mb,
+                 first_bucket_mb=0.0005)
+    xs, ys = data()
+    per = xs.shape[1] // world
+    for s in range(xs.shape[0]):
+        x = xs[s, rank * per:(rank + 1) * per]
+        y = ys[s, rank * per:(rank + 1) * per]
+        tr.train_step(x, y)
+    return tr
+
+
+if __name__ == "__main__":
+    mode, out = sys.argv[1], sys.argv[2]
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if mode == "fail" and rank == 1:
+        sys.exit(3)
+    if mode == "fail":
+        import time
+
+        time.sleep(60)  # would hang; the launcher must terminate us
+        sys.exit(0)
+    tr = train(rank, world, bucket_mb=0.001)
+    torch.save({"params": tr.flat.data.clone(), "buckets": tr.bucketer.num_buckets},
+               os.path.join(out, f"rank{rank}.pt"))

@@ -1,0 +1,99 @@
+"""Sweep launcher, --nproc launcher and the experiment CLI end to end (CPU)."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+TASK = os.path.join(HERE, "sweep_task.py")
+
+
+def _env(**kw):
+    e = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", **kw)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "HIP_VISIBLE_DEVICES"):
+        e.pop(k, None)
+    e.update(kw)
+    return e
+
+
+def test_grid_parsing():
+    from zookeeper_amd.sweep import expand, parse_grid, run_name
+
+    axes = parse_grid(["lr=[0.1,0.01]", "optimizer.wd=[0,1e-4,2e-4]", "name=['a']"])
+    combos = expand(axes)
+    assert len(combos) == 6
+    assert combos[0] == {"lr": 0.1, "optimizer.wd": 0, "name": "a"}
+    assert run_name({"optimizer.wd": 1e-4, "lr": 0.1}) == "optimizer-wd_0.0001__lr_0.1"
+
+
+@pytest.mark.timeout(300)
+def test_sweep_runs_grid_concurrently(tmp_path):
+    out = tmp_path / "out"
+    out.mkdir()
+    cmd = [sys.executable, TASK, "RecordConfig", f"out_dir={str(out)!r}",
+           "--grid", "lr=[0.1,0.2]", "--grid", "wd=[0.0,0.5]", "--max-parallel", "2"]
+    env = _env(ZK_SWEEP_DIR=str(tmp_path / "sweep"), HIP_VISIBLE_DEVICES="0,1,2,3")
+    res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stdout + res.stderr
+    recs = [json.load(open(out / f)) for f in sorted(os.listdir(out))]
+    assert sorted((r["lr"], r["wd"]) for r in recs) == [(0.1, 0.0), (0.1, 0.5), (0.2, 0.0), (0.2, 0.5)]
+    # each run saw exactly one (its own) GPU
+    assert all(len(r["hip_visible"].split(",")) == 1 for r in recs)
+    summary = json.load(open(tmp_path / "sweep" / "sweep.json"))
+    assert len(summary) == 4 and all(s["exit_code"] == 0 for s in summary)
+
+
+@pytest.mark.timeout(300)
+def test_sweep_reports_failed_runs(tmp_path):
+    cmd = [sys.executable, TASK, "RecordConfig", f"out_dir={str(tmp_path)!r}", "fail_if_lr=0.2",
+           "--grid", "lr=[0.1,0.2]"]
+    env = _env(ZK_SWEEP_DIR=str(tmp_path / "sweep"))
+    res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 1
+    summary = {s["name"]: s["exit_code"] for s in json.load(open(tmp_path / "sweep" / "sweep.json"))}
+    assert summary == {"lr_0.1": 0, "lr_0.2": 5}
+
+
+@pytest.mark.timeout(300)
+def test_nproc_launches_ranks(tmp_path):
+    cmd = [sys.executable, TASK, "RecordConfig", f"out_dir={str(tmp_path)!r}", "--nproc", "2"]
+    res = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr
+    recs = [json.load(open(tmp_path / f)) for f in sorted(os.listdir(tmp_path))]
+    assert sorted(r["rank"] for r in recs) == ["0", "1"]
+    assert all(r["world"] == "2" for r in recs)
+
+
+@pytest.mark.timeout(600)
+def test_example_smoke_epochs_zero():
+    """The reference CI smoke run: `larq_experiment.py BinaryNetMnist epochs=0`."""
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "larq_experiment.py"),
+                          "BinaryNetMnist", "epochs=0"], env=_env(), capture_output=True,
+                         text=True, timeout=500)
+    assert res.returncode == 0, res.stderr[-2000:]
+    assert "BinaryNetMnist(" in res.stdout
+
+
+@pytest.mark.timeout(900)
+def test_training_checkpoint_and_resume(tmp_path):
+    base = [sys.executable, os.path.join(ROOT, "examples", "larq_experiment.py"), "BinaryNetMnist",
+            "batch_size=8", "steps_per_epoch=2", "validate=False", "print_summary=False",
+            f"output_dir={str(tmp_path)!r}", "model.filters=32", "model.dense_units=64",
+            "dataset.num_train_examples=64"]
+    res = subprocess.run(base + ["epochs=1"], env=_env(), capture_output=True, text=True,
+                         timeout=600)
+    assert res.returncode == 0, res.stderr[-2000:]
+    run_dir = tmp_path / "BinaryNetMnist" / "run"
+    assert (run_dir / "checkpoints" / "step_00000002" / "model.pt").exists()
+    assert (run_dir / "config.json").exists()
+    lines = open(run_dir / "metrics.jsonl").read().strip().splitlines()
+    assert json.loads(lines[-1])["step"] == 2
+    res = subprocess.run(base + ["epochs=2"], env=_env(), capture_output=True, text=True,
+                         timeout=600)
+    assert res.returncode == 0, res.stderr[-2000:]
+    assert "resumed from" in res.stdout
+    assert (run_dir / "checkpoints" / "step_00000004").exists()

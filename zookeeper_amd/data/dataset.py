@@ -143,7 +143,9 @@ class SyntheticSource(Source):
         return self.num_examples
 
     def labels_for(self, idx: np.ndarray) -> np.ndarray:
-        h = _mix64(idx.astype(np.uint64) + np.uint64(self.seed) * np.uint64(0x9E3779B97F4A7C15))
+        with np.errstate(over="ignore"):
+            salt = np.uint64(self.seed) * np.uint64(0x9E3779B97F4A7C15)
+            h = _mix64(idx.astype(np.uint64) + salt)
         return (h % np.uint64(self.num_classes)).astype(np.int64)
 
     def get_batch(self, indices: np.ndarray) -> Batch:
