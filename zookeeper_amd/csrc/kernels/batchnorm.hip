@@ -138,8 +138,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   }
 }
 
-// dy = k1[c]*g - k2[c] - k3[c]*(y - mean[c])   [times 1{y>0} if relu]
-// with k1 = gamma*rstd, k2 = k1*mean(g), k3 = k1*rstd*mean(g*yhat)
+// dy = k1[c]*g + k0[c] - k3[c]*y   [times 1{y>0} if relu], with the folded
+// coefficients from bn_bwd_coef: k1 = gamma*rstd, k3 = k1*rstd*mean(g*yhat),
+// k0 = k3*mean - k1*mean(g).
 template <int CG>
 __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint16_t* __restrict__ g,
                                                         const int16_t* __restrict__ y,
@@ -154,9 +155,8 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint16_t* __restri
   for (int k = 0; k < 8; ++k) {
     const int c = cg * 8 + k;
     k1[k] = coef[c];
+    k0[k] = coef[C + c];
     k3[k] = coef[2 * C + c];
-    // fold the mean term: dy = k1*g + (k3*mu - k2) - k3*y
-    k0[k] = k3[k] * coef[3 * C + c] - coef[C + c];
   }
   for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
        r += (long long)gridDim.x * RB) {
@@ -177,6 +177,29 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint16_t* __restri
         make_uint4(zk::pack_bf16x2(o[0], o[1]), zk::pack_bf16x2(o[2], o[3]),
                    zk::pack_bf16x2(o[4], o[5]), zk::pack_bf16x2(o[6], o[7]));
   }
+}
+
+// Per-channel backward coefficients from the reductions (one tiny launch
+// instead of a chain of framework ops), plus gamma/beta gradients
+// accumulated straight into the parameters' gradient buffers:
+//   sums = [sum g, sum g*yhat];  coef = [k1, k0, k3]
+//   dgamma += sum g*yhat,  dbeta += sum g
+__global__ void bn_bwd_coef_kernel(const float* __restrict__ sums, const float* __restrict__ mean,
+                                   const float* __restrict__ rstd,
+                                   const float* __restrict__ gamma, double P, int C,
+                                   float* __restrict__ coef, float* __restrict__ dgamma,
+                                   float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float sg = sums[c], sgy = sums[C + c];
+  const float rs = rstd[c];
+  const float k1 = (gamma ? gamma[c] : 1.f) * rs;
+  const float k3 = k1 * rs * (float)(sgy / P);
+  coef[c] = k1;
+  coef[C + c] = k3 * mean[c] - k1 * (float)(sg / P);
+  coef[2 * C + c] = k3;
+  if (dgamma) dgamma[c] += sgy;
+  if (dbeta) dbeta[c] += sg;
 }
 
 // dx = dgrad * bit(mask) (+ dres), all [P][C]; mask packed [P][C/32]
@@ -299,6 +322,16 @@ ZK_EXPORT int zk_bn_bwd_dx(const void* g, const void* y, const void* coef, void*
     break;
   ZK_CG_SWITCH(C, ZK_DX_CASE)
 #undef ZK_DX_CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_bn_bwd_coef(const void* sums, const void* mean, const void* rstd,
+                             const void* gamma, double P, int C, void* coef, void* dgamma,
+                             void* dbeta, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, stream,
+                     (const float*)sums, (const float*)mean, (const float*)rstd,
+                     (const float*)gamma, P, C, (float*)coef, (float*)dgamma, (float*)dbeta);
   ZK_CHECK_LAUNCH();
   return 0;
 }

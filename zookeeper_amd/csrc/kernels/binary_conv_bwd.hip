@@ -545,6 +545,11 @@ ZK_EXPORT int zk_bconv_wgrad(const void* dy, const void* xbits, const void* w, v
     else
       variant = (Cout >= 256) ? 4 : 0;
   }
+  if (target_blocks <= 0) {
+    // Tuned split-K sizes (tools/tune_bconv.py): variants 3/5 like 1024-2048
+    // workgroups, the 128x192 tiles 512.
+    target_blocks = (variant == 0 || variant == 4) ? 512 : (variant == 3 ? 2048 : 1024);
+  }
   const int rc = wgrad_variant(variant, dy, xbits, w, dw, g, pad_ones, clip, target_blocks,
                                stream);
   if (rc) return rc;

@@ -88,6 +88,34 @@ def ptr(t: torch.Tensor) -> int:
     return t.data_ptr()
 
 
+def direct_grad(p, channels_last: bool = False):
+    """The gradient buffer a kernel may accumulate into directly, or None.
+
+    Parameters managed by :class:`~zookeeper_amd.parallel.flat.FlatParams`
+    carry ``_zk_direct_grad``: their ``.grad`` is a view into the flat fp32
+    gradient buffer, zeroed once per step.  Kernels then add their
+    contribution in place (no temporary, no framework accumulate kernel) and
+    call :func:`grad_ready`; the autograd function returns ``None`` for them.
+    """
+    if p is None or not getattr(p, "_zk_direct_grad", False):
+        return None
+    g = p.grad
+    if g is None or g.dtype != torch.float32:
+        return None
+    if channels_last and not g.is_contiguous(memory_format=torch.channels_last):
+        return None
+    if not channels_last and not g.is_contiguous():
+        return None
+    return g
+
+
+def grad_ready(p) -> None:
+    """Tell the data-parallel bucketer that ``p``'s gradient is complete."""
+    cb = getattr(p, "_zk_grad_ready", None)
+    if cb is not None:
+        cb()
+
+
 def check(code: int, what: str = "kernel") -> None:
     if code != 0:
         raise RuntimeError(f"{what} failed with hipError {code}")

@@ -29,7 +29,7 @@ from typing import Optional
 import torch
 
 from zookeeper_amd.nn.layers import same_padding
-from zookeeper_amd.ops._native import check, lib, stream_ptr
+from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
 
 
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
@@ -99,6 +99,7 @@ class _BinaryBlockFn(torch.autograd.Function):
                             Cout, st), "zk_bn_apply")
 
         ctx.save_for_backward(bits, mask, wt, y, mean, rstd, gamma, w_ohwi)
+        ctx.params = (weight, gamma, beta)
         ctx.geom = (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo)
         ctx.meta = meta
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
@@ -116,12 +117,30 @@ class _BinaryBlockFn(torch.autograd.Function):
         P = B * Ho * Wo
 
         g = _nhwc(dout.to(torch.bfloat16))
+        weight_p, gamma_p, beta_p = ctx.params
         sums = torch.zeros((2, Cout), dtype=torch.float32, device=dev)
         check(L.zk_bn_bwd_reduce(g.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                                  sums.data_ptr(), P, Cout, st), "zk_bn_bwd_reduce")
-        gam = gamma.detach() if gamma is not None else torch.ones_like(rstd)
-        k1 = gam * rstd
-        coef = torch.stack([k1, k1 * sums[0] / P, k1 * rstd * sums[1] / P, mean]).contiguous()
+        # BN coefficients + gamma/beta gradients in one launch; gradients go
+        # straight into the flat gradient buffer when the trainer manages it.
+        dg_direct = direct_grad(gamma_p) if ctx.has_gamma else None
+        db_direct = direct_grad(beta_p) if ctx.has_beta else None
+        dgamma = dg_direct if dg_direct is not None else (
+            torch.zeros(Cout, device=dev) if ctx.has_gamma else None)
+        dbeta = db_direct if db_direct is not None else (
+            torch.zeros(Cout, device=dev) if ctx.has_beta else None)
+        coef = torch.empty((3, Cout), dtype=torch.float32, device=dev)
+        check(L.zk_bn_bwd_coef(sums.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                               gamma.data_ptr() if gamma is not None else None, float(P), Cout,
+                               coef.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
+                               dbeta.data_ptr() if dbeta is not None else None, st),
+              "zk_bn_bwd_coef")
+        if dg_direct is not None:
+            grad_ready(gamma_p)
+            dgamma = None
+        if db_direct is not None:
+            grad_ready(beta_p)
+            dbeta = None
         dy = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=dev)
         check(L.zk_bn_bwd_dx(g.data_ptr(), y.data_ptr(), coef.data_ptr(), dy.data_ptr(), P,
                              Cout, int(act_relu), st), "zk_bn_bwd_dx")
@@ -139,15 +158,21 @@ class _BinaryBlockFn(torch.autograd.Function):
                                        dx.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
                                        stride, pt, pl, -1, st), "zk_bconv_dgrad")
                 dx = dx.permute(0, 3, 1, 2)
-            dw = torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev)
+            w_direct = direct_grad(weight_p, channels_last=True)
+            if w_direct is not None:
+                dw = w_direct.permute(0, 2, 3, 1)  # OHWI view of the flat gradient
+            else:
+                dw = torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev)
             check(L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w_ohwi.data_ptr(),
                                    dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride,
-                                   pt, pl, int(pad_ones), clip, 1024, -1, st), "zk_bconv_wgrad")
-            dweight = dw.permute(0, 3, 1, 2)
+                                   pt, pl, int(pad_ones), clip, 0, -1, st), "zk_bconv_wgrad")
+            if w_direct is not None:
+                grad_ready(weight_p)
+                dweight = None
+            else:
+                dweight = dw.permute(0, 3, 1, 2)
         else:
             dx, dweight = _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx)
-        dgamma = sums[1] if ctx.has_gamma else None
-        dbeta = sums[0] if ctx.has_beta else None
         dres_out = dout if ctx.has_residual else None
         return dx, dres_out, dweight, dgamma, dbeta, None, None
 

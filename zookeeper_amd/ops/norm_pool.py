@@ -10,7 +10,7 @@ from __future__ import annotations
 import torch
 
 from zookeeper_amd.nn.layers import same_padding
-from zookeeper_amd.ops._native import check, lib, stream_ptr
+from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
 
 
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
@@ -58,6 +58,7 @@ class _BatchNormFn(torch.autograd.Function):
         check(L.zk_bn_apply_bf16(xn.data_ptr(), coef.data_ptr(), y.data_ptr(), P, C, int(relu), st),
               "zk_bn_apply_bf16")
         ctx.save_for_backward(xn, y if relu else None, coef, gamma)
+        ctx.params = (gamma, beta)
         ctx.dim, ctx.P, ctx.C = dim, P, C
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
         return _back(y, dim)
@@ -75,18 +76,29 @@ class _BatchNormFn(torch.autograd.Function):
                                       y.data_ptr() if y is not None else None,
                                       coef.data_ptr(), sums.data_ptr(), P, C, st),
               "zk_bn_bwd_reduce_bf16")
-        mean, rstd = coef[2], coef[3]
-        gam = gamma.detach() if gamma is not None else torch.ones_like(rstd)
-        k1 = gam * rstd
-        k3 = k1 * rstd * sums[1] / P
-        k0 = k3 * mean - k1 * sums[0] / P
-        bcoef = torch.stack([k1, k0, k3]).contiguous()
+        gamma_p, beta_p = ctx.params
+        dg_direct = direct_grad(gamma_p) if ctx.has_gamma else None
+        db_direct = direct_grad(beta_p) if ctx.has_beta else None
+        dgamma = dg_direct if dg_direct is not None else (
+            torch.zeros(C, device=dev) if ctx.has_gamma else None)
+        dbeta = db_direct if db_direct is not None else (
+            torch.zeros(C, device=dev) if ctx.has_beta else None)
+        bcoef = torch.empty((3, C), dtype=torch.float32, device=dev)
+        check(L.zk_bn_bwd_coef(sums.data_ptr(), coef[2].data_ptr(), coef[3].data_ptr(),
+                               gamma.data_ptr() if gamma is not None else None, float(P), C,
+                               bcoef.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
+                               dbeta.data_ptr() if dbeta is not None else None, st),
+              "zk_bn_bwd_coef")
+        if dg_direct is not None:
+            grad_ready(gamma_p)
+            dgamma = None
+        if db_direct is not None:
+            grad_ready(beta_p)
+            dbeta = None
         dx = torch.empty_like(g)
         check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), xn.data_ptr(),
                                   y.data_ptr() if y is not None else None, bcoef.data_ptr(),
                                   dx.data_ptr(), P, C, st), "zk_bn_bwd_dx_bf16")
-        dgamma = sums[1].clone() if ctx.has_gamma else None
-        dbeta = sums[0].clone() if ctx.has_beta else None
         return _back(dx, ctx.dim), dgamma, dbeta, None, None
 
 

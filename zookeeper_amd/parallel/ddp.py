@@ -65,10 +65,15 @@ class GradBucketer:
         self._works: List = []
         self._launched = [False] * len(buckets)
         self._hooks = []
+        self._seen = [False] * len(flat.slots)
         self.enabled = world > 1
         if self.enabled:
             for i, s in enumerate(flat.slots):
-                self._hooks.append(s.param.register_post_accumulate_grad_hook(self._make_hook(i)))
+                hook = self._make_hook(i)
+                self._hooks.append(s.param.register_post_accumulate_grad_hook(hook))
+                # Fused kernels that write gradients in place (bypassing
+                # autograd accumulation) signal completion through this.
+                s.param._zk_grad_ready = lambda h=hook: h(None)
 
     @property
     def num_buckets(self) -> int:
@@ -76,6 +81,9 @@ class GradBucketer:
 
     def _make_hook(self, slot_index: int):
         def hook(_param):
+            if self._seen[slot_index]:
+                return
+            self._seen[slot_index] = True
             b = self.slot_bucket[slot_index]
             self._pending[b] -= 1
             if self._pending[b] == 0:
@@ -108,11 +116,15 @@ class GradBucketer:
         self._works.clear()
         self._pending = [len(b) for b in self.buckets]
         self._launched = [False] * len(self.buckets)
+        self._seen = [False] * len(self.flat.slots)
 
     def remove(self) -> None:
         for h in self._hooks:
             h.remove()
         self._hooks.clear()
+        for s in self.flat.slots:
+            if hasattr(s.param, "_zk_grad_ready"):
+                del s.param._zk_grad_ready
 
 
 def broadcast_module(module: torch.nn.Module, src: int = 0, group=None) -> None:

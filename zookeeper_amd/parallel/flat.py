@@ -73,6 +73,9 @@ class FlatParams:
             view.copy_(p.data)
             p.data = view
             p.grad = torch.as_strided(self.grad, p.shape, p.stride(), s.offset)
+            # Fused kernels may accumulate straight into this gradient view
+            # (see zookeeper_amd.ops._native.direct_grad).
+            p._zk_direct_grad = True
         self.slots = slots
 
     def zero_grad(self) -> None:
