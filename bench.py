@@ -28,6 +28,7 @@ from typing import Tuple
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 METRIC = "images/sec (whole node) BinaryResNet-E18 ImageNet at 1/2/4/8 MI355X"
+OTHER_METRIC = "images/sec (whole node) {model} ImageNet-shape training"
 
 
 def parse():
@@ -110,7 +111,7 @@ def main() -> int:
     global_batch = args.batch * info.world
     value = global_batch * args.steps / elapsed
     out = {
-        "metric": METRIC,
+        "metric": METRIC if args.model == "BinaryResNetE18" else OTHER_METRIC.format(model=args.model),
         "value": round(value, 2),
         "unit": "images/sec",
         "n_gpus": info.world,

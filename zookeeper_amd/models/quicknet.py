@@ -27,7 +27,8 @@ import torch.nn.functional as F
 
 from zookeeper_amd.core import Field, factory
 from zookeeper_amd.models.base import ModelFactory
-from zookeeper_amd.nn.layers import BatchNorm, GlobalAvgPool, QuantConv2d, glorot_normal_, pad_same_nhwc
+from zookeeper_amd.nn.layers import (BatchNorm, GlobalAvgPool, QuantConv2d, _use_native,
+                                     glorot_normal_, pad_same_nhwc)
 from zookeeper_amd.nn.quantizers import ste_sign
 
 
@@ -73,6 +74,11 @@ class BlurPool(nn.Module):
         self.channels = channels
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if _use_native(x):
+            from zookeeper_amd.ops import depthwise
+
+            if depthwise.supported(x, self.kernel):
+                return depthwise.depthwise_conv3x3(x, self.kernel, 2, "same")
         x = pad_same_nhwc(x, (3, 3), (2, 2))
         return F.conv2d(x, self.kernel.to(x.dtype), None, 2, 0, 1, self.channels)
 
@@ -85,7 +91,12 @@ class Transition(nn.Module):
         self.bn = BatchNorm(cout, momentum=0.9, eps=1e-5)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = F.max_pool2d(F.relu(x), 2, 1)
+        if _use_native(x) and x.shape[1] % 8 == 0:
+            from zookeeper_amd.ops.norm_pool import max_pool
+
+            x = F.relu(max_pool(x, 2, 1, "valid"))  # relu∘max == max∘relu
+        else:
+            x = F.max_pool2d(F.relu(x), 2, 1)
         return self.bn(self.conv(self.blur(x)))
 
 

@@ -40,9 +40,14 @@ def _use_native(x: torch.Tensor) -> bool:
     """HIP kernels run for bf16 tensors on the GPU when the library is loaded."""
     if not (x.is_cuda and x.dtype == torch.bfloat16):
         return False
-    from zookeeper_amd import ops
+    from zookeeper_amd.ops import _native
 
-    return ops.available()
+    if _native.available():
+        return True
+    if _native.load_error() == "disabled by ZK_NATIVE=0":
+        return False
+    # A GPU tensor without the kernels is a broken install, not a fallback.
+    raise RuntimeError(f"zookeeper_amd native library unavailable: {_native.load_error()}")
 
 
 def same_padding(size: int, kernel: int, stride: int, dilation: int = 1) -> Tuple[int, int]:
@@ -137,7 +142,17 @@ class QuantConv2d(nn.Module):
         w = self.weight
         return self.kernel_quantizer(w) if self.kernel_quantizer is not None else w
 
+    def _is_depthwise3x3(self) -> bool:
+        return (self.groups == self.in_channels == self.out_channels and self.kernel_size == (3, 3)
+                and self.stride[0] == self.stride[1] and self.input_quantizer is None
+                and self.kernel_quantizer is None and self.bias is None and self.pad_values == 0.0)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.groups > 1 and self._is_depthwise3x3() and _use_native(x):
+            from zookeeper_amd.ops import depthwise
+
+            if depthwise.supported(x, self.weight):
+                return depthwise.depthwise_conv3x3(x, self.weight, self.stride[0], self.padding)
         if self.input_quantizer is not None:
             x = self.input_quantizer(x)
         if self.padding == "same":

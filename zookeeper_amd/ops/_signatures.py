@@ -39,6 +39,10 @@ SIGNATURES = {
     "zk_bn_apply_bf16": (I32, [P, P, P, I64, I32, I32, P]),
     "zk_bn_bwd_reduce_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
     "zk_bn_bwd_dx_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
+    # depthwise convolution
+    "zk_dw_fwd": (I32, [P, P, P] + [I32] * 10 + [P]),
+    "zk_dw_dgrad": (I32, [P, P, P] + [I32] * 10 + [P]),
+    "zk_dw_wgrad": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_maxpool_fwd": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_maxpool_bwd": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_avgpool2_fwd": (I32, [P, P] + [I32] * 6 + [P]),
