@@ -63,3 +63,49 @@ def test_dgrad_wgrad(cin, cout, stride, hw, pad_ones):
     assert err_dx <= 1e-2 * ref_dx.abs().max().item() + 1e-2, err_dx
     err_dw = (dw.double() - ref_dw).abs().max().item()
     assert err_dw <= 1e-4 * ref_dw.abs().max().item() + 1e-3, err_dw
+
+
+@pytest.mark.parametrize("variant", list(range(12)))
+@pytest.mark.parametrize("cin,cout,stride,hw", [
+    (64, 64, 1, 12), (64, 128, 2, 12), (128, 128, 1, 7), (256, 512, 2, 8), (128, 64, 1, 9),
+    (128, 256, 2, 15)])
+def test_igemm_dgrad_matches_reference(variant, cin, cout, stride, hw):
+    """LDS-DMA ring implicit-GEMM dgrad (igemm.hip), every tile variant, vs
+    the fp64 ±1 conv gradient (STE mask + residual gradient fused)."""
+    from zookeeper_amd.nn.layers import pad_same_nhwc, same_padding
+    from zookeeper_amd.nn.quantizers import sign_pm1
+    from zookeeper_amd.ops._native import lib, stream_ptr
+
+    torch.manual_seed(1)
+    L, st = lib(), stream_ptr()
+    B = 3
+    x = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
+    w = torch.empty(cout, 3, 3, cin, device="cuda").uniform_(-1.2, 1.2)
+    pt, pb = same_padding(hw, 3, stride)
+    ho = (hw + pt + pb - 3) // stride + 1
+    dy = torch.randn(B, ho, ho, cout, device="cuda").to(torch.bfloat16)
+    nwords = x.numel() // 32
+    bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
+    mask = torch.empty(nwords, dtype=torch.int32, device="cuda")
+    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), nwords, 1.0, st) == 0
+    wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
+    wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
+    wt = torch.empty(9, cin, cout, dtype=torch.bfloat16, device="cuda")
+    assert L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(),
+                            cout, 9, cin, st) == 0
+    dres = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
+    dx = torch.full((B, hw, hw, cin), float("nan"), dtype=torch.bfloat16, device="cuda")
+    rc = L.zk_igemm_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(), dres.data_ptr(),
+                          dx.data_ptr(), B, hw, hw, cin, ho, ho, cout, 3, 3, stride, pt, pt,
+                          variant, st)
+    if rc != 0:
+        assert cin % 128 != 0 or variant == 3, f"variant {variant} rejected a supported shape"
+        pytest.skip("tile does not divide Cin")
+    torch.cuda.synchronize()
+    xs = sign_pm1(x.double()).permute(0, 3, 1, 2).requires_grad_(True)
+    ws = sign_pm1(w.double()).permute(0, 3, 1, 2)
+    xp = pad_same_nhwc(xs, (3, 3), (stride, stride), 0.0)
+    F.conv2d(xp, ws, stride=stride).backward(dy.double().permute(0, 3, 1, 2))
+    ref = xs.grad.permute(0, 2, 3, 1) * (x.double().abs() <= 1.0) + dres.double()
+    err = (dx.double() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err

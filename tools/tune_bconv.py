@@ -20,6 +20,7 @@ from zookeeper_amd.ops._native import lib, stream_ptr  # noqa: E402
 
 DG_VARIANTS = 8
 WG_VARIANTS = 8
+IG_VARIANTS = 12
 
 
 def timeit(fn, reps):
@@ -40,7 +41,10 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--only", default="fwd,dgrad,igemm,wgrad,miopen",
+                    help="comma list of kernel families to time")
     args = ap.parse_args()
+    fam = set(args.only.split(","))
     L, st = lib(), stream_ptr()
     B = args.batch
     shapes = sorted(set(stage_shapes((224, 224, 3))))
@@ -66,10 +70,14 @@ def main():
         stats = torch.zeros(2, cout, dtype=torch.int64, device="cuda")
         flops = 2.0 * B * Ho * Ho * cout * 9 * cin
         row = {"shape": [H, W, cin, cout, s], "gflop": flops / 1e9}
-        row["fwd_xnor_us"] = timeit(lambda: L.zk_bconv_fwd(
-            bits.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), y.data_ptr(), stats.data_ptr(),
-            B, H, W, cin, cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, st), args.reps)
-        for v in range(DG_VARIANTS):
+        if "fwd" in fam:
+            row["fwd_xnor_us"] = timeit(lambda: L.zk_bconv_fwd(
+                bits.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), y.data_ptr(), stats.data_ptr(),
+                B, H, W, cin, cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, st), args.reps)
+        ref_dx = None
+        for v in (range(DG_VARIANTS) if ("dgrad" in fam or "igemm" in fam) else ()):
+            if "dgrad" not in fam and v != 7:
+                continue
             rc = L.zk_bconv_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(), None,
                                   dx.data_ptr(), B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, v, st)
             if rc != 0:
@@ -79,7 +87,23 @@ def main():
             row[f"dgrad_v{v}_us"] = timeit(lambda: L.zk_bconv_dgrad(
                 dy.data_ptr(), wt.data_ptr(), mask.data_ptr(), None, dx.data_ptr(), B, H, W, cin,
                 Ho, Ho, cout, 3, 3, s, pt, pt, v, st), args.reps)
-        for v in range(WG_VARIANTS):
+            if v == 7:
+                torch.cuda.synchronize()
+                ref_dx = dx.float().clone()
+        for v in (range(IG_VARIANTS) if "igemm" in fam else ()):
+            dx.zero_()
+            rc = L.zk_igemm_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(), None,
+                                  dx.data_ptr(), B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, v, st)
+            torch.cuda.synchronize()
+            if rc != 0:
+                row[f"igd_v{v}_us"] = None
+                continue
+            if ref_dx is not None:
+                row[f"igd_v{v}_maxerr"] = (dx.float() - ref_dx).abs().max().item()
+            row[f"igd_v{v}_us"] = timeit(lambda: L.zk_igemm_dgrad(
+                dy.data_ptr(), wt.data_ptr(), mask.data_ptr(), None, dx.data_ptr(), B, H, W, cin,
+                Ho, Ho, cout, 3, 3, s, pt, pt, v, st), args.reps)
+        for v in (range(WG_VARIANTS) if "wgrad" in fam else ()):
             for tb in (512, 1024, 2048):
                 rc = L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w.data_ptr(), dw.data_ptr(),
                                       B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v, st)
@@ -92,14 +116,17 @@ def main():
         # library reference: bf16 conv backward on unpacked ±1 operands
         xs = torch.where(x >= 0, 1.0, -1.0).to(torch.bfloat16).permute(0, 3, 1, 2)
         wsn = torch.where(w >= 0, 1.0, -1.0).to(torch.bfloat16).permute(0, 3, 1, 2)
-        if s == 1:
+        if s == 1 and "miopen" in fam:
             row["miopen_bwd_us"] = timeit(lambda: torch.ops.aten.convolution_backward(
                 dy.permute(0, 3, 1, 2), xs, wsn, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
                 (True, True, False)), args.reps)
-        dgs = [row[k] for k in row if k.startswith("dgrad_v") and row[k]]
+        dgs = [row[k] for k in row if (k.startswith("dgrad_v") or k.startswith("igd_v"))
+               and k.endswith("_us") and row[k]]
         wgs = [row[k] for k in row if k.startswith("wgrad_v") and row[k]]
-        row["best_dgrad_tflops"] = flops / min(dgs) / 1e6
-        row["best_wgrad_tflops"] = flops / min(wgs) / 1e6
+        if dgs:
+            row["best_dgrad_tflops"] = flops / min(dgs) / 1e6
+        if wgs:
+            row["best_wgrad_tflops"] = flops / min(wgs) / 1e6
         results.append(row)
         print(json.dumps(row), flush=True)
     if args.out:

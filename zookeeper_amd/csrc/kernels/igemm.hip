@@ -1,0 +1,363 @@
+// Implicit-GEMM convolution main loop for gfx950: LDS-DMA (global_load_lds)
+// multi-stage ring, XOR-swizzled LDS image, 32x32 MFMA, transposed output.
+//
+// One template serves the binary-conv data gradient (bf16 operands,
+// v_mfma_f32_32x32x16_bf16).  The GEMM view of a KH x KW conv:
+//
+//   D[n][m] = sum_{tap t} sum_{k} Wt[t][n][k] * Act[pixel(m, t)][k]
+//
+//   dgrad: m = input pixel (of one stride-parity class), n = ci, k = co,
+//          Act = dY gathered at ((hi+pt-th)/s, (wi+pl-tw)/s), Wt = S^T [T][Cin][Cout]
+//
+// Design (cdna_hip_programming.md §5, MI355X_MICROARCH.md §LDS):
+//   * the activation rows are gathered per lane: every lane of a
+//     global_load_lds_dwordx4 supplies its own source address, so the
+//     implicit-GEMM gather costs nothing extra over a dense GEMM; rows that
+//     fall into the zero padding read a zero page instead;
+//   * the LDS image is linear per wave-instruction (glds writes base +
+//     lane*16) and conflict-free for the ds_read_b128 fragment reads by an
+//     XOR swizzle applied to the SOURCE chunk: slot = chunk ^ ((row >> SH) &
+//     (SPR-1)) - over every 16-lane group of ds_read_b128 the 16 rows land
+//     on 16 distinct 16-B bank slots;
+//   * NS-stage ring: NS-1 K-steps in flight; each K-step waits with a
+//     counted vmcnt for its own stage only, then one raw s_barrier (no
+//     __syncthreads: its implied vmcnt(0) would drain the ring);
+//   * the product is computed transposed (MFMA A = weight rows, MFMA B =
+//     pixel rows) so every lane owns one pixel and 4 consecutive channels
+//     per register group: the epilogue moves 8 B per access;
+//   * XCD-aware tile order: consecutive M tiles of one N tile share an XCD.
+#include "../common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct IGeom {
+  int B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl;
+};
+
+// 256 B of zeros: the source of every padded row.
+__device__ __attribute__((aligned(256))) uint4 g_zero_page[16];
+
+// global_load_lds_dwordx4 in inline asm.  With the builtin, hipcc treats the
+// DMA as an LDS store it cannot disambiguate and puts s_waitcnt vmcnt(0) in
+// front of the next ds_read, draining the ring every K-step; here the ring's
+// ordering is explicit (counted vmcnt + s_barrier, see the main loop).
+// M0 holds the wave-uniform LDS base; the compiler sets M0 itself before any
+// of its own M0 uses, so clobbering it here is safe.
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void glds16(const void* src, const void* lds_dst) {
+  const uint32_t base = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds_dst);
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(base)
+               : "m0");
+}
+#define ZK_GLDS16(src, dst) glds16((src), (dst))
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ f32x16 mfma_bf16(const uint4& a, const uint4& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// Bijective XCD remap of a linear block id (blocks L and L+8 share an XCD
+// under round-robin dispatch): XCD x gets the contiguous range of logical ids
+// [x*q + min(x, r), ...).
+__device__ __forceinline__ int xcd_linear(int L, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int x = L & 7, i = L >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+// ===========================================================================
+// dgrad
+// ===========================================================================
+template <int BM, int BN, int WM, int WN, int NS, int CB>
+__global__ __launch_bounds__(WM * WN * 64, 1) void igemm_dgrad_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ wt,
+    const uint32_t* __restrict__ mask, const uint16_t* __restrict__ dres,
+    uint16_t* __restrict__ dx, IGeom g, int m_tiles) {
+  constexpr int NWAVES = WM * WN;
+  // CB = bytes of K per row per stage (128 = 64 bf16, or 64)
+  constexpr int SPR = CB / 16;            // 16-B slots per row
+  constexpr int RPI = 1024 / CB;          // rows per wave-instruction
+  constexpr int SH = (CB == 128) ? 1 : 2; // swizzle shift (see header)
+  constexpr int A_INS = BM / RPI / NWAVES;  // glds per wave per stage
+  constexpr int B_INS = BN / RPI / NWAVES;
+  static_assert(A_INS >= 1 && B_INS >= 1 && BM % (RPI * NWAVES) == 0 &&
+                    BN % (RPI * NWAVES) == 0,
+                "tile / wave mismatch");
+  constexpr int LPS = A_INS + B_INS;  // vm ops per wave per stage
+  constexpr int STAGE = (BM + BN) * CB;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wm = wave / WN, wn = wave % WN;
+
+  // ---- tile coordinates (XCD-aware: the M tiles of one N tile are
+  // consecutive logical ids, so they share an L2 with that N tile's weights)
+  const int nwg = gridDim.x;
+  const int L = xcd_linear(blockIdx.x, nwg);
+  const int n_tiles = g.Cin / BN;
+  const int mtile = L % m_tiles;
+  const int ntile = L / m_tiles;
+  if (ntile >= n_tiles) return;
+  const int s = g.s;
+  const int ph = blockIdx.y / s, pw = blockIdx.y % s;
+  const int Hc = (g.H - ph + s - 1) / s, Wc = (g.W - pw + s - 1) / s;
+  const long long M = (long long)g.B * Hc * Wc;
+  const long long m0 = (long long)mtile * BM;
+  if (m0 >= M) return;
+  const int n0 = ntile * BN;
+
+  // taps of this parity class: th = th0 + i*s (no runtime-indexed arrays,
+  // which would live in scratch)
+  const int th0 = (ph + g.pt) % s, tw0 = (pw + g.pl) % s;
+  const int nth = (g.kh - th0 + s - 1) / s, ntw = (g.kw - tw0 + s - 1) / s;
+  const int T = nth * ntw;
+  const int RB = g.Cout * 2;           // bytes per dY row
+  const int kchunks = RB / CB;
+  const int NK = T * kchunks;
+
+  // ---- per-lane loader rows (A: pixels)
+  const int lrow = lane / SPR, lslot = lane % SPR;
+  int a_b[A_INS], a_h[A_INS], a_w[A_INS];
+  int a_sw[A_INS];
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int r = (j * NWAVES + wave) * RPI + lrow;
+    a_sw[j] = lslot ^ ((r >> SH) & (SPR - 1));
+    const long long m = m0 + r;
+    if (m < M) {
+      const int jw = (int)(m % Wc);
+      const long long rr = m / Wc;
+      a_h[j] = (int)(rr % Hc) * s + ph + g.pt;
+      a_w[j] = jw * s + pw + g.pl;
+      a_b[j] = (int)(rr / Hc);
+    } else {
+      a_b[j] = -1;
+      a_h[j] = a_w[j] = 0;
+    }
+  }
+  int b_sw[B_INS];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int r = (j * NWAVES + wave) * RPI + lrow;
+    b_sw[j] = lslot ^ ((r >> SH) & (SPR - 1));
+  }
+  const unsigned char* dyb = reinterpret_cast<const unsigned char*>(dy);
+  const unsigned char* wtb = reinterpret_cast<const unsigned char*>(wt);
+  const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
+
+  // Source pointers of the current tap (recomputed when the tap changes).
+  const unsigned char* a_src[A_INS];
+  int a_step[A_INS];  // CB for a real row, 0 for the zero page
+  const unsigned char* b_src[B_INS];
+  auto set_tap = [&](int ti) {
+    const int th = th0 + (ti / ntw) * s, tw = tw0 + (ti % ntw) * s;
+    const int t = th * g.kw + tw;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      const int hn = a_h[j] - th, wn_ = a_w[j] - tw;  // divisible by s
+      const int ho = (s == 1) ? hn : (hn >> 1);
+      const int wo = (s == 1) ? wn_ : (wn_ >> 1);
+      const bool ok = a_b[j] >= 0 && hn >= 0 && wn_ >= 0 && ho < g.Ho && wo < g.Wo;
+      a_src[j] = ok ? dyb + (((long long)a_b[j] * g.Ho + ho) * g.Wo + wo) * RB + a_sw[j] * 16
+                    : zp + a_sw[j] * 16;
+      a_step[j] = ok ? CB : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const int r = (j * NWAVES + wave) * RPI + lrow;
+      b_src[j] = wtb + ((long long)t * g.Cin + n0 + r) * RB + b_sw[j] * 16;
+    }
+  };
+  // Issue the glds of K-step ks into ring slot ks % NS.
+  int cur_tap = -1;
+  auto issue = [&](int ks) {
+    const int ti = ks / kchunks, kc = ks % kchunks;
+    if (ti != cur_tap) {
+      set_tap(ti);
+      cur_tap = ti;
+    }
+    unsigned char* st = smem + (ks % NS) * STAGE;
+    const int koff = kc * CB;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j)
+      ZK_GLDS16(a_src[j] + kc * a_step[j], st + (j * NWAVES + wave) * 1024);
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j)
+      ZK_GLDS16(b_src[j] + koff, st + BM * CB + (j * NWAVES + wave) * 1024);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int r32 = lane & 31, h = lane >> 5;
+  // fragment read offsets (bytes within a stage) for k-substep 0
+  int a_off[TM], b_off[TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) a_off[a] = (wm * WTM + a * 32 + r32) * CB;
+#pragma unroll
+  for (int b = 0; b < TN; ++b) b_off[b] = BM * CB + (wn * WTN + b * 32 + r32) * CB;
+
+  // prologue: NS-1 stages in flight
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < NK) issue(p);
+
+  for (int ks = 0; ks < NK; ++ks) {
+    // wait for this wave's loads of stage ks, then the barrier makes every
+    // wave's loads visible and frees slot (ks-1) % NS for re-issue.
+    if (ks + NS - 2 < NK)
+      wait_vmcnt<LPS * (NS - 2)>();
+    else
+      wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (ks + NS - 1 < NK) issue(ks + NS - 1);
+
+    const unsigned char* st = smem + (ks % NS) * STAGE;
+#pragma unroll
+    for (int sub = 0; sub < CB / 32; ++sub) {
+      const int chunk = 2 * sub + h;
+      uint4 af[TM], bfr[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const int row = wm * WTM + a * 32 + r32;
+        af[a] = *reinterpret_cast<const uint4*>(
+            st + a_off[a] + ((chunk ^ ((row >> SH) & (SPR - 1))) * 16));
+      }
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int row = wn * WTN + b * 32 + r32;
+        bfr[b] = *reinterpret_cast<const uint4*>(
+            st + b_off[b] + ((chunk ^ ((row >> SH) & (SPR - 1))) * 16));
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = mfma_bf16(bfr[b], af[a], acc[a][b]);
+    }
+  }
+
+  // ---- epilogue: lane = pixel, 4 consecutive channels per register group
+  const int CW = g.Cin >> 5;
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+    const long long mc = m0 + wm * WTM + a * 32 + r32;
+    if (mc >= M) continue;
+    const int jw = (int)(mc % Wc);
+    const long long rr = mc / Wc;
+    const long long m =
+        ((rr / Hc) * g.H + (long long)(rr % Hc) * s + ph) * g.W + (long long)jw * s + pw;
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int nb = n0 + wn * WTN + b * 32;
+      const uint32_t mw = mask ? mask[m * CW + (nb >> 5)] : 0xFFFFFFFFu;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int nl = 8 * q + 4 * h;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[e] = ((mw >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
+        const long long off = m * g.Cin + nb + nl;
+        if (dres) {
+          const uint2 d = *reinterpret_cast<const uint2*>(dres + off);
+          v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
+          v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
+          v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
+          v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
+        }
+        *reinterpret_cast<uint2*>(dx + off) =
+            make_uint2(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]));
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int CB = 128>
+int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const void* dres,
+                       void* dx, const IGeom& g, hipStream_t stream) {
+  if ((g.Cout * 2) % CB || g.Cin % BN || g.s > 2 || g.kh > 4 || g.kw > 4)
+    return (int)hipErrorInvalidValue;
+  constexpr int LDS = NS * (BM + BN) * CB;
+  static_assert(LDS <= 160 * 1024, "LDS");
+  auto kern = igemm_dgrad_kernel<BM, BN, WM, WN, NS, CB>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  const int Hc = (g.H + g.s - 1) / g.s, Wc = (g.W + g.s - 1) / g.s;
+  const long long Mc = (long long)g.B * Hc * Wc;
+  const int m_tiles = (int)((Mc + BM - 1) / BM);
+  const long long blocks = (long long)m_tiles * (g.Cin / BN);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks, g.s * g.s), dim3(WM * WN * 64), LDS, stream,
+                     (const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
+                     (const uint16_t*)dres, (uint16_t*)dx, g, m_tiles);
+  return 0;
+}
+
+int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
+                        const void* dres, void* dx, const IGeom& g, hipStream_t st) {
+#define ZK_IGD(...) return launch_igemm_dgrad<__VA_ARGS__>(dy, wt, mask, dres, dx, g, st)
+  switch (v) {
+    case 0: ZK_IGD(128, 128, 2, 2, 2);        // 64 KB: 2 WG/CU
+    case 1: ZK_IGD(128, 128, 2, 2, 4, 64);    // 64 KB, 3 K-steps of 32 in flight
+    case 2: ZK_IGD(256, 128, 4, 2, 2);        // 8 waves, 96 KB
+    case 3: ZK_IGD(128, 256, 2, 2, 2);        // wave tile 64x128, 96 KB
+    case 4: ZK_IGD(128, 64, 2, 2, 2);         // 48 KB: 3 WG/CU
+    case 5: ZK_IGD(128, 64, 2, 2, 3);         // 72 KB: 2 WG/CU
+    case 6: ZK_IGD(256, 64, 4, 1, 2);         // 80 KB: 2 WG/CU
+    case 7: ZK_IGD(128, 64, 2, 2, 4, 64);     // 48 KB, 3 in flight
+    case 8: ZK_IGD(256, 64, 4, 1, 4, 64);     // 80 KB, 3 in flight
+    case 9: ZK_IGD(64, 64, 2, 2, 2);          // 32 KB
+    case 10: ZK_IGD(128, 128, 2, 2, 4);       // 128 KB, 1 WG/CU
+    case 11: ZK_IGD(256, 128, 4, 2, 4, 64);   // 8 waves, 96 KB
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef ZK_IGD
+}
+
+}  // namespace
+
+// Same contract as zk_bconv_dgrad (binary_conv_bwd.hip): wt ±1 bf16
+// [T][Cin][Cout], mask / dres optional, Cout % 64 == 0, Cin % BN == 0.
+ZK_EXPORT int zk_igemm_dgrad(const void* dy, const void* wt, const void* mask, const void* dres,
+                             void* dx, int B, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                             int kh, int kw, int stride, int pt, int pl, int variant,
+                             hipStream_t stream) {
+  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+  if (variant < 0) {
+    // Tuned on MI355X (tools/tune_bconv.py --only igemm, E18 shapes, batch
+    // 256): 128x128 at 2 WG/CU for Cin >= 128 (8-wave 256x128 for the
+    // 256-channel stride-1 layers), 128x64 with a 4-deep 64-B ring for Cin=64.
+    if (Cin % 128 == 0)
+      variant = (Cin == 256 && stride == 1) ? 11 : 0;
+    else
+      variant = 7;
+  }
+  const int rc = igemm_dgrad_variant(variant, dy, wt, mask, dres, dx, g, stream);
+  if (rc) return rc;
+  ZK_CHECK_LAUNCH();
+  return 0;
+}

@@ -13,8 +13,9 @@ One autograd op per block (used by BinaryResNet-E and QuickNet on the
 5. ``zk_bn_apply``    out = scale·y + shift + residual, bf16.
 
 Backward: ``zk_bn_bwd_reduce`` (Σg, Σg·ŷ) → ``zk_bn_bwd_dx`` (dy, ReLU mask)
-→ ``zk_bconv_dgrad`` (MFMA implicit GEMM dy ⊛ sign(W)ᵀ with the input STE
-mask and the identity-residual gradient fused into its epilogue) and
+→ ``zk_igemm_dgrad`` (MFMA implicit GEMM dy ⊛ sign(W)ᵀ on an LDS-DMA ring,
+with the input STE mask and the identity-residual gradient fused into its
+epilogue) and
 ``zk_bconv_wgrad`` (MFMA implicit GEMM reading the packed sign bits of x
 directly, kernel STE mask in the epilogue, split-K fp32 atomics).
 
@@ -146,17 +147,17 @@ class _BinaryBlockFn(torch.autograd.Function):
                              Cout, int(act_relu), st), "zk_bn_bwd_dx")
 
         need_dx = ctx.needs_input_grad[0]
-        native = Cout % 64 == 0 and Cin % 64 == 0
+        native = Cout % 64 == 0 and Cin % 64 == 0 and stride <= 2 and kh <= 4 and kw <= 4
         dx = None
         if native:
             # MFMA implicit GEMMs; STE mask + residual gradient fused in dgrad.
             if need_dx:
                 dx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
                 dres = g if identity else None
-                check(L.zk_bconv_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(),
+                check(L.zk_igemm_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(),
                                        dres.data_ptr() if dres is not None else None,
                                        dx.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
-                                       stride, pt, pl, -1, st), "zk_bconv_dgrad")
+                                       stride, pt, pl, -1, st), "zk_igemm_dgrad")
                 dx = dx.permute(0, 3, 1, 2)
             w_direct = direct_grad(weight_p, channels_last=True)
             if w_direct is not None:
