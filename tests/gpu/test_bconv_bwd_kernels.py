@@ -33,7 +33,10 @@ def test_dgrad_wgrad(cin, cout, stride, hw, pad_ones):
     nwords = x.numel() // 32
     bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
     mask = torch.empty(nwords, dtype=torch.int32, device="cuda")
-    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), nwords, 1.0, st) == 0
+    sx = torch.empty_like(x)
+    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), sx.data_ptr(), nwords,
+                          1.0, st) == 0
+    assert torch.equal(sx.float(), torch.where(x.float() >= 0, 1.0, -1.0))
     wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
     wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
     wt = torch.empty(9, cin, cout, dtype=torch.bfloat16, device="cuda")
@@ -87,7 +90,10 @@ def test_igemm_dgrad_matches_reference(variant, cin, cout, stride, hw):
     nwords = x.numel() // 32
     bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
     mask = torch.empty(nwords, dtype=torch.int32, device="cuda")
-    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), nwords, 1.0, st) == 0
+    sx = torch.empty_like(x)
+    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), sx.data_ptr(), nwords,
+                          1.0, st) == 0
+    assert torch.equal(sx.float(), torch.where(x.float() >= 0, 1.0, -1.0))
     wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
     wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
     wt = torch.empty(9, cin, cout, dtype=torch.bfloat16, device="cuda")
@@ -109,3 +115,43 @@ def test_igemm_dgrad_matches_reference(variant, cin, cout, stride, hw):
     ref = xs.grad.permute(0, 2, 3, 1) * (x.double().abs() <= 1.0) + dres.double()
     err = (dx.double() - ref).abs().max().item()
     assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err
+
+
+@pytest.mark.parametrize("variant", list(range(8)))
+@pytest.mark.parametrize("cin,cout,stride,hw,pad_ones", [
+    (64, 64, 1, 12, 0), (64, 128, 2, 12, 0), (128, 128, 1, 7, 1), (256, 512, 2, 8, 0),
+    (128, 64, 1, 9, 1), (64, 192, 1, 5, 1)])
+def test_igemm_wgrad_matches_reference(variant, cin, cout, stride, hw, pad_ones):
+    """LDS-DMA ring implicit-GEMM wgrad (igemm.hip) on the bf16 sign(x)
+    image, every tile variant, vs the fp64 ±1 conv weight gradient."""
+    from zookeeper_amd.nn.layers import pad_same_nhwc, same_padding
+    from zookeeper_amd.nn.quantizers import sign_pm1
+    from zookeeper_amd.ops._native import lib, stream_ptr
+
+    torch.manual_seed(2)
+    L, st = lib(), stream_ptr()
+    B = 3
+    x = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
+    w = torch.empty(cout, 3, 3, cin, device="cuda").uniform_(-1.2, 1.2)
+    pt, pb = same_padding(hw, 3, stride)
+    ho = (hw + pt + pb - 3) // stride + 1
+    dy = torch.randn(B, ho, ho, cout, device="cuda").to(torch.bfloat16)
+    nwords = x.numel() // 32
+    bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
+    sx = torch.empty_like(x)
+    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), None, sx.data_ptr(), nwords, 1.0,
+                          st) == 0
+    dw = torch.zeros(cout, 3, 3, cin, device="cuda")
+    rc = L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w.data_ptr(), dw.data_ptr(), B, hw, hw,
+                          cin, ho, ho, cout, 3, 3, stride, pt, pt, pad_ones, 1.0, 256, variant,
+                          st)
+    if rc != 0:
+        pytest.skip("tile does not divide this shape")
+    torch.cuda.synchronize()
+    xs = sign_pm1(x.double()).permute(0, 3, 1, 2)
+    ws = sign_pm1(w.double()).permute(0, 3, 1, 2).requires_grad_(True)
+    xp = pad_same_nhwc(xs, (3, 3), (stride, stride), 1.0 if pad_ones else 0.0)
+    F.conv2d(xp, ws, stride=stride).backward(dy.double().permute(0, 3, 1, 2))
+    ref = ws.grad.permute(0, 2, 3, 1) * (w.double().abs() <= 1.0)
+    err = (dw.double() - ref).abs().max().item()
+    assert err <= 1e-4 * ref.abs().max().item() + 1e-3, err

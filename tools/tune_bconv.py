@@ -21,6 +21,7 @@ from zookeeper_amd.ops._native import lib, stream_ptr  # noqa: E402
 DG_VARIANTS = 8
 WG_VARIANTS = 8
 IG_VARIANTS = 12
+IGW_VARIANTS = 8
 
 
 def timeit(fn, reps):
@@ -58,7 +59,9 @@ def main():
         nwords = x.numel() // 32
         bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
         mask = torch.empty_like(bits)
-        L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), nwords, 1.0, st)
+        sx = torch.empty_like(x)
+        L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), sx.data_ptr(), nwords, 1.0,
+                       st)
         wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
         wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
         wt = torch.empty(9, cin, cout, dtype=torch.bfloat16, device="cuda")
@@ -103,7 +106,10 @@ def main():
             row[f"igd_v{v}_us"] = timeit(lambda: L.zk_igemm_dgrad(
                 dy.data_ptr(), wt.data_ptr(), mask.data_ptr(), None, dx.data_ptr(), B, H, W, cin,
                 Ho, Ho, cout, 3, 3, s, pt, pt, v, st), args.reps)
-        for v in (range(WG_VARIANTS) if "wgrad" in fam else ()):
+        ref_dw = None
+        for v in (range(WG_VARIANTS) if ("wgrad" in fam or "igw" in fam) else ()):
+            if "wgrad" not in fam and v != 5:
+                continue
             for tb in (512, 1024, 2048):
                 rc = L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w.data_ptr(), dw.data_ptr(),
                                       B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v, st)
@@ -112,6 +118,28 @@ def main():
                     continue
                 row[f"wgrad_v{v}_tb{tb}_us"] = timeit(lambda: L.zk_bconv_wgrad(
                     dy.data_ptr(), bits.data_ptr(), w.data_ptr(), dw.data_ptr(), B, H, W, cin, Ho,
+                    Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v, st), args.reps)
+                if ref_dw is None:
+                    dw.zero_()
+                    L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w.data_ptr(), dw.data_ptr(),
+                                     B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v, st)
+                    torch.cuda.synchronize()
+                    ref_dw = dw.clone()
+        for v in (range(IGW_VARIANTS) if "igw" in fam else ()):
+            for tb in (512, 1024, 2048):
+                dw.zero_()
+                rc = L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w.data_ptr(), dw.data_ptr(),
+                                      B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v,
+                                      st)
+                torch.cuda.synchronize()
+                if rc != 0:
+                    row[f"igw_v{v}_tb{tb}_us"] = None
+                    continue
+                if ref_dw is not None:
+                    row[f"igw_v{v}_tb{tb}_relerr"] = ((dw - ref_dw).abs().max() /
+                                                      ref_dw.abs().max()).item()
+                row[f"igw_v{v}_tb{tb}_us"] = timeit(lambda: L.zk_igemm_wgrad(
+                    dy.data_ptr(), sx.data_ptr(), w.data_ptr(), dw.data_ptr(), B, H, W, cin, Ho,
                     Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v, st), args.reps)
         # library reference: bf16 conv backward on unpacked ±1 operands
         xs = torch.where(x >= 0, 1.0, -1.0).to(torch.bfloat16).permute(0, 3, 1, 2)
@@ -122,7 +150,8 @@ def main():
                 (True, True, False)), args.reps)
         dgs = [row[k] for k in row if (k.startswith("dgrad_v") or k.startswith("igd_v"))
                and k.endswith("_us") and row[k]]
-        wgs = [row[k] for k in row if k.startswith("wgrad_v") and row[k]]
+        wgs = [row[k] for k in row if (k.startswith("wgrad_v") or k.startswith("igw_v"))
+               and k.endswith("_us") and row[k]]
         if dgs:
             row["best_dgrad_tflops"] = flops / min(dgs) / 1e6
         if wgs:

@@ -42,6 +42,7 @@ constexpr int NT = 256;
 __global__ __launch_bounds__(256) void sign_pack_kernel(const uint16_t* __restrict__ x,
                                                         uint32_t* __restrict__ bits,
                                                         uint32_t* __restrict__ mask,
+                                                        uint16_t* __restrict__ xs,
                                                         long long nwords, float clip) {
   for (long long w = blockIdx.x * (long long)blockDim.x + threadIdx.x; w < nwords;
        w += (long long)gridDim.x * blockDim.x) {
@@ -51,16 +52,21 @@ __global__ __launch_bounds__(256) void sign_pack_kernel(const uint16_t* __restri
     for (int q = 0; q < 4; ++q) {
       uint4 v = src[q];
       uint32_t u[4] = {v.x, v.y, v.z, v.w};
+      uint32_t o[4];
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
+        o[h] = 0;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const float f = zk::bf16_to_f32((uint16_t)(u[h] >> (16 * s)));
           const int i = q * 8 + h * 2 + s;
           b |= (uint32_t)(f >= 0.f) << i;
           mk |= (uint32_t)(fabsf(f) <= clip) << i;
+          o[h] |= (f >= 0.f ? 0x3F80u : 0xBF80u) << (16 * s);
         }
       }
+      // sign(x) as bf16 +-1: the operand of the MFMA weight gradient
+      if (xs) reinterpret_cast<uint4*>(xs + 32 * w)[q] = make_uint4(o[0], o[1], o[2], o[3]);
     }
     bits[w] = b;
     if (mask) mask[w] = mk;
@@ -350,10 +356,11 @@ int grid_for(long long work, int per_block = 256, int cap = 16384) {
 
 }  // namespace
 
-ZK_EXPORT int zk_sign_pack(const void* x, void* bits, void* mask, long long nwords, float clip,
-                           hipStream_t stream) {
+ZK_EXPORT int zk_sign_pack(const void* x, void* bits, void* mask, void* xs, long long nwords,
+                           float clip, hipStream_t stream) {
   hipLaunchKernelGGL(sign_pack_kernel, dim3(grid_for(nwords)), dim3(256), 0, stream,
-                     (const uint16_t*)x, (uint32_t*)bits, (uint32_t*)mask, nwords, clip);
+                     (const uint16_t*)x, (uint32_t*)bits, (uint32_t*)mask, (uint16_t*)xs,
+                     nwords, clip);
   ZK_CHECK_LAUNCH();
   return 0;
 }

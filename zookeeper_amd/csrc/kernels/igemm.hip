@@ -338,6 +338,263 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
 #undef ZK_IGD
 }
 
+
+// ===========================================================================
+// wgrad:  dW[co][n = (t, ci)] = sum_p dY[p][co] * sx[pixel(p, t)][ci]
+//   K = output pixels (split over blockIdx-derived splits), both operands are
+//   [pixel][channel] row images in LDS read with ds_read_b64_tr_b16.
+//   sx = sign(x) as bf16 +-1 [B][H][W][Cin] (written by zk_sign_pack);
+//   padded taps read the zero page (pad_values 0) or the +1 page.
+// ===========================================================================
+// 512 B of bf16 +1.0 (0x3F80): padded taps of pad_values=1 convs.
+__device__ __attribute__((aligned(256))) uint32_t g_ones_page_bf16[128] = {
+#define ZK_ONE4 0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u
+#define ZK_ONE16 ZK_ONE4, ZK_ONE4, ZK_ONE4, ZK_ONE4
+    ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16
+#undef ZK_ONE16
+#undef ZK_ONE4
+};
+
+// XOR swizzle of the 16-B slot of row r for [k][m] images read transposed
+// (cdna_hip_programming.md T10 (b) for 256-B multiples; a 4-slot flip on odd
+// row pairs for 128-B / 384-B rows).
+template <int RBYTES>
+__device__ __forceinline__ int tr_swz(int r) {
+  if constexpr (RBYTES % 256 == 0)
+    return ((r & 3) << 2) | ((r >> 2) & 3);
+  else
+    return ((r >> 1) & 1) << 2;
+}
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// 32x32x16 operand (8 consecutive k of one column) from a swizzled [k][col]
+// image with RBYTES-byte rows: lane l: g = l>>4, i = l&15, q = i>>2, p = i&3
+// reads rows k0 + 8*(g>>1) + q (+4), columns c0 + 16*(g&1) + 4p .. +3.
+template <int RBYTES>
+__device__ __forceinline__ uint4 tr_frag_swz(const unsigned char* tile, int k0, int c0,
+                                             int lane) {
+  const int gq = lane >> 4, i = lane & 15;
+  const int q = i >> 2, p = i & 3;
+  const int row = k0 + 8 * (gq >> 1) + q;
+  const int colb = (c0 + 16 * (gq & 1) + 4 * p) * 2;  // byte within the row
+  const int slot = colb >> 4, inner = colb & 15;
+  const int o0 = row * RBYTES + ((slot ^ tr_swz<RBYTES>(row)) << 4) + inner;
+  const int o1 = (row + 4) * RBYTES + ((slot ^ tr_swz<RBYTES>(row + 4)) << 4) + inner;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(uintptr_t)(const __attribute__((
+          address_space(3))) void*)(tile + o0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(uintptr_t)(const __attribute__((
+          address_space(3))) void*)(tile + o1));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(uint4, v);
+}
+
+// q = n / d for 0 <= n < 2^24 via a float reciprocal and one correction.
+__device__ __forceinline__ int fdiv(int n, int d, float inv) {
+  int q = (int)((float)n * inv);
+  const int r = n - q * d;
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int NS>
+__global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ sx,
+    const float* __restrict__ w, float* __restrict__ dw, IGeom g, int pad_ones, float clip,
+    int k_per_split, int m_tiles, int n_tiles) {
+  constexpr int NWAVES = WM * WN;
+  constexpr int RA = BM * 2, RBB = BN * 2;      // bytes per pixel row of A / B
+  constexpr int SA = BK * RA, SB = BK * RBB;    // bytes per stage
+  static_assert(SA % (1024 * NWAVES) == 0 && SB % (1024 * NWAVES) == 0, "stage / waves");
+  constexpr int A_INS = SA / 1024 / NWAVES, B_INS = SB / 1024 / NWAVES;
+  constexpr int LPS = A_INS + B_INS;
+  constexpr int STAGE = SA + SB;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wm = wave / WN, wn = wave % WN;
+
+  // logical id: consecutive ids = tiles of one split (share dY / sx rows in
+  // one XCD's L2)
+  const int L = xcd_linear(blockIdx.x, gridDim.x);
+  const int tiles = m_tiles * n_tiles;
+  const int split = L / tiles, tile = L % tiles;
+  const int m0 = (tile % m_tiles) * BM;  // co
+  const int n0 = (tile / m_tiles) * BN;  // flattened (t, ci)
+  const int P = g.B * g.Ho * g.Wo;
+  const int kbeg = split * k_per_split;
+  if (kbeg >= P) return;
+  int kend = kbeg + k_per_split;
+  if (kend > P) kend = P;
+  const int NK = (kend - kbeg + BK - 1) / BK;
+
+  const unsigned char* dyb = reinterpret_cast<const unsigned char*>(dy);
+  const unsigned char* sxb = reinterpret_cast<const unsigned char*>(sx);
+  const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
+  const unsigned char* pp = pad_ones ? reinterpret_cast<const unsigned char*>(g_ones_page_bf16)
+                                     : zp;
+  const float invWo = 1.0f / (float)g.Wo, invHo = 1.0f / (float)g.Ho;
+
+  // Per-lane fixed parts of the loader: (row within stage, byte within row)
+  int a_row[A_INS], a_byte[A_INS];
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int off = ((j * NWAVES + wave) * 64 + lane) * 16;
+    a_row[j] = off / RA;
+    const int slot = (off % RA) >> 4;
+    a_byte[j] = m0 * 2 + ((slot ^ tr_swz<RA>(a_row[j])) << 4);
+  }
+  int b_row[B_INS], b_th[B_INS], b_tw[B_INS], b_cib[B_INS];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int off = ((j * NWAVES + wave) * 64 + lane) * 16;
+    b_row[j] = off / RBB;
+    const int slot = (off % RBB) >> 4;
+    const int n = n0 + ((slot ^ tr_swz<RBB>(b_row[j])) << 3);  // first column of the chunk
+    const int t = n / g.Cin;
+    b_th[j] = t / g.kw - g.pt;
+    b_tw[j] = t % g.kw - g.pl;
+    b_cib[j] = (n % g.Cin) * 2;
+  }
+
+  auto issue = [&](int ks) {
+    unsigned char* st = smem + (ks % NS) * STAGE;
+    const int k0 = kbeg + ks * BK;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      const int p = k0 + a_row[j];
+      const unsigned char* src =
+          p < kend ? dyb + (long long)p * (g.Cout * 2) + a_byte[j] : zp;
+      ZK_GLDS16(src, st + (j * NWAVES + wave) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const int p = k0 + b_row[j];
+      const unsigned char* src = zp;
+      if (p < kend) {
+        const int q1 = fdiv(p, g.Wo, invWo);
+        const int wo = p - q1 * g.Wo;
+        const int b = fdiv(q1, g.Ho, invHo);
+        const int ho = q1 - b * g.Ho;
+        const int hi = ho * g.s + b_th[j], wi = wo * g.s + b_tw[j];
+        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+          src = sxb + (((long long)b * g.H + hi) * g.W + wi) * (g.Cin * 2) + b_cib[j];
+        else
+          src = pp;
+      }
+      ZK_GLDS16(src, st + SA + (j * NWAVES + wave) * 1024);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < NK) issue(p);
+  for (int ks = 0; ks < NK; ++ks) {
+    if (ks + NS - 2 < NK)
+      wait_vmcnt<LPS * (NS - 2)>();
+    else
+      wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (ks + NS - 1 < NK) issue(ks + NS - 1);
+    const unsigned char* st = smem + (ks % NS) * STAGE;
+#pragma unroll
+    for (int sub = 0; sub < BK / 16; ++sub) {
+      uint4 af[TM], bfr[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) af[a] = tr_frag_swz<RA>(st, sub * 16, wm * WTM + a * 32, lane);
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        bfr[b] = tr_frag_swz<RBB>(st + SA, sub * 16, wn * WTN + b * 32, lane);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = mfma_bf16(af[a], bfr[b], acc[a][b]);
+    }
+  }
+
+  // epilogue: kernel STE mask, split-K fp32 atomics into dW [Cout][T*Cin]
+  const int h = lane >> 5, r32 = lane & 31;
+  const int NTOT = g.kh * g.kw * g.Cin;
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int n = n0 + wn * WTN + b * 32 + r32;
+        const long long idx = (long long)co * NTOT + n;
+        if (fabsf(w[idx]) <= clip) atomicAdd(dw + idx, acc[a][b][r]);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int NS>
+int launch_igemm_wgrad(const void* dy, const void* sx, const void* w, void* dw, const IGeom& g,
+                       int pad_ones, float clip, int target_blocks, hipStream_t stream) {
+  const int NTOT = g.kh * g.kw * g.Cin;
+  if (g.Cout % BM || NTOT % BN || g.Cin % 8) return (int)hipErrorInvalidValue;
+  const long long P = (long long)g.B * g.Ho * g.Wo;
+  if (P >= (1 << 24)) return (int)hipErrorInvalidValue;  // fdiv range
+  constexpr int LDS = NS * BK * (BM + BN) * 2;
+  static_assert(LDS <= 160 * 1024, "LDS");
+  auto kern = igemm_wgrad_kernel<BM, BN, WM, WN, BK, NS>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  const int m_tiles = g.Cout / BM, n_tiles = NTOT / BN;
+  const long long tiles = (long long)m_tiles * n_tiles;
+  long long splits = (target_blocks + tiles - 1) / tiles;
+  const long long max_splits = (P + 4 * BK - 1) / (4 * BK);  // >= 4 K-steps per split
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  long long kps = (P + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  splits = (P + kps - 1) / kps;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * splits)), dim3(WM * WN * 64), LDS, stream,
+                     (const uint16_t*)dy, (const uint16_t*)sx, (const float*)w, (float*)dw, g,
+                     pad_ones, clip, (int)kps, m_tiles, n_tiles);
+  return 0;
+}
+
+int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, void* dw,
+                        const IGeom& g, int po, float clip, int tb, hipStream_t st) {
+#define ZK_IGW(...) \
+  return launch_igemm_wgrad<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, st)
+  switch (v) {
+    case 0: ZK_IGW(128, 128, 2, 2, 32, 2);
+    case 1: ZK_IGW(128, 128, 2, 2, 32, 4);
+    case 2: ZK_IGW(128, 192, 2, 2, 32, 3);
+    case 3: ZK_IGW(64, 192, 2, 2, 32, 4);
+    case 4: ZK_IGW(128, 128, 2, 2, 64, 2);
+    case 5: ZK_IGW(64, 128, 2, 2, 32, 4);
+    case 6: ZK_IGW(128, 256, 2, 2, 32, 2);
+    case 7: ZK_IGW(64, 64, 2, 2, 32, 4);
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef ZK_IGW
+}
+
 }  // namespace
 
 // Same contract as zk_bconv_dgrad (binary_conv_bwd.hip): wt ±1 bf16
@@ -357,6 +614,31 @@ ZK_EXPORT int zk_igemm_dgrad(const void* dy, const void* wt, const void* mask, c
       variant = 7;
   }
   const int rc = igemm_dgrad_variant(variant, dy, wt, mask, dres, dx, g, stream);
+  if (rc) return rc;
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// dW fp32 [Cout][T][Cin] accumulated in place (zeroed by the caller or the
+// flat gradient buffer itself).  sx: sign(x) bf16 +-1 [B][H][W][Cin].
+ZK_EXPORT int zk_igemm_wgrad(const void* dy, const void* sx, const void* w, void* dw, int B,
+                             int H, int W, int Cin, int Ho, int Wo, int Cout, int kh, int kw,
+                             int stride, int pt, int pl, int pad_ones, float clip,
+                             int target_blocks, int variant, hipStream_t stream) {
+  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+  if (variant < 0) {
+    // Tuned on MI355X (tools/tune_bconv.py --only igw, E18 shapes, batch 256)
+    if (Cin == 64 || Cout % 128 != 0) {
+      variant = 7;
+      if (target_blocks <= 0) target_blocks = 2048;
+    } else {
+      variant = 0;
+      if (target_blocks <= 0) target_blocks = (Cin == 128 && stride == 1) ? 1024 : 512;
+    }
+  }
+  if (target_blocks <= 0) target_blocks = 1024;
+  const int rc = igemm_wgrad_variant(variant, dy, sx, w, dw, g, pad_ones, clip, target_blocks,
+                                     stream);
   if (rc) return rc;
   ZK_CHECK_LAUNCH();
   return 0;

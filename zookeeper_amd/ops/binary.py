@@ -56,7 +56,13 @@ class _BinaryBlockFn(torch.autograd.Function):
         nwords = B * H * W * Cin // 32
         bits = torch.empty(nwords, dtype=torch.int32, device=dev)
         mask = torch.empty(nwords, dtype=torch.int32, device=dev)
-        check(L.zk_sign_pack(xn.data_ptr(), bits.data_ptr(), mask.data_ptr(), nwords, clip, st),
+        # sign(x) as bf16 ±1 is the weight-gradient GEMM operand; only
+        # materialised when a backward pass will run.
+        need_sx = (torch.is_grad_enabled() and weight.requires_grad and Cout % 64 == 0
+                   and Cin % 64 == 0)
+        sx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev) if need_sx else None
+        check(L.zk_sign_pack(xn.data_ptr(), bits.data_ptr(), mask.data_ptr(),
+                             sx.data_ptr() if sx is not None else None, nwords, clip, st),
               "zk_sign_pack")
 
         w_ohwi = weight.permute(0, 2, 3, 1).contiguous()  # no copy for channels_last
@@ -99,7 +105,7 @@ class _BinaryBlockFn(torch.autograd.Function):
                             res.data_ptr() if res is not None else None, out.data_ptr(), P,
                             Cout, st), "zk_bn_apply")
 
-        ctx.save_for_backward(bits, mask, wt, y, mean, rstd, gamma, w_ohwi)
+        ctx.save_for_backward(bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx)
         ctx.params = (weight, gamma, beta)
         ctx.geom = (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo)
         ctx.meta = meta
@@ -109,7 +115,7 @@ class _BinaryBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        bits, mask, wt, y, mean, rstd, gamma, w_ohwi = ctx.saved_tensors
+        bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx = ctx.saved_tensors
         (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
         (_, act_relu, clip, pad_ones, identity) = ctx.meta
         dev = dout.device
@@ -164,9 +170,14 @@ class _BinaryBlockFn(torch.autograd.Function):
                 dw = w_direct.permute(0, 2, 3, 1)  # OHWI view of the flat gradient
             else:
                 dw = torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev)
-            check(L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w_ohwi.data_ptr(),
-                                   dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride,
-                                   pt, pl, int(pad_ones), clip, 0, -1, st), "zk_bconv_wgrad")
+            if sx is not None:
+                check(L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w_ohwi.data_ptr(),
+                                       dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride,
+                                       pt, pl, int(pad_ones), clip, 0, -1, st), "zk_igemm_wgrad")
+            else:
+                check(L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w_ohwi.data_ptr(),
+                                       dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride,
+                                       pt, pl, int(pad_ones), clip, 0, -1, st), "zk_bconv_wgrad")
             if w_direct is not None:
                 grad_ready(weight_p)
                 dweight = None
