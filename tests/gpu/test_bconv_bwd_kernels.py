@@ -40,7 +40,7 @@ def test_dgrad_wgrad(cin, cout, stride, hw, pad_ones):
     wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
     wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
     wt = torch.empty(9, cin, cout, dtype=torch.bfloat16, device="cuda")
-    assert L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(),
+    assert L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(), None,
                             cout, 9, cin, st) == 0
     dres = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
     dx = torch.empty(B, hw, hw, cin, dtype=torch.bfloat16, device="cuda")
@@ -97,7 +97,7 @@ def test_igemm_dgrad_matches_reference(variant, cin, cout, stride, hw):
     wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
     wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
     wt = torch.empty(9, cin, cout, dtype=torch.bfloat16, device="cuda")
-    assert L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(),
+    assert L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(), None,
                             cout, 9, cin, st) == 0
     dres = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
     dx = torch.full((B, hw, hw, cin), float("nan"), dtype=torch.bfloat16, device="cuda")
@@ -155,3 +155,48 @@ def test_igemm_wgrad_matches_reference(variant, cin, cout, stride, hw, pad_ones)
     ref = ws.grad.permute(0, 2, 3, 1) * (w.double().abs() <= 1.0)
     err = (dw.double() - ref).abs().max().item()
     assert err <= 1e-4 * ref.abs().max().item() + 1e-3, err
+
+
+@pytest.mark.parametrize("variant", list(range(12)))
+@pytest.mark.parametrize("cin,cout,stride,hw,pad_ones,relu", [
+    (64, 64, 1, 12, 0, 0), (64, 128, 2, 12, 0, 1), (128, 128, 1, 7, 1, 1),
+    (256, 512, 2, 8, 0, 0), (128, 64, 1, 9, 1, 0), (512, 128, 1, 5, 0, 1)])
+def test_igemm_fwd_matches_reference(variant, cin, cout, stride, hw, pad_ones, relu):
+    """MFMA forward (igemm.hip) on the sign image: exact int16 output and
+    exact int64 (sum, sum of squares) per channel, every tile variant."""
+    from zookeeper_amd.nn.layers import pad_same_nhwc, same_padding
+    from zookeeper_amd.nn.quantizers import sign_pm1
+    from zookeeper_amd.ops._native import lib, stream_ptr
+
+    torch.manual_seed(3)
+    L, st = lib(), stream_ptr()
+    B = 3
+    x = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
+    w = torch.randn(cout, 3, 3, cin, device="cuda")
+    pt, pb = same_padding(hw, 3, stride)
+    ho = (hw + pt + pb - 3) // stride + 1
+    nwords = x.numel() // 32
+    mask = torch.empty(nwords, dtype=torch.int32, device="cuda")
+    sx = torch.empty_like(x)
+    assert L.zk_sign_pack(x.data_ptr(), None, mask.data_ptr(), sx.data_ptr(), nwords, 1.0,
+                          st) == 0
+    wf = torch.empty(9, cout, cin, dtype=torch.bfloat16, device="cuda")
+    assert L.zk_weight_pack(w.data_ptr(), None, None, None, wf.data_ptr(), cout, 9, cin, st) == 0
+    y = torch.full((B, ho, ho, cout), -12345, dtype=torch.int16, device="cuda")
+    stats = torch.zeros(2, cout, dtype=torch.int64, device="cuda")
+    rc = L.zk_igemm_fwd(sx.data_ptr(), wf.data_ptr(), y.data_ptr(), stats.data_ptr(), B, hw, hw,
+                        cin, cout, 3, 3, stride, pt, pt, ho, ho, pad_ones, relu, variant, st)
+    if rc != 0:
+        pytest.skip("tile does not divide this shape")
+    torch.cuda.synchronize()
+    xs = sign_pm1(x.double()).permute(0, 3, 1, 2)
+    ws = sign_pm1(w.double()).permute(0, 3, 1, 2)
+    xp = pad_same_nhwc(xs, (3, 3), (stride, stride), 1.0 if pad_ones else 0.0)
+    ref = torch.nn.functional.conv2d(xp, ws, stride=stride).permute(0, 2, 3, 1)
+    if relu:
+        ref = ref.clamp_min(0)
+    ref = ref.round().long()
+    assert torch.equal(y.long(), ref)
+    flat = ref.reshape(-1, cout)
+    assert torch.equal(stats[0].cpu(), flat.sum(0).cpu())
+    assert torch.equal(stats[1].cpu(), (flat * flat).sum(0).cpu())

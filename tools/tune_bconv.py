@@ -22,6 +22,7 @@ DG_VARIANTS = 8
 WG_VARIANTS = 8
 IG_VARIANTS = 12
 IGW_VARIANTS = 8
+IGF_VARIANTS = 12
 
 
 def timeit(fn, reps):
@@ -65,8 +66,8 @@ def main():
         wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
         wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
         wt = torch.empty(9, cin, cout, dtype=torch.bfloat16, device="cuda")
-        L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(), cout, 9,
-                         cin, st)
+        L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(), None, cout,
+                         9, cin, st)
         dx = torch.empty_like(x)
         dw = torch.zeros(cout, 3, 3, cin, device="cuda")
         y = torch.empty(B, Ho, Ho, cout, dtype=torch.int16, device="cuda")
@@ -77,6 +78,30 @@ def main():
             row["fwd_xnor_us"] = timeit(lambda: L.zk_bconv_fwd(
                 bits.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), y.data_ptr(), stats.data_ptr(),
                 B, H, W, cin, cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, st), args.reps)
+        if "igf" in fam:
+            wf = torch.empty(9, cout, cin, dtype=torch.bfloat16, device="cuda")
+            L.zk_weight_pack(w.data_ptr(), None, None, None, wf.data_ptr(), cout, 9, cin, st)
+            yref = None
+            if "fwd" in fam:
+                stats.zero_()
+                L.zk_bconv_fwd(bits.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), y.data_ptr(),
+                               stats.data_ptr(), B, H, W, cin, cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0,
+                               st)
+                torch.cuda.synchronize()
+                yref = y.clone()
+            for v in range(IGF_VARIANTS):
+                y.zero_()
+                rc = L.zk_igemm_fwd(sx.data_ptr(), wf.data_ptr(), y.data_ptr(), stats.data_ptr(),
+                                    B, H, W, cin, cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, v, st)
+                torch.cuda.synchronize()
+                if rc != 0:
+                    row[f"igf_v{v}_us"] = None
+                    continue
+                if yref is not None:
+                    row[f"igf_v{v}_exact"] = bool(torch.equal(y, yref))
+                row[f"igf_v{v}_us"] = timeit(lambda: L.zk_igemm_fwd(
+                    sx.data_ptr(), wf.data_ptr(), y.data_ptr(), stats.data_ptr(), B, H, W, cin,
+                    cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, v, st), args.reps)
         ref_dx = None
         for v in (range(DG_VARIANTS) if ("dgrad" in fam or "igemm" in fam) else ()):
             if "dgrad" not in fam and v != 7:

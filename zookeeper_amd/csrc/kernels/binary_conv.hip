@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void sign_pack_kernel(const uint16_t* __restri
       // sign(x) as bf16 +-1: the operand of the MFMA weight gradient
       if (xs) reinterpret_cast<uint4*>(xs + 32 * w)[q] = make_uint4(o[0], o[1], o[2], o[3]);
     }
-    bits[w] = b;
+    if (bits) bits[w] = b;
     if (mask) mask[w] = mk;
   }
 }
@@ -83,6 +83,7 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restric
                                                           uint32_t* __restrict__ wbits,
                                                           int* __restrict__ wpop,
                                                           uint16_t* __restrict__ wt,
+                                                          uint16_t* __restrict__ wf,
                                                           long long nwords, int CW, int T,
                                                           int Cout) {
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -97,8 +98,26 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restric
     b |= (uint32_t)(v.z >= 0.f) << (4 * q + 2);
     b |= (uint32_t)(v.w >= 0.f) << (4 * q + 3);
   }
-  wbits[i] = b;
-  atomicAdd(wpop + i / CW, __popc(b));
+  if (wbits) {
+    wbits[i] = b;
+    atomicAdd(wpop + i / CW, __popc(b));
+  }
+  if (wf) {  // [T][Cout][Cin]: the forward GEMM's K-contiguous operand
+    const int wd = (int)(i % CW);
+    const long long ct = i / CW;
+    const int t = (int)(ct % T), co = (int)(ct / T);
+    uint4* dst = reinterpret_cast<uint4*>(wf + (((long long)t * Cout + co) * CW + wd) * 32);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 8 * q + 2 * e;
+        o[e] = (((b >> k) & 1) ? 0x3F80u : 0xBF80u) | ((((b >> (k + 1)) & 1) ? 0x3F80u : 0xBF80u) << 16);
+      }
+      dst[q] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
   if (wt) {
     const int wd = (int)(i % CW);
     const long long ct = i / CW;
@@ -365,14 +384,14 @@ ZK_EXPORT int zk_sign_pack(const void* x, void* bits, void* mask, void* xs, long
   return 0;
 }
 
-ZK_EXPORT int zk_weight_pack(const void* w, void* wbits, void* wpop, void* wt, int Cout,
-                             int T, int Cin, hipStream_t stream) {
+ZK_EXPORT int zk_weight_pack(const void* w, void* wbits, void* wpop, void* wt, void* wf,
+                             int Cout, int T, int Cin, hipStream_t stream) {
   if (Cin % 32) return (int)hipErrorInvalidValue;
   const long long nwords = (long long)Cout * T * (Cin / 32);
-  hipMemsetAsync(wpop, 0, sizeof(int) * (size_t)Cout * T, stream);
+  if (wpop) hipMemsetAsync(wpop, 0, sizeof(int) * (size_t)Cout * T, stream);
   hipLaunchKernelGGL(weight_pack_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0,
                      stream, (const float*)w, (uint32_t*)wbits, (int*)wpop, (uint16_t*)wt,
-                     nwords, Cin / 32, T, Cout);
+                     (uint16_t*)wf, nwords, Cin / 32, T, Cout);
   ZK_CHECK_LAUNCH();
   return 0;
 }

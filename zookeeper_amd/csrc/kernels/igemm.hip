@@ -39,6 +39,14 @@ struct IGeom {
 
 // 256 B of zeros: the source of every padded row.
 __device__ __attribute__((aligned(256))) uint4 g_zero_page[16];
+// 512 B of bf16 +1.0 (0x3F80): padded taps of pad_values=1 convs.
+__device__ __attribute__((aligned(256))) uint32_t g_ones_page_bf16[128] = {
+#define ZK_ONE4 0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u
+#define ZK_ONE16 ZK_ONE4, ZK_ONE4, ZK_ONE4, ZK_ONE4
+    ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16
+#undef ZK_ONE16
+#undef ZK_ONE4
+};
 
 // global_load_lds_dwordx4 in inline asm.  With the builtin, hipcc treats the
 // DMA as an LDS store it cannot disambiguate and puts s_waitcnt vmcnt(0) in
@@ -76,13 +84,40 @@ __device__ __forceinline__ int xcd_linear(int L, int nwg) {
 }
 
 // ===========================================================================
-// dgrad
+// Convolution-shaped implicit GEMM, transposed product D[n][pixel]:
+//   FWD=false (dgrad): pixels = input pixels of one stride-parity class
+//     (blockIdx.y), n = ci, K = (tap, co), A = dY, B = S^T [T][Cin][Cout];
+//     epilogue: STE mask bits, + dres, bf16 dx.
+//   FWD=true (binary forward): pixels = output pixels, n = co,
+//     K = (tap, ci), A = sign(x) bf16 +-1, B = sign(W) bf16 [T][Cout][Cin];
+//     padded taps read the zero / +1 page; the fp32 accumulators hold exact
+//     integers.  Epilogue: optional ReLU, int16 y, per-channel sum and
+//     sum of squares (int32 in-wave, int64 block atomics).
 // ===========================================================================
-template <int BM, int BN, int WM, int WN, int NS, int CB>
-__global__ __launch_bounds__(WM * WN * 64, 1) void igemm_dgrad_kernel(
-    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ wt,
-    const uint32_t* __restrict__ mask, const uint16_t* __restrict__ dres,
-    uint16_t* __restrict__ dx, IGeom g, int m_tiles) {
+struct ConvArgs {
+  const uint16_t* act;   // dY (dgrad) / sign(x) (fwd)
+  const uint16_t* wgt;   // [T][N][K-channels] bf16 +-1
+  const uint32_t* mask;  // dgrad: STE mask bits of x (optional)
+  const uint16_t* dres;  // dgrad: residual gradient (optional)
+  void* out;             // dgrad: dx bf16 / fwd: y int16
+  unsigned long long* stats;  // fwd: [2][Cout] int64 (sum, sum of squares)
+  int pad_ones, relu;    // fwd
+};
+
+// Sum over the 32 lanes of each wave half (DPP within rows of 16, then one
+// cross-row swap); every lane of the half ends with the total.
+__device__ __forceinline__ int half_sum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
+  v += __shfl_xor(v, 16, 64);
+  return v;
+}
+
+template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB>
+__global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs args, IGeom g,
+                                                                     int m_tiles) {
   constexpr int NWAVES = WM * WN;
   // CB = bytes of K per row per stage (128 = 64 bf16, or 64)
   constexpr int SPR = CB / 16;            // 16-B slots per row
@@ -97,35 +132,40 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_dgrad_kernel(
   constexpr int STAGE = (BM + BN) * CB;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(!FWD || TM <= 4, "in-wave int32 sums of squares need TM <= 4");
 
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int wm = wave / WN, wn = wave % WN;
+  const int NCH = FWD ? g.Cout : g.Cin;   // GEMM N
+  const int KCH = FWD ? g.Cin : g.Cout;   // channels per tap along K
 
   // ---- tile coordinates (XCD-aware: the M tiles of one N tile are
   // consecutive logical ids, so they share an L2 with that N tile's weights)
   const int nwg = gridDim.x;
   const int L = xcd_linear(blockIdx.x, nwg);
-  const int n_tiles = g.Cin / BN;
+  const int n_tiles = NCH / BN;
   const int mtile = L % m_tiles;
   const int ntile = L / m_tiles;
   if (ntile >= n_tiles) return;
   const int s = g.s;
-  const int ph = blockIdx.y / s, pw = blockIdx.y % s;
-  const int Hc = (g.H - ph + s - 1) / s, Wc = (g.W - pw + s - 1) / s;
+  const int ph = FWD ? 0 : blockIdx.y / s, pw = FWD ? 0 : blockIdx.y % s;
+  const int Hc = FWD ? g.Ho : (g.H - ph + s - 1) / s;
+  const int Wc = FWD ? g.Wo : (g.W - pw + s - 1) / s;
   const long long M = (long long)g.B * Hc * Wc;
   const long long m0 = (long long)mtile * BM;
   if (m0 >= M) return;
   const int n0 = ntile * BN;
 
-  // taps of this parity class: th = th0 + i*s (no runtime-indexed arrays,
-  // which would live in scratch)
-  const int th0 = (ph + g.pt) % s, tw0 = (pw + g.pl) % s;
-  const int nth = (g.kh - th0 + s - 1) / s, ntw = (g.kw - tw0 + s - 1) / s;
+  // taps: all of them (fwd) or those of this parity class (dgrad):
+  // th = th0 + i*s (no runtime-indexed arrays, which would live in scratch)
+  const int ts = FWD ? 1 : s;
+  const int th0 = FWD ? 0 : (ph + g.pt) % s, tw0 = FWD ? 0 : (pw + g.pl) % s;
+  const int nth = (g.kh - th0 + ts - 1) / ts, ntw = (g.kw - tw0 + ts - 1) / ts;
   const int T = nth * ntw;
-  const int RB = g.Cout * 2;           // bytes per dY row
+  const int RB = KCH * 2;              // bytes per activation / weight row
   const int kchunks = RB / CB;
   const int NK = T * kchunks;
 
@@ -141,9 +181,15 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_dgrad_kernel(
     if (m < M) {
       const int jw = (int)(m % Wc);
       const long long rr = m / Wc;
-      a_h[j] = (int)(rr % Hc) * s + ph + g.pt;
-      a_w[j] = jw * s + pw + g.pl;
+      const int jh = (int)(rr % Hc);
       a_b[j] = (int)(rr / Hc);
+      if (FWD) {
+        a_h[j] = jh * s - g.pt;
+        a_w[j] = jw * s - g.pl;
+      } else {
+        a_h[j] = jh * s + ph + g.pt;
+        a_w[j] = jw * s + pw + g.pl;
+      }
     } else {
       a_b[j] = -1;
       a_h[j] = a_w[j] = 0;
@@ -155,31 +201,43 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_dgrad_kernel(
     const int r = (j * NWAVES + wave) * RPI + lrow;
     b_sw[j] = lslot ^ ((r >> SH) & (SPR - 1));
   }
-  const unsigned char* dyb = reinterpret_cast<const unsigned char*>(dy);
-  const unsigned char* wtb = reinterpret_cast<const unsigned char*>(wt);
+  const unsigned char* actb = reinterpret_cast<const unsigned char*>(args.act);
+  const unsigned char* wtb = reinterpret_cast<const unsigned char*>(args.wgt);
   const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
+  const unsigned char* padp =
+      (FWD && args.pad_ones) ? reinterpret_cast<const unsigned char*>(g_ones_page_bf16) : zp;
 
   // Source pointers of the current tap (recomputed when the tap changes).
   const unsigned char* a_src[A_INS];
-  int a_step[A_INS];  // CB for a real row, 0 for the zero page
+  int a_step[A_INS];  // CB for a real row, 0 for a padding page
   const unsigned char* b_src[B_INS];
   auto set_tap = [&](int ti) {
-    const int th = th0 + (ti / ntw) * s, tw = tw0 + (ti % ntw) * s;
+    const int th = th0 + (ti / ntw) * ts, tw = tw0 + (ti % ntw) * ts;
     const int t = th * g.kw + tw;
 #pragma unroll
     for (int j = 0; j < A_INS; ++j) {
-      const int hn = a_h[j] - th, wn_ = a_w[j] - tw;  // divisible by s
-      const int ho = (s == 1) ? hn : (hn >> 1);
-      const int wo = (s == 1) ? wn_ : (wn_ >> 1);
-      const bool ok = a_b[j] >= 0 && hn >= 0 && wn_ >= 0 && ho < g.Ho && wo < g.Wo;
-      a_src[j] = ok ? dyb + (((long long)a_b[j] * g.Ho + ho) * g.Wo + wo) * RB + a_sw[j] * 16
-                    : zp + a_sw[j] * 16;
+      long long pix;
+      bool ok;
+      if (FWD) {
+        const int hi = a_h[j] + th, wi = a_w[j] + tw;
+        ok = hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+        pix = ((long long)a_b[j] * g.H + hi) * g.W + wi;
+      } else {
+        const int hn = a_h[j] - th, wn_ = a_w[j] - tw;  // divisible by s
+        const int ho = (s == 1) ? hn : (hn >> 1);
+        const int wo = (s == 1) ? wn_ : (wn_ >> 1);
+        ok = hn >= 0 && wn_ >= 0 && ho < g.Ho && wo < g.Wo;
+        pix = ((long long)a_b[j] * g.Ho + ho) * g.Wo + wo;
+      }
+      const unsigned char* pad = a_b[j] >= 0 ? padp : zp;  // tail rows: zeros
+      ok = ok && a_b[j] >= 0;
+      a_src[j] = ok ? actb + pix * RB + a_sw[j] * 16 : pad + a_sw[j] * 16;
       a_step[j] = ok ? CB : 0;
     }
 #pragma unroll
     for (int j = 0; j < B_INS; ++j) {
       const int r = (j * NWAVES + wave) * RPI + lrow;
-      b_src[j] = wtb + ((long long)t * g.Cin + n0 + r) * RB + b_sw[j] * 16;
+      b_src[j] = wtb + ((long long)t * NCH + n0 + r) * RB + b_sw[j] * 16;
     }
   };
   // Issue the glds of K-step ks into ring slot ks % NS.
@@ -256,37 +314,103 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_dgrad_kernel(
     }
   }
 
-  // ---- epilogue: lane = pixel, 4 consecutive channels per register group
-  const int CW = g.Cin >> 5;
+  if constexpr (FWD) {
+    // ---- forward epilogue: lane = output pixel; exact integer results
+    int16_t* y = reinterpret_cast<int16_t*>(args.out);
+    int csum[TN][16], csq[TN][16];
 #pragma unroll
-  for (int a = 0; a < TM; ++a) {
-    const long long mc = m0 + wm * WTM + a * 32 + r32;
-    if (mc >= M) continue;
-    const int jw = (int)(mc % Wc);
-    const long long rr = mc / Wc;
-    const long long m =
-        ((rr / Hc) * g.H + (long long)(rr % Hc) * s + ph) * g.W + (long long)jw * s + pw;
+    for (int b = 0; b < TN; ++b)
 #pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int nb = n0 + wn * WTN + b * 32;
-      const uint32_t mw = mask ? mask[m * CW + (nb >> 5)] : 0xFFFFFFFFu;
+      for (int r = 0; r < 16; ++r) csum[b][r] = csq[b][r] = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int nl = 8 * q + 4 * h;
-        float v[4];
+    for (int a = 0; a < TM; ++a) {
+      const long long mc = m0 + wm * WTM + a * 32 + r32;
+      const bool live = mc < M;
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          v[e] = ((mw >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
-        const long long off = m * g.Cin + nb + nl;
-        if (dres) {
-          const uint2 d = *reinterpret_cast<const uint2*>(dres + off);
-          v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
-          v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
-          v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
-          v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
+      for (int b = 0; b < TN; ++b) {
+        const int nb = n0 + wn * WTN + b * 32;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          int v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            int t = (int)acc[a][b][4 * q + e];  // exact: |t| <= K
+            if (args.relu) t = t > 0 ? t : 0;
+            if (!live) t = 0;
+            v[e] = t;
+            csum[b][4 * q + e] += t;
+            csq[b][4 * q + e] += t * t;
+          }
+          if (live)
+            *reinterpret_cast<uint2*>(y + mc * g.Cout + nb + 8 * q + 4 * h) =
+                make_uint2((uint32_t)(uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16),
+                           (uint32_t)(uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16));
         }
-        *reinterpret_cast<uint2*>(dx + off) =
-            make_uint2(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]));
+      }
+    }
+    // statistics: reduce over the wave's 32 pixels per half, then over the
+    // WM waves sharing these channels (LDS), one int64 atomic per channel.
+    __builtin_amdgcn_s_barrier();  // all waves are done with the ring
+    int* red = reinterpret_cast<int*>(smem);  // [WM][2][BN]
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int s1 = half_sum(csum[b][r]);
+        const int s2 = half_sum(csq[b][r]);
+        if (r32 == 0) {
+          const int nl = wn * WTN + b * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          red[(wm * 2 + 0) * BN + nl] = s1;
+          red[(wm * 2 + 1) * BN + nl] = s2;
+        }
+      }
+    __syncthreads();
+    for (int c = tid; c < 2 * BN; c += NWAVES * 64) {
+      const int which = c / BN, nl = c % BN;
+      long long tot = 0;
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        const int v = red[(i * 2 + which) * BN + nl];
+        tot += which ? (long long)(unsigned int)v : (long long)v;  // squares: unsigned
+      }
+      atomicAdd(args.stats + which * g.Cout + n0 + nl, (unsigned long long)tot);
+    }
+  } else {
+    // ---- dgrad epilogue: lane = pixel, 4 consecutive channels per group
+    uint16_t* dx = reinterpret_cast<uint16_t*>(args.out);
+    const uint32_t* mask = args.mask;
+    const uint16_t* dres = args.dres;
+    const int CW = g.Cin >> 5;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const long long mc = m0 + wm * WTM + a * 32 + r32;
+      if (mc >= M) continue;
+      const int jw = (int)(mc % Wc);
+      const long long rr = mc / Wc;
+      const long long m =
+          ((rr / Hc) * g.H + (long long)(rr % Hc) * s + ph) * g.W + (long long)jw * s + pw;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int nb = n0 + wn * WTN + b * 32;
+        const uint32_t mw = mask ? mask[m * CW + (nb >> 5)] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int nl = 8 * q + 4 * h;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e] = ((mw >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
+          const long long off = m * g.Cin + nb + nl;
+          if (dres) {
+            const uint2 d = *reinterpret_cast<const uint2*>(dres + off);
+            v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
+            v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
+            v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
+            v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
+          }
+          *reinterpret_cast<uint2*>(dx + off) =
+              make_uint2(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]));
+        }
       }
     }
   }
@@ -299,7 +423,7 @@ int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const v
     return (int)hipErrorInvalidValue;
   constexpr int LDS = NS * (BM + BN) * CB;
   static_assert(LDS <= 160 * 1024, "LDS");
-  auto kern = igemm_dgrad_kernel<BM, BN, WM, WN, NS, CB>;
+  auto kern = igemm_conv_kernel<false, BM, BN, WM, WN, NS, CB>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -311,10 +435,56 @@ int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const v
   const long long Mc = (long long)g.B * Hc * Wc;
   const int m_tiles = (int)((Mc + BM - 1) / BM);
   const long long blocks = (long long)m_tiles * (g.Cin / BN);
+  ConvArgs args{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
+                (const uint16_t*)dres, dx, nullptr, 0, 0};
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, g.s * g.s), dim3(WM * WN * 64), LDS, stream,
-                     (const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
-                     (const uint16_t*)dres, (uint16_t*)dx, g, m_tiles);
+                     args, g, m_tiles);
   return 0;
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int CB = 128>
+int launch_igemm_fwd(const void* sx, const void* wf, void* y, void* stats, const IGeom& g,
+                     int pad_ones, int relu, hipStream_t stream) {
+  if ((g.Cin * 2) % CB || g.Cout % BN) return (int)hipErrorInvalidValue;
+  constexpr int LDS = NS * (BM + BN) * CB;
+  static_assert(LDS <= 160 * 1024, "LDS");
+  auto kern = igemm_conv_kernel<true, BM, BN, WM, WN, NS, CB>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  const long long Mo = (long long)g.B * g.Ho * g.Wo;
+  const int m_tiles = (int)((Mo + BM - 1) / BM);
+  const long long blocks = (long long)m_tiles * (g.Cout / BN);
+  ConvArgs args{(const uint16_t*)sx, (const uint16_t*)wf, nullptr, nullptr, y,
+                (unsigned long long*)stats, pad_ones, relu};
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks, 1), dim3(WM * WN * 64), LDS, stream, args, g,
+                     m_tiles);
+  return 0;
+}
+
+int igemm_fwd_variant(int v, const void* sx, const void* wf, void* y, void* stats,
+                      const IGeom& g, int po, int relu, hipStream_t st) {
+#define ZK_IGF(...) return launch_igemm_fwd<__VA_ARGS__>(sx, wf, y, stats, g, po, relu, st)
+  switch (v) {
+    case 0: ZK_IGF(128, 128, 2, 2, 2);
+    case 1: ZK_IGF(128, 128, 2, 2, 4, 64);
+    case 2: ZK_IGF(256, 128, 4, 2, 2);
+    case 3: ZK_IGF(128, 256, 2, 2, 2);
+    case 4: ZK_IGF(128, 64, 2, 2, 2);
+    case 5: ZK_IGF(128, 64, 2, 2, 3);
+    case 6: ZK_IGF(256, 64, 4, 1, 2);
+    case 7: ZK_IGF(128, 64, 2, 2, 4, 64);
+    case 8: ZK_IGF(256, 64, 4, 1, 4, 64);
+    case 9: ZK_IGF(64, 64, 2, 2, 2);
+    case 10: ZK_IGF(128, 128, 2, 2, 4);
+    case 11: ZK_IGF(256, 128, 4, 2, 4, 64);
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef ZK_IGF
 }
 
 int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
@@ -346,15 +516,6 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
 //   sx = sign(x) as bf16 +-1 [B][H][W][Cin] (written by zk_sign_pack);
 //   padded taps read the zero page (pad_values 0) or the +1 page.
 // ===========================================================================
-// 512 B of bf16 +1.0 (0x3F80): padded taps of pad_values=1 convs.
-__device__ __attribute__((aligned(256))) uint32_t g_ones_page_bf16[128] = {
-#define ZK_ONE4 0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u
-#define ZK_ONE16 ZK_ONE4, ZK_ONE4, ZK_ONE4, ZK_ONE4
-    ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16, ZK_ONE16
-#undef ZK_ONE16
-#undef ZK_ONE4
-};
-
 // XOR swizzle of the 16-B slot of row r for [k][m] images read transposed
 // (cdna_hip_programming.md T10 (b) for 256-B multiples; a 4-slot flip on odd
 // row pairs for 128-B / 384-B rows).
@@ -639,6 +800,27 @@ ZK_EXPORT int zk_igemm_wgrad(const void* dy, const void* sx, const void* w, void
   if (target_blocks <= 0) target_blocks = 1024;
   const int rc = igemm_wgrad_variant(variant, dy, sx, w, dw, g, pad_ones, clip, target_blocks,
                                      stream);
+  if (rc) return rc;
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// Binary forward on MFMA: y int16 [B][Ho][Wo][Cout] = conv(sign x, sign W)
+// (+ReLU), stats [2][Cout] int64 += (sum y, sum y^2) (zeroed by the caller).
+// sx: bf16 +-1 [B][H][W][Cin]; wf: bf16 +-1 [T][Cout][Cin].
+ZK_EXPORT int zk_igemm_fwd(const void* sx, const void* wf, void* y, void* stats, int B, int H,
+                           int W, int Cin, int Cout, int kh, int kw, int stride, int pt, int pl,
+                           int Ho, int Wo, int pad_ones, int relu, int variant,
+                           hipStream_t stream) {
+  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+  if (variant < 0) {
+    // Tuned on MI355X (tools/tune_bconv.py --only igf, E18 shapes, batch 256)
+    if (Cin == 64 || Cout % 128 != 0)
+      variant = (Cout == 64) ? 8 : 7;
+    else
+      variant = (stride == 1 && Cout >= 256) ? 11 : 0;
+  }
+  const int rc = igemm_fwd_variant(variant, sx, wf, y, stats, g, pad_ones, relu, stream);
   if (rc) return rc;
   ZK_CHECK_LAUNCH();
   return 0;

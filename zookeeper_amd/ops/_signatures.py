@@ -21,11 +21,12 @@ SIGNATURES = {
     "zk_normalize_flip_c3": (I32, [P, P, I32, I32, I32, FP, FP, I32, U64, P]),
     # binary convolution
     "zk_sign_pack": (I32, [P, P, P, P, I64, F32, P]),
-    "zk_weight_pack": (I32, [P, P, P, P, I32, I32, I32, P]),
+    "zk_weight_pack": (I32, [P, P, P, P, P, I32, I32, I32, P]),
     "zk_unpack_sign": (I32, [P, P, I64, P]),
     "zk_bconv_fwd": (I32, [P, P, P, P, P] + [I32] * 14 + [P]),
     "zk_bconv_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
     "zk_igemm_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
+    "zk_igemm_fwd": (I32, [P, P, P, P] + [I32] * 15 + [P]),
     "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P]),
     "zk_bconv_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P]),
     # batch norm

@@ -1,26 +1,28 @@
 """Fused binary residual block: ``out = BN(act(bconv(sign(x)))) + residual``.
 
 One autograd op per block (used by BinaryResNet-E and QuickNet on the
-``hip`` backend).  Forward kernels (``csrc/kernels/binary_conv.hip``,
-``batchnorm.hip``):
+``hip`` backend).  Forward kernels:
 
-1. ``zk_sign_pack``   x bf16 → sign bits + STE mask bits (|x| ≤ clip), 1 bit each;
-2. ``zk_weight_pack`` latent fp32 kernel → sign bits, per-tap popcounts, ±1 bf16;
-3. ``zk_bconv_fwd``   XNOR-popcount implicit GEMM on LDS bit tiles → exact
-   int16 output (+ optional ReLU) and exact int64 BN statistics;
+1. ``zk_sign_pack``   x bf16 → STE mask bits (|x| ≤ clip) and the sign image
+   sx (bf16 ±1); packed sign bits only for the XNOR fallback;
+2. ``zk_weight_pack`` latent fp32 kernel → ±1 bf16 as [T][Cout][Cin]
+   (forward) and [T][Cin][Cout] (dgrad);
+3. ``zk_igemm_fwd``   MFMA implicit GEMM on an LDS-DMA ring (igemm.hip) →
+   exact int16 output (+ optional ReLU) and exact int64 BN statistics
+   (``zk_bconv_fwd``, XNOR-popcount on bit tiles, for channel counts that do
+   not tile by 64);
 4. ``zk_bn_finalize`` per-channel scale/shift, running statistics (Keras
    momentum, Bessel-corrected variance);
 5. ``zk_bn_apply``    out = scale·y + shift + residual, bf16.
 
-Backward: ``zk_bn_bwd_reduce`` (Σg, Σg·ŷ) → ``zk_bn_bwd_dx`` (dy, ReLU mask)
-→ ``zk_igemm_dgrad`` (MFMA implicit GEMM dy ⊛ sign(W)ᵀ on an LDS-DMA ring,
-with the input STE mask and the identity-residual gradient fused into its
-epilogue) and
-``zk_bconv_wgrad`` (MFMA implicit GEMM reading the packed sign bits of x
-directly, kernel STE mask in the epilogue, split-K fp32 atomics).
+Backward: ``zk_bn_bwd_reduce`` (Σg, Σg·ŷ) → ``zk_bn_bwd_coef`` →
+``zk_bn_bwd_dx`` (dy, ReLU mask) → ``zk_igemm_dgrad`` (dy ⊛ sign(W)ᵀ with
+the input STE mask and the identity-residual gradient fused into its
+epilogue) and ``zk_igemm_wgrad`` (dyᵀ ⊛ sx, kernel STE mask in the
+epilogue, split-K fp32 atomics straight into the flat gradient buffer).
 
-Saved for backward: 2 bits per input element (sign, STE mask), the int16
-conv output and per-channel vectors — no bf16 copy of the input.
+Saved for backward: the STE mask bits, the sign image, the int16 conv
+output and per-channel vectors — no bf16 copy of the real-valued input.
 """
 
 from __future__ import annotations
@@ -41,7 +43,7 @@ def _nhwc(t: torch.Tensor) -> torch.Tensor:
 class _BinaryBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, gamma, beta, bn, meta):
-        (stride, act_relu, clip, pad_ones, identity) = meta
+        (stride, act_relu, clip, pad_ones, identity, will_backward) = meta
         B, Cin, H, W = x.shape
         Cout, _, kh, kw = weight.shape
         T = kh * kw
@@ -54,31 +56,43 @@ class _BinaryBlockFn(torch.autograd.Function):
 
         xn = _nhwc(x)
         nwords = B * H * W * Cin // 32
-        bits = torch.empty(nwords, dtype=torch.int32, device=dev)
+        # MFMA path (igemm.hip) for channel counts that tile by 64: the
+        # forward and both gradients run as bf16 ±1 implicit GEMMs on the
+        # sign image sx; otherwise the XNOR-popcount forward on packed bits.
+        mfma = Cout % 64 == 0 and Cin % 64 == 0 and stride <= 2 and kh <= 4 and kw <= 4
+        bits = None if mfma else torch.empty(nwords, dtype=torch.int32, device=dev)
         mask = torch.empty(nwords, dtype=torch.int32, device=dev)
-        # sign(x) as bf16 ±1 is the weight-gradient GEMM operand; only
-        # materialised when a backward pass will run.
-        need_sx = (torch.is_grad_enabled() and weight.requires_grad and Cout % 64 == 0
-                   and Cin % 64 == 0)
-        sx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev) if need_sx else None
-        check(L.zk_sign_pack(xn.data_ptr(), bits.data_ptr(), mask.data_ptr(),
-                             sx.data_ptr() if sx is not None else None, nwords, clip, st),
-              "zk_sign_pack")
+        sx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev) if mfma else None
+        check(L.zk_sign_pack(xn.data_ptr(), bits.data_ptr() if bits is not None else None,
+                             mask.data_ptr(), sx.data_ptr() if sx is not None else None, nwords,
+                             clip, st), "zk_sign_pack")
 
         w_ohwi = weight.permute(0, 2, 3, 1).contiguous()  # no copy for channels_last
-        wbits = torch.empty(Cout * T * Cin // 32, dtype=torch.int32, device=dev)
-        wpop = torch.empty(Cout * T, dtype=torch.int32, device=dev)
-        # ±1 kernel transposed to [T][Cin][Cout] for the dgrad GEMM.
-        wt = torch.empty((T, Cin, Cout), dtype=torch.bfloat16, device=dev)
-        check(L.zk_weight_pack(w_ohwi.data_ptr(), wbits.data_ptr(), wpop.data_ptr(),
-                               wt.data_ptr(), Cout, T, Cin, st), "zk_weight_pack")
+        wbits = None if mfma else torch.empty(Cout * T * Cin // 32, dtype=torch.int32, device=dev)
+        wpop = None if mfma else torch.empty(Cout * T, dtype=torch.int32, device=dev)
+        # ±1 kernel as [T][Cout][Cin] (forward GEMM) and transposed to
+        # [T][Cin][Cout] for the dgrad GEMM (only when a backward will run).
+        wf = torch.empty((T, Cout, Cin), dtype=torch.bfloat16, device=dev) if mfma else None
+        wt = (torch.empty((T, Cin, Cout), dtype=torch.bfloat16, device=dev)
+              if will_backward else None)
+        _p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        check(L.zk_weight_pack(w_ohwi.data_ptr(), _p(wbits), _p(wpop), _p(wt), _p(wf), Cout, T,
+                               Cin, st), "zk_weight_pack")
 
         P = B * Ho * Wo
         y = torch.empty((B, Ho, Wo, Cout), dtype=torch.int16, device=dev)
         stats = torch.zeros((2, Cout), dtype=torch.int64, device=dev)
-        check(L.zk_bconv_fwd(bits.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), y.data_ptr(),
-                             stats.data_ptr(), B, H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho,
-                             Wo, int(pad_ones), int(act_relu), st), "zk_bconv_fwd")
+        if mfma:
+            check(L.zk_igemm_fwd(sx.data_ptr(), wf.data_ptr(), y.data_ptr(), stats.data_ptr(), B,
+                                 H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(pad_ones),
+                                 int(act_relu), -1, st), "zk_igemm_fwd")
+        else:
+            check(L.zk_bconv_fwd(bits.data_ptr(), wbits.data_ptr(), wpop.data_ptr(),
+                                 y.data_ptr(), stats.data_ptr(), B, H, W, Cin, Cout, kh, kw,
+                                 stride, pt, pl, Ho, Wo, int(pad_ones), int(act_relu), st),
+                  "zk_bconv_fwd")
+        if not will_backward:
+            sx = None
 
         scale = torch.empty(Cout, dtype=torch.float32, device=dev)
         shift = torch.empty_like(scale)
@@ -117,7 +131,7 @@ class _BinaryBlockFn(torch.autograd.Function):
     def backward(ctx, dout):
         bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx = ctx.saved_tensors
         (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
-        (_, act_relu, clip, pad_ones, identity) = ctx.meta
+        (_, act_relu, clip, pad_ones, identity, _) = ctx.meta
         dev = dout.device
         st = stream_ptr(dev)
         L = lib()
@@ -194,7 +208,7 @@ def _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx):
     not a multiple of 64): bf16 library convolution backward on unpacked ±1
     operands, then the fused STE/residual kernel."""
     (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
-    (_, _, clip, pad_ones, identity) = ctx.meta
+    (_, _, clip, pad_ones, identity, _) = ctx.meta
     dev = dy.device
     st = stream_ptr(dev)
     L = lib()
@@ -248,6 +262,9 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
     identity = residual is x
     if residual is not None and not identity and residual.dtype != torch.bfloat16:
         residual = residual.to(torch.bfloat16)
-    meta = (conv.stride[0], act == "relu", float(clip_value), pad_value == 1.0, identity)
+    will_backward = torch.is_grad_enabled() and (
+        x.requires_grad or conv.weight.requires_grad or bn.training)
+    meta = (conv.stride[0], act == "relu", float(clip_value), pad_value == 1.0, identity,
+            will_backward)
     return _BinaryBlockFn.apply(x, None if identity else residual, conv.weight, bn.weight,
                                 bn.bias, bn, meta)
