@@ -1,0 +1,88 @@
+"""Fused ImageNet stem (stem.hip) vs the same modules run one by one
+(library conv + bf16 BN/pool kernels), training mode: output, running
+statistics and every parameter gradient."""
+
+import copy
+
+import pytest
+import torch
+
+from zookeeper_amd.nn.layers import BatchNorm, ImageStem, MaxPool2d, QuantConv2d
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from zookeeper_amd import ops
+
+    assert ops.available(), ops.load_error()
+
+
+def _stem(with_bn2):
+    mods = [QuantConv2d(3, 64, 7, 2, "same", kernel_initializer="he_normal"),
+            BatchNorm(64, 0.9, 1e-5, activation="relu"), MaxPool2d(3, 2, "same")]
+    if with_bn2:
+        mods.append(BatchNorm(64, 0.9, 1e-5))
+    return ImageStem(*mods)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("hw,with_bn2", [(64, True), (56, False), (224, True)])
+def test_fused_stem_matches_unfused(hw, with_bn2):
+    """The fused bf16 stem must be as close to the fp32 oracle as the
+    unfused bf16 path (library conv + bf16 BN/pool kernels) is: the weight
+    gradient goes through a dense bf16 dy1 with large cancelling BN terms in
+    both, so only relative-to-baseline accuracy is meaningful there."""
+    torch.manual_seed(0)
+    fused = _stem(with_bn2).cuda().to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        for m in fused.modules():
+            if isinstance(m, BatchNorm):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.3, 0.3)
+    unfused = copy.deepcopy(fused)
+    oracle = copy.deepcopy(fused).float()
+    B = 4 if hw == 224 else 6
+    x = torch.randn(B, 3, hw, hw, device="cuda").to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    assert fused._fusable(x)
+    y = fused(x)
+    y_bf = torch.nn.Sequential.forward(unfused, x)
+    y_ref = torch.nn.Sequential.forward(oracle, x.float())
+    assert y.shape == y_ref.shape
+    assert _rel(y, y_ref) < max(1.5 * _rel(y_bf, y_ref), 1e-2)
+    g = torch.randn_like(y_ref).to(torch.bfloat16)
+    y.backward(g)
+    y_bf.backward(g)
+    y_ref.backward(g.float())
+    for (n, p), (_, q), (_, r) in zip(fused.named_parameters(), unfused.named_parameters(),
+                                      oracle.named_parameters()):
+        assert p.grad is not None, n
+        e_fused, e_lib = _rel(p.grad, r.grad), _rel(q.grad, r.grad)
+        assert e_fused < max(1.5 * e_lib, 2e-2), (n, e_fused, e_lib)
+    for (n, b), (_, c) in zip(fused.named_buffers(), oracle.named_buffers()):
+        torch.testing.assert_close(b, c, atol=3e-3, rtol=3e-3)
+
+
+def test_fused_stem_eval_matches():
+    torch.manual_seed(1)
+    fused = _stem(True).cuda().to(memory_format=torch.channels_last).eval()
+    with torch.no_grad():
+        for m in fused.modules():
+            if isinstance(m, BatchNorm):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 2.0)
+    x = torch.randn(2, 3, 64, 64, device="cuda").to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    ref = copy.deepcopy(fused).float()
+    with torch.no_grad():
+        assert fused._fusable(x)
+        y = fused(x)
+        y_ref = torch.nn.Sequential.forward(ref, x.float())
+    assert _rel(y, y_ref) < 2e-2

@@ -35,6 +35,7 @@ from zookeeper_amd.models.base import ModelFactory
 from zookeeper_amd.nn.layers import (
     AvgPool2d,
     BatchNorm,
+    ImageStem,
     GlobalAvgPool,
     MaxPool2d,
     QuantConv2d,
@@ -95,7 +96,7 @@ class BinaryResNetE(nn.Module):
                 MaxPool2d(3, 2, "same"),
                 BatchNorm(initial_filters, momentum=0.9, eps=1e-5),
             ]
-        self.stem = nn.Sequential(*stem)
+        self.stem = ImageStem(*stem)
         body = []
         cin = initial_filters
         for stage, (n, f) in enumerate(zip(blocks, filters)):

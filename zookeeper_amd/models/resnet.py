@@ -15,7 +15,8 @@ import torch.nn.functional as F
 
 from zookeeper_amd.core import Field, factory
 from zookeeper_amd.models.base import ModelFactory
-from zookeeper_amd.nn.layers import BatchNorm, GlobalAvgPool, MaxPool2d, QuantConv2d, glorot_normal_
+from zookeeper_amd.nn.layers import (BatchNorm, GlobalAvgPool, ImageStem, MaxPool2d, QuantConv2d,
+                                     glorot_normal_)
 
 
 class Bottleneck(nn.Module):
@@ -48,7 +49,7 @@ class ResNetModule(nn.Module):
     def __init__(self, input_shape, num_classes: int, blocks: Sequence[int] = (3, 4, 6, 3)):
         super().__init__()
         c = input_shape[2]
-        self.stem = nn.Sequential(
+        self.stem = ImageStem(
             QuantConv2d(c, 64, 7, 2, "same", kernel_initializer="he_normal"),
             BatchNorm(64, 0.9, 1e-5, activation="relu"),
             MaxPool2d(3, 2, "same"),

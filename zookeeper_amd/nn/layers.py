@@ -303,3 +303,43 @@ def apply_constraints(model: nn.Module) -> None:
         fn = getattr(m, "apply_constraints", None)
         if fn is not None and m is not model:
             fn()
+
+
+class ImageStem(nn.Sequential):
+    """``conv → BN(+ReLU) → MaxPool [→ BN]`` ImageNet stem as an
+    ``nn.Sequential`` (parameter names ``0.weight``, ``1.weight``, ...).
+
+    On bf16 GPU tensors the whole stem runs as the fused HIP pipeline of
+    :mod:`zookeeper_amd.ops.stem` (MFMA conv with BN statistics in its
+    epilogue, BN+ReLU+pool in one pass, sparse pool backward); otherwise
+    the modules run one after the other.
+    """
+
+    def _fusable(self, x: torch.Tensor) -> bool:
+        if not _use_native(x) or len(self) not in (3, 4):
+            return False
+        conv, bn1, pool = self[0], self[1], self[2]
+        bn2 = self[3] if len(self) == 4 else None
+        if not (isinstance(conv, QuantConv2d) and isinstance(bn1, BatchNorm)
+                and isinstance(pool, MaxPool2d) and bn1.activation == "relu"
+                and pool.padding == "same" and (bn2 is None or (isinstance(bn2, BatchNorm)
+                                                               and bn2.activation is None))):
+            return False
+        k, s = _pair(pool.pool_size), _pair(pool.stride)
+        if k[0] != k[1] or s[0] != s[1]:
+            return False
+        # the fused backward assumes batch statistics whenever it runs
+        if torch.is_grad_enabled() and not (bn1.training and (bn2 is None or bn2.training)):
+            return False
+        from zookeeper_amd.ops import stem
+
+        return stem.supported(x, conv, bn1, k[0], s[0])
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self._fusable(x):
+            from zookeeper_amd.ops.stem import fused_stem
+
+            pool = self[2]
+            return fused_stem(x, self[0], self[1], _pair(pool.pool_size)[0],
+                              _pair(pool.stride)[0], self[3] if len(self) == 4 else None)
+        return super().forward(x)

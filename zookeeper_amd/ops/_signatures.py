@@ -13,6 +13,7 @@ F32 = C.c_float
 
 U64 = C.c_uint64
 FP = C.POINTER(C.c_float)
+IP = C.POINTER(C.c_int)
 
 SIGNATURES = {
     # host runtime
@@ -46,6 +47,18 @@ SIGNATURES = {
     "zk_dw_fwd": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_dw_dgrad": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_dw_wgrad": (I32, [P, P, P] + [I32] * 10 + [P]),
+    # fused ImageNet stem
+    "zk_stem_pack_input": (I32, [P, P] + [I32] * 8 + [P]),
+    "zk_stem_pack_weight": (I32, [P, P] + [I32] * 4 + [P]),
+    "zk_stem_conv_fwd": (I32, [P, P, P, P] + [I32] * 11 + [IP, P]),
+    "zk_stem_max_parts": (I32, [I32, I32, I32]),
+    "zk_stem_max_pool_parts": (I32, []),
+    "zk_bn_finalize_partials": (I32, [P, I32, I32, C.c_double, P, P, F32, F32, P, P, P, P]),
+    "zk_reduce_partials": (I32, [P, I32, I32, P, P]),
+    "zk_stem_pool_fwd": (I32, [P, P, P, P, P] + [I32] * 10 + [IP, P]),
+    "zk_stem_pool_bwd_sums": (I32, [P, P, P, P, P] + [I32] * 10 + [IP, P]),
+    "zk_stem_dy1": (I32, [P, P, P, P, P, P] + [I32] * 10 + [P]),
+    "zk_stem_wgrad": (I32, [P, P, P] + [I32] * 11 + [P]),
     "zk_maxpool_fwd": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_maxpool_bwd": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_avgpool2_fwd": (I32, [P, P] + [I32] * 6 + [P]),

@@ -1,0 +1,210 @@
+"""Fused ImageNet stem (``csrc/kernels/stem.hip``):
+conv KxK/2 (3 input channels) → BN → ReLU → max-pool 3×3/2 [→ BN].
+
+BinaryResNet-E18 (and ResNet-50 without the trailing BN) spend a fifth of
+a training step here when the stem runs as library conv + separate
+BN / ReLU / pool passes over the 112×112×64 activation.  The fused version:
+
+forward   pack (zero-padded 4-channel image, bf16 [KH][Cout][32] kernel) →
+          MFMA conv with BN-1 partial sums in the epilogue → BN-1 finalize →
+          BN-1 + ReLU + max-pool (+ argmax tap, BN-2 partial sums) in one
+          pass → BN-2 finalize → BN-2 apply;
+backward  BN-2 backward (bf16 kernels of ``norm_pool``) → BN-1 sums from
+          the pooled side (sparse) → dense dy1 in one pass → MFMA weight
+          gradient straight into the flat gradient buffer.
+
+The image itself never needs a gradient; the op is only used when it does
+not (``x.requires_grad`` is False).
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from zookeeper_amd.nn.layers import same_padding
+from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
+
+
+def supported(x: torch.Tensor, conv, bn1, pool_k: int, pool_s: int) -> bool:
+    Cout, Cin, KH, KW = conv.weight.shape
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and not x.requires_grad
+            and Cin <= 4 and Cout == 64 and KH <= 8 and KW <= 8 and conv.stride == (2, 2)
+            and conv.padding == "same" and conv.bias is None and conv.groups == 1
+            and conv.input_quantizer is None and conv.kernel_quantizer is None
+            and pool_k * pool_k <= 255)
+
+
+def _bn_eval_coef(bn, C, dev):
+    rstd = torch.rsqrt(bn.running_var + bn.eps)
+    g = bn.weight if bn.weight is not None else torch.ones_like(rstd)
+    b = bn.bias if bn.bias is not None else torch.zeros_like(rstd)
+    coef = torch.empty((4, C), dtype=torch.float32, device=dev)
+    coef[0] = g * rstd
+    coef[1] = b - bn.running_mean * coef[0]
+    coef[2] = bn.running_mean
+    coef[3] = rstd
+    return coef
+
+
+def _bn_bwd_coef(L, st, sums, coef, gamma_p, beta_p, P, C, dev):
+    """BN backward coefficients [k1, k0, k3]; γ/β gradients go into the flat
+    buffer when the trainer manages it, else are returned."""
+    dg = direct_grad(gamma_p) if gamma_p is not None else None
+    db = direct_grad(beta_p) if beta_p is not None else None
+    dgamma = dg if dg is not None else (torch.zeros(C, device=dev) if gamma_p is not None else None)
+    dbeta = db if db is not None else (torch.zeros(C, device=dev) if beta_p is not None else None)
+    bcoef = torch.empty((3, C), dtype=torch.float32, device=dev)
+    check(L.zk_bn_bwd_coef(sums.data_ptr(), coef[2].data_ptr(), coef[3].data_ptr(),
+                           gamma_p.data_ptr() if gamma_p is not None else None, float(P), C,
+                           bcoef.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
+                           dbeta.data_ptr() if dbeta is not None else None, st), "zk_bn_bwd_coef")
+    if dg is not None:
+        grad_ready(gamma_p)
+        dgamma = None
+    if db is not None:
+        grad_ready(beta_p)
+        dbeta = None
+    return bcoef, dgamma, dbeta
+
+
+class _StemFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, g1, b1, g2, b2, bn1, bn2, pool):
+        pk, ps = pool
+        B, Cin, H, W = x.shape
+        Cout, _, KH, KW = weight.shape
+        s = 2
+        pt, pb = same_padding(H, KH, s)
+        pl, pr = same_padding(W, KW, s)
+        Ho, Wo = (H + pt + pb - KH) // s + 1, (W + pl + pr - KW) // s + 1
+        Hp = (Ho - 1) * s + KH
+        Wp = (Wo - 1) * s + 8
+        Wp += Wp % 2
+        dev = x.device
+        st = stream_ptr(dev)
+        L = lib()
+
+        xn = x.permute(0, 2, 3, 1).contiguous()
+        xp = torch.empty((B, Hp, Wp, 4), dtype=torch.bfloat16, device=dev)
+        check(L.zk_stem_pack_input(xn.data_ptr(), xp.data_ptr(), B, H, W, Cin, Hp, Wp, pt, pl,
+                                   st), "zk_stem_pack_input")
+        w_ohwi = weight.detach().permute(0, 2, 3, 1).contiguous()
+        ws = torch.empty((KH, Cout, 32), dtype=torch.bfloat16, device=dev)
+        check(L.zk_stem_pack_weight(w_ohwi.data_ptr(), ws.data_ptr(), Cout, KH, KW, Cin, st),
+              "zk_stem_pack_weight")
+        y1 = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=dev)
+        part = torch.empty((L.zk_stem_max_parts(B, Ho, Wo), 2, Cout), dtype=torch.float32,
+                           device=dev)
+        nb = ctypes.c_int(0)  # number of partial-sum rows, written by the launcher
+        check(L.zk_stem_conv_fwd(xp.data_ptr(), ws.data_ptr(), y1.data_ptr(), part.data_ptr(), B,
+                                 Cin, Cout, KH, KW, s, Ho, Wo, Hp, Wp, -1, ctypes.byref(nb), st),
+              "zk_stem_conv_fwd")
+        P1 = B * Ho * Wo
+        if bn1.training:
+            coef1 = torch.empty((4, Cout), dtype=torch.float32, device=dev)
+            check(L.zk_bn_finalize_partials(part.data_ptr(), nb.value, Cout, float(P1),
+                                            g1.data_ptr() if g1 is not None else None,
+                                            b1.data_ptr() if b1 is not None else None, bn1.eps,
+                                            bn1.momentum, bn1.running_mean.data_ptr(),
+                                            bn1.running_var.data_ptr(), coef1.data_ptr(), st),
+                  "zk_bn_finalize_partials")
+        else:
+            coef1 = _bn_eval_coef(bn1, Cout, dev)
+
+        pt2, pb2 = same_padding(Ho, pk, ps)
+        pl2, pr2 = same_padding(Wo, pk, ps)
+        H2, W2 = (Ho + pt2 + pb2 - pk) // ps + 1, (Wo + pl2 + pr2 - pk) // ps + 1
+        p = torch.empty((B, H2, W2, Cout), dtype=torch.bfloat16, device=dev)
+        arg = torch.empty((B, H2, W2, Cout), dtype=torch.uint8, device=dev)
+        want_part2 = bn2 is not None and bn2.training
+        part2 = torch.empty((L.zk_stem_max_pool_parts(), 2, Cout), dtype=torch.float32,
+                            device=dev) if want_part2 else None
+        nb2 = ctypes.c_int(0)
+        check(L.zk_stem_pool_fwd(y1.data_ptr(), coef1.data_ptr(), p.data_ptr(), arg.data_ptr(),
+                                 part2.data_ptr() if part2 is not None else None, B, Ho, Wo, Cout,
+                                 H2, W2, pk, ps, pt2, pl2, ctypes.byref(nb2), st),
+              "zk_stem_pool_fwd")
+        P2 = B * H2 * W2
+        coef2 = None
+        out = p
+        if bn2 is not None:
+            if bn2.training:
+                coef2 = torch.empty((4, Cout), dtype=torch.float32, device=dev)
+                check(L.zk_bn_finalize_partials(part2.data_ptr(), nb2.value, Cout, float(P2),
+                                                g2.data_ptr() if g2 is not None else None,
+                                                b2.data_ptr() if b2 is not None else None,
+                                                bn2.eps, bn2.momentum,
+                                                bn2.running_mean.data_ptr(),
+                                                bn2.running_var.data_ptr(), coef2.data_ptr(), st),
+                      "zk_bn_finalize_partials")
+            else:
+                coef2 = _bn_eval_coef(bn2, Cout, dev)
+            out = torch.empty_like(p)
+            check(L.zk_bn_apply_bf16(p.data_ptr(), coef2.data_ptr(), out.data_ptr(), P2, Cout, 0,
+                                     st), "zk_bn_apply_bf16")
+        ctx.save_for_backward(xp, y1, arg, p, coef1, coef2, g1, g2)
+        ctx.params = (weight, g1, b1, g2, b2)
+        ctx.geom = (B, Cin, Cout, KH, KW, s, Ho, Wo, Hp, Wp, H2, W2, pk, ps, pt2, pl2)
+        ctx.has_bn2 = bn2 is not None
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dout):
+        xp, y1, arg, p, coef1, coef2, g1, g2 = ctx.saved_tensors
+        weight, g1p, b1p, g2p, b2p = ctx.params
+        (B, Cin, Cout, KH, KW, s, Ho, Wo, Hp, Wp, H2, W2, pk, ps, pt2, pl2) = ctx.geom
+        dev = dout.device
+        st = stream_ptr(dev)
+        L = lib()
+        P2 = B * H2 * W2
+        g = dout.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+        dg2 = db2 = None
+        if ctx.has_bn2:
+            sums2 = torch.zeros((2, Cout), dtype=torch.float32, device=dev)
+            check(L.zk_bn_bwd_reduce_bf16(g.data_ptr(), p.data_ptr(), None, coef2.data_ptr(),
+                                          sums2.data_ptr(), P2, Cout, st), "zk_bn_bwd_reduce_bf16")
+            bcoef2, dg2, db2 = _bn_bwd_coef(L, st, sums2, coef2, g2p, b2p, P2, Cout, dev)
+            dp = torch.empty_like(g)
+            check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), p.data_ptr(), None, bcoef2.data_ptr(),
+                                      dp.data_ptr(), P2, Cout, st), "zk_bn_bwd_dx_bf16")
+        else:
+            dp = g
+        part = torch.empty((L.zk_stem_max_pool_parts(), 2, Cout), dtype=torch.float32,
+                           device=dev)
+        nb = ctypes.c_int(0)
+        check(L.zk_stem_pool_bwd_sums(dp.data_ptr(), arg.data_ptr(), y1.data_ptr(),
+                                      coef1.data_ptr(), part.data_ptr(), B, Ho, Wo, Cout, H2, W2,
+                                      pk, ps, pt2, pl2, ctypes.byref(nb), st),
+              "zk_stem_pool_bwd_sums")
+        sums1 = torch.empty((2, Cout), dtype=torch.float32, device=dev)
+        check(L.zk_reduce_partials(part.data_ptr(), nb.value, 2 * Cout, sums1.data_ptr(), st),
+              "zk_reduce_partials")
+        P1 = B * Ho * Wo
+        bcoef1, dg1, db1 = _bn_bwd_coef(L, st, sums1, coef1, g1p, b1p, P1, Cout, dev)
+        dy1 = torch.empty_like(y1)
+        check(L.zk_stem_dy1(dp.data_ptr(), arg.data_ptr(), y1.data_ptr(), coef1.data_ptr(),
+                            bcoef1.data_ptr(), dy1.data_ptr(), B, Ho, Wo, Cout, H2, W2, pk, ps,
+                            pt2, pl2, st), "zk_stem_dy1")
+        dweight = None
+        if ctx.needs_input_grad[1]:
+            target = direct_grad(weight, channels_last=True)
+            if target is not None:
+                dw = target.permute(0, 2, 3, 1)  # OHWI view of the flat gradient
+            else:
+                dw = torch.zeros((Cout, KH, KW, Cin), dtype=torch.float32, device=dev)
+            check(L.zk_stem_wgrad(dy1.data_ptr(), xp.data_ptr(), dw.data_ptr(), B, Cin, Cout, KH,
+                                  KW, s, Ho, Wo, Hp, Wp, 0, st), "zk_stem_wgrad")
+            if target is not None:
+                grad_ready(weight)
+            else:
+                dweight = dw.permute(0, 3, 1, 2)
+        return None, dweight, dg1, db1, dg2, db2, None, None, None
+
+
+def fused_stem(x: torch.Tensor, conv, bn1, pool_k: int = 3, pool_s: int = 2, bn2=None):
+    """``bn2(maxpool(relu(bn1(conv(x)))))`` with the fused stem kernels."""
+    return _StemFn.apply(x, conv.weight, bn1.weight, bn1.bias,
+                         bn2.weight if bn2 is not None else None,
+                         bn2.bias if bn2 is not None else None, bn1, bn2, (pool_k, pool_s))
