@@ -109,30 +109,45 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
   const int kchunks = RB / CB;
   const int NK = T * kchunks;
 
-  // ---- per-lane loader rows (A: pixels)
+  // ---- per-lane loader rows (A: pixels).  Every tap of a row is the row's
+  // tap-0 source plus a uniform offset (fwd: +(ih*W + iw) pixels, dgrad:
+  // -(ih*Wo + iw) pixels), valid iff bit ih of a_hm and bit iw of a_wm are
+  // set: the per-tap address work is a shift, an and and a select.
   const int lrow = lane / SPR, lslot = lane % SPR;
-  int a_b[A_INS], a_h[A_INS], a_w[A_INS];
-  int a_sw[A_INS];
+  const unsigned char* actb = reinterpret_cast<const unsigned char*>(args.act);
+  const unsigned char* wtb = reinterpret_cast<const unsigned char*>(args.wgt);
+  const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
+  const unsigned char* padp =
+      (FWD && args.pad_ones) ? reinterpret_cast<const unsigned char*>(g_ones_page_bf16) : zp;
+  const unsigned char* a_base[A_INS];  // tap-0 source (may point outside: masked)
+  const unsigned char* a_pad[A_INS];   // padding page (+ swizzled slot)
+  uint32_t a_hm[A_INS], a_wm[A_INS];
 #pragma unroll
   for (int j = 0; j < A_INS; ++j) {
     const int r = (j * NWAVES + wave) * RPI + lrow;
-    a_sw[j] = lslot ^ ((r >> SH) & (SPR - 1));
+    const int sw = lslot ^ ((r >> SH) & (SPR - 1));
     const long long m = m0 + r;
+    a_hm[j] = a_wm[j] = 0;
+    a_base[j] = zp;
+    a_pad[j] = zp + sw * 16;  // tail rows: zeros
     if (m < M) {
       const int jw = (int)(m % Wc);
       const long long rr = m / Wc;
       const int jh = (int)(rr % Hc);
-      a_b[j] = (int)(rr / Hc);
+      const int b = (int)(rr / Hc);
+      a_pad[j] = padp + sw * 16;
       if (FWD) {
-        a_h[j] = jh * s - g.pt;
-        a_w[j] = jw * s - g.pl;
+        const int h0 = jh * s - g.pt + th0, w0 = jw * s - g.pl + tw0;
+        for (int i = 0; i < nth; ++i) a_hm[j] |= (uint32_t)(h0 + i >= 0 && h0 + i < g.H) << i;
+        for (int i = 0; i < ntw; ++i) a_wm[j] |= (uint32_t)(w0 + i >= 0 && w0 + i < g.W) << i;
+        a_base[j] = actb + (((long long)b * g.H + h0) * g.W + w0) * RB + sw * 16;
       } else {
-        a_h[j] = jh * s + ph + g.pt;
-        a_w[j] = jw * s + pw + g.pl;
+        // tap index i: ho = (jh*s + ph + pt - th0)/s - i
+        const int ho0 = (jh * s + ph + g.pt - th0) / s, wo0 = (jw * s + pw + g.pl - tw0) / s;
+        for (int i = 0; i < nth; ++i) a_hm[j] |= (uint32_t)(ho0 - i >= 0 && ho0 - i < g.Ho) << i;
+        for (int i = 0; i < ntw; ++i) a_wm[j] |= (uint32_t)(wo0 - i >= 0 && wo0 - i < g.Wo) << i;
+        a_base[j] = actb + (((long long)b * g.Ho + ho0) * g.Wo + wo0) * RB + sw * 16;
       }
-    } else {
-      a_b[j] = -1;
-      a_h[j] = a_w[j] = 0;
     }
   }
   int b_sw[B_INS];
@@ -141,37 +156,21 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
     const int r = (j * NWAVES + wave) * RPI + lrow;
     b_sw[j] = lslot ^ ((r >> SH) & (SPR - 1));
   }
-  const unsigned char* actb = reinterpret_cast<const unsigned char*>(args.act);
-  const unsigned char* wtb = reinterpret_cast<const unsigned char*>(args.wgt);
-  const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
-  const unsigned char* padp =
-      (FWD && args.pad_ones) ? reinterpret_cast<const unsigned char*>(g_ones_page_bf16) : zp;
 
   // Source pointers of the current tap (recomputed when the tap changes).
   const unsigned char* a_src[A_INS];
   int a_step[A_INS];  // CB for a real row, 0 for a padding page
   const unsigned char* b_src[B_INS];
   auto set_tap = [&](int ti) {
-    const int th = th0 + (ti / ntw) * ts, tw = tw0 + (ti % ntw) * ts;
+    const int ih = ti / ntw, iw = ti % ntw;
+    const int th = th0 + ih * ts, tw = tw0 + iw * ts;
     const int t = th * g.kw + tw;
+    const long long off =
+        (FWD ? ((long long)ih * g.W + iw) : -((long long)ih * g.Wo + iw)) * RB;
 #pragma unroll
     for (int j = 0; j < A_INS; ++j) {
-      long long pix;
-      bool ok;
-      if (FWD) {
-        const int hi = a_h[j] + th, wi = a_w[j] + tw;
-        ok = hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
-        pix = ((long long)a_b[j] * g.H + hi) * g.W + wi;
-      } else {
-        const int hn = a_h[j] - th, wn_ = a_w[j] - tw;  // divisible by s
-        const int ho = (s == 1) ? hn : (hn >> 1);
-        const int wo = (s == 1) ? wn_ : (wn_ >> 1);
-        ok = hn >= 0 && wn_ >= 0 && ho < g.Ho && wo < g.Wo;
-        pix = ((long long)a_b[j] * g.Ho + ho) * g.Wo + wo;
-      }
-      const unsigned char* pad = a_b[j] >= 0 ? padp : zp;  // tail rows: zeros
-      ok = ok && a_b[j] >= 0;
-      a_src[j] = ok ? actb + pix * RB + a_sw[j] * 16 : pad + a_sw[j] * 16;
+      const bool ok = (a_hm[j] >> ih) & (a_wm[j] >> iw) & 1u;
+      a_src[j] = ok ? a_base[j] + off : a_pad[j];
       a_step[j] = ok ? CB : 0;
     }
 #pragma unroll
@@ -250,60 +249,52 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < TN; ++b) acc[a][b] = mfma_bf16(bfr[b], af[a], acc[a][b]);
+        for (int b = 0; b < TN; ++b)
+          // fwd: D[pixel][co] (lane = channel: in-lane BN statistics);
+          // dgrad: D[ci][pixel] (lane = pixel: 8-B mask/residual epilogue)
+          acc[a][b] = FWD ? mfma_bf16(af[a], bfr[b], acc[a][b])
+                          : mfma_bf16(bfr[b], af[a], acc[a][b]);
     }
   }
 
   if constexpr (FWD) {
-    // ---- forward epilogue: lane = output pixel; exact integer results
+    // ---- forward epilogue: lane = output channel, registers = pixels;
+    // the fp32 accumulators hold exact integers (|v| <= K)
     int16_t* y = reinterpret_cast<int16_t*>(args.out);
-    int csum[TN][16], csq[TN][16];
+    int csum[TN], csq[TN];
 #pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) csum[b][r] = csq[b][r] = 0;
+    for (int b = 0; b < TN; ++b) csum[b] = csq[b] = 0;
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
-      const long long mc = m0 + wm * WTM + a * 32 + r32;
-      const bool live = mc < M;
 #pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int nb = n0 + wn * WTN + b * 32;
+      for (int r = 0; r < 16; ++r) {
+        const long long mc = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const bool live = mc < M;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          int v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            int t = (int)acc[a][b][4 * q + e];  // exact: |t| <= K
-            if (args.relu) t = t > 0 ? t : 0;
-            if (!live) t = 0;
-            v[e] = t;
-            csum[b][4 * q + e] += t;
-            csq[b][4 * q + e] += t * t;
-          }
-          if (live)
-            *reinterpret_cast<uint2*>(y + mc * g.Cout + nb + 8 * q + 4 * h) =
-                make_uint2((uint32_t)(uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16),
-                           (uint32_t)(uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16));
+        for (int b = 0; b < TN; ++b) {
+          int t = (int)acc[a][b][r];
+          if (args.relu) t = t > 0 ? t : 0;
+          if (!live) t = 0;
+          csum[b] += t;
+          csq[b] += t * t;  // < 2^32 as unsigned for TM <= 4, K <= 4608
+          if (live) y[mc * g.Cout + n0 + wn * WTN + b * 32 + r32] = (int16_t)t;
         }
       }
     }
-    // statistics: reduce over the wave's 32 pixels per half, then over the
-    // WM waves sharing these channels (LDS), one int64 atomic per channel.
+    // statistics: the two wave halves hold the same channels, then the WM
+    // waves sharing these channels combine in LDS; one int64 atomic each.
     __builtin_amdgcn_s_barrier();  // all waves are done with the ring
     int* red = reinterpret_cast<int*>(smem);  // [WM][2][BN]
 #pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int s1 = half_sum(csum[b][r]);
-        const int s2 = half_sum(csq[b][r]);
-        if (r32 == 0) {
-          const int nl = wn * WTN + b * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          red[(wm * 2 + 0) * BN + nl] = s1;
-          red[(wm * 2 + 1) * BN + nl] = s2;
-        }
+    for (int b = 0; b < TN; ++b) {
+      const int s1 = csum[b] + __shfl_xor(csum[b], 32, 64);
+      const int s2 = csq[b] + __shfl_xor(csq[b], 32, 64);
+      if (h == 0) {
+        const int nl = wn * WTN + b * 32 + r32;
+        red[(wm * 2 + 0) * BN + nl] = s1;
+        red[(wm * 2 + 1) * BN + nl] = s2;
       }
+    }
     __syncthreads();
     for (int c = tid; c < 2 * BN; c += NWAVES * 64) {
       const int which = c / BN, nl = c % BN;
