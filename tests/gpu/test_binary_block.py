@@ -134,3 +134,36 @@ def test_bconv_forward_exact_integers():
         assert torch.equal(y.double(), ref), (cin, cout, stride, hw, pad_ones)
         assert torch.equal(stats[0].double(), ref.sum(dim=(0, 1, 2)))
         assert torch.equal(stats[1].double(), (ref * ref).sum(dim=(0, 1, 2)))
+
+
+def test_chained_blocks_reuse_fused_quantisation():
+    """Block 1's BN epilogue quantises its output for block 2 (sign image +
+    STE mask, ``_zk_sign``); the chain must match recomputing them."""
+    _setup()
+    from zookeeper_amd import ops
+
+    torch.manual_seed(5)
+    b1 = BinaryResBlock(64, 64, 1).cuda().to(memory_format=torch.channels_last)
+    b2 = BinaryResBlock(64, 128, 2).cuda().to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        for b in (b1, b2):
+            b.bn.weight.uniform_(0.5, 1.5)
+            b.bn.bias.uniform_(-0.5, 0.5)
+    x = (torch.randn(4, 64, 14, 14, device="cuda") * 1.5).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    g = torch.randn(4, 128, 7, 7, device="cuda").to(torch.bfloat16)
+    results = []
+    for fused in (True, False):
+        c1, c2 = copy.deepcopy(b1), copy.deepcopy(b2)
+        xx = x.clone().requires_grad_(True)
+        h = ops.binary_block(xx, xx, c1.conv, c1.bn, quantize_output=fused)
+        assert hasattr(h, "_zk_sign") == fused
+        res = c2.downsample(h) if c2.downsample is not None else h
+        out = ops.binary_block(h, res, c2.conv, c2.bn)
+        out.backward(g)
+        results.append((out.float(), xx.grad.float(), c1.conv.weight.grad.clone(),
+                        c2.conv.weight.grad.clone()))
+    (o1, *g1), (o2, *g2) = results
+    torch.testing.assert_close(o1, o2, atol=0, rtol=0)  # forward is deterministic
+    for a, b in zip(g1, g2):  # fp32 atomics in the reductions: order-dependent
+        assert ((a - b).norm() / b.norm()).item() < 1e-3

@@ -53,7 +53,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const int16_t* __restrict
                                                        const float* __restrict__ shift,
                                                        const uint16_t* __restrict__ res,
                                                        uint16_t* __restrict__ out,
-                                                       long long P) {
+                                                       long long P,
+                                                       uint16_t* __restrict__ sx = nullptr,
+                                                       uint8_t* __restrict__ smask = nullptr,
+                                                       float clip = 1.f) {
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;
   const int cg = threadIdx.x % CG;
@@ -80,9 +83,26 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const int16_t* __restrict
         o[2 * k + 1] += zk::bf16_to_f32((uint16_t)(rr[k] >> 16));
       }
     }
-    reinterpret_cast<uint4*>(out)[i] =
-        make_uint4(zk::pack_bf16x2(o[0], o[1]), zk::pack_bf16x2(o[2], o[3]),
-                   zk::pack_bf16x2(o[4], o[5]), zk::pack_bf16x2(o[6], o[7]));
+    const uint4 ov = make_uint4(zk::pack_bf16x2(o[0], o[1]), zk::pack_bf16x2(o[2], o[3]),
+                                zk::pack_bf16x2(o[4], o[5]), zk::pack_bf16x2(o[6], o[7]));
+    reinterpret_cast<uint4*>(out)[i] = ov;
+    if (sx) {
+      // the NEXT binary block's input quantisation, from the stored bf16
+      // values: sign image (bf16 +-1) and STE mask bits (|x| <= clip)
+      const uint32_t ow[4] = {ov.x, ov.y, ov.z, ov.w};
+      uint32_t sw[4];
+      uint32_t mk = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float lo = zk::bf16_to_f32((uint16_t)(ow[k] & 0xffff));
+        const float hi = zk::bf16_to_f32((uint16_t)(ow[k] >> 16));
+        sw[k] = (lo >= 0.f ? 0x3F80u : 0xBF80u) | ((hi >= 0.f ? 0x3F80u : 0xBF80u) << 16);
+        mk |= (uint32_t)(fabsf(lo) <= clip) << (2 * k);
+        mk |= (uint32_t)(fabsf(hi) <= clip) << (2 * k + 1);
+      }
+      reinterpret_cast<uint4*>(sx)[i] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+      smask[i] = (uint8_t)mk;  // byte i = channels 8i..8i+7 of the packed mask words
+    }
   }
 }
 
@@ -281,6 +301,25 @@ ZK_EXPORT int zk_bn_apply(const void* y, const void* scale, const void* shift, c
     hipLaunchKernelGGL(bn_apply_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, stream,    \
                        (const int16_t*)y, (const float*)scale, (const float*)shift,         \
                        (const uint16_t*)res, (uint16_t*)out, P);                            \
+    break;
+  ZK_CG_SWITCH(C, ZK_APPLY_CASE)
+#undef ZK_APPLY_CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// zk_bn_apply + the next binary layer's input quantisation (sign image sx
+// bf16 +-1 and STE mask bits |out| <= clip, packed like zk_sign_pack's).
+ZK_EXPORT int zk_bn_apply_sign(const void* y, const void* scale, const void* shift,
+                               const void* res, void* out, void* sx, void* mask, float clip,
+                               long long P, int C, hipStream_t stream) {
+  if (C % 32) return (int)hipErrorInvalidValue;
+#define ZK_APPLY_CASE(cg)                                                                   \
+  case cg:                                                                                  \
+    hipLaunchKernelGGL(bn_apply_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, stream,    \
+                       (const int16_t*)y, (const float*)scale, (const float*)shift,         \
+                       (const uint16_t*)res, (uint16_t*)out, P, (uint16_t*)sx,              \
+                       (uint8_t*)mask, clip);                                               \
     break;
   ZK_CG_SWITCH(C, ZK_APPLY_CASE)
 #undef ZK_APPLY_CASE

@@ -43,7 +43,7 @@ def _nhwc(t: torch.Tensor) -> torch.Tensor:
 class _BinaryBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, gamma, beta, bn, meta):
-        (stride, act_relu, clip, pad_ones, identity, will_backward) = meta
+        (stride, act_relu, clip, pad_ones, identity, will_backward, next_sign) = meta
         B, Cin, H, W = x.shape
         Cout, _, kh, kw = weight.shape
         T = kh * kw
@@ -60,12 +60,19 @@ class _BinaryBlockFn(torch.autograd.Function):
         # forward and both gradients run as bf16 ±1 implicit GEMMs on the
         # sign image sx; otherwise the XNOR-popcount forward on packed bits.
         mfma = Cout % 64 == 0 and Cin % 64 == 0 and stride <= 2 and kh <= 4 and kw <= 4
-        bits = None if mfma else torch.empty(nwords, dtype=torch.int32, device=dev)
-        mask = torch.empty(nwords, dtype=torch.int32, device=dev)
-        sx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev) if mfma else None
-        check(L.zk_sign_pack(xn.data_ptr(), bits.data_ptr() if bits is not None else None,
-                             mask.data_ptr(), sx.data_ptr() if sx is not None else None, nwords,
-                             clip, st), "zk_sign_pack")
+        # The previous block may already have quantised this input in its BN
+        # epilogue (zk_bn_apply_sign): reuse its sign image and STE mask.
+        cached = getattr(x, "_zk_sign", None)
+        if (mfma and cached is not None and cached[0] == clip
+                and tuple(cached[1].shape) == (B, H, W, Cin)):
+            bits, sx, mask = None, cached[1], cached[2]
+        else:
+            bits = None if mfma else torch.empty(nwords, dtype=torch.int32, device=dev)
+            mask = torch.empty(nwords, dtype=torch.int32, device=dev)
+            sx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev) if mfma else None
+            check(L.zk_sign_pack(xn.data_ptr(), bits.data_ptr() if bits is not None else None,
+                                 mask.data_ptr(), sx.data_ptr() if sx is not None else None,
+                                 nwords, clip, st), "zk_sign_pack")
 
         w_ohwi = weight.permute(0, 2, 3, 1).contiguous()  # no copy for channels_last
         wbits = None if mfma else torch.empty(Cout * T * Cin // 32, dtype=torch.int32, device=dev)
@@ -115,9 +122,19 @@ class _BinaryBlockFn(torch.autograd.Function):
 
         res = xn if identity else (_nhwc(residual) if residual is not None else None)
         out = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=dev)
-        check(L.zk_bn_apply(y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
-                            res.data_ptr() if res is not None else None, out.data_ptr(), P,
-                            Cout, st), "zk_bn_apply")
+        if next_sign is not None and Cout % 64 == 0:
+            # also quantise the output for the next binary block (same clip)
+            sx_next = torch.empty_like(out)
+            mask_next = torch.empty(P * Cout // 32, dtype=torch.int32, device=dev)
+            check(L.zk_bn_apply_sign(y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                                     res.data_ptr() if res is not None else None,
+                                     out.data_ptr(), sx_next.data_ptr(), mask_next.data_ptr(),
+                                     clip, P, Cout, st), "zk_bn_apply_sign")
+            next_sign[:] = [clip, sx_next, mask_next]
+        else:
+            check(L.zk_bn_apply(y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                                res.data_ptr() if res is not None else None, out.data_ptr(), P,
+                                Cout, st), "zk_bn_apply")
 
         ctx.save_for_backward(bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx)
         ctx.params = (weight, gamma, beta)
@@ -131,7 +148,7 @@ class _BinaryBlockFn(torch.autograd.Function):
     def backward(ctx, dout):
         bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx = ctx.saved_tensors
         (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
-        (_, act_relu, clip, pad_ones, identity, _) = ctx.meta
+        (_, act_relu, clip, pad_ones, identity, _, _) = ctx.meta
         dev = dout.device
         st = stream_ptr(dev)
         L = lib()
@@ -208,7 +225,7 @@ def _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx):
     not a multiple of 64): bf16 library convolution backward on unpacked ±1
     operands, then the fused STE/residual kernel."""
     (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
-    (_, _, clip, pad_ones, identity, _) = ctx.meta
+    (_, _, clip, pad_ones, identity, _, _) = ctx.meta
     dev = dy.device
     st = stream_ptr(dev)
     L = lib()
@@ -245,13 +262,18 @@ def _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx):
 
 def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
                  act: Optional[str] = None, clip_value: float = 1.0,
-                 pad_value: float = 0.0) -> torch.Tensor:
+                 pad_value: float = 0.0, quantize_output: bool = True) -> torch.Tensor:
     """Run ``bn(act(conv(x))) + residual`` with the fused HIP kernels.
 
     ``conv`` must be a binary ``QuantConv2d`` (ste_sign input and kernel,
     ``same`` padding), ``bn`` a :class:`~zookeeper_amd.nn.BatchNorm`.
     ``residual`` may be ``x`` itself (identity shortcut, fused into the
     backward) or a separately computed tensor, or ``None``.
+
+    With ``quantize_output`` the BN epilogue also writes the sign image and
+    STE mask of the output for the next binary block (attached to the
+    returned tensor as ``_zk_sign``; a block with the same clip value reuses
+    them instead of re-reading its input).
     """
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)
@@ -264,7 +286,12 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
         residual = residual.to(torch.bfloat16)
     will_backward = torch.is_grad_enabled() and (
         x.requires_grad or conv.weight.requires_grad or bn.training)
+    holder: list = [] if quantize_output else None
     meta = (conv.stride[0], act == "relu", float(clip_value), pad_value == 1.0, identity,
-            will_backward)
-    return _BinaryBlockFn.apply(x, None if identity else residual, conv.weight, bn.weight,
-                                bn.bias, bn, meta)
+            will_backward, holder)
+    out = _BinaryBlockFn.apply(x, None if identity else residual, conv.weight, bn.weight,
+                               bn.bias, bn, meta)
+    if holder:
+        # consumed by the next binary block (same clip) instead of re-reading out
+        out._zk_sign = tuple(holder)
+    return out
