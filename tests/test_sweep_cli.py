@@ -97,3 +97,20 @@ def test_training_checkpoint_and_resume(tmp_path):
     assert res.returncode == 0, res.stderr[-2000:]
     assert "resumed from" in res.stdout
     assert (run_dir / "checkpoints" / "step_00000004").exists()
+
+
+@pytest.mark.timeout(900)
+def test_cifar10_binarynet_task_runs_on_cpu(tmp_path):
+    """BASELINE.json config 4: the CIFAR-10 BinaryNet @task end to end on the
+    CPU (world_size 1): trains, validates, checkpoints, logs metrics."""
+    cmd = [sys.executable, os.path.join(ROOT, "examples", "larq_experiment.py"), "BinaryNetCifar10",
+           "epochs=1", "batch_size=8", "steps_per_epoch=3", "print_summary=False",
+           f"output_dir={str(tmp_path)!r}", "model.filters=32", "model.dense_units=64",
+           "dataset.num_train_examples=64", "dataset.num_validation_examples=16"]
+    res = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=800)
+    assert res.returncode == 0, res.stderr[-2000:]
+    run_dir = tmp_path / "BinaryNetCifar10" / "run"
+    lines = open(run_dir / "metrics.jsonl").read().strip().splitlines()
+    recs = [json.loads(line) for line in lines]
+    assert any(r.get("step") == 3 for r in recs)
+    assert (run_dir / "checkpoints" / "step_00000003" / "model.pt").exists()

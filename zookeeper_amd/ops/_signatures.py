@@ -48,6 +48,9 @@ SIGNATURES = {
     "zk_dw_fwd": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_dw_dgrad": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_dw_wgrad": (I32, [P, P, P] + [I32] * 10 + [P]),
+    # softmax cross-entropy
+    "zk_xent_fwd": (I32, [P, P, P, P, P, I32, I32, F32, P]),
+    "zk_xent_bwd": (I32, [P, P, P, P, P, I32, I32, F32, P]),
     # fused ImageNet stem
     "zk_stem_pack_input": (I32, [P, P] + [I32] * 8 + [P]),
     "zk_stem_pack_weight": (I32, [P, P] + [I32] * 4 + [P]),
