@@ -117,13 +117,16 @@ def test_igemm_dgrad_matches_reference(variant, cin, cout, stride, hw):
     assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err
 
 
+@pytest.mark.parametrize("slab", [False, True])
 @pytest.mark.parametrize("variant", list(range(8)))
 @pytest.mark.parametrize("cin,cout,stride,hw,pad_ones", [
     (64, 64, 1, 12, 0), (64, 128, 2, 12, 0), (128, 128, 1, 7, 1), (256, 512, 2, 8, 0),
     (128, 64, 1, 9, 1), (64, 192, 1, 5, 1)])
-def test_igemm_wgrad_matches_reference(variant, cin, cout, stride, hw, pad_ones):
+def test_igemm_wgrad_matches_reference(variant, cin, cout, stride, hw, pad_ones, slab):
     """LDS-DMA ring implicit-GEMM wgrad (igemm.hip) on the bf16 sign(x)
-    image, every tile variant, vs the fp64 ±1 conv weight gradient."""
+    image, every tile variant, split-K by fp32 atomics or by workspace slabs
+    + reduce kernel, accumulating into dw, vs the fp64 ±1 conv weight
+    gradient."""
     from zookeeper_amd.nn.layers import pad_same_nhwc, same_padding
     from zookeeper_amd.nn.quantizers import sign_pm1
     from zookeeper_amd.ops._native import lib, stream_ptr
@@ -141,18 +144,25 @@ def test_igemm_wgrad_matches_reference(variant, cin, cout, stride, hw, pad_ones)
     sx = torch.empty_like(x)
     assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), None, sx.data_ptr(), nwords, 1.0,
                           st) == 0
-    dw = torch.zeros(cout, 3, 3, cin, device="cuda")
+    dw = torch.full((cout, 3, 3, cin), 0.25, device="cuda")  # accumulates into dw
+    ws = None
+    if slab:
+        nbytes = L.zk_igemm_wgrad_ws_bytes(B, cin, ho, ho, cout, 3, 3, stride, 256, variant)
+        if nbytes <= 0:
+            pytest.skip("tile does not divide this shape")
+        ws = torch.empty(nbytes // 4, device="cuda")
     rc = L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w.data_ptr(), dw.data_ptr(), B, hw, hw,
                           cin, ho, ho, cout, 3, 3, stride, pt, pt, pad_ones, 1.0, 256, variant,
-                          st)
+                          ws.data_ptr() if ws is not None else None,
+                          ws.numel() * 4 if ws is not None else 0, st)
     if rc != 0:
         pytest.skip("tile does not divide this shape")
     torch.cuda.synchronize()
     xs = sign_pm1(x.double()).permute(0, 3, 1, 2)
-    ws = sign_pm1(w.double()).permute(0, 3, 1, 2).requires_grad_(True)
+    wsgn = sign_pm1(w.double()).permute(0, 3, 1, 2).requires_grad_(True)
     xp = pad_same_nhwc(xs, (3, 3), (stride, stride), 1.0 if pad_ones else 0.0)
-    F.conv2d(xp, ws, stride=stride).backward(dy.double().permute(0, 3, 1, 2))
-    ref = ws.grad.permute(0, 2, 3, 1) * (w.double().abs() <= 1.0)
+    F.conv2d(xp, wsgn, stride=stride).backward(dy.double().permute(0, 3, 1, 2))
+    ref = wsgn.grad.permute(0, 2, 3, 1) * (w.double().abs() <= 1.0) + 0.25
     err = (dw.double() - ref).abs().max().item()
     assert err <= 1e-4 * ref.abs().max().item() + 1e-3, err
 

@@ -12,8 +12,8 @@ ROOT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                     "zookeeper_amd", "csrc")
 
 _DEF = re.compile(
-    r'(?:ZK_EXPORT|extern\s+"C"\s+__attribute__\(\(visibility\("default"\)\)\))\s+int\s+'
-    r"(zk_\w+)\s*\(([^)]*)\)", re.S)
+    r'(?:ZK_EXPORT|extern\s+"C"\s+__attribute__\(\(visibility\("default"\)\)\))\s+'
+    r"(?:int|long long)\s+(zk_\w+)\s*\(([^)]*)\)", re.S)
 
 
 def _kind(param: str) -> str:

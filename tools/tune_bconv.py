@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--slab", type=int, default=1, help="wgrad split-K via workspace slabs")
     ap.add_argument("--only", default="fwd,dgrad,igemm,wgrad,miopen",
                     help="comma list of kernel families to time")
     args = ap.parse_args()
@@ -153,9 +154,13 @@ def main():
         for v in (range(IGW_VARIANTS) if "igw" in fam else ()):
             for tb in (512, 1024, 2048):
                 dw.zero_()
+                nb = L.zk_igemm_wgrad_ws_bytes(B, cin, Ho, Ho, cout, 3, 3, s, tb, v)
+                wsb = torch.empty(max(nb, 4) // 4, device="cuda") if args.slab else None
+                wsp = wsb.data_ptr() if wsb is not None else None
+                wsn = wsb.numel() * 4 if wsb is not None else 0
                 rc = L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w.data_ptr(), dw.data_ptr(),
                                       B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v,
-                                      st)
+                                      wsp, wsn, st)
                 torch.cuda.synchronize()
                 if rc != 0:
                     row[f"igw_v{v}_tb{tb}_us"] = None
@@ -165,7 +170,7 @@ def main():
                                                       ref_dw.abs().max()).item()
                 row[f"igw_v{v}_tb{tb}_us"] = timeit(lambda: L.zk_igemm_wgrad(
                     dy.data_ptr(), sx.data_ptr(), w.data_ptr(), dw.data_ptr(), B, H, W, cin, Ho,
-                    Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v, st), args.reps)
+                    Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v, wsp, wsn, st), args.reps)
         # library reference: bf16 conv backward on unpacked ±1 operands
         xs = torch.where(x >= 0, 1.0, -1.0).to(torch.bfloat16).permute(0, 3, 1, 2)
         wsn = torch.where(w >= 0, 1.0, -1.0).to(torch.bfloat16).permute(0, 3, 1, 2)

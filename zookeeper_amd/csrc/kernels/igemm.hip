@@ -450,8 +450,8 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
 template <int BM, int BN, int WM, int WN, int BK, int NS>
 __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ sx,
-    const float* __restrict__ w, float* __restrict__ dw, IGeom g, int pad_ones, float clip,
-    int k_per_split, int m_tiles, int n_tiles) {
+    const float* __restrict__ w, float* __restrict__ dw, float* __restrict__ slab, IGeom g,
+    int pad_ones, float clip, int k_per_split, int m_tiles, int n_tiles) {
   constexpr int NWAVES = WM * WN;
   constexpr int RA = BM * 2, RBB = BN * 2;      // bytes per pixel row of A / B
   constexpr int SA = BK * RA, SB = BK * RBB;    // bytes per stage
@@ -574,9 +574,13 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
     }
   }
 
-  // epilogue: kernel STE mask, split-K fp32 atomics into dW [Cout][T*Cin]
+  // epilogue.  slab mode: plain stores of this split's partial dW into
+  // slab[split][Cout][T*Cin] (summed + masked by wgrad_reduce_kernel: plain
+  // stores run at ~6 TB/s, fp32 atomics at ~1.3 TB/s of added bytes).
+  // Otherwise: kernel STE mask and fp32 atomics straight into dW.
   const int h = lane >> 5, r32 = lane & 31;
   const int NTOT = g.kh * g.kw * g.Cin;
+  float* sl = slab ? slab + (long long)split * g.Cout * NTOT : nullptr;
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
 #pragma unroll
@@ -586,19 +590,90 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
       for (int b = 0; b < TN; ++b) {
         const int n = n0 + wn * WTN + b * 32 + r32;
         const long long idx = (long long)co * NTOT + n;
-        if (fabsf(w[idx]) <= clip) atomicAdd(dw + idx, acc[a][b][r]);
+        if (sl)
+          sl[idx] = acc[a][b][r];
+        else if (fabsf(w[idx]) <= clip)
+          atomicAdd(dw + idx, acc[a][b][r]);
       }
     }
   }
 }
 
+// dW[i] += [|w[i]| <= clip] * sum_s slab[s][i].  Block = 16 float4 columns
+// x 16 split lanes (each lane sums every 16th split), then an LDS reduction:
+// many splits (small dW, long K) still spread over many threads.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float4* __restrict__ slab,
+                                                           int splits, long long n4,
+                                                           const float4* __restrict__ w,
+                                                           float clip, float4* __restrict__ dw) {
+  const int c = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const long long i = (long long)blockIdx.x * 16 + c;
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4)
+    for (int sp = sl; sp < splits; sp += 16) {
+      const float4 v = slab[(long long)sp * n4 + i];
+      t.x += v.x;
+      t.y += v.y;
+      t.z += v.z;
+      t.w += v.w;
+    }
+  __shared__ float4 red[16][17];
+  red[sl][c] = t;
+  __syncthreads();
+  if (sl == 0 && i < n4) {
+    for (int k = 1; k < 16; ++k) {
+      const float4 v = red[k][c];
+      t.x += v.x;
+      t.y += v.y;
+      t.z += v.z;
+      t.w += v.w;
+    }
+    const float4 wv = w[i];
+    float4 d = dw[i];
+    d.x += fabsf(wv.x) <= clip ? t.x : 0.f;
+    d.y += fabsf(wv.y) <= clip ? t.y : 0.f;
+    d.z += fabsf(wv.z) <= clip ? t.z : 0.f;
+    d.w += fabsf(wv.w) <= clip ? t.w : 0.f;
+    dw[i] = d;
+  }
+}
+
+struct WgradPlan {
+  int m_tiles, n_tiles, splits, kps;
+};
+
+template <int BM, int BN, int BK>
+bool plan_wgrad(const IGeom& g, int target_blocks, WgradPlan& p) {
+  const int NTOT = g.kh * g.kw * g.Cin;
+  if (g.Cout % BM || NTOT % BN || g.Cin % 8) return false;
+  const long long P = (long long)g.B * g.Ho * g.Wo;
+  if (P >= (1 << 24)) return false;  // fdiv range
+  p.m_tiles = g.Cout / BM;
+  p.n_tiles = NTOT / BN;
+  const long long tiles = (long long)p.m_tiles * p.n_tiles;
+  long long splits = (target_blocks + tiles - 1) / tiles;
+  const long long max_splits = (P + 4 * BK - 1) / (4 * BK);  // >= 4 K-steps per split
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  long long kps = (P + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  p.splits = (int)((P + kps - 1) / kps);
+  p.kps = (int)kps;
+  return true;
+}
+
 template <int BM, int BN, int WM, int WN, int BK, int NS>
 int launch_igemm_wgrad(const void* dy, const void* sx, const void* w, void* dw, const IGeom& g,
-                       int pad_ones, float clip, int target_blocks, hipStream_t stream) {
+                       int pad_ones, float clip, int target_blocks, void* ws, long long ws_bytes,
+                       long long* ws_needed, hipStream_t stream) {
+  WgradPlan p;
+  if (!plan_wgrad<BM, BN, BK>(g, target_blocks, p)) return (int)hipErrorInvalidValue;
   const int NTOT = g.kh * g.kw * g.Cin;
-  if (g.Cout % BM || NTOT % BN || g.Cin % 8) return (int)hipErrorInvalidValue;
-  const long long P = (long long)g.B * g.Ho * g.Wo;
-  if (P >= (1 << 24)) return (int)hipErrorInvalidValue;  // fdiv range
+  const long long slab_bytes = (long long)p.splits * g.Cout * NTOT * 4;
+  if (ws_needed) {  // size query only
+    *ws_needed = slab_bytes;
+    return 0;
+  }
   constexpr int LDS = NS * BK * (BM + BN) * 2;
   static_assert(LDS <= 160 * 1024, "LDS");
   auto kern = igemm_wgrad_kernel<BM, BN, WM, WN, BK, NS>;
@@ -609,25 +684,25 @@ int launch_igemm_wgrad(const void* dy, const void* sx, const void* w, void* dw, 
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  const int m_tiles = g.Cout / BM, n_tiles = NTOT / BN;
-  const long long tiles = (long long)m_tiles * n_tiles;
-  long long splits = (target_blocks + tiles - 1) / tiles;
-  const long long max_splits = (P + 4 * BK - 1) / (4 * BK);  // >= 4 K-steps per split
-  if (splits > max_splits) splits = max_splits;
-  if (splits < 1) splits = 1;
-  long long kps = (P + splits - 1) / splits;
-  kps = (kps + BK - 1) / BK * BK;
-  splits = (P + kps - 1) / kps;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * splits)), dim3(WM * WN * 64), LDS, stream,
-                     (const uint16_t*)dy, (const uint16_t*)sx, (const float*)w, (float*)dw, g,
-                     pad_ones, clip, (int)kps, m_tiles, n_tiles);
+  float* slab = (ws && ws_bytes >= slab_bytes && NTOT % 4 == 0) ? (float*)ws : nullptr;
+  const long long tiles = (long long)p.m_tiles * p.n_tiles;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * p.splits)), dim3(WM * WN * 64), LDS, stream,
+                     (const uint16_t*)dy, (const uint16_t*)sx, (const float*)w, (float*)dw, slab,
+                     g, pad_ones, clip, p.kps, p.m_tiles, p.n_tiles);
+  if (slab) {
+    const long long n4 = (long long)g.Cout * NTOT / 4;
+    const long long blocks = (n4 + 15) / 16;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                       (const float4*)slab, p.splits, n4, (const float4*)w, clip, (float4*)dw);
+  }
   return 0;
 }
 
 int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, void* dw,
-                        const IGeom& g, int po, float clip, int tb, hipStream_t st) {
+                        const IGeom& g, int po, float clip, int tb, void* ws, long long wsb,
+                        long long* need, hipStream_t st) {
 #define ZK_IGW(...) \
-  return launch_igemm_wgrad<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, st)
+  return launch_igemm_wgrad<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, ws, wsb, need, st)
   switch (v) {
     case 0: ZK_IGW(128, 128, 2, 2, 32, 2);
     case 1: ZK_IGW(128, 128, 2, 2, 32, 4);
@@ -666,29 +741,55 @@ ZK_EXPORT int zk_igemm_dgrad(const void* dy, const void* wt, const void* mask, c
   return 0;
 }
 
-// dW fp32 [Cout][T][Cin] accumulated in place (zeroed by the caller or the
-// flat gradient buffer itself).  sx: sign(x) bf16 +-1 [B][H][W][Cin].
-ZK_EXPORT int zk_igemm_wgrad(const void* dy, const void* sx, const void* w, void* dw, int B,
-                             int H, int W, int Cin, int Ho, int Wo, int Cout, int kh, int kw,
-                             int stride, int pt, int pl, int pad_ones, float clip,
-                             int target_blocks, int variant, hipStream_t stream) {
-  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+namespace {
+void wgrad_defaults(const IGeom& g, int& variant, int& target_blocks) {
   if (variant < 0) {
     // Tuned on MI355X (tools/tune_bconv.py --only igw, E18 shapes, batch 256)
-    if (Cin == 64 || Cout % 128 != 0) {
+    // (slab split-K reduction)
+    if (g.Cin == 64 && g.s == 2 && g.Cout % 128 == 0 && (9 * g.Cin) % 192 == 0) {
+      variant = 2;
+      if (target_blocks <= 0) target_blocks = 512;
+    } else if (g.Cin == 64 || g.Cout % 128 != 0) {
       variant = 7;
       if (target_blocks <= 0) target_blocks = 2048;
     } else {
       variant = 0;
-      if (target_blocks <= 0) target_blocks = (Cin == 128 && stride == 1) ? 1024 : 512;
+      if (target_blocks <= 0) target_blocks = (g.s == 1) ? 1024 : 512;
     }
   }
   if (target_blocks <= 0) target_blocks = 1024;
+}
+}  // namespace
+
+// dW fp32 [Cout][T][Cin] accumulated in place (zeroed by the caller or the
+// flat gradient buffer itself).  sx: sign(x) bf16 +-1 [B][H][W][Cin].
+// workspace (optional, zk_igemm_wgrad_ws_bytes) switches the split-K
+// reduction from fp32 atomics to per-split slabs + one reduce kernel.
+ZK_EXPORT int zk_igemm_wgrad(const void* dy, const void* sx, const void* w, void* dw, int B,
+                             int H, int W, int Cin, int Ho, int Wo, int Cout, int kh, int kw,
+                             int stride, int pt, int pl, int pad_ones, float clip,
+                             int target_blocks, int variant, void* workspace,
+                             long long ws_bytes, hipStream_t stream) {
+  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+  wgrad_defaults(g, variant, target_blocks);
   const int rc = igemm_wgrad_variant(variant, dy, sx, w, dw, g, pad_ones, clip, target_blocks,
-                                     stream);
+                                     workspace, ws_bytes, nullptr, stream);
   if (rc) return rc;
   ZK_CHECK_LAUNCH();
   return 0;
+}
+
+// Workspace bytes zk_igemm_wgrad needs for slab mode (-1: shape unsupported).
+ZK_EXPORT long long zk_igemm_wgrad_ws_bytes(int B, int Cin, int Ho, int Wo, int Cout, int kh,
+                                            int kw, int stride, int target_blocks,
+                                            int variant) {
+  IGeom g{B, 0, 0, Cin, Ho, Wo, Cout, kh, kw, stride, 0, 0};
+  wgrad_defaults(g, variant, target_blocks);
+  long long need = -1;
+  if (igemm_wgrad_variant(variant, nullptr, nullptr, nullptr, nullptr, g, 0, 0.f,
+                          target_blocks, nullptr, 0, &need, nullptr) != 0)
+    return -1;
+  return need;
 }
 
 // Binary forward on MFMA: y int16 [B][Ho][Wo][Cout] = conv(sign x, sign W)

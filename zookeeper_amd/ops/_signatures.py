@@ -28,7 +28,8 @@ SIGNATURES = {
     "zk_bconv_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
     "zk_igemm_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
     "zk_igemm_fwd": (I32, [P, P, P, P] + [I32] * 15 + [P]),
-    "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P]),
+    "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),
+    "zk_igemm_wgrad_ws_bytes": (I64, [I32] * 10),
     "zk_bconv_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P]),
     # batch norm
     "zk_bn_finalize": (I32, [P, I32, C.c_double, P, P, F32, F32, P, P, P, P, P, P, P]),

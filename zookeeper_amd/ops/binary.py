@@ -202,9 +202,16 @@ class _BinaryBlockFn(torch.autograd.Function):
             else:
                 dw = torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev)
             if sx is not None:
+                # split-K partial sums go to a workspace slab (plain stores)
+                # and one reduce kernel adds them, masked, into dw
+                ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, Ho, Wo, Cout, kh, kw, stride, 0, -1)
+                ws = (torch.empty(max(ws_bytes, 0) // 4, dtype=torch.float32, device=dev)
+                      if ws_bytes > 0 else None)
                 check(L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w_ohwi.data_ptr(),
                                        dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride,
-                                       pt, pl, int(pad_ones), clip, 0, -1, st), "zk_igemm_wgrad")
+                                       pt, pl, int(pad_ones), clip, 0, -1,
+                                       ws.data_ptr() if ws is not None else None,
+                                       max(ws_bytes, 0), st), "zk_igemm_wgrad")
             else:
                 check(L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w_ohwi.data_ptr(),
                                        dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride,
