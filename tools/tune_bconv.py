@@ -20,9 +20,9 @@ from zookeeper_amd.ops._native import lib, stream_ptr  # noqa: E402
 
 DG_VARIANTS = 8
 WG_VARIANTS = 8
-IG_VARIANTS = 12
+IG_VARIANTS = 15
 IGW_VARIANTS = 8
-IGF_VARIANTS = 12
+IGF_VARIANTS = 15
 
 
 def timeit(fn, reps):

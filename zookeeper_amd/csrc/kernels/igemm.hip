@@ -230,30 +230,41 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
     if (ks + NS - 1 < NK) issue(ks + NS - 1);
 
     const unsigned char* st = smem + (ks % NS) * STAGE;
-#pragma unroll
-    for (int sub = 0; sub < CB / 32; ++sub) {
+    // fragment reads are double-buffered across the k-substeps: the reads of
+    // substep sub+1 are in flight while the MFMAs of substep sub issue.
+    constexpr int NSUB = CB / 32;
+    uint4 af[2][TM], bfr[2][TN];
+    auto read_frags = [&](int sub, int set) {
       const int chunk = 2 * sub + h;
-      uint4 af[TM], bfr[TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
         const int row = wm * WTM + a * 32 + r32;
-        af[a] = *reinterpret_cast<const uint4*>(
+        af[set][a] = *reinterpret_cast<const uint4*>(
             st + a_off[a] + ((chunk ^ ((row >> SH) & (SPR - 1))) * 16));
       }
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
         const int row = wn * WTN + b * 32 + r32;
-        bfr[b] = *reinterpret_cast<const uint4*>(
+        bfr[set][b] = *reinterpret_cast<const uint4*>(
             st + b_off[b] + ((chunk ^ ((row >> SH) & (SPR - 1))) * 16));
       }
+    };
+    read_frags(0, 0);
+#pragma unroll
+    for (int sub = 0; sub < NSUB; ++sub) {
+      if (sub + 1 < NSUB) read_frags(sub + 1, (sub + 1) & 1);
+      // keep the next substep's reads ahead of this substep's MFMAs (the
+      // scheduler would otherwise sink them to reuse the registers)
+      __builtin_amdgcn_sched_barrier(0);
+      const int cs = sub & 1;
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b)
           // fwd: D[pixel][co] (lane = channel: in-lane BN statistics);
           // dgrad: D[ci][pixel] (lane = pixel: 8-B mask/residual epilogue)
-          acc[a][b] = FWD ? mfma_bf16(af[a], bfr[b], acc[a][b])
-                          : mfma_bf16(bfr[b], af[a], acc[a][b]);
+          acc[a][b] = FWD ? mfma_bf16(af[cs][a], bfr[cs][b], acc[a][b])
+                          : mfma_bf16(bfr[cs][b], af[cs][a], acc[a][b]);
     }
   }
 
@@ -413,6 +424,9 @@ int igemm_fwd_variant(int v, const void* sx, const void* wf, void* y, void* stat
     case 9: ZK_IGF(64, 64, 2, 2, 2);
     case 10: ZK_IGF(128, 128, 2, 2, 4);
     case 11: ZK_IGF(256, 128, 4, 2, 4, 64);
+    case 12: ZK_IGF(256, 256, 4, 2, 3, 64);
+    case 13: ZK_IGF(256, 256, 2, 4, 3, 64);
+    case 14: ZK_IGF(256, 256, 4, 2, 2, 128);
     default: return (int)hipErrorInvalidValue;
   }
 #undef ZK_IGF
@@ -434,6 +448,9 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
     case 9: ZK_IGD(64, 64, 2, 2, 2);          // 32 KB
     case 10: ZK_IGD(128, 128, 2, 2, 4);       // 128 KB, 1 WG/CU
     case 11: ZK_IGD(256, 128, 4, 2, 4, 64);   // 8 waves, 96 KB
+    case 12: ZK_IGD(256, 256, 4, 2, 3, 64);   // 8 waves, 96 KB: 2x bytes/FLOP of 128x128
+    case 13: ZK_IGD(256, 256, 2, 4, 3, 64);
+    case 14: ZK_IGD(256, 256, 4, 2, 2, 128);  // 128 KB
     default: return (int)hipErrorInvalidValue;
   }
 #undef ZK_IGD
@@ -559,18 +576,29 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
     __builtin_amdgcn_s_barrier();
     if (ks + NS - 1 < NK) issue(ks + NS - 1);
     const unsigned char* st = smem + (ks % NS) * STAGE;
+    // double-buffered transposed fragment reads (see igemm_conv_kernel)
+    constexpr int NSUB = BK / 16;
+    uint4 af[2][TM], bfr[2][TN];
+    auto read_frags = [&](int sub, int set) {
 #pragma unroll
-    for (int sub = 0; sub < BK / 16; ++sub) {
-      uint4 af[TM], bfr[TN];
-#pragma unroll
-      for (int a = 0; a < TM; ++a) af[a] = tr_frag_swz<RA>(st, sub * 16, wm * WTM + a * 32, lane);
+      for (int a = 0; a < TM; ++a)
+        af[set][a] = tr_frag_swz<RA>(st, sub * 16, wm * WTM + a * 32, lane);
 #pragma unroll
       for (int b = 0; b < TN; ++b)
-        bfr[b] = tr_frag_swz<RBB>(st + SA, sub * 16, wn * WTN + b * 32, lane);
+        bfr[set][b] = tr_frag_swz<RBB>(st + SA, sub * 16, wn * WTN + b * 32, lane);
+    };
+    read_frags(0, 0);
+#pragma unroll
+    for (int sub = 0; sub < NSUB; ++sub) {
+      if (sub + 1 < NSUB) read_frags(sub + 1, (sub + 1) & 1);
+      // keep the next substep's reads ahead of this substep's MFMAs (the
+      // scheduler would otherwise sink them to reuse the registers)
+      __builtin_amdgcn_sched_barrier(0);
+      const int cs = sub & 1;
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < TN; ++b) acc[a][b] = mfma_bf16(af[a], bfr[b], acc[a][b]);
+        for (int b = 0; b < TN; ++b) acc[a][b] = mfma_bf16(af[cs][a], bfr[cs][b], acc[a][b]);
     }
   }
 
@@ -730,8 +758,10 @@ ZK_EXPORT int zk_igemm_dgrad(const void* dy, const void* wt, const void* mask, c
     // Tuned on MI355X (tools/tune_bconv.py --only igemm, E18 shapes, batch
     // 256): 128x128 at 2 WG/CU for Cin >= 128 (8-wave 256x128 for the
     // 256-channel stride-1 layers), 128x64 with a 4-deep 64-B ring for Cin=64.
+    // 256x256 (v14) halves the LDS-fill bytes per FLOP; it pays where the
+    // grid still has ~200 tiles (the 256-channel stride-1 layers).
     if (Cin % 128 == 0)
-      variant = (Cin == 256 && stride == 1) ? 11 : 0;
+      variant = (Cin == 256 && stride == 1) ? 14 : 0;
     else
       variant = 7;
   }
@@ -804,8 +834,10 @@ ZK_EXPORT int zk_igemm_fwd(const void* sx, const void* wf, void* y, void* stats,
     // Tuned on MI355X (tools/tune_bconv.py --only igf, E18 shapes, batch 256)
     if (Cin == 64 || Cout % 128 != 0)
       variant = (Cout == 64) ? 8 : 7;
+    else if (Cout == 256)
+      variant = 14;  // 256x256: half the LDS-fill bytes per FLOP, ~200 tiles
     else
-      variant = (stride == 1 && Cout >= 256) ? 11 : 0;
+      variant = 0;
   }
   const int rc = igemm_fwd_variant(variant, sx, wf, y, stats, g, pad_ones, relu, stream);
   if (rc) return rc;
