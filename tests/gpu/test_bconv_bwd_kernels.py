@@ -118,7 +118,7 @@ def test_igemm_dgrad_matches_reference(variant, cin, cout, stride, hw):
 
 
 @pytest.mark.parametrize("slab", [False, True])
-@pytest.mark.parametrize("variant", list(range(8)))
+@pytest.mark.parametrize("variant", list(range(13)))
 @pytest.mark.parametrize("cin,cout,stride,hw,pad_ones", [
     (64, 64, 1, 12, 0), (64, 128, 2, 12, 0), (128, 128, 1, 7, 1), (256, 512, 2, 8, 0),
     (128, 64, 1, 9, 1), (64, 192, 1, 5, 1)])

@@ -21,7 +21,7 @@ from zookeeper_amd.ops._native import lib, stream_ptr  # noqa: E402
 DG_VARIANTS = 8
 WG_VARIANTS = 8
 IG_VARIANTS = 15
-IGW_VARIANTS = 8
+IGW_VARIANTS = 13
 IGF_VARIANTS = 15
 
 

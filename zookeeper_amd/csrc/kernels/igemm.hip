@@ -740,6 +740,11 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
     case 5: ZK_IGW(64, 128, 2, 2, 32, 4);
     case 6: ZK_IGW(128, 256, 2, 2, 32, 2);
     case 7: ZK_IGW(64, 64, 2, 2, 32, 4);
+    case 8: ZK_IGW(256, 256, 4, 2, 32, 2);   // 8 waves, 64 KB
+    case 9: ZK_IGW(256, 256, 2, 4, 32, 2);
+    case 10: ZK_IGW(256, 128, 4, 2, 32, 2);
+    case 11: ZK_IGW(128, 256, 2, 4, 32, 2);
+    case 12: ZK_IGW(256, 256, 4, 2, 32, 3);  // 96 KB
     default: return (int)hipErrorInvalidValue;
   }
 #undef ZK_IGW
@@ -783,8 +788,10 @@ void wgrad_defaults(const IGeom& g, int& variant, int& target_blocks) {
       variant = 7;
       if (target_blocks <= 0) target_blocks = 2048;
     } else {
-      variant = 0;
-      if (target_blocks <= 0) target_blocks = (g.s == 1) ? 1024 : 512;
+      variant = 4;  // 128x128, 64-pixel K-steps
+      if (target_blocks <= 0)
+        target_blocks = (g.Cout >= 512 && g.s == 1) ? 2048
+                        : (g.Cin >= 256 || g.Cout >= 512) ? 1024 : 512;
     }
   }
   if (target_blocks <= 0) target_blocks = 1024;
