@@ -20,9 +20,9 @@ from zookeeper_amd.ops._native import lib, stream_ptr  # noqa: E402
 
 DG_VARIANTS = 8
 WG_VARIANTS = 8
-IG_VARIANTS = 15
+IG_VARIANTS = list(range(15)) + list(range(20, 28))
 IGW_VARIANTS = 13
-IGF_VARIANTS = 15
+IGF_VARIANTS = list(range(15)) + list(range(20, 28))
 
 
 def timeit(fn, reps):
@@ -90,7 +90,7 @@ def main():
                                st)
                 torch.cuda.synchronize()
                 yref = y.clone()
-            for v in range(IGF_VARIANTS):
+            for v in IGF_VARIANTS:
                 y.zero_()
                 rc = L.zk_igemm_fwd(sx.data_ptr(), wf.data_ptr(), y.data_ptr(), stats.data_ptr(),
                                     B, H, W, cin, cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, v, st)
@@ -119,7 +119,7 @@ def main():
             if v == 7:
                 torch.cuda.synchronize()
                 ref_dx = dx.float().clone()
-        for v in (range(IG_VARIANTS) if "igemm" in fam else ()):
+        for v in (IG_VARIANTS if "igemm" in fam else ()):
             dx.zero_()
             rc = L.zk_igemm_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(), None,
                                   dx.data_ptr(), B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, v, st)

@@ -358,6 +358,277 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
   }
 }
 
+// ===========================================================================
+// 3x3 stride-1 'same' convolutions with horizontal tap reuse ("conv3").
+//
+// The three taps tw of one kernel row th read the SAME activation rows
+// shifted by one pixel: with pixels flattened over (b, h, w), tap (th, tw)
+// of output pixel m reads row m + dh(th)*W + dw(tw), dw in {-1, 0, 1}.  So a
+// K-step loads BM + 2 activation rows ONCE (plus the three taps' weight
+// rows) and the MFMAs of tap tw read LDS rows shifted by dw + 1 — a third of
+// the activation LDS-fill bytes of igemm_conv_kernel.  Rows that belong to
+// another image row / image (left/right/top/bottom padding) are loaded
+// unconditionally and their fragments zeroed per lane (validity bit masks).
+//   FWD:  q = m + (th-1)*W + (tw-1)       DGRAD: q = m + (1-th)*W + (1-tw)
+// ===========================================================================
+template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB>
+__global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs args, IGeom g,
+                                                                      int m_tiles) {
+  constexpr int NWAVES = WM * WN;
+  constexpr int SPR = CB / 16, RPI = 1024 / CB, SH = (CB == 128) ? 1 : 2;
+  constexpr int A_INS = (BM + 2 + RPI * NWAVES - 1) / (RPI * NWAVES);  // glds per wave
+  constexpr int AR = A_INS * RPI * NWAVES;                             // A rows staged
+  constexpr int B_INS = 3 * BN / RPI / NWAVES;
+  static_assert(B_INS >= 1 && (3 * BN) % (RPI * NWAVES) == 0, "tile / wave mismatch");
+  constexpr int LPS = A_INS + B_INS;
+  constexpr int STAGE = (AR + 3 * BN) * CB;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(!FWD || TM <= 4, "in-wave int32 sums of squares need TM <= 4");
+
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave / WN, wn = wave % WN;
+  const int NCH = FWD ? g.Cout : g.Cin, KCH = FWD ? g.Cin : g.Cout;
+  const int L = xcd_linear(blockIdx.x, gridDim.x);
+  const int n_tiles = NCH / BN;
+  const int mtile = L % m_tiles, ntile = L / m_tiles;
+  if (ntile >= n_tiles) return;
+  const int H = g.H, W = g.W;
+  const long long M = (long long)g.B * H * W;
+  const long long m0 = (long long)mtile * BM;
+  if (m0 >= M) return;
+  const int n0 = ntile * BN;
+  const int RB = KCH * 2, kchunks = RB / CB, NK = 3 * kchunks;
+  const unsigned char* actb = reinterpret_cast<const unsigned char*>(args.act);
+  const unsigned char* wtb = reinterpret_cast<const unsigned char*>(args.wgt);
+  const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
+  const unsigned char* padp =
+      (FWD && args.pad_ones) ? reinterpret_cast<const unsigned char*>(g_ones_page_bf16) : zp;
+  const int lrow = lane / SPR, lslot = lane % SPR;
+  const int r32 = lane & 31, h = lane >> 5;
+
+  // per-lane validity of the wave's output pixels: bit th of vh[a], bit tw of vw[a]
+  uint32_t vh[TM], vw[TM];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+    const long long m = m0 + wm * WTM + a * 32 + r32;
+    vh[a] = vw[a] = 0;
+    if (m < M) {
+      const int w = (int)(m % W), hh = (int)((m / W) % H);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int dh = FWD ? t - 1 : 1 - t;
+        vh[a] |= (uint32_t)(hh + dh >= 0 && hh + dh < H) << t;
+        vw[a] |= (uint32_t)(w + dh >= 0 && w + dh < W) << t;  // dw(t) == dh(t)
+      }
+    }
+  }
+
+  auto issue = [&](int ks) {
+    const int th = ks / kchunks, kc = ks % kchunks;
+    const int dh = FWD ? th - 1 : 1 - th;
+    unsigned char* st = smem + (ks % NS) * STAGE;
+    const long long base = m0 + (long long)dh * W - 1;  // LDS row 0
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      const int r = (j * NWAVES + wave) * RPI + lrow;
+      const int sw = lslot ^ ((r >> SH) & (SPR - 1));
+      const long long q = base + r;
+      // padding taps / tail rows are masked on the fragments; this only
+      // keeps every address inside the tensor
+      const unsigned char* src = (q >= 0 && q < M) ? actb + q * RB + kc * CB + sw * 16
+                                                   : zp + sw * 16;
+      ZK_GLDS16(src, st + (j * NWAVES + wave) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const int r = (j * NWAVES + wave) * RPI + lrow;  // 0 .. 3*BN-1
+      const int tw = r / BN, n = r % BN;
+      const int t = th * 3 + tw;
+      const int sw = lslot ^ ((n >> SH) & (SPR - 1));
+      ZK_GLDS16(wtb + ((long long)t * NCH + n0 + n) * RB + kc * CB + sw * 16,
+                st + AR * CB + (j * NWAVES + wave) * 1024);
+    }
+  };
+  (void)padp;
+  // value of a padding tap's fragment: 0, or bf16 +1 pairs for pad_values=1
+  const uint32_t padv = (FWD && args.pad_ones) ? 0x3F803F80u : 0u;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < NK) issue(p);
+  for (int ks = 0; ks < NK; ++ks) {
+    if (ks + NS - 2 < NK)
+      wait_vmcnt<LPS * (NS - 2)>();
+    else
+      wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (ks + NS - 1 < NK) issue(ks + NS - 1);
+    const unsigned char* st = smem + (ks % NS) * STAGE;
+    const int th = ks / kchunks;
+    uint32_t okh[TM];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) okh[a] = (vh[a] >> th) & 1u;
+    // (tw, substep) flattened, fragment reads double-buffered
+    constexpr int NSUB = CB / 32, NIT = 3 * NSUB;
+    uint4 af[2][TM], bfr[2][TN];
+    auto read_frags = [&](int it, int set) {
+      const int tw = it / NSUB, sub = it % NSUB;
+      const int chunk = 2 * sub + h;
+      const int dw1 = FWD ? tw : 2 - tw;  // dw + 1: LDS row shift of this tap
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const int row = wm * WTM + a * 32 + r32 + dw1;
+        uint4 v = *reinterpret_cast<const uint4*>(
+            st + row * CB + ((chunk ^ ((row >> SH) & (SPR - 1))) * 16));
+        const bool ok = okh[a] & (vw[a] >> tw) & 1u;
+        if (!ok) v = make_uint4(padv, padv, padv, padv);  // padding tap: 0 or +1
+        af[set][a] = v;
+      }
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int n = wn * WTN + b * 32 + r32;
+        bfr[set][b] = *reinterpret_cast<const uint4*>(
+            st + AR * CB + (tw * BN + n) * CB + ((chunk ^ ((n >> SH) & (SPR - 1))) * 16));
+      }
+    };
+    read_frags(0, 0);
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      if (it + 1 < NIT) read_frags(it + 1, (it + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const int cs = it & 1;
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = FWD ? mfma_bf16(af[cs][a], bfr[cs][b], acc[a][b])
+                          : mfma_bf16(bfr[cs][b], af[cs][a], acc[a][b]);
+    }
+  }
+
+  if constexpr (FWD) {
+    // ---- forward epilogue (as igemm_conv_kernel): lane = channel
+    int16_t* y = reinterpret_cast<int16_t*>(args.out);
+    int csum[TN], csq[TN];
+#pragma unroll
+    for (int b = 0; b < TN; ++b) csum[b] = csq[b] = 0;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long mc = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const bool live = mc < M;
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          int t = (int)acc[a][b][r];
+          if (args.relu) t = t > 0 ? t : 0;
+          if (!live) t = 0;
+          csum[b] += t;
+          csq[b] += t * t;
+          if (live) y[mc * g.Cout + n0 + wn * WTN + b * 32 + r32] = (int16_t)t;
+        }
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+    int* red = reinterpret_cast<int*>(smem);  // [WM][2][BN]
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int s1 = csum[b] + __shfl_xor(csum[b], 32, 64);
+      const int s2 = csq[b] + __shfl_xor(csq[b], 32, 64);
+      if (h == 0) {
+        const int nl = wn * WTN + b * 32 + r32;
+        red[(wm * 2 + 0) * BN + nl] = s1;
+        red[(wm * 2 + 1) * BN + nl] = s2;
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < 2 * BN; c += NWAVES * 64) {
+      const int which = c / BN, nl = c % BN;
+      long long tot = 0;
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        const int v = red[(i * 2 + which) * BN + nl];
+        tot += which ? (long long)(unsigned int)v : (long long)v;
+      }
+      atomicAdd(args.stats + which * g.Cout + n0 + nl, (unsigned long long)tot);
+    }
+  } else {
+    // ---- dgrad epilogue (stride 1: the pixel index is the row index)
+    uint16_t* dx = reinterpret_cast<uint16_t*>(args.out);
+    const uint32_t* mask = args.mask;
+    const uint16_t* dres = args.dres;
+    const int CW = g.Cin >> 5;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const long long m = m0 + wm * WTM + a * 32 + r32;
+      if (m >= M) continue;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int nb = n0 + wn * WTN + b * 32;
+        const uint32_t mw = mask ? mask[m * CW + (nb >> 5)] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int nl = 8 * q + 4 * h;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e] = ((mw >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
+          const long long off = m * g.Cin + nb + nl;
+          if (dres) {
+            const uint2 d = *reinterpret_cast<const uint2*>(dres + off);
+            v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
+            v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
+            v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
+            v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
+          }
+          *reinterpret_cast<uint2*>(dx + off) =
+              make_uint2(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]));
+        }
+      }
+    }
+  }
+}
+
+// conv3 applies to 3x3, stride 1, pads (1, 1) ('same'), pad value 0.
+bool conv3_ok(const IGeom& g, int /*pad_ones: handled on the fragments*/) {
+  return g.kh == 3 && g.kw == 3 && g.s == 1 && g.pt == 1 && g.pl == 1 && g.Ho == g.H &&
+         g.Wo == g.W;
+}
+
+template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB>
+int launch_conv3(const ConvArgs& args, const IGeom& g, hipStream_t stream) {
+  const int NCH = FWD ? g.Cout : g.Cin, KCH = FWD ? g.Cin : g.Cout;
+  if ((KCH * 2) % CB || NCH % BN || !conv3_ok(g, args.pad_ones)) return (int)hipErrorInvalidValue;
+  constexpr int NW = WM * WN, RPI = 1024 / CB;
+  constexpr int AR = (BM + 2 + RPI * NW - 1) / (RPI * NW) * RPI * NW;
+  constexpr int LDS = NS * (AR + 3 * BN) * CB;
+  static_assert(LDS <= 160 * 1024, "LDS");
+  auto kern = igemm_conv3_kernel<FWD, BM, BN, WM, WN, NS, CB>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  const long long M = (long long)g.B * g.H * g.W;
+  const int m_tiles = (int)((M + BM - 1) / BM);
+  hipLaunchKernelGGL(kern, dim3((unsigned)((long long)m_tiles * (NCH / BN))), dim3(NW * 64), LDS,
+                     stream, args, g, m_tiles);
+  return 0;
+}
+
 template <int BM, int BN, int WM, int WN, int NS, int CB = 128>
 int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const void* dres,
                        void* dx, const IGeom& g, hipStream_t stream) {
@@ -427,6 +698,21 @@ int igemm_fwd_variant(int v, const void* sx, const void* wf, void* y, void* stat
     case 12: ZK_IGF(256, 256, 4, 2, 3, 64);
     case 13: ZK_IGF(256, 256, 2, 4, 3, 64);
     case 14: ZK_IGF(256, 256, 4, 2, 2, 128);
+#define ZK_IGF3(...)                                                                    \
+  {                                                                                     \
+    ConvArgs a{(const uint16_t*)sx, (const uint16_t*)wf, nullptr, nullptr, y,           \
+               (unsigned long long*)stats, po, relu};                                   \
+    return launch_conv3<true, __VA_ARGS__>(a, g, st);                                   \
+  }
+    case 20: ZK_IGF3(256, 64, 4, 1, 2, 128)
+    case 21: ZK_IGF3(256, 64, 4, 1, 3, 64)
+    case 22: ZK_IGF3(128, 64, 2, 2, 2, 128)
+    case 23: ZK_IGF3(128, 128, 2, 2, 2, 64)
+    case 24: ZK_IGF3(256, 128, 4, 2, 2, 64)
+    case 25: ZK_IGF3(256, 256, 4, 2, 2, 64)
+    case 26: ZK_IGF3(128, 128, 2, 2, 3, 64)
+    case 27: ZK_IGF3(256, 64, 4, 1, 2, 64)
+#undef ZK_IGF3
     default: return (int)hipErrorInvalidValue;
   }
 #undef ZK_IGF
@@ -451,6 +737,21 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
     case 12: ZK_IGD(256, 256, 4, 2, 3, 64);   // 8 waves, 96 KB: 2x bytes/FLOP of 128x128
     case 13: ZK_IGD(256, 256, 2, 4, 3, 64);
     case 14: ZK_IGD(256, 256, 4, 2, 2, 128);  // 128 KB
+#define ZK_IGD3(...)                                                                    \
+  {                                                                                     \
+    ConvArgs a{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,         \
+               (const uint16_t*)dres, dx, nullptr, 0, 0};                               \
+    return launch_conv3<false, __VA_ARGS__>(a, g, st);                                  \
+  }
+    case 20: ZK_IGD3(256, 64, 4, 1, 2, 128)
+    case 21: ZK_IGD3(256, 64, 4, 1, 3, 64)
+    case 22: ZK_IGD3(128, 64, 2, 2, 2, 128)
+    case 23: ZK_IGD3(128, 128, 2, 2, 2, 64)
+    case 24: ZK_IGD3(256, 128, 4, 2, 2, 64)
+    case 25: ZK_IGD3(256, 256, 4, 2, 2, 64)
+    case 26: ZK_IGD3(128, 128, 2, 2, 3, 64)
+    case 27: ZK_IGD3(256, 64, 4, 1, 2, 64)
+#undef ZK_IGD3
     default: return (int)hipErrorInvalidValue;
   }
 #undef ZK_IGD
@@ -764,9 +1065,19 @@ ZK_EXPORT int zk_igemm_dgrad(const void* dy, const void* wt, const void* mask, c
     // 256): 128x128 at 2 WG/CU for Cin >= 128 (8-wave 256x128 for the
     // 256-channel stride-1 layers), 128x64 with a 4-deep 64-B ring for Cin=64.
     // 256x256 (v14) halves the LDS-fill bytes per FLOP; it pays where the
-    // grid still has ~200 tiles (the 256-channel stride-1 layers).
-    if (Cin % 128 == 0)
-      variant = (Cin == 256 && stride == 1) ? 14 : 0;
+    // grid still has ~200 tiles (the 256-channel stride-1 layers).  conv3
+    // (20+: horizontal tap reuse) for the other stride-1 3x3 layers.
+    const bool c3 = conv3_ok(g, 0);
+    if (Cin == 256 && stride == 1)
+      variant = 14;
+    else if (c3 && Cin == 512)
+      variant = 24;
+    else if (c3 && Cin == 128)
+      variant = 23;
+    else if (c3 && Cin == 64)
+      variant = 27;
+    else if (Cin % 128 == 0)
+      variant = 0;
     else
       variant = 7;
   }
@@ -839,7 +1150,14 @@ ZK_EXPORT int zk_igemm_fwd(const void* sx, const void* wf, void* y, void* stats,
   IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
   if (variant < 0) {
     // Tuned on MI355X (tools/tune_bconv.py --only igf, E18 shapes, batch 256)
-    if (Cin == 64 || Cout % 128 != 0)
+    const bool c3 = conv3_ok(g, pad_ones);
+    if (c3 && Cout == 64)
+      variant = 27;  // conv3: horizontal tap reuse
+    else if (c3 && Cout == 128)
+      variant = 27;
+    else if (c3 && Cout == 512)
+      variant = 24;
+    else if (Cin == 64 || Cout % 128 != 0)
       variant = (Cout == 64) ? 8 : 7;
     else if (Cout == 256)
       variant = 14;  // 256x256: half the LDS-fill bytes per FLOP, ~200 tiles
