@@ -212,3 +212,29 @@ def test_igemm_fwd_matches_reference(variant, cin, cout, stride, hw, pad_ones, r
     flat = ref.reshape(-1, cout)
     assert torch.equal(stats[0].cpu(), flat.sum(0).cpu())
     assert torch.equal(stats[1].cpu(), (flat * flat).sum(0).cpu())
+
+
+@pytest.mark.parametrize("cout,taps,cin", [(64, 9, 64), (128, 9, 256), (512, 1, 256)])
+def test_weight_pack_tiled_matches_per_word(cout, taps, cin):
+    """The LDS-tiled packer (no bit outputs) writes the same wf / wt as the
+    per-word kernel (which also produces the XNOR bits)."""
+    from zookeeper_amd.ops._native import lib, stream_ptr
+
+    L, st = lib(), stream_ptr()
+    w = torch.randn(cout, taps, cin, device="cuda")
+    w[0, 0, :8] = 0.0  # sign(0) = +1
+    wf = torch.empty(taps, cout, cin, dtype=torch.bfloat16, device="cuda")
+    wt = torch.empty(taps, cin, cout, dtype=torch.bfloat16, device="cuda")
+    assert L.zk_weight_pack(w.data_ptr(), None, None, wt.data_ptr(), wf.data_ptr(), cout, taps,
+                            cin, st) == 0
+    wbits = torch.empty(cout * taps * cin // 32, dtype=torch.int32, device="cuda")
+    wpop = torch.empty(cout * taps, dtype=torch.int32, device="cuda")
+    wt2 = torch.empty_like(wt)
+    wf2 = torch.empty_like(wf)
+    assert L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt2.data_ptr(),
+                            wf2.data_ptr(), cout, taps, cin, st) == 0
+    torch.cuda.synchronize()
+    ref = torch.where(w >= 0, 1.0, -1.0)
+    assert torch.equal(wf.float(), ref.permute(1, 0, 2))
+    assert torch.equal(wt.float(), ref.permute(1, 2, 0))
+    assert torch.equal(wf, wf2) and torch.equal(wt, wt2)

@@ -86,3 +86,28 @@ def test_fused_stem_eval_matches():
         y = fused(x)
         y_ref = torch.nn.Sequential.forward(ref, x.float())
     assert _rel(y, y_ref) < 2e-2
+
+
+def test_fused_stem_sign_handoff_matches_sign_pack():
+    """With ``sign_clip`` the stem's last BN pass also emits the first binary
+    block's sign image and STE mask; they must equal zk_sign_pack of the
+    stem output bit for bit."""
+    from zookeeper_amd.ops._native import lib, stream_ptr
+
+    torch.manual_seed(2)
+    stem = _stem(True).cuda().to(memory_format=torch.channels_last)
+    stem.sign_clip = 0.75
+    x = torch.randn(3, 3, 64, 64, device="cuda").to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = stem(x)
+    clip, sx, mask = y._zk_sign
+    assert clip == 0.75
+    yn = y.permute(0, 2, 3, 1).contiguous()
+    nwords = yn.numel() // 32
+    ref_mask = torch.empty(nwords, dtype=torch.int32, device="cuda")
+    ref_sx = torch.empty_like(yn)
+    assert lib().zk_sign_pack(yn.data_ptr(), None, ref_mask.data_ptr(), ref_sx.data_ptr(),
+                              nwords, 0.75, stream_ptr(y.device)) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(sx.view(torch.int16), ref_sx.view(torch.int16))
+    assert torch.equal(mask, ref_mask)

@@ -129,6 +129,61 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restric
   }
 }
 
+// Tiled variant for the MFMA path (no bits): one block per (tap, 64 ci, 64
+// co) tile, staged through LDS so both the forward layout wf [T][Cout][Cin]
+// and the transposed dgrad layout wt [T][Cin][Cout] are written with
+// coalesced 16-B stores (the per-word kernel writes wt with 2-B scattered
+// stores at stride Cout).
+__global__ __launch_bounds__(256) void weight_pack_tiled_kernel(const float* __restrict__ w,
+                                                                uint16_t* __restrict__ wt,
+                                                                uint16_t* __restrict__ wf,
+                                                                int T, int Cin, int Cout) {
+  __shared__ uint16_t tile[64][64 + 8];  // [co][ci] +-1 bf16, padded rows
+  const int t = blockIdx.x, ci0 = blockIdx.y * 64, co0 = blockIdx.z * 64;
+  const int tid = threadIdx.x;
+  // load: 64 co rows x 64 ci (fp32) = 1024 float4; 4 per thread
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = tid + j * 256;
+    const int co = i / 16, c4 = (i % 16) * 4;
+    const float4 v =
+        *reinterpret_cast<const float4*>(w + ((long long)(co0 + co) * T + t) * Cin + ci0 + c4);
+    tile[co][c4 + 0] = v.x >= 0.f ? 0x3F80 : 0xBF80;
+    tile[co][c4 + 1] = v.y >= 0.f ? 0x3F80 : 0xBF80;
+    tile[co][c4 + 2] = v.z >= 0.f ? 0x3F80 : 0xBF80;
+    tile[co][c4 + 3] = v.w >= 0.f ? 0x3F80 : 0xBF80;
+  }
+  __syncthreads();
+  // wf[t][co][ci]: 64 rows x 128 B = 512 uint4; 2 per thread
+  if (wf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = tid + j * 256;
+      const int co = i / 8, c8 = (i % 8) * 8;
+      uint32_t u[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        u[k] = (uint32_t)tile[co][c8 + 2 * k] | ((uint32_t)tile[co][c8 + 2 * k + 1] << 16);
+      *reinterpret_cast<uint4*>(wf + ((long long)t * Cout + co0 + co) * Cin + ci0 + c8) =
+          make_uint4(u[0], u[1], u[2], u[3]);
+    }
+  }
+  // wt[t][ci][co]: transposed read of the tile
+  if (wt) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = tid + j * 256;
+      const int ci = i / 8, o8 = (i % 8) * 8;
+      uint32_t u[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        u[k] = (uint32_t)tile[o8 + 2 * k][ci] | ((uint32_t)tile[o8 + 2 * k + 1][ci] << 16);
+      *reinterpret_cast<uint4*>(wt + ((long long)t * Cin + ci0 + ci) * Cout + co0 + o8) =
+          make_uint4(u[0], u[1], u[2], u[3]);
+    }
+  }
+}
+
 // --------------------------------------------------------------------------
 // XNOR-popcount implicit-GEMM forward
 // --------------------------------------------------------------------------
@@ -387,6 +442,12 @@ ZK_EXPORT int zk_sign_pack(const void* x, void* bits, void* mask, void* xs, long
 ZK_EXPORT int zk_weight_pack(const void* w, void* wbits, void* wpop, void* wt, void* wf,
                              int Cout, int T, int Cin, hipStream_t stream) {
   if (Cin % 32) return (int)hipErrorInvalidValue;
+  if (!wbits && !wpop && Cin % 64 == 0 && Cout % 64 == 0) {
+    hipLaunchKernelGGL(weight_pack_tiled_kernel, dim3(T, Cin / 64, Cout / 64), dim3(256), 0,
+                       stream, (const float*)w, (uint16_t*)wt, (uint16_t*)wf, T, Cin, Cout);
+    ZK_CHECK_LAUNCH();
+    return 0;
+  }
   const long long nwords = (long long)Cout * T * (Cin / 32);
   if (wpop) hipMemsetAsync(wpop, 0, sizeof(int) * (size_t)Cout * T, stream);
   hipLaunchKernelGGL(weight_pack_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0,

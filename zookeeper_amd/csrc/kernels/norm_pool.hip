@@ -96,7 +96,10 @@ template <int CG>
 __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __restrict__ x,
                                                             const float* __restrict__ coef,
                                                             uint16_t* __restrict__ y, long long P,
-                                                            int relu) {
+                                                            int relu,
+                                                            uint16_t* __restrict__ sx = nullptr,
+                                                            uint8_t* __restrict__ smask = nullptr,
+                                                            float clip = 1.f) {
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;
   const int cg = threadIdx.x % CG;
@@ -115,7 +118,25 @@ __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __re
       v[k] = sc[k] * v[k] + sh[k];
       if (relu) v[k] = fmaxf(v[k], 0.f);
     }
-    store8_bf16(y + r * C + cg * 8, v);
+    const uint32_t ow[4] = {zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
+                            zk::pack_bf16x2(v[4], v[5]), zk::pack_bf16x2(v[6], v[7])};
+    *reinterpret_cast<uint4*>(y + r * C + cg * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    if (sx) {
+      // next binary layer's input quantisation from the stored bf16 values
+      // (same layout as batchnorm.hip's bn_apply_kernel / zk_sign_pack)
+      uint32_t sw[4];
+      uint32_t mk = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float lo = zk::bf16_to_f32((uint16_t)(ow[k] & 0xffff));
+        const float hi = zk::bf16_to_f32((uint16_t)(ow[k] >> 16));
+        sw[k] = (lo >= 0.f ? 0x3F80u : 0xBF80u) | ((hi >= 0.f ? 0x3F80u : 0xBF80u) << 16);
+        mk |= (uint32_t)(fabsf(lo) <= clip) << (2 * k);
+        mk |= (uint32_t)(fabsf(hi) <= clip) << (2 * k + 1);
+      }
+      *reinterpret_cast<uint4*>(sx + r * C + cg * 8) = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+      smask[r * CG + cg] = (uint8_t)mk;
+    }
   }
 }
 
@@ -404,6 +425,24 @@ ZK_EXPORT int zk_bn_apply_bf16(const void* x, const void* coef, void* y, long lo
   case cg:                                                                                 \
     hipLaunchKernelGGL(bn_apply_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,  \
                        (const uint16_t*)x, (const float*)coef, (uint16_t*)y, P, relu);     \
+    break;
+  ZK_CG_CASES(C, CASE)
+#undef CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// zk_bn_apply_bf16 + the next binary layer's sign image (bf16 +-1) and STE
+// mask bits (|y| <= clip), packed like zk_sign_pack's.
+ZK_EXPORT int zk_bn_apply_bf16_sign(const void* x, const void* coef, void* y, void* sx,
+                                    void* mask, float clip, long long P, int C, int relu,
+                                    hipStream_t st) {
+  if (C % 32) return (int)hipErrorInvalidValue;
+#define CASE(cg)                                                                           \
+  case cg:                                                                                 \
+    hipLaunchKernelGGL(bn_apply_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,  \
+                       (const uint16_t*)x, (const float*)coef, (uint16_t*)y, P, relu,      \
+                       (uint16_t*)sx, (uint8_t*)mask, clip);                               \
     break;
   ZK_CG_CASES(C, CASE)
 #undef CASE

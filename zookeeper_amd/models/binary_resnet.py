@@ -97,6 +97,8 @@ class BinaryResNetE(nn.Module):
                 BatchNorm(initial_filters, momentum=0.9, eps=1e-5),
             ]
         self.stem = ImageStem(*stem)
+        # the first binary block's ste_sign clip: the fused stem pre-quantises for it
+        self.stem.sign_clip = 1.0
         body = []
         cin = initial_filters
         for stage, (n, f) in enumerate(zip(blocks, filters)):

@@ -313,7 +313,13 @@ class ImageStem(nn.Sequential):
     :mod:`zookeeper_amd.ops.stem` (MFMA conv with BN statistics in its
     epilogue, BN+ReLU+pool in one pass, sparse pool backward); otherwise
     the modules run one after the other.
+
+    ``sign_clip``: when set (by a model whose next layer is a binary block
+    quantising its input with this clip value), the fused stem also emits
+    that block's sign image / STE mask in its final BN pass.
     """
+
+    sign_clip: Optional[float] = None
 
     def _fusable(self, x: torch.Tensor) -> bool:
         if not _use_native(x) or len(self) not in (3, 4):
@@ -341,5 +347,6 @@ class ImageStem(nn.Sequential):
 
             pool = self[2]
             return fused_stem(x, self[0], self[1], _pair(pool.pool_size)[0],
-                              _pair(pool.stride)[0], self[3] if len(self) == 4 else None)
+                              _pair(pool.stride)[0], self[3] if len(self) == 4 else None,
+                              sign_clip=self.sign_clip)
         return super().forward(x)

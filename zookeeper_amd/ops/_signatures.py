@@ -43,6 +43,7 @@ SIGNATURES = {
     "zk_bn_stats_bf16": (I32, [P, P, I64, I32, P]),
     "zk_bn_finalize_f64": (I32, [P, I32, C.c_double, P, P, F32, F32, P, P, P, P]),
     "zk_bn_apply_bf16": (I32, [P, P, P, I64, I32, I32, P]),
+    "zk_bn_apply_bf16_sign": (I32, [P, P, P, P, P, F32, I64, I32, I32, P]),
     "zk_bn_bwd_reduce_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
     "zk_bn_bwd_dx_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
     # depthwise convolution

@@ -20,6 +20,7 @@ not (``x.requires_grad`` is False).
 from __future__ import annotations
 
 import ctypes
+from typing import Optional
 
 import torch
 
@@ -72,7 +73,7 @@ def _bn_bwd_coef(L, st, sums, coef, gamma_p, beta_p, P, C, dev):
 class _StemFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, g1, b1, g2, b2, bn1, bn2, pool):
-        pk, ps = pool
+        pk, ps, sign_clip, holder = pool
         B, Cin, H, W = x.shape
         Cout, _, KH, KW = weight.shape
         s = 2
@@ -142,8 +143,17 @@ class _StemFn(torch.autograd.Function):
             else:
                 coef2 = _bn_eval_coef(bn2, Cout, dev)
             out = torch.empty_like(p)
-            check(L.zk_bn_apply_bf16(p.data_ptr(), coef2.data_ptr(), out.data_ptr(), P2, Cout, 0,
-                                     st), "zk_bn_apply_bf16")
+            if holder is not None and Cout % 32 == 0:
+                # also quantise the output for the first binary block
+                sx = torch.empty_like(p)
+                mask = torch.empty(P2 * Cout // 32, dtype=torch.int32, device=dev)
+                check(L.zk_bn_apply_bf16_sign(p.data_ptr(), coef2.data_ptr(), out.data_ptr(),
+                                              sx.data_ptr(), mask.data_ptr(), sign_clip, P2,
+                                              Cout, 0, st), "zk_bn_apply_bf16_sign")
+                holder[:] = [sign_clip, sx, mask]
+            else:
+                check(L.zk_bn_apply_bf16(p.data_ptr(), coef2.data_ptr(), out.data_ptr(), P2,
+                                         Cout, 0, st), "zk_bn_apply_bf16")
         ctx.save_for_backward(xp, y1, arg, p, coef1, coef2, g1, g2)
         ctx.params = (weight, g1, b1, g2, b2)
         ctx.geom = (B, Cin, Cout, KH, KW, s, Ho, Wo, Hp, Wp, H2, W2, pk, ps, pt2, pl2)
@@ -203,8 +213,18 @@ class _StemFn(torch.autograd.Function):
         return None, dweight, dg1, db1, dg2, db2, None, None, None
 
 
-def fused_stem(x: torch.Tensor, conv, bn1, pool_k: int = 3, pool_s: int = 2, bn2=None):
-    """``bn2(maxpool(relu(bn1(conv(x)))))`` with the fused stem kernels."""
-    return _StemFn.apply(x, conv.weight, bn1.weight, bn1.bias,
-                         bn2.weight if bn2 is not None else None,
-                         bn2.bias if bn2 is not None else None, bn1, bn2, (pool_k, pool_s))
+def fused_stem(x: torch.Tensor, conv, bn1, pool_k: int = 3, pool_s: int = 2, bn2=None,
+               sign_clip: Optional[float] = None):
+    """``bn2(maxpool(relu(bn1(conv(x)))))`` with the fused stem kernels.
+
+    With ``sign_clip`` (and ``bn2``) the final BN pass also writes the sign
+    image and STE mask (|y| <= sign_clip) of the output, attached as
+    ``_zk_sign`` for the first binary block (see ``ops.binary_block``)."""
+    holder = [] if (sign_clip is not None and bn2 is not None) else None
+    out = _StemFn.apply(x, conv.weight, bn1.weight, bn1.bias,
+                        bn2.weight if bn2 is not None else None,
+                        bn2.bias if bn2 is not None else None, bn1, bn2,
+                        (pool_k, pool_s, float(sign_clip or 0.0), holder))
+    if holder:
+        out._zk_sign = tuple(holder)
+    return out
