@@ -15,7 +15,9 @@
 
 namespace {
 
-__global__ void bn_finalize_kernel(const unsigned long long* __restrict__ stats, int C,
+// Consumers re-zero the accumulators they read (stats / sums), so callers can
+// keep one persistent zeroed buffer per layer instead of a fill per step.
+__global__ void bn_finalize_kernel(unsigned long long* __restrict__ stats, int C,
                                    double P, const float* __restrict__ gamma,
                                    const float* __restrict__ beta, float eps, float momentum,
                                    float* __restrict__ running_mean,
@@ -26,6 +28,8 @@ __global__ void bn_finalize_kernel(const unsigned long long* __restrict__ stats,
   if (c >= C) return;
   const double s1 = (double)(long long)stats[c];
   const double s2 = (double)(long long)stats[C + c];
+  stats[c] = 0;
+  stats[C + c] = 0;
   const double mean = s1 / P;
   double var = s2 / P - mean * mean;
   if (var < 0) var = 0;
@@ -204,7 +208,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint16_t* __restri
 // accumulated straight into the parameters' gradient buffers:
 //   sums = [sum g, sum g*yhat];  coef = [k1, k0, k3]
 //   dgamma += sum g*yhat,  dbeta += sum g
-__global__ void bn_bwd_coef_kernel(const float* __restrict__ sums, const float* __restrict__ mean,
+__global__ void bn_bwd_coef_kernel(float* __restrict__ sums, const float* __restrict__ mean,
                                    const float* __restrict__ rstd,
                                    const float* __restrict__ gamma, double P, int C,
                                    float* __restrict__ coef, float* __restrict__ dgamma,
@@ -212,6 +216,8 @@ __global__ void bn_bwd_coef_kernel(const float* __restrict__ sums, const float* 
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const float sg = sums[c], sgy = sums[C + c];
+  sums[c] = 0.f;
+  sums[C + c] = 0.f;
   const float rs = rstd[c];
   const float k1 = (gamma ? gamma[c] : 1.f) * rs;
   const float k3 = k1 * rs * (float)(sgy / P);
@@ -267,7 +273,7 @@ ZK_EXPORT int zk_bn_finalize(const void* stats, int C, double P, const void* gam
                              void* running_var, void* scale, void* shift, void* mean,
                              void* rstd, hipStream_t stream) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream,
-                     (const unsigned long long*)stats, C, P, (const float*)gamma,
+                     (unsigned long long*)stats, C, P, (const float*)gamma,
                      (const float*)beta, eps, momentum, (float*)running_mean,
                      (float*)running_var, (float*)scale, (float*)shift, (float*)mean,
                      (float*)rstd);
@@ -369,7 +375,7 @@ ZK_EXPORT int zk_bn_bwd_coef(const void* sums, const void* mean, const void* rst
                              const void* gamma, double P, int C, void* coef, void* dgamma,
                              void* dbeta, hipStream_t stream) {
   hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, stream,
-                     (const float*)sums, (const float*)mean, (const float*)rstd,
+                     (float*)sums, (const float*)mean, (const float*)rstd,
                      (const float*)gamma, P, C, (float*)coef, (float*)dgamma, (float*)dbeta);
   ZK_CHECK_LAUNCH();
   return 0;

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void bn_stats_bf16_kernel(const uint16_t* __re
   }
 }
 
-__global__ void bn_finalize_f64_kernel(const double* __restrict__ sums, int C, double P,
+__global__ void bn_finalize_f64_kernel(double* __restrict__ sums, int C, double P,
                                        const float* __restrict__ gamma,
                                        const float* __restrict__ beta, float eps, float momentum,
                                        float* __restrict__ rmean, float* __restrict__ rvar,
@@ -77,6 +77,8 @@ __global__ void bn_finalize_f64_kernel(const double* __restrict__ sums, int C, d
   if (c >= C) return;
   const double mean = sums[c] / P;
   double var = sums[C + c] / P - mean * mean;
+  sums[c] = 0.0;  // re-zeroed for the next use (persistent per-layer buffer)
+  sums[C + c] = 0.0;
   if (var < 0) var = 0;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
   const float g = gamma ? gamma[c] : 1.f;
@@ -412,7 +414,7 @@ ZK_EXPORT int zk_bn_finalize_f64(const void* sums, int C, double P, const void* 
                                  const void* beta, float eps, float momentum, void* rmean,
                                  void* rvar, void* coef, hipStream_t st) {
   hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
-                     (const double*)sums, C, P, (const float*)gamma, (const float*)beta, eps,
+                     (double*)sums, C, P, (const float*)gamma, (const float*)beta, eps,
                      momentum, (float*)rmean, (float*)rvar, (float*)coef);
   ZK_CHECK_LAUNCH();
   return 0;

@@ -153,6 +153,12 @@ class QuantConv2d(nn.Module):
 
             if depthwise.supported(x, self.weight):
                 return depthwise.depthwise_conv3x3(x, self.weight, self.stride[0], self.padding)
+        if (self.input_quantizer is None and self.kernel_quantizer is None
+                and self.kernel_size == (1, 1) and _use_native(x)):
+            from zookeeper_amd.ops import pointwise
+
+            if pointwise.supported(x, self.weight, self.stride, self.groups):
+                return pointwise.conv1x1(x, self.weight, self.bias)
         if self.input_quantizer is not None:
             x = self.input_quantizer(x)
         if self.padding == "same":

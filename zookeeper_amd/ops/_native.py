@@ -109,6 +109,23 @@ def direct_grad(p, channels_last: bool = False):
     return g
 
 
+def zeroed_scratch(owner, name: str, shape, dtype: torch.dtype,
+                   device: torch.device) -> torch.Tensor:
+    """A persistent accumulator kept on ``owner`` (a module), zero when handed
+    out.  Only for accumulators whose consuming kernel re-zeroes them after
+    reading (BN ``stats`` → ``zk_bn_finalize`` / ``zk_bn_finalize_f64``,
+    BN-backward ``sums`` → ``zk_bn_bwd_coef``): that replaces a fill kernel
+    per layer and step.  The owner's ``__dict__`` holds it, so it is not
+    part of ``state_dict``."""
+    cache = owner.__dict__.setdefault("_zk_scratch", {})
+    shape = tuple(shape)
+    buf = cache.get(name)
+    if buf is None or buf.shape != shape or buf.dtype != dtype or buf.device != device:
+        buf = torch.zeros(shape, dtype=dtype, device=device)
+        cache[name] = buf
+    return buf
+
+
 def grad_ready(p) -> None:
     """Tell the data-parallel bucketer that ``p``'s gradient is complete."""
     cb = getattr(p, "_zk_grad_ready", None)

@@ -32,7 +32,8 @@ from typing import Optional
 import torch
 
 from zookeeper_amd.nn.layers import same_padding
-from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
+from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
+                                        zeroed_scratch)
 
 
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
@@ -88,7 +89,9 @@ class _BinaryBlockFn(torch.autograd.Function):
 
         P = B * Ho * Wo
         y = torch.empty((B, Ho, Wo, Cout), dtype=torch.int16, device=dev)
-        stats = torch.zeros((2, Cout), dtype=torch.int64, device=dev)
+        # persistent accumulator, re-zeroed by zk_bn_finalize (eval: no finalize)
+        stats = (zeroed_scratch(bn, "stats_i64", (2, Cout), torch.int64, dev) if bn.training
+                 else torch.zeros((2, Cout), dtype=torch.int64, device=dev))
         if mfma:
             check(L.zk_igemm_fwd(sx.data_ptr(), wf.data_ptr(), y.data_ptr(), stats.data_ptr(), B,
                                  H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(pad_ones),
@@ -140,6 +143,7 @@ class _BinaryBlockFn(torch.autograd.Function):
         ctx.params = (weight, gamma, beta)
         ctx.geom = (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo)
         ctx.meta = meta
+        ctx.bn = bn
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
         ctx.has_residual = residual is not None and not identity
         return out.permute(0, 3, 1, 2)
@@ -156,7 +160,7 @@ class _BinaryBlockFn(torch.autograd.Function):
 
         g = _nhwc(dout.to(torch.bfloat16))
         weight_p, gamma_p, beta_p = ctx.params
-        sums = torch.zeros((2, Cout), dtype=torch.float32, device=dev)
+        sums = zeroed_scratch(ctx.bn, "bwd_sums", (2, Cout), torch.float32, dev)
         check(L.zk_bn_bwd_reduce(g.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                                  sums.data_ptr(), P, Cout, st), "zk_bn_bwd_reduce")
         # BN coefficients + gamma/beta gradients in one launch; gradients go

@@ -10,7 +10,8 @@ from __future__ import annotations
 import torch
 
 from zookeeper_amd.nn.layers import same_padding
-from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
+from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
+                                        zeroed_scratch)
 
 
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
@@ -38,7 +39,7 @@ class _BatchNormFn(torch.autograd.Function):
         L = lib()
         coef = torch.empty((4, C), dtype=torch.float32, device=dev)
         if bn.training:
-            sums = torch.zeros((2, C), dtype=torch.float64, device=dev)
+            sums = zeroed_scratch(bn, "stats_f64", (2, C), torch.float64, dev)
             check(L.zk_bn_stats_bf16(xn.data_ptr(), sums.data_ptr(), P, C, st), "zk_bn_stats_bf16")
             check(L.zk_bn_finalize_f64(sums.data_ptr(), C, float(P),
                                        gamma.data_ptr() if gamma is not None else None,
@@ -60,6 +61,7 @@ class _BatchNormFn(torch.autograd.Function):
         ctx.save_for_backward(xn, y if relu else None, coef, gamma)
         ctx.params = (gamma, beta)
         ctx.dim, ctx.P, ctx.C = dim, P, C
+        ctx.bn = bn
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
         return _back(y, dim)
 
@@ -71,7 +73,7 @@ class _BatchNormFn(torch.autograd.Function):
         st = stream_ptr(dev)
         L = lib()
         g = _nhwc(dy.to(torch.bfloat16))
-        sums = torch.zeros((2, C), dtype=torch.float32, device=dev)
+        sums = zeroed_scratch(ctx.bn, "bwd_sums", (2, C), torch.float32, dev)
         check(L.zk_bn_bwd_reduce_bf16(g.data_ptr(), xn.data_ptr(),
                                       y.data_ptr() if y is not None else None,
                                       coef.data_ptr(), sums.data_ptr(), P, C, st),

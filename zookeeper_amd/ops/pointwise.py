@@ -1,0 +1,134 @@
+"""1×1 (pointwise) float convolution as implicit GEMMs on the MFMA kernels.
+
+A 1×1 stride-1 convolution over an NHWC (channels_last) activation is the
+GEMM ``[P, Cin] × [Cin, Cout]`` with ``P = B·H·W`` — no im2col, no layout
+change.  The binary-conv kernels of ``igemm.hip`` are plain bf16 MFMA
+GEMMs underneath, so they run these float GEMMs directly:
+
+forward   ``y = x · Wᵀ``: the dgrad kernel with its roles renamed (act = x,
+          "weights" = W as [N = Cout][K = Cin]), bf16 out;
+backward  ``dx = dy · W``: the dgrad kernel proper (weights Wᵀ [Cin][Cout]);
+          ``dW += dyᵀ · x``: the split-K weight-gradient kernel with the clip
+          mask disabled (clip = +inf), accumulated in fp32 straight into the
+          flat gradient buffer.
+
+Shapes whose channel counts do not tile by 64, or with a bias, go to plain
+bf16 GEMMs (hipBLASLt via ``torch.mm``; the weight gradient with
+``out_dtype=float32``).  MIOpen would run them as generic implicit GEMMs plus
+separate bias / zero / cast kernels.
+
+Used by BinaryResNet-E's downsampling shortcuts (AvgPool → 1×1 conv → BN),
+QuickNet's transition 1×1 convs and ResNet-50's bottleneck 1×1 convs
+(stride 1).  The reference has no kernels of its own; the
+float convs it delegates to Keras are covered by this + MIOpen.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
+
+_INF = float("inf")
+
+
+def supported(x: torch.Tensor, weight: torch.Tensor, stride, groups: int) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and weight.dim() == 4 and weight.shape[2:] == (1, 1) and groups == 1
+            and tuple(stride) == (1, 1) and x.shape[1] == weight.shape[1])
+
+
+def _rows(x: torch.Tensor) -> torch.Tensor:
+    """[B, C, H, W] (any layout) → contiguous [B·H·W, C] (a view when the
+    input is channels_last)."""
+    xn = x.permute(0, 2, 3, 1)
+    if not xn.is_contiguous():
+        xn = xn.contiguous()
+    return xn.reshape(-1, x.shape[1])
+
+
+def _mfma_ok(Cin: int, Cout: int, P: int, bias) -> bool:
+    return bias is None and Cin % 64 == 0 and Cout % 64 == 0 and P < (1 << 24)
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        B, Cin, H, W = x.shape
+        Cout = weight.shape[0]
+        x2 = _rows(x)
+        w2 = weight.detach().reshape(Cout, Cin).to(torch.bfloat16)
+        mfma = _mfma_ok(Cin, Cout, x2.shape[0], bias)
+        if mfma:
+            y2 = torch.empty((x2.shape[0], Cout), dtype=torch.bfloat16, device=x.device)
+            # dgrad kernel, roles renamed: N = Cout ("Cin"), K = Cin ("Cout")
+            check(lib().zk_igemm_dgrad(x2.data_ptr(), w2.data_ptr(), None, None, y2.data_ptr(),
+                                       B, H, W, Cout, H, W, Cin, 1, 1, 1, 0, 0, -1,
+                                       stream_ptr(x.device)), "zk_igemm_dgrad(1x1 fwd)")
+        elif bias is not None:
+            y2 = torch.addmm(bias.detach().to(torch.bfloat16), x2, w2.t())
+        else:
+            y2 = torch.mm(x2, w2.t())
+        ctx.save_for_backward(x2, w2)
+        ctx.params = (weight, bias)
+        ctx.shape = (B, Cin, H, W, Cout)
+        ctx.mfma = mfma
+        return y2.view(B, H, W, Cout).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2, w2 = ctx.saved_tensors
+        weight, bias = ctx.params
+        B, Cin, H, W, Cout = ctx.shape
+        g2 = _rows(dout.to(torch.bfloat16))
+        dev = g2.device
+        dx = dweight = dbias = None
+        if ctx.needs_input_grad[0]:
+            if ctx.mfma:
+                dx2 = torch.empty((g2.shape[0], Cin), dtype=torch.bfloat16, device=dev)
+                wt = w2.t().contiguous()  # [Cin][Cout]
+                check(lib().zk_igemm_dgrad(g2.data_ptr(), wt.data_ptr(), None, None,
+                                           dx2.data_ptr(), B, H, W, Cin, H, W, Cout, 1, 1, 1,
+                                           0, 0, -1, stream_ptr(dev)), "zk_igemm_dgrad(1x1)")
+            else:
+                dx2 = torch.mm(g2, w2)
+            dx = dx2.view(B, H, W, Cin).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            target = direct_grad(weight)
+            if ctx.mfma:
+                dw = target.view(Cout, Cin) if target is not None else torch.zeros(
+                    (Cout, Cin), dtype=torch.float32, device=dev)
+                L = lib()
+                ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Cout, 1, 1, 1, 0, -1)
+                ws = (torch.empty(ws_bytes // 4, dtype=torch.float32, device=dev)
+                      if ws_bytes > 0 else None)
+                wf = weight.detach().reshape(Cout, Cin)
+                if wf.dtype != torch.float32 or not wf.is_contiguous():
+                    wf = wf.float().contiguous()
+                check(L.zk_igemm_wgrad(g2.data_ptr(), x2.data_ptr(), wf.data_ptr(), dw.data_ptr(),
+                                       B, H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0, 0, _INF, 0, -1,
+                                       ws.data_ptr() if ws is not None else None,
+                                       max(ws_bytes, 0), stream_ptr(dev)),
+                      "zk_igemm_wgrad(1x1)")
+                if target is None:
+                    dweight = dw.view(Cout, Cin, 1, 1)
+            elif target is not None:
+                t2 = target.view(Cout, Cin)
+                torch.ops.aten.addmm.dtype_out(t2, g2.t(), x2, torch.float32, out=t2)
+            else:
+                dweight = torch.ops.aten.mm.dtype(g2.t(), x2, torch.float32).view(
+                    Cout, Cin, 1, 1)
+            if target is not None:
+                grad_ready(weight)
+        if bias is not None and ctx.needs_input_grad[2]:
+            dbias = g2.float().sum(0)
+        return dx, dweight, dbias
+
+
+def conv1x1(x: torch.Tensor, weight: torch.Tensor,
+            bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``F.conv2d(x, weight, bias)`` for a 1×1 stride-1 kernel, as GEMMs.
+    Returns a channels_last bf16 tensor."""
+    return _Conv1x1Fn.apply(x, weight, bias)

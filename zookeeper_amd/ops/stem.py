@@ -25,7 +25,8 @@ from typing import Optional
 import torch
 
 from zookeeper_amd.nn.layers import same_padding
-from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
+from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
+                                        zeroed_scratch)
 
 
 def supported(x: torch.Tensor, conv, bn1, pool_k: int, pool_s: int) -> bool:
@@ -158,6 +159,7 @@ class _StemFn(torch.autograd.Function):
         ctx.params = (weight, g1, b1, g2, b2)
         ctx.geom = (B, Cin, Cout, KH, KW, s, Ho, Wo, Hp, Wp, H2, W2, pk, ps, pt2, pl2)
         ctx.has_bn2 = bn2 is not None
+        ctx.bn2 = bn2
         return out.permute(0, 3, 1, 2)
 
     @staticmethod
@@ -172,7 +174,7 @@ class _StemFn(torch.autograd.Function):
         g = dout.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
         dg2 = db2 = None
         if ctx.has_bn2:
-            sums2 = torch.zeros((2, Cout), dtype=torch.float32, device=dev)
+            sums2 = zeroed_scratch(ctx.bn2, "bwd_sums", (2, Cout), torch.float32, dev)
             check(L.zk_bn_bwd_reduce_bf16(g.data_ptr(), p.data_ptr(), None, coef2.data_ptr(),
                                           sums2.data_ptr(), P2, Cout, st), "zk_bn_bwd_reduce_bf16")
             bcoef2, dg2, db2 = _bn_bwd_coef(L, st, sums2, coef2, g2p, b2p, P2, Cout, dev)
