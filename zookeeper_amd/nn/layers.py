@@ -21,6 +21,7 @@ i.e. physically OHWI — the layout the HIP implicit-GEMM kernels consume.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple, Union
 
 import torch
@@ -34,6 +35,11 @@ IntPair = Union[int, Tuple[int, int]]
 
 def _pair(v: IntPair) -> Tuple[int, int]:
     return (v, v) if isinstance(v, int) else tuple(v)  # type: ignore[return-value]
+
+
+# 1x1 convs as MFMA / hipBLASLt GEMMs (ops/pointwise.py); ZK_PW_GEMM=0 keeps
+# them on the library convolution (A/B measurements)
+_PW_GEMM = os.environ.get("ZK_PW_GEMM", "1") != "0"
 
 
 def _use_native(x: torch.Tensor) -> bool:
@@ -154,11 +160,11 @@ class QuantConv2d(nn.Module):
             if depthwise.supported(x, self.weight):
                 return depthwise.depthwise_conv3x3(x, self.weight, self.stride[0], self.padding)
         if (self.input_quantizer is None and self.kernel_quantizer is None
-                and self.kernel_size == (1, 1) and _use_native(x)):
+                and self.kernel_size == (1, 1) and _PW_GEMM and _use_native(x)):
             from zookeeper_amd.ops import pointwise
 
-            if pointwise.supported(x, self.weight, self.stride, self.groups):
-                return pointwise.conv1x1(x, self.weight, self.bias)
+            if pointwise.supported(x, self.weight, self.stride, self.groups, self.bias):
+                return pointwise.conv1x1(x, self.weight)
         if self.input_quantizer is not None:
             x = self.input_quantizer(x)
         if self.padding == "same":

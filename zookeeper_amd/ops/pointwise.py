@@ -12,10 +12,9 @@ backward  ``dx = dy · W``: the dgrad kernel proper (weights Wᵀ [Cin][Cout]);
           mask disabled (clip = +inf), accumulated in fp32 straight into the
           flat gradient buffer.
 
-Shapes whose channel counts do not tile by 64, or with a bias, go to plain
-bf16 GEMMs (hipBLASLt via ``torch.mm``; the weight gradient with
-``out_dtype=float32``).  MIOpen would run them as generic implicit GEMMs plus
-separate bias / zero / cast kernels.
+Shapes whose channel counts do not tile by 64, or with a bias, stay on the
+library convolution (``supported`` is False): as plain hipBLASLt GEMMs
+their weight gradient (K = B·H·W, tiny M·N) measured up to 10× slower.
 
 Used by BinaryResNet-E's downsampling shortcuts (AvgPool → 1×1 conv → BN),
 QuickNet's transition 1×1 convs and ResNet-50's bottleneck 1×1 convs
@@ -34,10 +33,13 @@ from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, strea
 _INF = float("inf")
 
 
-def supported(x: torch.Tensor, weight: torch.Tensor, stride, groups: int) -> bool:
+def supported(x: torch.Tensor, weight: torch.Tensor, stride, groups: int,
+              bias: Optional[torch.Tensor] = None) -> bool:
     return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
             and weight.dim() == 4 and weight.shape[2:] == (1, 1) and groups == 1
-            and tuple(stride) == (1, 1) and x.shape[1] == weight.shape[1])
+            and tuple(stride) == (1, 1) and x.shape[1] == weight.shape[1]
+            and bias is None and x.shape[1] % 64 == 0 and weight.shape[0] % 64 == 0
+            and x.shape[0] * x.shape[2] * x.shape[3] < (1 << 24))
 
 
 def _rows(x: torch.Tensor) -> torch.Tensor:
@@ -49,86 +51,63 @@ def _rows(x: torch.Tensor) -> torch.Tensor:
     return xn.reshape(-1, x.shape[1])
 
 
-def _mfma_ok(Cin: int, Cout: int, P: int, bias) -> bool:
-    return bias is None and Cin % 64 == 0 and Cout % 64 == 0 and P < (1 << 24)
-
-
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight):
         B, Cin, H, W = x.shape
         Cout = weight.shape[0]
         x2 = _rows(x)
         w2 = weight.detach().reshape(Cout, Cin).to(torch.bfloat16)
-        mfma = _mfma_ok(Cin, Cout, x2.shape[0], bias)
-        if mfma:
-            y2 = torch.empty((x2.shape[0], Cout), dtype=torch.bfloat16, device=x.device)
-            # dgrad kernel, roles renamed: N = Cout ("Cin"), K = Cin ("Cout")
-            check(lib().zk_igemm_dgrad(x2.data_ptr(), w2.data_ptr(), None, None, y2.data_ptr(),
-                                       B, H, W, Cout, H, W, Cin, 1, 1, 1, 0, 0, -1,
-                                       stream_ptr(x.device)), "zk_igemm_dgrad(1x1 fwd)")
-        elif bias is not None:
-            y2 = torch.addmm(bias.detach().to(torch.bfloat16), x2, w2.t())
-        else:
-            y2 = torch.mm(x2, w2.t())
+        y2 = torch.empty((x2.shape[0], Cout), dtype=torch.bfloat16, device=x.device)
+        # dgrad kernel, roles renamed: N = Cout ("Cin"), K = Cin ("Cout")
+        check(lib().zk_igemm_dgrad(x2.data_ptr(), w2.data_ptr(), None, None, y2.data_ptr(),
+                                   B, H, W, Cout, H, W, Cin, 1, 1, 1, 0, 0, -1,
+                                   stream_ptr(x.device)), "zk_igemm_dgrad(1x1 fwd)")
         ctx.save_for_backward(x2, w2)
-        ctx.params = (weight, bias)
+        ctx.weight = weight
         ctx.shape = (B, Cin, H, W, Cout)
-        ctx.mfma = mfma
         return y2.view(B, H, W, Cout).permute(0, 3, 1, 2)
 
     @staticmethod
     def backward(ctx, dout):
         x2, w2 = ctx.saved_tensors
-        weight, bias = ctx.params
+        weight = ctx.weight
         B, Cin, H, W, Cout = ctx.shape
         g2 = _rows(dout.to(torch.bfloat16))
         dev = g2.device
-        dx = dweight = dbias = None
+        L = lib()
+        st = stream_ptr(dev)
+        dx = dweight = None
         if ctx.needs_input_grad[0]:
-            if ctx.mfma:
-                dx2 = torch.empty((g2.shape[0], Cin), dtype=torch.bfloat16, device=dev)
-                wt = w2.t().contiguous()  # [Cin][Cout]
-                check(lib().zk_igemm_dgrad(g2.data_ptr(), wt.data_ptr(), None, None,
-                                           dx2.data_ptr(), B, H, W, Cin, H, W, Cout, 1, 1, 1,
-                                           0, 0, -1, stream_ptr(dev)), "zk_igemm_dgrad(1x1)")
-            else:
-                dx2 = torch.mm(g2, w2)
+            dx2 = torch.empty((g2.shape[0], Cin), dtype=torch.bfloat16, device=dev)
+            wt = w2.t().contiguous()  # [Cin][Cout]
+            check(L.zk_igemm_dgrad(g2.data_ptr(), wt.data_ptr(), None, None, dx2.data_ptr(), B,
+                                   H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0, -1, st),
+                  "zk_igemm_dgrad(1x1)")
             dx = dx2.view(B, H, W, Cin).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             target = direct_grad(weight)
-            if ctx.mfma:
-                dw = target.view(Cout, Cin) if target is not None else torch.zeros(
-                    (Cout, Cin), dtype=torch.float32, device=dev)
-                L = lib()
-                ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Cout, 1, 1, 1, 0, -1)
-                ws = (torch.empty(ws_bytes // 4, dtype=torch.float32, device=dev)
-                      if ws_bytes > 0 else None)
-                wf = weight.detach().reshape(Cout, Cin)
-                if wf.dtype != torch.float32 or not wf.is_contiguous():
-                    wf = wf.float().contiguous()
-                check(L.zk_igemm_wgrad(g2.data_ptr(), x2.data_ptr(), wf.data_ptr(), dw.data_ptr(),
-                                       B, H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0, 0, _INF, 0, -1,
-                                       ws.data_ptr() if ws is not None else None,
-                                       max(ws_bytes, 0), stream_ptr(dev)),
-                      "zk_igemm_wgrad(1x1)")
-                if target is None:
-                    dweight = dw.view(Cout, Cin, 1, 1)
-            elif target is not None:
-                t2 = target.view(Cout, Cin)
-                torch.ops.aten.addmm.dtype_out(t2, g2.t(), x2, torch.float32, out=t2)
-            else:
-                dweight = torch.ops.aten.mm.dtype(g2.t(), x2, torch.float32).view(
-                    Cout, Cin, 1, 1)
+            dw = target.view(Cout, Cin) if target is not None else torch.zeros(
+                (Cout, Cin), dtype=torch.float32, device=dev)
+            ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Cout, 1, 1, 1, 0, -1)
+            ws = (torch.empty(ws_bytes // 4, dtype=torch.float32, device=dev)
+                  if ws_bytes > 0 else None)
+            wf = weight.detach().reshape(Cout, Cin)
+            if wf.dtype != torch.float32 or not wf.is_contiguous():
+                wf = wf.float().contiguous()
+            # clip = +inf: the kernel's |w| <= clip gradient mask is all-pass
+            check(L.zk_igemm_wgrad(g2.data_ptr(), x2.data_ptr(), wf.data_ptr(), dw.data_ptr(), B,
+                                   H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0, 0, _INF, 0, -1,
+                                   ws.data_ptr() if ws is not None else None, max(ws_bytes, 0),
+                                   st), "zk_igemm_wgrad(1x1)")
             if target is not None:
                 grad_ready(weight)
-        if bias is not None and ctx.needs_input_grad[2]:
-            dbias = g2.float().sum(0)
-        return dx, dweight, dbias
+            else:
+                dweight = dw.view(Cout, Cin, 1, 1)
+        return dx, dweight
 
 
-def conv1x1(x: torch.Tensor, weight: torch.Tensor,
-            bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``F.conv2d(x, weight, bias)`` for a 1×1 stride-1 kernel, as GEMMs.
-    Returns a channels_last bf16 tensor."""
-    return _Conv1x1Fn.apply(x, weight, bias)
+def conv1x1(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """``F.conv2d(x, weight)`` for a 1×1 stride-1 kernel (see ``supported``),
+    as MFMA implicit GEMMs.  Returns a channels_last bf16 tensor."""
+    return _Conv1x1Fn.apply(x, weight)
