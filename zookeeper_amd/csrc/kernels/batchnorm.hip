@@ -130,17 +130,34 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     sg[k] = 0.f;
     sgy[k] = 0.f;
   }
-  for (long long r = (long long)blockIdx.x * RB + r0; r < P; r += (long long)gridDim.x * RB) {
-    const long long off = r * C + cg * 8;
-    const uint4 gv = *reinterpret_cast<const uint4*>(g + off);
-    const uint4 yv = *reinterpret_cast<const uint4*>(y + off);
-    const uint32_t gg[4] = {gv.x, gv.y, gv.z, gv.w};
-    const int16_t* yy = reinterpret_cast<const int16_t*>(&yv);
+  // UR rows per thread in flight per iteration (loads first, then math):
+  // one 16-B load pair per iteration left HBM latency-bound (~3.7 TB/s)
+  constexpr int UR = 4;
+  const long long rstep = (long long)gridDim.x * RB;
+  for (long long r = (long long)blockIdx.x * RB + r0; r < P; r += UR * rstep) {
+    uint4 gv[UR], yv[UR];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float gk = zk::bf16_to_f32((uint16_t)(gg[k >> 1] >> (16 * (k & 1))));
-      sg[k] += gk;
-      sgy[k] += gk * ((float)yy[k] - mu[k]) * rs[k];
+    for (int u = 0; u < UR; ++u) {
+      const long long ru = r + u * rstep;
+      gv[u] = make_uint4(0, 0, 0, 0);
+      yv[u] = make_uint4(0, 0, 0, 0);
+      if (ru < P) {
+        const long long off = ru * C + cg * 8;
+        gv[u] = *reinterpret_cast<const uint4*>(g + off);
+        yv[u] = *reinterpret_cast<const uint4*>(y + off);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UR; ++u) {
+      // rows past P loaded zeros: g = 0 adds nothing to either sum
+      const uint32_t gg[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
+      const int16_t* yy = reinterpret_cast<const int16_t*>(&yv[u]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gk = zk::bf16_to_f32((uint16_t)(gg[k >> 1] >> (16 * (k & 1))));
+        sg[k] += gk;
+        sgy[k] += gk * ((float)yy[k] - mu[k]) * rs[k];
+      }
     }
   }
   __shared__ float red[2][256][9];
@@ -335,7 +352,9 @@ ZK_EXPORT int zk_bn_apply_sign(const void* y, const void* scale, const void* shi
 
 ZK_EXPORT int zk_bn_bwd_reduce(const void* g, const void* y, const void* mean, const void* rstd,
                                void* sums, long long P, int C, hipStream_t stream) {
-  const int blocks = 1024;
+  // 512 blocks x 4 rows in flight per thread: enough bytes in flight for
+  // HBM, few enough per-block atomics into the 2*C sums
+  const int blocks = 512;
 #define ZK_RED_CASE(cg)                                                                   \
   case cg:                                                                                \
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<cg>, dim3(blocks), dim3(256), 0, stream,      \

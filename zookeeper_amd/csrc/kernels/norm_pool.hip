@@ -40,14 +40,25 @@ __global__ __launch_bounds__(256) void bn_stats_bf16_kernel(const uint16_t* __re
   constexpr int RB = 256 / CG;
   const int cg = threadIdx.x % CG;
   float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
-       r += (long long)gridDim.x * RB) {
-    float v[8];
-    load8_bf16(x + r * C + cg * 8, v);
+  constexpr int UR = 4;  // rows in flight per thread (loads first, then math)
+  const long long rstep = (long long)gridDim.x * RB;
+  for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P; r += UR * rstep) {
+    uint4 q[UR];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      s1[k] += v[k];
-      s2[k] += v[k] * v[k];
+    for (int u = 0; u < UR; ++u) {
+      const long long ru = r + u * rstep;
+      q[u] = ru < P ? *reinterpret_cast<const uint4*>(x + ru * C + cg * 8)
+                    : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < UR; ++u) {
+      const uint32_t w4[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float v = zk::bf16_to_f32((uint16_t)(w4[k >> 1] >> (16 * (k & 1))));
+        s1[k] += v;
+        s2[k] += v * v;
+      }
     }
   }
   __shared__ float red[2][256][9];
@@ -157,21 +168,35 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
     rs[k] = coef[3 * C + cg * 8 + k];
     sg[k] = sgx[k] = 0.f;
   }
-  for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
-       r += (long long)gridDim.x * RB) {
-    float gv[8], xv[8];
-    load8_bf16(g + r * C + cg * 8, gv);
-    load8_bf16(x + r * C + cg * 8, xv);
-    if (y) {  // fused ReLU: gradient only where the output was positive
-      float yv[8];
-      load8_bf16(y + r * C + cg * 8, yv);
+  constexpr int UR = 4;  // rows in flight per thread (loads first, then math)
+  const long long rstep = (long long)gridDim.x * RB;
+  for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P; r += UR * rstep) {
+    uint4 gq[UR], xq[UR], yq[UR];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+    for (int u = 0; u < UR; ++u) {
+      const long long ru = r + u * rstep;
+      const bool in = ru < P;
+      const long long off = ru * C + cg * 8;
+      gq[u] = in ? *reinterpret_cast<const uint4*>(g + off) : make_uint4(0, 0, 0, 0);
+      xq[u] = in ? *reinterpret_cast<const uint4*>(x + off) : make_uint4(0, 0, 0, 0);
+      // fused ReLU: gradient only where the output was positive
+      yq[u] = (in && y) ? *reinterpret_cast<const uint4*>(y + off)
+                        : make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      sg[k] += gv[k];
-      sgx[k] += gv[k] * (xv[k] - mu[k]) * rs[k];
+    for (int u = 0; u < UR; ++u) {
+      const uint32_t g4[4] = {gq[u].x, gq[u].y, gq[u].z, gq[u].w};
+      const uint32_t x4[4] = {xq[u].x, xq[u].y, xq[u].z, xq[u].w};
+      const uint32_t y4[4] = {yq[u].x, yq[u].y, yq[u].z, yq[u].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int sh = 16 * (k & 1);
+        float gk = zk::bf16_to_f32((uint16_t)(g4[k >> 1] >> sh));
+        const float xk = zk::bf16_to_f32((uint16_t)(x4[k >> 1] >> sh));
+        if (!(zk::bf16_to_f32((uint16_t)(y4[k >> 1] >> sh)) > 0.f)) gk = 0.f;
+        sg[k] += gk;
+        sgx[k] += gk * (xk - mu[k]) * rs[k];
+      }
     }
   }
   __shared__ float red[2][256][9];
@@ -372,6 +397,13 @@ int rows_grid(long long P, int C) {
   return b < 1 ? 1 : (int)b;
 }
 
+// reductions: fewer blocks (each with 4 rows in flight per thread) so the
+// per-block atomics into the 2*C accumulators do not serialise
+int red_grid(long long P, int C) {
+  const int b = rows_grid(P, C);
+  return b > 512 ? 512 : b;
+}
+
 int flat_grid(long long work) {
   long long b = (work + 255) / 256;
   if (b > 16384) b = 16384;
@@ -400,7 +432,7 @@ ZK_EXPORT int zk_bn_stats_bf16(const void* x, void* sums, long long P, int C, hi
   if (C % 8) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                           \
   case cg:                                                                                 \
-    hipLaunchKernelGGL(bn_stats_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,  \
+    hipLaunchKernelGGL(bn_stats_bf16_kernel<cg>, dim3(red_grid(P, C)), dim3(256), 0, st,   \
                        (const uint16_t*)x, (double*)sums, P);                              \
     break;
   ZK_CG_CASES(C, CASE)
@@ -458,7 +490,7 @@ ZK_EXPORT int zk_bn_bwd_reduce_bf16(const void* g, const void* x, const void* y,
   if (C % 8) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                              \
   case cg:                                                                                    \
-    hipLaunchKernelGGL(bn_bwd_reduce_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st, \
+    hipLaunchKernelGGL(bn_bwd_reduce_bf16_kernel<cg>, dim3(red_grid(P, C)), dim3(256), 0, st, \
                        (const uint16_t*)g, (const uint16_t*)x, (const uint16_t*)y,            \
                        (const float*)coef, (float*)sums, P);                                  \
     break;
