@@ -34,13 +34,13 @@ def test_dgrad_wgrad(cin, cout, stride, hw, pad_ones):
     bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
     mask = torch.empty(nwords, dtype=torch.int32, device="cuda")
     sx = torch.empty_like(x)
-    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), sx.data_ptr(), nwords,
+    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), sx.data_ptr(), None, nwords,
                           1.0, st) == 0
     assert torch.equal(sx.float(), torch.where(x.float() >= 0, 1.0, -1.0))
     wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
     wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
     wt = torch.empty(9, cin, cout, dtype=torch.bfloat16, device="cuda")
-    assert L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(), None,
+    assert L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(), None, None,
                             cout, 9, cin, st) == 0
     dres = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
     dx = torch.empty(B, hw, hw, cin, dtype=torch.bfloat16, device="cuda")
@@ -91,13 +91,13 @@ def test_igemm_dgrad_matches_reference(variant, cin, cout, stride, hw):
     bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
     mask = torch.empty(nwords, dtype=torch.int32, device="cuda")
     sx = torch.empty_like(x)
-    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), sx.data_ptr(), nwords,
+    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), sx.data_ptr(), None, nwords,
                           1.0, st) == 0
     assert torch.equal(sx.float(), torch.where(x.float() >= 0, 1.0, -1.0))
     wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
     wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
     wt = torch.empty(9, cin, cout, dtype=torch.bfloat16, device="cuda")
-    assert L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(), None,
+    assert L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(), None, None,
                             cout, 9, cin, st) == 0
     dres = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
     dx = torch.full((B, hw, hw, cin), float("nan"), dtype=torch.bfloat16, device="cuda")
@@ -144,7 +144,7 @@ def test_igemm_wgrad_matches_reference(variant, cin, cout, stride, hw, pad_ones,
     nwords = x.numel() // 32
     bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
     sx = torch.empty_like(x)
-    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), None, sx.data_ptr(), nwords, 1.0,
+    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), None, sx.data_ptr(), None, nwords, 1.0,
                           st) == 0
     dw = torch.full((cout, 3, 3, cin), 0.25, device="cuda")  # accumulates into dw
     ws = None
@@ -190,14 +190,14 @@ def test_igemm_fwd_matches_reference(variant, cin, cout, stride, hw, pad_ones, r
     nwords = x.numel() // 32
     mask = torch.empty(nwords, dtype=torch.int32, device="cuda")
     sx = torch.empty_like(x)
-    assert L.zk_sign_pack(x.data_ptr(), None, mask.data_ptr(), sx.data_ptr(), nwords, 1.0,
+    assert L.zk_sign_pack(x.data_ptr(), None, mask.data_ptr(), sx.data_ptr(), None, nwords, 1.0,
                           st) == 0
     wf = torch.empty(9, cout, cin, dtype=torch.bfloat16, device="cuda")
-    assert L.zk_weight_pack(w.data_ptr(), None, None, None, wf.data_ptr(), cout, 9, cin, st) == 0
+    assert L.zk_weight_pack(w.data_ptr(), None, None, None, wf.data_ptr(), None, cout, 9, cin, st) == 0
     y = torch.full((B, ho, ho, cout), -12345, dtype=torch.int16, device="cuda")
     stats = torch.zeros(2, cout, dtype=torch.int64, device="cuda")
     rc = L.zk_igemm_fwd(sx.data_ptr(), wf.data_ptr(), y.data_ptr(), stats.data_ptr(), B, hw, hw,
-                        cin, cout, 3, 3, stride, pt, pt, ho, ho, pad_ones, relu, variant, st)
+                        cin, cout, 3, 3, stride, pt, pt, ho, ho, pad_ones, relu, variant, 1, st)
     if rc != 0:
         pytest.skip("tile does not divide this shape")
     torch.cuda.synchronize()
@@ -225,14 +225,14 @@ def test_weight_pack_tiled_matches_per_word(cout, taps, cin):
     w[0, 0, :8] = 0.0  # sign(0) = +1
     wf = torch.empty(taps, cout, cin, dtype=torch.bfloat16, device="cuda")
     wt = torch.empty(taps, cin, cout, dtype=torch.bfloat16, device="cuda")
-    assert L.zk_weight_pack(w.data_ptr(), None, None, wt.data_ptr(), wf.data_ptr(), cout, taps,
+    assert L.zk_weight_pack(w.data_ptr(), None, None, wt.data_ptr(), wf.data_ptr(), None, cout, taps,
                             cin, st) == 0
     wbits = torch.empty(cout * taps * cin // 32, dtype=torch.int32, device="cuda")
     wpop = torch.empty(cout * taps, dtype=torch.int32, device="cuda")
     wt2 = torch.empty_like(wt)
     wf2 = torch.empty_like(wf)
     assert L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt2.data_ptr(),
-                            wf2.data_ptr(), cout, taps, cin, st) == 0
+                            wf2.data_ptr(), None, cout, taps, cin, st) == 0
     torch.cuda.synchronize()
     ref = torch.where(w >= 0, 1.0, -1.0)
     assert torch.equal(wf.float(), ref.permute(1, 0, 2))

@@ -113,10 +113,10 @@ def test_bconv_forward_exact_integers():
         st = stream_ptr()
         nwords = x.numel() // 32
         bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
-        L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), None, None, nwords, 1.0, st)
+        L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), None, None, None, nwords, 1.0, st)
         wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
         wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
-        L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), None, None, cout, 9,
+        L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), None, None, None, cout, 9,
                          cin, st)
         from zookeeper_amd.nn.layers import same_padding
         pt, pb = same_padding(hw, 3, stride)

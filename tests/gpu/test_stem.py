@@ -100,14 +100,17 @@ def test_fused_stem_sign_handoff_matches_sign_pack():
     x = torch.randn(3, 3, 64, 64, device="cuda").to(torch.bfloat16)
     x = x.contiguous(memory_format=torch.channels_last)
     y = stem(x)
-    clip, sx, mask = y._zk_sign
+    clip, sx, mask, sx4 = y._zk_sign
     assert clip == 0.75
     yn = y.permute(0, 2, 3, 1).contiguous()
     nwords = yn.numel() // 32
     ref_mask = torch.empty(nwords, dtype=torch.int32, device="cuda")
     ref_sx = torch.empty_like(yn)
+    ref_sx4 = torch.empty(yn.shape[:3] + (yn.shape[3] // 2,), dtype=torch.uint8, device="cuda")
     assert lib().zk_sign_pack(yn.data_ptr(), None, ref_mask.data_ptr(), ref_sx.data_ptr(),
-                              nwords, 0.75, stream_ptr(y.device)) == 0
+                              ref_sx4.data_ptr(), nwords, 0.75, stream_ptr(y.device)) == 0
     torch.cuda.synchronize()
     assert torch.equal(sx.view(torch.int16), ref_sx.view(torch.int16))
     assert torch.equal(mask, ref_mask)
+    if sx4 is not None:
+        assert torch.equal(sx4, ref_sx4)

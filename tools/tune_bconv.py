@@ -23,6 +23,7 @@ WG_VARIANTS = 8
 IG_VARIANTS = list(range(15)) + list(range(20, 28))
 IGW_VARIANTS = 13
 IGF_VARIANTS = list(range(15)) + list(range(20, 28))
+IGF4_VARIANTS = [-1] + list(range(10)) + list(range(20, 29))
 
 
 def timeit(fn, reps):
@@ -62,17 +63,17 @@ def main():
         bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
         mask = torch.empty_like(bits)
         sx = torch.empty_like(x)
-        L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), sx.data_ptr(), nwords, 1.0,
+        L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), mask.data_ptr(), sx.data_ptr(), None, nwords, 1.0,
                        st)
         wbits = torch.empty(cout * 9 * cin // 32, dtype=torch.int32, device="cuda")
         wpop = torch.empty(cout * 9, dtype=torch.int32, device="cuda")
         wt = torch.empty(9, cin, cout, dtype=torch.bfloat16, device="cuda")
-        L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(), None, cout,
+        L.zk_weight_pack(w.data_ptr(), wbits.data_ptr(), wpop.data_ptr(), wt.data_ptr(), None, None, cout,
                          9, cin, st)
         dx = torch.empty_like(x)
         dw = torch.zeros(cout, 3, 3, cin, device="cuda")
         y = torch.empty(B, Ho, Ho, cout, dtype=torch.int16, device="cuda")
-        stats = torch.zeros(2, cout, dtype=torch.int64, device="cuda")
+        stats = torch.zeros(32, 2, cout, dtype=torch.int64, device="cuda")  # striped
         flops = 2.0 * B * Ho * Ho * cout * 9 * cin
         row = {"shape": [H, W, cin, cout, s], "gflop": flops / 1e9}
         if "fwd" in fam:
@@ -81,7 +82,7 @@ def main():
                 B, H, W, cin, cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, st), args.reps)
         if "igf" in fam:
             wf = torch.empty(9, cout, cin, dtype=torch.bfloat16, device="cuda")
-            L.zk_weight_pack(w.data_ptr(), None, None, None, wf.data_ptr(), cout, 9, cin, st)
+            L.zk_weight_pack(w.data_ptr(), None, None, None, wf.data_ptr(), None, cout, 9, cin, st)
             yref = None
             if "fwd" in fam:
                 stats.zero_()
@@ -93,7 +94,7 @@ def main():
             for v in IGF_VARIANTS:
                 y.zero_()
                 rc = L.zk_igemm_fwd(sx.data_ptr(), wf.data_ptr(), y.data_ptr(), stats.data_ptr(),
-                                    B, H, W, cin, cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, v, st)
+                                    B, H, W, cin, cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, v, 32, st)
                 torch.cuda.synchronize()
                 if rc != 0:
                     row[f"igf_v{v}_us"] = None
@@ -102,7 +103,32 @@ def main():
                     row[f"igf_v{v}_exact"] = bool(torch.equal(y, yref))
                 row[f"igf_v{v}_us"] = timeit(lambda: L.zk_igemm_fwd(
                     sx.data_ptr(), wf.data_ptr(), y.data_ptr(), stats.data_ptr(), B, H, W, cin,
-                    cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, v, st), args.reps)
+                    cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, v, 32, st), args.reps)
+        if "igf4" in fam:
+            # MX-FP4 forward: e2m1 sign images, every variant checked against
+            # the default one bit for bit
+            sx4 = torch.empty(B, H, W, cin // 2, dtype=torch.uint8, device="cuda")
+            L.zk_sign_pack(x.data_ptr(), None, None, None, sx4.data_ptr(), nwords, 1.0, st)
+            wf4 = torch.empty(9, cout, cin // 2, dtype=torch.uint8, device="cuda")
+            L.zk_weight_pack(w.data_ptr(), None, None, None, None, wf4.data_ptr(), cout, 9, cin,
+                             st)
+            yref4 = None
+            for v in IGF4_VARIANTS:
+                y.zero_()
+                rc = L.zk_igemm_fwd_fp4(sx4.data_ptr(), wf4.data_ptr(), y.data_ptr(),
+                                        stats.data_ptr(), B, H, W, cin, cout, 3, 3, s, pt, pt, Ho,
+                                        Ho, 0, 0, v, 32, st)
+                torch.cuda.synchronize()
+                if rc != 0:
+                    row[f"igf4_v{v}_us"] = None
+                    continue
+                if yref4 is None:
+                    yref4 = y.clone()
+                else:
+                    row[f"igf4_v{v}_exact"] = bool(torch.equal(y, yref4))
+                row[f"igf4_v{v}_us"] = timeit(lambda: L.zk_igemm_fwd_fp4(
+                    sx4.data_ptr(), wf4.data_ptr(), y.data_ptr(), stats.data_ptr(), B, H, W, cin,
+                    cout, 3, 3, s, pt, pt, Ho, Ho, 0, 0, v, 32, st), args.reps)
         ref_dx = None
         for v in (range(DG_VARIANTS) if ("dgrad" in fam or "igemm" in fam) else ()):
             if "dgrad" not in fam and v != 7:

@@ -38,6 +38,11 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
 }
 
+// sign(v) as an e2m1 (FP4) nibble: +1 = 0x2 for v >= 0, -1 = 0xA otherwise.
+// Sign images pack two channels per byte, the even channel in the low nibble
+// (the operands of the MX-FP4 binary forward, igemm.hip).
+__device__ __forceinline__ uint32_t fp4_sign(float v) { return v >= 0.f ? 0x2u : 0xAu; }
+
 // splitmix64-style hash for per-example random decisions (flip, crops).
 __device__ __forceinline__ uint32_t hash_u32(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;

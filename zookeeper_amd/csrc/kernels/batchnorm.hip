@@ -17,19 +17,32 @@ namespace {
 
 // Consumers re-zero the accumulators they read (stats / sums), so callers can
 // keep one persistent zeroed buffer per layer instead of a fill per step.
-__global__ void bn_finalize_kernel(unsigned long long* __restrict__ stats, int C,
-                                   double P, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, float eps, float momentum,
-                                   float* __restrict__ running_mean,
-                                   float* __restrict__ running_var, float* __restrict__ scale,
-                                   float* __restrict__ shift, float* __restrict__ mean_out,
-                                   float* __restrict__ rstd_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const double s1 = (double)(long long)stats[c];
-  const double s2 = (double)(long long)stats[C + c];
-  stats[c] = 0;
-  stats[C + c] = 0;
+// stats: [stripes][2][C] exact int64 copies (the conv epilogues spread their
+// atomics over them).  A group of 32 lanes owns one channel: lane k sums
+// copies k, k+32, ... and the group reduces with cross-lane shuffles.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(
+    unsigned long long* __restrict__ stats, int C, int stripes, double P,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    float* __restrict__ running_mean, float* __restrict__ running_var, float* __restrict__ scale,
+    float* __restrict__ shift, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int k = threadIdx.x & 31;
+  const int c = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (c >= C) return;  // uniform over the 32-lane group
+  long long t1 = 0, t2 = 0;
+  for (int j = k; j < stripes; j += 32) {
+    t1 += (long long)stats[(2LL * j) * C + c];
+    t2 += (long long)stats[(2LL * j + 1) * C + c];
+    stats[(2LL * j) * C + c] = 0;
+    stats[(2LL * j + 1) * C + c] = 0;
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    t1 += __shfl_xor(t1, o, 32);
+    t2 += __shfl_xor(t2, o, 32);
+  }
+  if (k != 0) return;
+  const double s1 = (double)t1;
+  const double s2 = (double)t2;
   const double mean = s1 / P;
   double var = s2 / P - mean * mean;
   if (var < 0) var = 0;
@@ -60,7 +73,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const int16_t* __restrict
                                                        long long P,
                                                        uint16_t* __restrict__ sx = nullptr,
                                                        uint8_t* __restrict__ smask = nullptr,
-                                                       float clip = 1.f) {
+                                                       float clip = 1.f,
+                                                       uint32_t* __restrict__ sx4 = nullptr) {
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;
   const int cg = threadIdx.x % CG;
@@ -90,12 +104,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const int16_t* __restrict
     const uint4 ov = make_uint4(zk::pack_bf16x2(o[0], o[1]), zk::pack_bf16x2(o[2], o[3]),
                                 zk::pack_bf16x2(o[4], o[5]), zk::pack_bf16x2(o[6], o[7]));
     reinterpret_cast<uint4*>(out)[i] = ov;
-    if (sx) {
+    if (sx || sx4) {
       // the NEXT binary block's input quantisation, from the stored bf16
-      // values: sign image (bf16 +-1) and STE mask bits (|x| <= clip)
+      // values: sign image (bf16 +-1 for the weight gradient, e2m1 nibbles
+      // for the MX-FP4 forward) and STE mask bits (|x| <= clip)
       const uint32_t ow[4] = {ov.x, ov.y, ov.z, ov.w};
       uint32_t sw[4];
-      uint32_t mk = 0;
+      uint32_t mk = 0, n4 = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float lo = zk::bf16_to_f32((uint16_t)(ow[k] & 0xffff));
@@ -103,9 +118,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const int16_t* __restrict
         sw[k] = (lo >= 0.f ? 0x3F80u : 0xBF80u) | ((hi >= 0.f ? 0x3F80u : 0xBF80u) << 16);
         mk |= (uint32_t)(fabsf(lo) <= clip) << (2 * k);
         mk |= (uint32_t)(fabsf(hi) <= clip) << (2 * k + 1);
+        n4 |= (zk::fp4_sign(lo) | (zk::fp4_sign(hi) << 4)) << (8 * k);
       }
-      reinterpret_cast<uint4*>(sx)[i] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
-      smask[i] = (uint8_t)mk;  // byte i = channels 8i..8i+7 of the packed mask words
+      if (sx) reinterpret_cast<uint4*>(sx)[i] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+      if (smask) smask[i] = (uint8_t)mk;  // byte i = channels 8i..8i+7 of the packed mask words
+      if (sx4) sx4[i] = n4;               // 8 channels = 4 bytes of the [P][C/2] e2m1 image
     }
   }
 }
@@ -285,12 +302,14 @@ int grid_for(long long work, int cap = 4096) {
 
 }  // namespace
 
-ZK_EXPORT int zk_bn_finalize(const void* stats, int C, double P, const void* gamma,
+// stats: [stripes][2][C] int64 (sum, sum of squares), re-zeroed here.
+ZK_EXPORT int zk_bn_finalize(const void* stats, int C, int stripes, double P, const void* gamma,
                              const void* beta, float eps, float momentum, void* running_mean,
                              void* running_var, void* scale, void* shift, void* mean,
                              void* rstd, hipStream_t stream) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream,
-                     (unsigned long long*)stats, C, P, (const float*)gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 7) / 8), dim3(256), 0, stream,
+                     (unsigned long long*)stats, C, stripes < 1 ? 1 : stripes, P,
+                     (const float*)gamma,
                      (const float*)beta, eps, momentum, (float*)running_mean,
                      (float*)running_var, (float*)scale, (float*)shift, (float*)mean,
                      (float*)rstd);
@@ -332,17 +351,18 @@ ZK_EXPORT int zk_bn_apply(const void* y, const void* scale, const void* shift, c
 }
 
 // zk_bn_apply + the next binary layer's input quantisation (sign image sx
-// bf16 +-1 and STE mask bits |out| <= clip, packed like zk_sign_pack's).
+// bf16 +-1, STE mask bits |out| <= clip and the e2m1 sign image sx4, packed
+// like zk_sign_pack's; each optional).
 ZK_EXPORT int zk_bn_apply_sign(const void* y, const void* scale, const void* shift,
-                               const void* res, void* out, void* sx, void* mask, float clip,
-                               long long P, int C, hipStream_t stream) {
+                               const void* res, void* out, void* sx, void* mask, void* sx4,
+                               float clip, long long P, int C, hipStream_t stream) {
   if (C % 32) return (int)hipErrorInvalidValue;
 #define ZK_APPLY_CASE(cg)                                                                   \
   case cg:                                                                                  \
     hipLaunchKernelGGL(bn_apply_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, stream,    \
                        (const int16_t*)y, (const float*)scale, (const float*)shift,         \
                        (const uint16_t*)res, (uint16_t*)out, P, (uint16_t*)sx,              \
-                       (uint8_t*)mask, clip);                                               \
+                       (uint8_t*)mask, clip, (uint32_t*)sx4);                               \
     break;
   ZK_CG_SWITCH(C, ZK_APPLY_CASE)
 #undef ZK_APPLY_CASE

@@ -43,16 +43,18 @@ __global__ __launch_bounds__(256) void sign_pack_kernel(const uint16_t* __restri
                                                         uint32_t* __restrict__ bits,
                                                         uint32_t* __restrict__ mask,
                                                         uint16_t* __restrict__ xs,
+                                                        uint4* __restrict__ xs4,
                                                         long long nwords, float clip) {
   for (long long w = blockIdx.x * (long long)blockDim.x + threadIdx.x; w < nwords;
        w += (long long)gridDim.x * blockDim.x) {
     const uint4* src = reinterpret_cast<const uint4*>(x + 32 * w);
-    uint32_t b = 0, mk = 0;
+    uint32_t b = 0, mk = 0, n4[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       uint4 v = src[q];
       uint32_t u[4] = {v.x, v.y, v.z, v.w};
       uint32_t o[4];
+      n4[q] = 0;
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
         o[h] = 0;
@@ -63,6 +65,7 @@ __global__ __launch_bounds__(256) void sign_pack_kernel(const uint16_t* __restri
           b |= (uint32_t)(f >= 0.f) << i;
           mk |= (uint32_t)(fabsf(f) <= clip) << i;
           o[h] |= (f >= 0.f ? 0x3F80u : 0xBF80u) << (16 * s);
+          n4[q] |= zk::fp4_sign(f) << (4 * (h * 2 + s));
         }
       }
       // sign(x) as bf16 +-1: the operand of the MFMA weight gradient
@@ -70,6 +73,8 @@ __global__ __launch_bounds__(256) void sign_pack_kernel(const uint16_t* __restri
     }
     if (bits) bits[w] = b;
     if (mask) mask[w] = mk;
+    // sign(x) as e2m1 nibbles: the operand of the MX-FP4 forward
+    if (xs4) xs4[w] = make_uint4(n4[0], n4[1], n4[2], n4[3]);
   }
 }
 
@@ -133,10 +138,12 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restric
 // co) tile, staged through LDS so both the forward layout wf [T][Cout][Cin]
 // and the transposed dgrad layout wt [T][Cin][Cout] are written with
 // coalesced 16-B stores (the per-word kernel writes wt with 2-B scattered
-// stores at stride Cout).
+// stores at stride Cout); wf4 is the forward layout as e2m1 nibbles
+// [T][Cout][Cin/2] for the MX-FP4 forward.
 __global__ __launch_bounds__(256) void weight_pack_tiled_kernel(const float* __restrict__ w,
                                                                 uint16_t* __restrict__ wt,
                                                                 uint16_t* __restrict__ wf,
+                                                                uint8_t* __restrict__ wf4,
                                                                 int T, int Cin, int Cout) {
   __shared__ uint16_t tile[64][64 + 8];  // [co][ci] +-1 bf16, padded rows
   const int t = blockIdx.x, ci0 = blockIdx.y * 64, co0 = blockIdx.z * 64;
@@ -167,6 +174,21 @@ __global__ __launch_bounds__(256) void weight_pack_tiled_kernel(const float* __r
       *reinterpret_cast<uint4*>(wf + ((long long)t * Cout + co0 + co) * Cin + ci0 + c8) =
           make_uint4(u[0], u[1], u[2], u[3]);
     }
+  }
+  // wf4[t][co][ci/2]: 64 rows x 32 B = 128 uint4
+  if (wf4 && tid < 128) {
+    const int co = tid >> 1, hf = tid & 1;
+    uint32_t u[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t nb = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        nb |= ((tile[co][hf * 32 + 8 * k + e] & 0x8000u) ? 0xAu : 0x2u) << (4 * e);
+      u[k] = nb;
+    }
+    *reinterpret_cast<uint4*>(wf4 + (((long long)t * Cout + co0 + co) * Cin + ci0) / 2 +
+                              hf * 16) = make_uint4(u[0], u[1], u[2], u[3]);
   }
   // wt[t][ci][co]: transposed read of the tile
   if (wt) {
@@ -430,21 +452,27 @@ int grid_for(long long work, int per_block = 256, int cap = 16384) {
 
 }  // namespace
 
-ZK_EXPORT int zk_sign_pack(const void* x, void* bits, void* mask, void* xs, long long nwords,
-                           float clip, hipStream_t stream) {
+// xs: bf16 +-1 image (optional), xs4: e2m1 +-1 image [.][C/2] (optional).
+ZK_EXPORT int zk_sign_pack(const void* x, void* bits, void* mask, void* xs, void* xs4,
+                           long long nwords, float clip, hipStream_t stream) {
   hipLaunchKernelGGL(sign_pack_kernel, dim3(grid_for(nwords)), dim3(256), 0, stream,
                      (const uint16_t*)x, (uint32_t*)bits, (uint32_t*)mask, (uint16_t*)xs,
-                     nwords, clip);
+                     (uint4*)xs4, nwords, clip);
   ZK_CHECK_LAUNCH();
   return 0;
 }
 
+// wf4 (e2m1 forward layout) needs the tiled path: no bit outputs, Cin and
+// Cout multiples of 64.
 ZK_EXPORT int zk_weight_pack(const void* w, void* wbits, void* wpop, void* wt, void* wf,
-                             int Cout, int T, int Cin, hipStream_t stream) {
+                             void* wf4, int Cout, int T, int Cin, hipStream_t stream) {
   if (Cin % 32) return (int)hipErrorInvalidValue;
-  if (!wbits && !wpop && Cin % 64 == 0 && Cout % 64 == 0) {
+  const bool tiled = !wbits && !wpop && Cin % 64 == 0 && Cout % 64 == 0;
+  if (wf4 && !tiled) return (int)hipErrorInvalidValue;
+  if (tiled) {
     hipLaunchKernelGGL(weight_pack_tiled_kernel, dim3(T, Cin / 64, Cout / 64), dim3(256), 0,
-                       stream, (const float*)w, (uint16_t*)wt, (uint16_t*)wf, T, Cin, Cout);
+                       stream, (const float*)w, (uint16_t*)wt, (uint16_t*)wf, (uint8_t*)wf4, T,
+                       Cin, Cout);
     ZK_CHECK_LAUNCH();
     return 0;
   }

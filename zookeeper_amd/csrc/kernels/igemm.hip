@@ -51,18 +51,20 @@ struct ConvArgs {
   const uint32_t* mask;  // dgrad: STE mask bits of x (optional)
   const uint16_t* dres;  // dgrad: residual gradient (optional)
   void* out;             // dgrad: dx bf16 / fwd: y int16
-  unsigned long long* stats;  // fwd: [2][Cout] int64 (sum, sum of squares)
+  unsigned long long* stats;  // fwd: [stripes][2][Cout] int64 (sum, sum of squares)
   int pad_ones, relu;    // fwd
+  int stripes;           // fwd: copies of the statistics; block b adds into copy b % stripes
 };
 
-template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB>
+template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB, bool F4 = false>
 __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs args, IGeom g,
                                                                      int m_tiles) {
   constexpr int NWAVES = WM * WN;
-  // CB = bytes of K per row per stage (128 = 64 bf16, or 64)
+  // CB = bytes of K per row per stage (128 = 64 bf16, 64, or 32)
   constexpr int SPR = CB / 16;            // 16-B slots per row
   constexpr int RPI = 1024 / CB;          // rows per wave-instruction
-  constexpr int SH = (CB == 128) ? 1 : 2; // swizzle shift (see header)
+  constexpr int SH = (CB == 128) ? 1 : (CB == 64) ? 2 : 3;  // swizzle shift (see header)
+  static_assert(!F4 || FWD, "e2m1 operands: the +-1 x +-1 forward only");
   constexpr int A_INS = BM / RPI / NWAVES;  // glds per wave per stage
   constexpr int B_INS = BN / RPI / NWAVES;
   static_assert(A_INS >= 1 && B_INS >= 1 && BM % (RPI * NWAVES) == 0 &&
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
   const int th0 = FWD ? 0 : (ph + g.pt) % s, tw0 = FWD ? 0 : (pw + g.pl) % s;
   const int nth = (g.kh - th0 + ts - 1) / ts, ntw = (g.kw - tw0 + ts - 1) / ts;
   const int T = nth * ntw;
-  const int RB = KCH * 2;              // bytes per activation / weight row
+  const int RB = F4 ? KCH / 2 : KCH * 2;  // bytes per activation / weight row
   const int kchunks = RB / CB;
   const int NK = T * kchunks;
 
@@ -118,7 +120,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
   const unsigned char* wtb = reinterpret_cast<const unsigned char*>(args.wgt);
   const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
   const unsigned char* padp =
-      (FWD && args.pad_ones) ? reinterpret_cast<const unsigned char*>(g_ones_page_bf16) : zp;
+      (FWD && args.pad_ones)
+          ? (F4 ? reinterpret_cast<const unsigned char*>(g_ones_page_fp4)
+                : reinterpret_cast<const unsigned char*>(g_ones_page_bf16))
+          : zp;
   const unsigned char* a_base[A_INS];  // tap-0 source (may point outside: masked)
   const unsigned char* a_pad[A_INS];   // padding page (+ swizzled slot)
   uint32_t a_hm[A_INS], a_wm[A_INS];
@@ -263,7 +268,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
         for (int b = 0; b < TN; ++b)
           // fwd: D[pixel][co] (lane = channel: in-lane BN statistics);
           // dgrad: D[ci][pixel] (lane = pixel: 8-B mask/residual epilogue)
-          acc[a][b] = FWD ? mfma_bf16(af[cs][a], bfr[cs][b], acc[a][b])
+          acc[a][b] = FWD ? (F4 ? mfma_fp4(af[cs][a], bfr[cs][b], acc[a][b])
+                                : mfma_bf16(af[cs][a], bfr[cs][b], acc[a][b]))
                           : mfma_bf16(bfr[cs][b], af[cs][a], acc[a][b]);
     }
   }
@@ -307,6 +313,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
       }
     }
     __syncthreads();
+    // striped copies: thousands of blocks adding into one [2][Cout] array
+    // serialise on its cache lines (the stage-1 forward was bound by it)
+    const int stripe = args.stripes > 1 ? (int)(blockIdx.x % args.stripes) : 0;
+    unsigned long long* st_out = args.stats + (long long)stripe * 2 * g.Cout;
     for (int c = tid; c < 2 * BN; c += NWAVES * 64) {
       const int which = c / BN, nl = c % BN;
       long long tot = 0;
@@ -315,7 +325,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
         const int v = red[(i * 2 + which) * BN + nl];
         tot += which ? (long long)(unsigned int)v : (long long)v;  // squares: unsigned
       }
-      atomicAdd(args.stats + which * g.Cout + n0 + nl, (unsigned long long)tot);
+      atomicAdd(st_out + which * g.Cout + n0 + nl, (unsigned long long)tot);
     }
   } else {
     // ---- dgrad epilogue: lane = pixel, 4 consecutive channels per group
@@ -371,11 +381,12 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
 // unconditionally and their fragments zeroed per lane (validity bit masks).
 //   FWD:  q = m + (th-1)*W + (tw-1)       DGRAD: q = m + (1-th)*W + (1-tw)
 // ===========================================================================
-template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB>
+template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB, bool F4 = false>
 __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs args, IGeom g,
                                                                       int m_tiles) {
   constexpr int NWAVES = WM * WN;
-  constexpr int SPR = CB / 16, RPI = 1024 / CB, SH = (CB == 128) ? 1 : 2;
+  constexpr int SPR = CB / 16, RPI = 1024 / CB, SH = (CB == 128) ? 1 : (CB == 64) ? 2 : 3;
+  static_assert(!F4 || FWD, "e2m1 operands: the +-1 x +-1 forward only");
   constexpr int A_INS = (BM + 2 + RPI * NWAVES - 1) / (RPI * NWAVES);  // glds per wave
   constexpr int AR = A_INS * RPI * NWAVES;                             // A rows staged
   constexpr int B_INS = 3 * BN / RPI / NWAVES;
@@ -399,7 +410,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
   const long long m0 = (long long)mtile * BM;
   if (m0 >= M) return;
   const int n0 = ntile * BN;
-  const int RB = KCH * 2, kchunks = RB / CB, NK = 3 * kchunks;
+  const int RB = F4 ? KCH / 2 : KCH * 2, kchunks = RB / CB, NK = 3 * kchunks;
   const unsigned char* actb = reinterpret_cast<const unsigned char*>(args.act);
   const unsigned char* wtb = reinterpret_cast<const unsigned char*>(args.wgt);
   const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
@@ -453,7 +464,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
   };
   (void)padp;
   // value of a padding tap's fragment: 0, or bf16 +1 pairs for pad_values=1
-  const uint32_t padv = (FWD && args.pad_ones) ? 0x3F803F80u : 0u;
+  const uint32_t padv = (FWD && args.pad_ones) ? (F4 ? 0x22222222u : 0x3F803F80u) : 0u;
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -512,7 +523,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b)
-          acc[a][b] = FWD ? mfma_bf16(af[cs][a], bfr[cs][b], acc[a][b])
+          acc[a][b] = FWD ? (F4 ? mfma_fp4(af[cs][a], bfr[cs][b], acc[a][b])
+                                : mfma_bf16(af[cs][a], bfr[cs][b], acc[a][b]))
                           : mfma_bf16(bfr[cs][b], af[cs][a], acc[a][b]);
     }
   }
@@ -553,6 +565,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
       }
     }
     __syncthreads();
+    const int stripe = args.stripes > 1 ? (int)(blockIdx.x % args.stripes) : 0;
+    unsigned long long* st_out = args.stats + (long long)stripe * 2 * g.Cout;
     for (int c = tid; c < 2 * BN; c += NWAVES * 64) {
       const int which = c / BN, nl = c % BN;
       long long tot = 0;
@@ -561,7 +575,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
         const int v = red[(i * 2 + which) * BN + nl];
         tot += which ? (long long)(unsigned int)v : (long long)v;
       }
-      atomicAdd(args.stats + which * g.Cout + n0 + nl, (unsigned long long)tot);
+      atomicAdd(st_out + which * g.Cout + n0 + nl, (unsigned long long)tot);
     }
   } else {
     // ---- dgrad epilogue (stride 1: the pixel index is the row index)
@@ -606,15 +620,16 @@ bool conv3_ok(const IGeom& g, int /*pad_ones: handled on the fragments*/) {
          g.Wo == g.W;
 }
 
-template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB>
+template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB, bool F4 = false>
 int launch_conv3(const ConvArgs& args, const IGeom& g, hipStream_t stream) {
   const int NCH = FWD ? g.Cout : g.Cin, KCH = FWD ? g.Cin : g.Cout;
-  if ((KCH * 2) % CB || NCH % BN || !conv3_ok(g, args.pad_ones)) return (int)hipErrorInvalidValue;
+  const int RB = F4 ? KCH / 2 : KCH * 2;
+  if (RB % CB || NCH % BN || !conv3_ok(g, args.pad_ones)) return (int)hipErrorInvalidValue;
   constexpr int NW = WM * WN, RPI = 1024 / CB;
   constexpr int AR = (BM + 2 + RPI * NW - 1) / (RPI * NW) * RPI * NW;
   constexpr int LDS = NS * (AR + 3 * BN) * CB;
   static_assert(LDS <= 160 * 1024, "LDS");
-  auto kern = igemm_conv3_kernel<FWD, BM, BN, WM, WN, NS, CB>;
+  auto kern = igemm_conv3_kernel<FWD, BM, BN, WM, WN, NS, CB, F4>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -649,19 +664,20 @@ int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const v
   const int m_tiles = (int)((Mc + BM - 1) / BM);
   const long long blocks = (long long)m_tiles * (g.Cin / BN);
   ConvArgs args{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
-                (const uint16_t*)dres, dx, nullptr, 0, 0};
+                (const uint16_t*)dres, dx, nullptr, 0, 0, 1};
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, g.s * g.s), dim3(WM * WN * 64), LDS, stream,
                      args, g, m_tiles);
   return 0;
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int CB = 128>
+template <int BM, int BN, int WM, int WN, int NS, int CB = 128, bool F4 = false>
 int launch_igemm_fwd(const void* sx, const void* wf, void* y, void* stats, const IGeom& g,
-                     int pad_ones, int relu, hipStream_t stream) {
-  if ((g.Cin * 2) % CB || g.Cout % BN) return (int)hipErrorInvalidValue;
+                     int pad_ones, int relu, int stripes, hipStream_t stream) {
+  const int RB = F4 ? g.Cin / 2 : g.Cin * 2;
+  if (RB % CB || g.Cout % BN) return (int)hipErrorInvalidValue;
   constexpr int LDS = NS * (BM + BN) * CB;
   static_assert(LDS <= 160 * 1024, "LDS");
-  auto kern = igemm_conv_kernel<true, BM, BN, WM, WN, NS, CB>;
+  auto kern = igemm_conv_kernel<true, BM, BN, WM, WN, NS, CB, F4>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -673,15 +689,15 @@ int launch_igemm_fwd(const void* sx, const void* wf, void* y, void* stats, const
   const int m_tiles = (int)((Mo + BM - 1) / BM);
   const long long blocks = (long long)m_tiles * (g.Cout / BN);
   ConvArgs args{(const uint16_t*)sx, (const uint16_t*)wf, nullptr, nullptr, y,
-                (unsigned long long*)stats, pad_ones, relu};
+                (unsigned long long*)stats, pad_ones, relu, stripes};
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, 1), dim3(WM * WN * 64), LDS, stream, args, g,
                      m_tiles);
   return 0;
 }
 
 int igemm_fwd_variant(int v, const void* sx, const void* wf, void* y, void* stats,
-                      const IGeom& g, int po, int relu, hipStream_t st) {
-#define ZK_IGF(...) return launch_igemm_fwd<__VA_ARGS__>(sx, wf, y, stats, g, po, relu, st)
+                      const IGeom& g, int po, int relu, int ns, hipStream_t st) {
+#define ZK_IGF(...) return launch_igemm_fwd<__VA_ARGS__>(sx, wf, y, stats, g, po, relu, ns, st)
   switch (v) {
     case 0: ZK_IGF(128, 128, 2, 2, 2);
     case 1: ZK_IGF(128, 128, 2, 2, 4, 64);
@@ -701,7 +717,7 @@ int igemm_fwd_variant(int v, const void* sx, const void* wf, void* y, void* stat
 #define ZK_IGF3(...)                                                                    \
   {                                                                                     \
     ConvArgs a{(const uint16_t*)sx, (const uint16_t*)wf, nullptr, nullptr, y,           \
-               (unsigned long long*)stats, po, relu};                                   \
+               (unsigned long long*)stats, po, relu, ns};                               \
     return launch_conv3<true, __VA_ARGS__>(a, g, st);                                   \
   }
     case 20: ZK_IGF3(256, 64, 4, 1, 2, 128)
@@ -716,6 +732,48 @@ int igemm_fwd_variant(int v, const void* sx, const void* wf, void* y, void* stat
     default: return (int)hipErrorInvalidValue;
   }
 #undef ZK_IGF
+}
+
+// MX-FP4 forward tiles (e2m1 operands, RB = Cin/2 bytes per row): CB must
+// divide Cin/2, so Cin = 64 runs 32-B K rows (SH = 3 swizzle), Cin = 128
+// 64-B rows, Cin >= 256 64- or 128-B rows.  One MFMA covers 64 channels of
+// one tap, 4x the K of a bf16 K-step over the same LDS bytes.
+int igemm_fwd4_variant(int v, const void* sx, const void* wf, void* y, void* stats,
+                       const IGeom& g, int po, int relu, int ns, hipStream_t st) {
+#define ZK_IGF4(BM, BN, WM, WN, NS, CB) \
+  return launch_igemm_fwd<BM, BN, WM, WN, NS, CB, true>(sx, wf, y, stats, g, po, relu, ns, st)
+#define ZK_IGF43(BM, BN, WM, WN, NS, CB)                                                  \
+  {                                                                                       \
+    ConvArgs a{(const uint16_t*)sx, (const uint16_t*)wf, nullptr, nullptr, y,             \
+               (unsigned long long*)stats, po, relu, ns};                                 \
+    return launch_conv3<true, BM, BN, WM, WN, NS, CB, true>(a, g, st);                    \
+  }
+  switch (v) {
+    // any stride (igemm_conv_kernel)
+    case 0: ZK_IGF4(128, 128, 2, 2, 2, 32);
+    case 1: ZK_IGF4(128, 128, 2, 2, 2, 64);
+    case 2: ZK_IGF4(128, 128, 2, 2, 2, 128);
+    case 3: ZK_IGF4(256, 128, 4, 2, 2, 128);
+    case 4: ZK_IGF4(128, 64, 2, 1, 2, 32);
+    case 5: ZK_IGF4(256, 256, 4, 2, 2, 128);
+    case 6: ZK_IGF4(128, 128, 2, 2, 3, 64);
+    case 7: ZK_IGF4(256, 128, 4, 2, 2, 64);
+    case 8: ZK_IGF4(128, 64, 2, 1, 2, 64);
+    case 9: ZK_IGF4(128, 64, 2, 1, 2, 128);
+    // 3x3 stride 1 with horizontal tap reuse (igemm_conv3_kernel)
+    case 20: ZK_IGF43(128, 64, 2, 1, 2, 32)
+    case 21: ZK_IGF43(256, 64, 2, 1, 2, 32)
+    case 22: ZK_IGF43(128, 128, 2, 2, 2, 64)
+    case 23: ZK_IGF43(256, 128, 4, 2, 2, 64)
+    case 24: ZK_IGF43(128, 128, 2, 2, 2, 128)
+    case 25: ZK_IGF43(128, 256, 2, 2, 2, 64)
+    case 26: ZK_IGF43(256, 256, 4, 2, 2, 64)
+    case 27: ZK_IGF43(256, 64, 4, 1, 2, 64)
+    case 28: ZK_IGF43(128, 64, 2, 1, 3, 32)
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef ZK_IGF43
+#undef ZK_IGF4
 }
 
 int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
@@ -740,7 +798,7 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
 #define ZK_IGD3(...)                                                                    \
   {                                                                                     \
     ConvArgs a{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,         \
-               (const uint16_t*)dres, dx, nullptr, 0, 0};                               \
+               (const uint16_t*)dres, dx, nullptr, 0, 0, 1};                            \
     return launch_conv3<false, __VA_ARGS__>(a, g, st);                                  \
   }
     case 20: ZK_IGD3(256, 64, 4, 1, 2, 128)
@@ -1141,11 +1199,12 @@ ZK_EXPORT long long zk_igemm_wgrad_ws_bytes(int B, int Cin, int Ho, int Wo, int 
 }
 
 // Binary forward on MFMA: y int16 [B][Ho][Wo][Cout] = conv(sign x, sign W)
-// (+ReLU), stats [2][Cout] int64 += (sum y, sum y^2) (zeroed by the caller).
+// (+ReLU), stats [stat_stripes][2][Cout] int64 += (sum y, sum y^2) (zeroed
+// by the caller; the copies are summed by zk_bn_finalize).
 // sx: bf16 +-1 [B][H][W][Cin]; wf: bf16 +-1 [T][Cout][Cin].
 ZK_EXPORT int zk_igemm_fwd(const void* sx, const void* wf, void* y, void* stats, int B, int H,
                            int W, int Cin, int Cout, int kh, int kw, int stride, int pt, int pl,
-                           int Ho, int Wo, int pad_ones, int relu, int variant,
+                           int Ho, int Wo, int pad_ones, int relu, int variant, int stat_stripes,
                            hipStream_t stream) {
   IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
   if (variant < 0) {
@@ -1164,7 +1223,45 @@ ZK_EXPORT int zk_igemm_fwd(const void* sx, const void* wf, void* y, void* stats,
     else
       variant = 0;
   }
-  const int rc = igemm_fwd_variant(variant, sx, wf, y, stats, g, pad_ones, relu, stream);
+  const int rc =
+      igemm_fwd_variant(variant, sx, wf, y, stats, g, pad_ones, relu, stat_stripes, stream);
+  if (rc) return rc;
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// Binary forward on MX-FP4 MFMA (v_mfma_f32_32x32x64_f8f6f4, e2m1 operands):
+// the contract of zk_igemm_fwd with 4-bit sign images -- sx4: e2m1 +-1
+// [B][H][W][Cin/2 bytes] (channel 2j in the low nibble of byte j; zk_sign_pack
+// / the BN epilogues write it), wf4: [T][Cout][Cin/2] (zk_weight_pack).
+// Cin % 64 == 0.  4x the MFMA rate and a quarter of the operand bytes of the
+// bf16 form, the same exact integer outputs and statistics.
+ZK_EXPORT int zk_igemm_fwd_fp4(const void* sx4, const void* wf4, void* y, void* stats, int B,
+                               int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pt,
+                               int pl, int Ho, int Wo, int pad_ones, int relu, int variant,
+                               int stat_stripes, hipStream_t stream) {
+  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+  if (Cin % 64 || Cout % 64) return (int)hipErrorInvalidValue;
+  if (variant < 0) {
+    const bool c3 = conv3_ok(g, pad_ones);
+    // Tuned on MI355X (tools/tune_bconv.py --only igf4, E18 shapes, batch 256)
+    if (c3 && Cin == 64)
+      variant = 20;
+    else if (c3 && Cin == 256 && Cout % 256 == 0)
+      variant = 26;
+    else if (c3 && Cin >= 256 && Cout % 128 == 0)
+      variant = 23;
+    else if (c3)
+      variant = 27;
+    else if (Cin == 64)
+      variant = Cout % 128 == 0 ? 0 : 4;
+    else if (Cin == 128)
+      variant = Cout % 128 == 0 ? 6 : 8;
+    else
+      variant = Cout % 128 == 0 ? 1 : 8;
+  }
+  const int rc =
+      igemm_fwd4_variant(variant, sx4, wf4, y, stats, g, pad_ones, relu, stat_stripes, stream);
   if (rc) return rc;
   ZK_CHECK_LAUNCH();
   return 0;

@@ -50,6 +50,31 @@ __device__ __forceinline__ f32x16 mfma_bf16(const uint4& a, const uint4& b, cons
                                                  __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
+// MX MFMA with both operands e2m1 (FP4), unscaled (scale operands 0 select
+// v_mfma_f32_32x32x64_f8f6f4): 4x the K of the bf16 32x32x16 form in the
+// same cycles (MI355X_MICROARCH.md, matrix-core table).  +1 / -1 / 0 are
+// exact in e2m1 (0x2 / 0xA / 0x0), so a +-1 GEMM accumulates the same exact
+// integers as the bf16 form.  A lane supplies 16 B (32 nibbles) of its row
+// per operand -- the same bytes per lane as a bf16 32x32x16 fragment -- so
+// the bf16 kernels' LDS images and fragment reads serve unchanged, at 4x the
+// K per byte.  A and B share the lane/nibble -> k map, so the products pair
+// up whatever that map is.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x16 mfma_fp4(const uint4& a, const uint4& b, const f32x16& c) {
+  const i32x8 av = {(int)a.x, (int)a.y, (int)a.z, (int)a.w, 0, 0, 0, 0};
+  const i32x8 bv = {(int)b.x, (int)b.y, (int)b.z, (int)b.w, 0, 0, 0, 0};
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, c, 4, 4, 0, 0, 0, 0);
+}
+
+// 256 B of e2m1 +1 pairs (0x22): padded taps of pad_values=1 convs on fp4 images.
+__device__ __attribute__((aligned(256))) uint32_t g_ones_page_fp4[64] = {
+#define ZK_F4_4 0x22222222u, 0x22222222u, 0x22222222u, 0x22222222u
+#define ZK_F4_16 ZK_F4_4, ZK_F4_4, ZK_F4_4, ZK_F4_4
+    ZK_F4_16, ZK_F4_16, ZK_F4_16, ZK_F4_16
+#undef ZK_F4_16
+#undef ZK_F4_4
+};
+
 // Bijective XCD remap of a linear block id (blocks L and L+8 share an XCD
 // under round-robin dispatch): XCD x gets the contiguous range of logical ids
 // [x*q + min(x, r), ...).

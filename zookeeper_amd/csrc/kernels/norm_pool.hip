@@ -112,7 +112,8 @@ __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __re
                                                             int relu,
                                                             uint16_t* __restrict__ sx = nullptr,
                                                             uint8_t* __restrict__ smask = nullptr,
-                                                            float clip = 1.f) {
+                                                            float clip = 1.f,
+                                                            uint32_t* __restrict__ sx4 = nullptr) {
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;
   const int cg = threadIdx.x % CG;
@@ -134,11 +135,11 @@ __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __re
     const uint32_t ow[4] = {zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
                             zk::pack_bf16x2(v[4], v[5]), zk::pack_bf16x2(v[6], v[7])};
     *reinterpret_cast<uint4*>(y + r * C + cg * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
-    if (sx) {
+    if (sx || sx4) {
       // next binary layer's input quantisation from the stored bf16 values
       // (same layout as batchnorm.hip's bn_apply_kernel / zk_sign_pack)
       uint32_t sw[4];
-      uint32_t mk = 0;
+      uint32_t mk = 0, n4 = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float lo = zk::bf16_to_f32((uint16_t)(ow[k] & 0xffff));
@@ -146,9 +147,12 @@ __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __re
         sw[k] = (lo >= 0.f ? 0x3F80u : 0xBF80u) | ((hi >= 0.f ? 0x3F80u : 0xBF80u) << 16);
         mk |= (uint32_t)(fabsf(lo) <= clip) << (2 * k);
         mk |= (uint32_t)(fabsf(hi) <= clip) << (2 * k + 1);
+        n4 |= (zk::fp4_sign(lo) | (zk::fp4_sign(hi) << 4)) << (8 * k);
       }
-      *reinterpret_cast<uint4*>(sx + r * C + cg * 8) = make_uint4(sw[0], sw[1], sw[2], sw[3]);
-      smask[r * CG + cg] = (uint8_t)mk;
+      if (sx)
+        *reinterpret_cast<uint4*>(sx + r * C + cg * 8) = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+      if (smask) smask[r * CG + cg] = (uint8_t)mk;
+      if (sx4) sx4[r * CG + cg] = n4;
     }
   }
 }
@@ -469,14 +473,14 @@ ZK_EXPORT int zk_bn_apply_bf16(const void* x, const void* coef, void* y, long lo
 // zk_bn_apply_bf16 + the next binary layer's sign image (bf16 +-1) and STE
 // mask bits (|y| <= clip), packed like zk_sign_pack's.
 ZK_EXPORT int zk_bn_apply_bf16_sign(const void* x, const void* coef, void* y, void* sx,
-                                    void* mask, float clip, long long P, int C, int relu,
-                                    hipStream_t st) {
+                                    void* mask, void* sx4, float clip, long long P, int C,
+                                    int relu, hipStream_t st) {
   if (C % 32) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                           \
   case cg:                                                                                 \
     hipLaunchKernelGGL(bn_apply_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,  \
                        (const uint16_t*)x, (const float*)coef, (uint16_t*)y, P, relu,      \
-                       (uint16_t*)sx, (uint8_t*)mask, clip);                               \
+                       (uint16_t*)sx, (uint8_t*)mask, clip, (uint32_t*)sx4);               \
     break;
   ZK_CG_CASES(C, CASE)
 #undef CASE

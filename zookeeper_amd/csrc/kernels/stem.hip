@@ -311,11 +311,18 @@ __device__ __forceinline__ void block_partials(const float (&s1)[8], const float
   }
 }
 
+// The pool kernels index pool outputs / channel groups in 32 bits (the
+// launchers check the bounds; 64-bit div/mod per output dominated them) and
+// take the pool stride / window as template constants when they are the
+// ImageNet stems' 3x3/2 (S_ = K_ = 0: from the geometry).
+
 // relu(scale*y1+shift) -> k x k / s max pool ('same', -inf padding); argmax
 // tap (0..k*k-1, first maximum); BN2 partial sums of the stored bf16 output.
+template <int S_, int K_>
 __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(
     const uint16_t* __restrict__ y1, const float* __restrict__ coef, uint16_t* __restrict__ p,
     uint8_t* __restrict__ arg, float* __restrict__ part, PoolGeom g) {
+  const int s = S_ ? S_ : g.s, kk = K_ ? K_ : g.k;
   const int CG = g.C / 8, R = 256 / CG;
   const int cg = threadIdx.x % CG;
   float a[8], sh[8];
@@ -325,12 +332,10 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(
     sh[k] = coef[g.C + cg * 8 + k];
   }
   float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const long long P2 = (long long)g.B * g.Ho * g.Wo;
-  for (long long o = (long long)blockIdx.x * R + threadIdx.x / CG; o < P2;
-       o += (long long)gridDim.x * R) {
-    const int ow = (int)(o % g.Wo);
-    const long long q = o / g.Wo;
-    const int oh = (int)(q % g.Ho), b = (int)(q / g.Ho);
+  const int P2 = g.B * g.Ho * g.Wo;
+  for (int o = blockIdx.x * R + threadIdx.x / CG; o < P2; o += gridDim.x * R) {
+    const int ow = o % g.Wo, q = o / g.Wo;
+    const int oh = q % g.Ho, b = q / g.Ho;
     float best[8];
     uint32_t bi[8];
 #pragma unroll
@@ -338,15 +343,25 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(
       best[k] = -1.f;
       bi[k] = 0;
     }
-    for (int th = 0; th < g.k; ++th) {
-      const int hi = oh * g.s - g.pt + th;
-      if (hi < 0 || hi >= g.H) continue;
-      for (int tw = 0; tw < g.k; ++tw) {
-        const int wi = ow * g.s - g.pl + tw;
-        if (wi < 0 || wi >= g.W) continue;
+    if constexpr (K_ > 0) {
+      // all taps' loads in flight first, then the max scan
+      constexpr int KK = K_ * K_;
+      uint4 tv[KK];
+      uint32_t valid = 0;
+#pragma unroll
+      for (int t = 0; t < KK; ++t) {
+        const int hi = oh * s - g.pt + t / K_, wi = ow * s - g.pl + t % K_;
+        const bool ok = hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+        valid |= (uint32_t)ok << t;
+        tv[t] = ok ? *reinterpret_cast<const uint4*>(
+                         y1 + ((long long)(b * g.H + hi) * g.W + wi) * g.C + cg * 8)
+                   : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < KK; ++t) {
+        if (!((valid >> t) & 1u)) continue;
         float v[8];
-        ld8(y1 + (((long long)b * g.H + hi) * g.W + wi) * g.C + cg * 8, v);
-        const uint32_t t = th * g.k + tw;
+        ld8(reinterpret_cast<const uint16_t*>(&tv[t]), v);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float u = fmaxf(fmaf(a[k], v[k], sh[k]), 0.f);
@@ -356,10 +371,31 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(
           }
         }
       }
+    } else {
+      for (int th = 0; th < kk; ++th) {
+        const int hi = oh * s - g.pt + th;
+        if (hi < 0 || hi >= g.H) continue;
+        for (int tw = 0; tw < kk; ++tw) {
+          const int wi = ow * s - g.pl + tw;
+          if (wi < 0 || wi >= g.W) continue;
+          float v[8];
+          ld8(y1 + ((long long)(b * g.H + hi) * g.W + wi) * g.C + cg * 8, v);
+          const uint32_t t = th * kk + tw;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float u = fmaxf(fmaf(a[k], v[k], sh[k]), 0.f);
+            if (u > best[k]) {
+              best[k] = u;
+              bi[k] = t;
+            }
+          }
+        }
+      }
     }
     const uint4 pk = pack8(best);
-    *reinterpret_cast<uint4*>(p + o * g.C + cg * 8) = pk;
-    *reinterpret_cast<uint2*>(arg + o * g.C + cg * 8) =
+    const long long off = (long long)o * g.C + cg * 8;
+    *reinterpret_cast<uint4*>(p + off) = pk;
+    *reinterpret_cast<uint2*>(arg + off) =
         make_uint2(bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
                    bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
     float stored[8];
@@ -374,59 +410,70 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(
 }
 
 // BN1 backward sums (sum du, sum du*yhat) from the pooled side: every pool
-// output routes dp to its argmax tap q; du(q) = dp * [scale*y1(q)+shift > 0].
+// output routes dp to its argmax tap q, du(q) = dp * [u(q) > 0].  The pooled
+// value p IS u(q) = gamma*yhat(q) + beta when positive (bf16-rounded), so
+// yhat(q) = (p - beta) / gamma needs no gather of y1.  A thread holding a
+// channel with |beta| > 8|gamma| (where p's rounding would be amplified) or
+// gamma = 0 takes the exact path instead: y1 at the argmax tap, gathered
+// with whole-tap vector loads.
+template <int S_, int K_>
 __global__ __launch_bounds__(256) void stem_pool_bwd_sums_kernel(
     const uint16_t* __restrict__ dp, const uint8_t* __restrict__ arg,
-    const uint16_t* __restrict__ y1, const float* __restrict__ coef, float* __restrict__ part,
-    PoolGeom g) {
+    const uint16_t* __restrict__ y1, const uint16_t* __restrict__ pooled,
+    const float* __restrict__ coef, float* __restrict__ part, PoolGeom g) {
+  const int s = S_ ? S_ : g.s, kk = K_ ? K_ : g.k;
   const int CG = g.C / 8, R = 256 / CG;
   const int cg = threadIdx.x % CG;
-  float a[8], sh[8], mean[8], rstd[8];
+  float mean[8], rstd[8], bet[8], igm[8];
+  bool gather = false;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    a[k] = coef[cg * 8 + k];
-    sh[k] = coef[g.C + cg * 8 + k];
+    const float a = coef[cg * 8 + k], sh = coef[g.C + cg * 8 + k];
     mean[k] = coef[2 * g.C + cg * 8 + k];
     rstd[k] = coef[3 * g.C + cg * 8 + k];
+    const float gm = a / rstd[k];  // gamma
+    bet[k] = fmaf(a, mean[k], sh);  // beta
+    igm[k] = gm != 0.f ? 1.f / gm : 0.f;
+    gather |= !(fabsf(gm) > 0.f && fabsf(bet[k]) <= 8.f * fabsf(gm));
   }
   float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const long long P2 = (long long)g.B * g.Ho * g.Wo;
-  for (long long o = (long long)blockIdx.x * R + threadIdx.x / CG; o < P2;
-       o += (long long)gridDim.x * R) {
-    const int ow = (int)(o % g.Wo);
-    const long long q = o / g.Wo;
-    const int oh = (int)(q % g.Ho), b = (int)(q / g.Ho);
-    float gv[8];
-    ld8(dp + o * g.C + cg * 8, gv);
-    const uint2 av = *reinterpret_cast<const uint2*>(arg + o * g.C + cg * 8);
-    const uint32_t aw[2] = {av.x, av.y};
-    float yq[8];  // y1 at each channel's argmax tap (whole-tap vector loads)
+  const int P2 = g.B * g.Ho * g.Wo;
+  for (int o = blockIdx.x * R + threadIdx.x / CG; o < P2; o += gridDim.x * R) {
+    const long long off = (long long)o * g.C + cg * 8;
+    float gv[8], pv[8], yh[8];
+    ld8(dp + off, gv);
+    ld8(pooled + off, pv);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) yq[k] = 0.f;
-    for (int th = 0; th < g.k; ++th) {
-      const int hi = oh * g.s - g.pt + th;
-      if (hi < 0 || hi >= g.H) continue;
-      for (int tw = 0; tw < g.k; ++tw) {
-        const int wi = ow * g.s - g.pl + tw;
-        if (wi < 0 || wi >= g.W) continue;
-        const uint32_t t = th * g.k + tw;
-        bool any = false;
+    for (int k = 0; k < 8; ++k) yh[k] = (pv[k] - bet[k]) * igm[k];
+    if (gather) {
+      const int ow = o % g.Wo, q = o / g.Wo;
+      const int oh = q % g.Ho, b = q / g.Ho;
+      const uint2 av = *reinterpret_cast<const uint2*>(arg + off);
+      const uint32_t aw[2] = {av.x, av.y};
+      for (int th = 0; th < kk; ++th) {
+        const int hi = oh * s - g.pt + th;
+        if (hi < 0 || hi >= g.H) continue;
+        for (int tw = 0; tw < kk; ++tw) {
+          const int wi = ow * s - g.pl + tw;
+          if (wi < 0 || wi >= g.W) continue;
+          const uint32_t t = th * kk + tw;
+          bool any = false;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) any |= ((aw[k >> 2] >> (8 * (k & 3))) & 0xff) == t;
-        if (!any) continue;
-        float v[8];
-        ld8(y1 + (((long long)b * g.H + hi) * g.W + wi) * g.C + cg * 8, v);
+          for (int k = 0; k < 8; ++k) any |= ((aw[k >> 2] >> (8 * (k & 3))) & 0xff) == t;
+          if (!any) continue;
+          float v[8];
+          ld8(y1 + ((long long)(b * g.H + hi) * g.W + wi) * g.C + cg * 8, v);
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (((aw[k >> 2] >> (8 * (k & 3))) & 0xff) == t) yq[k] = v[k];
+          for (int k = 0; k < 8; ++k)
+            if (((aw[k >> 2] >> (8 * (k & 3))) & 0xff) == t) yh[k] = (v[k] - mean[k]) * rstd[k];
+        }
       }
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float yv = yq[k];
-      const float du = (fmaf(a[k], yv, sh[k]) > 0.f) ? gv[k] : 0.f;
+      const float du = pv[k] > 0.f ? gv[k] : 0.f;
       s1[k] += du;
-      s2[k] += du * (yv - mean[k]) * rstd[k];
+      s2[k] += du * yh[k];
     }
   }
   block_partials(s1, s2, part, g.C);
@@ -438,14 +485,16 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_sums_kernel(
 // stride cell; with k <= s + 1 every such pixel is covered only by the pool
 // outputs (oh-1..oh) x (ow-1..ow) (pt, pl <= s - 1), whose argmax / dp are
 // loaded once, unconditionally.
+template <int S_, int K_>
 __global__ __launch_bounds__(256) void stem_dy1_kernel(
     const uint16_t* __restrict__ dp, const uint8_t* __restrict__ arg,
     const uint16_t* __restrict__ y1, const float* __restrict__ coef,
     const float* __restrict__ bcoef, uint16_t* __restrict__ dy1, PoolGeom g) {
-  const int CG = g.C / 8;
-  const long long total = (long long)g.B * g.Ho * g.Wo * CG;
+  const int s = S_ ? S_ : g.s, kk = K_ ? K_ : g.k;
+  const int CG = g.C / 8, lg = __builtin_ctz(CG);  // CG divides 256: a power of two
+  const int total = g.B * g.Ho * g.Wo * CG;
   // the grid stride is a multiple of CG, so every thread keeps one channel group
-  const int cg = (int)((blockIdx.x * (long long)blockDim.x + threadIdx.x) % CG);
+  const int cg = (blockIdx.x * blockDim.x + threadIdx.x) & (CG - 1);
   float a1[8], s1v[8], k1[8], k0[8], k3[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -456,12 +505,10 @@ __global__ __launch_bounds__(256) void stem_dy1_kernel(
     k0[k] = bcoef[g.C + c];
     k3[k] = bcoef[2 * g.C + c];
   }
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long o = i / CG;
-    const int ow = (int)(o % g.Wo);
-    const long long q = o / g.Wo;
-    const int oh = (int)(q % g.Ho), b = (int)(q / g.Ho);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int o = i >> lg;
+    const int ow = o % g.Wo, q = o / g.Wo;
+    const int oh = q % g.Ho, b = q / g.Ho;
     // candidate outputs (oh-1+dy, ow-1+dx), dy, dx in {0, 1}
     uint32_t aw[2][2][2];
     float gv[2][2][8];
@@ -471,47 +518,65 @@ __global__ __launch_bounds__(256) void stem_dy1_kernel(
       for (int dx = 0; dx < 2; ++dx) {
         const int ch = oh - 1 + dy, cw = ow - 1 + dx;
         if (ch >= 0 && cw >= 0) {
-          const long long oo = ((long long)b * g.Ho + ch) * g.Wo + cw;
-          const uint2 av = *reinterpret_cast<const uint2*>(arg + oo * g.C + cg * 8);
+          const long long oo = ((long long)(b * g.Ho + ch) * g.Wo + cw) * g.C + cg * 8;
+          const uint2 av = *reinterpret_cast<const uint2*>(arg + oo);
           aw[dy][dx][0] = av.x;
           aw[dy][dx][1] = av.y;
-          ld8(dp + oo * g.C + cg * 8, gv[dy][dx]);
+          ld8(dp + oo, gv[dy][dx]);
         } else {
           aw[dy][dx][0] = aw[dy][dx][1] = 0xFFFFFFFFu;  // tap 255: never matches
 #pragma unroll
           for (int k = 0; k < 8; ++k) gv[dy][dx][k] = 0.f;
         }
       }
-    for (int sy = 0; sy < g.s; ++sy) {
-      const int hh = oh * g.s - g.pt + sy;
+    // the stride cell's y1 rows: loads in flight before the routing math
+    constexpr int SC = S_ > 0 ? S_ * S_ : 4;
+    uint4 yq[SC];
+    if constexpr (S_ > 0) {
+#pragma unroll
+      for (int c2 = 0; c2 < SC; ++c2) {
+        const int hh = oh * s - g.pt + c2 / S_, ww = ow * s - g.pl + c2 % S_;
+        yq[c2] = (hh >= 0 && hh < g.H && ww >= 0 && ww < g.W)
+                     ? *reinterpret_cast<const uint4*>(
+                           y1 + ((long long)(b * g.H + hh) * g.W + ww) * g.C + cg * 8)
+                     : make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int sy = 0; sy < s; ++sy) {
+      const int hh = oh * s - g.pt + sy;
       if (hh < 0 || hh >= g.H) continue;
-      for (int sx = 0; sx < g.s; ++sx) {
-        const int ww = ow * g.s - g.pl + sx;
+#pragma unroll
+      for (int sx = 0; sx < s; ++sx) {
+        const int ww = ow * s - g.pl + sx;
         if (ww < 0 || ww >= g.W) continue;
         float du[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int dy = 0; dy < 2; ++dy) {
-          const int th = hh - ((oh - 1 + dy) * g.s - g.pt);
-          if (th < 0 || th >= g.k) continue;
+          const int th = hh - ((oh - 1 + dy) * s - g.pt);
+          if (th < 0 || th >= kk) continue;
 #pragma unroll
           for (int dx = 0; dx < 2; ++dx) {
-            const int tw = ww - ((ow - 1 + dx) * g.s - g.pl);
-            if (tw < 0 || tw >= g.k) continue;
-            const uint32_t t = th * g.k + tw;
+            const int tw = ww - ((ow - 1 + dx) * s - g.pl);
+            if (tw < 0 || tw >= kk) continue;
+            const uint32_t t = th * kk + tw;
 #pragma unroll
             for (int k = 0; k < 8; ++k)
               if (((aw[dy][dx][k >> 2] >> (8 * (k & 3))) & 0xff) == t) du[k] += gv[dy][dx][k];
           }
         }
-        const long long pix = ((long long)b * g.H + hh) * g.W + ww;
+        const long long pix = ((long long)(b * g.H + hh) * g.W + ww) * g.C + cg * 8;
         float yv[8], o8[8];
-        ld8(y1 + pix * g.C + cg * 8, yv);
+        if constexpr (S_ > 0)
+          ld8(reinterpret_cast<const uint16_t*>(&yq[sy * S_ + sx]), yv);
+        else
+          ld8(y1 + pix, yv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float u = fmaf(a1[k], yv[k], s1v[k]);
           o8[k] = k1[k] * (u > 0.f ? du[k] : 0.f) + k0[k] - k3[k] * yv[k];
         }
-        *reinterpret_cast<uint4*>(dy1 + pix * g.C + cg * 8) = pack8(o8);
+        *reinterpret_cast<uint4*>(dy1 + pix) = pack8(o8);
       }
     }
   }
@@ -750,26 +815,33 @@ ZK_EXPORT int zk_reduce_partials(const void* part, int nb, int n, void* out, hip
 ZK_EXPORT int zk_stem_pool_fwd(const void* y1, const void* coef, void* p, void* arg, void* part,
                                int B, int H, int W, int C, int Ho, int Wo, int k, int s, int pt,
                                int pl, int* nparts, hipStream_t st) {
-  if (C % 8 || 256 % (C / 8) || k * k > 255) return (int)hipErrorInvalidValue;
+  if (C % 8 || 256 % (C / 8) || k * k > 255 || (long long)B * Ho * Wo >= (1LL << 31))
+    return (int)hipErrorInvalidValue;
   PoolGeom g{B, H, W, C, Ho, Wo, k, s, pt, pl};
   const int grid = pool_grid((long long)B * Ho * Wo, C);
   if (nparts) *nparts = grid;
-  hipLaunchKernelGGL(stem_pool_fwd_kernel, dim3(grid), dim3(256), 0, st, (const uint16_t*)y1,
-                     (const float*)coef, (uint16_t*)p, (uint8_t*)arg, (float*)part, g);
+  auto kern = (s == 2 && k == 3) ? stem_pool_fwd_kernel<2, 3> : stem_pool_fwd_kernel<0, 0>;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, (const uint16_t*)y1, (const float*)coef,
+                     (uint16_t*)p, (uint8_t*)arg, (float*)part, g);
   ZK_CHECK_LAUNCH();
   return 0;
 }
 
+// pooled: the pool output p of zk_stem_pool_fwd (relu'd BN-1 values at the
+// argmax taps), read instead of gathering y1 there.
 ZK_EXPORT int zk_stem_pool_bwd_sums(const void* dp, const void* arg, const void* y1,
-                                    const void* coef, void* part, int B, int H, int W, int C,
-                                    int Ho, int Wo, int k, int s, int pt, int pl, int* nparts,
-                                    hipStream_t st) {
-  if (C % 8 || 256 % (C / 8)) return (int)hipErrorInvalidValue;
+                                    const void* pooled, const void* coef, void* part, int B, int H,
+                                    int W, int C, int Ho, int Wo, int k, int s, int pt, int pl,
+                                    int* nparts, hipStream_t st) {
+  if (C % 8 || 256 % (C / 8) || (long long)B * Ho * Wo >= (1LL << 31))
+    return (int)hipErrorInvalidValue;
   PoolGeom g{B, H, W, C, Ho, Wo, k, s, pt, pl};
   const int grid = pool_grid((long long)B * Ho * Wo, C);
   if (nparts) *nparts = grid;
-  hipLaunchKernelGGL(stem_pool_bwd_sums_kernel, dim3(grid), dim3(256), 0, st,
-                     (const uint16_t*)dp, (const uint8_t*)arg, (const uint16_t*)y1,
+  auto kern =
+      (s == 2 && k == 3) ? stem_pool_bwd_sums_kernel<2, 3> : stem_pool_bwd_sums_kernel<0, 0>;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, (const uint16_t*)dp,
+                     (const uint8_t*)arg, (const uint16_t*)y1, (const uint16_t*)pooled,
                      (const float*)coef, (float*)part, g);
   ZK_CHECK_LAUNCH();
   return 0;
@@ -783,11 +855,13 @@ ZK_EXPORT int zk_stem_dy1(const void* dp, const void* arg, const void* y1, const
   if (C % 8 || 256 % (C / 8) || k > s + 1 || pt >= s || pl >= s || pt < 0 || pl < 0 ||
       (long long)Ho * s < H + pt || (long long)Wo * s < W + pl)
     return (int)hipErrorInvalidValue;
-  PoolGeom g{B, H, W, C, Ho, Wo, k, s, pt, pl};
   const long long work = (long long)B * Ho * Wo * (C / 8);
+  if (work >= (1LL << 31)) return (int)hipErrorInvalidValue;
+  PoolGeom g{B, H, W, C, Ho, Wo, k, s, pt, pl};
   long long blocks = (work + 255) / 256;
-  if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(stem_dy1_kernel, dim3((int)blocks), dim3(256), 0, st, (const uint16_t*)dp,
+  if (blocks > 32768) blocks = 32768;
+  auto kern = (s == 2 && k == 3) ? stem_dy1_kernel<2, 3> : stem_dy1_kernel<0, 0>;
+  hipLaunchKernelGGL(kern, dim3((int)blocks), dim3(256), 0, st, (const uint16_t*)dp,
                      (const uint8_t*)arg, (const uint16_t*)y1, (const float*)coef,
                      (const float*)bcoef, (uint16_t*)dy1, g);
   ZK_CHECK_LAUNCH();

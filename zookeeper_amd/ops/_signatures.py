@@ -21,20 +21,21 @@ SIGNATURES = {
     # preprocessing
     "zk_normalize_flip_c3": (I32, [P, P, I32, I32, I32, FP, FP, I32, U64, P]),
     # binary convolution
-    "zk_sign_pack": (I32, [P, P, P, P, I64, F32, P]),
-    "zk_weight_pack": (I32, [P, P, P, P, P, I32, I32, I32, P]),
+    "zk_sign_pack": (I32, [P, P, P, P, P, I64, F32, P]),
+    "zk_weight_pack": (I32, [P, P, P, P, P, P, I32, I32, I32, P]),
     "zk_unpack_sign": (I32, [P, P, I64, P]),
     "zk_bconv_fwd": (I32, [P, P, P, P, P] + [I32] * 14 + [P]),
     "zk_bconv_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
     "zk_igemm_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
-    "zk_igemm_fwd": (I32, [P, P, P, P] + [I32] * 15 + [P]),
+    "zk_igemm_fwd": (I32, [P, P, P, P] + [I32] * 16 + [P]),
+    "zk_igemm_fwd_fp4": (I32, [P, P, P, P] + [I32] * 16 + [P]),
     "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),
     "zk_igemm_wgrad_ws_bytes": (I64, [I32] * 10),
     "zk_bconv_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P]),
     # batch norm
-    "zk_bn_finalize": (I32, [P, I32, C.c_double, P, P, F32, F32, P, P, P, P, P, P, P]),
+    "zk_bn_finalize": (I32, [P, I32, I32, C.c_double, P, P, F32, F32, P, P, P, P, P, P, P]),
     "zk_bn_apply": (I32, [P, P, P, P, P, I64, I32, P]),
-    "zk_bn_apply_sign": (I32, [P, P, P, P, P, P, P, F32, I64, I32, P]),
+    "zk_bn_apply_sign": (I32, [P, P, P, P, P, P, P, P, F32, I64, I32, P]),
     "zk_bn_bwd_reduce": (I32, [P, P, P, P, P, I64, I32, P]),
     "zk_bn_bwd_dx": (I32, [P, P, P, P, I64, I32, I32, P]),
     "zk_ste_combine": (I32, [P, P, P, P, I64, P]),
@@ -43,7 +44,7 @@ SIGNATURES = {
     "zk_bn_stats_bf16": (I32, [P, P, I64, I32, P]),
     "zk_bn_finalize_f64": (I32, [P, I32, C.c_double, P, P, F32, F32, P, P, P, P]),
     "zk_bn_apply_bf16": (I32, [P, P, P, I64, I32, I32, P]),
-    "zk_bn_apply_bf16_sign": (I32, [P, P, P, P, P, F32, I64, I32, I32, P]),
+    "zk_bn_apply_bf16_sign": (I32, [P, P, P, P, P, P, F32, I64, I32, I32, P]),
     "zk_bn_bwd_reduce_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
     "zk_bn_bwd_dx_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
     # depthwise convolution
@@ -62,7 +63,7 @@ SIGNATURES = {
     "zk_bn_finalize_partials": (I32, [P, I32, I32, C.c_double, P, P, F32, F32, P, P, P, P]),
     "zk_reduce_partials": (I32, [P, I32, I32, P, P]),
     "zk_stem_pool_fwd": (I32, [P, P, P, P, P] + [I32] * 10 + [IP, P]),
-    "zk_stem_pool_bwd_sums": (I32, [P, P, P, P, P] + [I32] * 10 + [IP, P]),
+    "zk_stem_pool_bwd_sums": (I32, [P, P, P, P, P, P] + [I32] * 10 + [IP, P]),
     "zk_stem_dy1": (I32, [P, P, P, P, P, P] + [I32] * 10 + [P]),
     "zk_stem_wgrad": (I32, [P, P, P] + [I32] * 11 + [P]),
     "zk_maxpool_fwd": (I32, [P, P, P] + [I32] * 10 + [P]),

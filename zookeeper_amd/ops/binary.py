@@ -3,13 +3,16 @@
 One autograd op per block (used by BinaryResNet-E and QuickNet on the
 ``hip`` backend).  Forward kernels:
 
-1. ``zk_sign_pack``   x bf16 → STE mask bits (|x| ≤ clip) and the sign image
-   sx (bf16 ±1); packed sign bits only for the XNOR fallback;
-2. ``zk_weight_pack`` latent fp32 kernel → ±1 bf16 as [T][Cout][Cin]
-   (forward) and [T][Cin][Cout] (dgrad);
-3. ``zk_igemm_fwd``   MFMA implicit GEMM on an LDS-DMA ring (igemm.hip) →
-   exact int16 output (+ optional ReLU) and exact int64 BN statistics
-   (``zk_bconv_fwd``, XNOR-popcount on bit tiles, for channel counts that do
+1. ``zk_sign_pack``   x bf16 → STE mask bits (|x| ≤ clip), the sign image
+   sx (bf16 ±1, weight-gradient operand) and sx4 (e2m1 ±1 nibbles, forward
+   operand); packed sign bits only for the XNOR fallback;
+2. ``zk_weight_pack`` latent fp32 kernel → ±1 as e2m1 [T][Cout][Cin/2]
+   (forward) and bf16 [T][Cin][Cout] (dgrad);
+3. ``zk_igemm_fwd_fp4`` MX-FP4 MFMA implicit GEMM (v_mfma_f32_32x32x64_f8f6f4,
+   ±1 exact in e2m1, 4× the bf16 MFMA rate) on an LDS-DMA ring
+   (igemm.hip) → exact int16 output (+ optional ReLU) and exact int64 BN
+   statistics (``ZK_BCONV_FP4=0``: the bf16 MFMA form ``zk_igemm_fwd``;
+   ``zk_bconv_fwd``, XNOR-popcount on bit tiles, for channel counts that do
    not tile by 64);
 4. ``zk_bn_finalize`` per-channel scale/shift, running statistics (Keras
    momentum, Bessel-corrected variance);
@@ -27,6 +30,7 @@ output and per-channel vectors — no bf16 copy of the real-valued input.
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -34,6 +38,15 @@ import torch
 from zookeeper_amd.nn.layers import same_padding
 from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
                                         zeroed_scratch)
+
+
+# Binary forward on MX-FP4 MFMA (4x the bf16 rate); ZK_BCONV_FP4=0 selects
+# the bf16 MFMA form (same exact integer outputs).
+FP4 = os.environ.get("ZK_BCONV_FP4", "1") != "0"
+# Copies of the forward BN statistics the conv blocks add into (block b into
+# copy b % STAT_STRIPES; zk_bn_finalize sums them): one [2][Cout] array took
+# thousands of serialised int64 atomics per cache line on the 56x56 layers.
+STAT_STRIPES = 32
 
 
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
@@ -61,41 +74,59 @@ class _BinaryBlockFn(torch.autograd.Function):
         # forward and both gradients run as bf16 ±1 implicit GEMMs on the
         # sign image sx; otherwise the XNOR-popcount forward on packed bits.
         mfma = Cout % 64 == 0 and Cin % 64 == 0 and stride <= 2 and kh <= 4 and kw <= 4
+        fp4 = mfma and FP4
         # The previous block may already have quantised this input in its BN
-        # epilogue (zk_bn_apply_sign): reuse its sign image and STE mask.
+        # epilogue (zk_bn_apply_sign): reuse its sign images and STE mask.
         cached = getattr(x, "_zk_sign", None)
+        sx4 = None
         if (mfma and cached is not None and cached[0] == clip
-                and tuple(cached[1].shape) == (B, H, W, Cin)):
+                and tuple(cached[1].shape) == (B, H, W, Cin)
+                and (not fp4 or (len(cached) > 3 and cached[3] is not None))):
             bits, sx, mask = None, cached[1], cached[2]
+            sx4 = cached[3] if fp4 else None
         else:
             bits = None if mfma else torch.empty(nwords, dtype=torch.int32, device=dev)
             mask = torch.empty(nwords, dtype=torch.int32, device=dev)
-            sx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev) if mfma else None
+            # bf16 image: the weight-gradient operand (and the bf16 forward's)
+            sx = (torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
+                  if mfma and (will_backward or not fp4) else None)
+            sx4 = (torch.empty((B, H, W, Cin // 2), dtype=torch.uint8, device=dev)
+                   if fp4 else None)
             check(L.zk_sign_pack(xn.data_ptr(), bits.data_ptr() if bits is not None else None,
                                  mask.data_ptr(), sx.data_ptr() if sx is not None else None,
-                                 nwords, clip, st), "zk_sign_pack")
+                                 sx4.data_ptr() if sx4 is not None else None, nwords, clip, st),
+                  "zk_sign_pack")
 
         w_ohwi = weight.permute(0, 2, 3, 1).contiguous()  # no copy for channels_last
         wbits = None if mfma else torch.empty(Cout * T * Cin // 32, dtype=torch.int32, device=dev)
         wpop = None if mfma else torch.empty(Cout * T, dtype=torch.int32, device=dev)
-        # ±1 kernel as [T][Cout][Cin] (forward GEMM) and transposed to
-        # [T][Cin][Cout] for the dgrad GEMM (only when a backward will run).
-        wf = torch.empty((T, Cout, Cin), dtype=torch.bfloat16, device=dev) if mfma else None
+        # ±1 kernel as [T][Cout][Cin] (forward GEMM: e2m1 nibbles, or bf16)
+        # and transposed to [T][Cin][Cout] bf16 for the dgrad GEMM (only when
+        # a backward will run).
+        wf = (torch.empty((T, Cout, Cin), dtype=torch.bfloat16, device=dev)
+              if mfma and not fp4 else None)
+        wf4 = torch.empty((T, Cout, Cin // 2), dtype=torch.uint8, device=dev) if fp4 else None
         wt = (torch.empty((T, Cin, Cout), dtype=torch.bfloat16, device=dev)
               if will_backward else None)
         _p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
-        check(L.zk_weight_pack(w_ohwi.data_ptr(), _p(wbits), _p(wpop), _p(wt), _p(wf), Cout, T,
-                               Cin, st), "zk_weight_pack")
+        check(L.zk_weight_pack(w_ohwi.data_ptr(), _p(wbits), _p(wpop), _p(wt), _p(wf), _p(wf4),
+                               Cout, T, Cin, st), "zk_weight_pack")
 
         P = B * Ho * Wo
         y = torch.empty((B, Ho, Wo, Cout), dtype=torch.int16, device=dev)
         # persistent accumulator, re-zeroed by zk_bn_finalize (eval: no finalize)
-        stats = (zeroed_scratch(bn, "stats_i64", (2, Cout), torch.int64, dev) if bn.training
-                 else torch.zeros((2, Cout), dtype=torch.int64, device=dev))
-        if mfma:
+        stats = (zeroed_scratch(bn, "stats_i64", (STAT_STRIPES, 2, Cout), torch.int64, dev)
+                 if bn.training
+                 else torch.zeros((STAT_STRIPES, 2, Cout), dtype=torch.int64, device=dev))
+        if fp4:
+            check(L.zk_igemm_fwd_fp4(sx4.data_ptr(), wf4.data_ptr(), y.data_ptr(),
+                                     stats.data_ptr(), B, H, W, Cin, Cout, kh, kw, stride, pt, pl,
+                                     Ho, Wo, int(pad_ones), int(act_relu), -1, STAT_STRIPES,
+                                     st), "zk_igemm_fwd_fp4")
+        elif mfma:
             check(L.zk_igemm_fwd(sx.data_ptr(), wf.data_ptr(), y.data_ptr(), stats.data_ptr(), B,
                                  H, W, Cin, Cout, kh, kw, stride, pt, pl, Ho, Wo, int(pad_ones),
-                                 int(act_relu), -1, st), "zk_igemm_fwd")
+                                 int(act_relu), -1, STAT_STRIPES, st), "zk_igemm_fwd")
         else:
             check(L.zk_bconv_fwd(bits.data_ptr(), wbits.data_ptr(), wpop.data_ptr(),
                                  y.data_ptr(), stats.data_ptr(), B, H, W, Cin, Cout, kh, kw,
@@ -111,7 +142,8 @@ class _BinaryBlockFn(torch.autograd.Function):
         gp = gamma.data_ptr() if gamma is not None else None
         bp = beta.data_ptr() if beta is not None else None
         if bn.training:
-            check(L.zk_bn_finalize(stats.data_ptr(), Cout, float(P), gp, bp, bn.eps, bn.momentum,
+            # (the XNOR kernel adds into copy 0 only; the others stay zero)
+            check(L.zk_bn_finalize(stats.data_ptr(), Cout, STAT_STRIPES, float(P), gp, bp, bn.eps, bn.momentum,
                                    bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                                    scale.data_ptr(), shift.data_ptr(), mean.data_ptr(),
                                    rstd.data_ptr(), st), "zk_bn_finalize")
@@ -129,11 +161,14 @@ class _BinaryBlockFn(torch.autograd.Function):
             # also quantise the output for the next binary block (same clip)
             sx_next = torch.empty_like(out)
             mask_next = torch.empty(P * Cout // 32, dtype=torch.int32, device=dev)
+            sx4_next = (torch.empty((B, Ho, Wo, Cout // 2), dtype=torch.uint8, device=dev)
+                        if FP4 else None)
             check(L.zk_bn_apply_sign(y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
                                      res.data_ptr() if res is not None else None,
                                      out.data_ptr(), sx_next.data_ptr(), mask_next.data_ptr(),
+                                     sx4_next.data_ptr() if sx4_next is not None else None,
                                      clip, P, Cout, st), "zk_bn_apply_sign")
-            next_sign[:] = [clip, sx_next, mask_next]
+            next_sign[:] = [clip, sx_next, mask_next, sx4_next]
         else:
             check(L.zk_bn_apply(y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
                                 res.data_ptr() if res is not None else None, out.data_ptr(), P,
@@ -281,10 +316,11 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
     ``residual`` may be ``x`` itself (identity shortcut, fused into the
     backward) or a separately computed tensor, or ``None``.
 
-    With ``quantize_output`` the BN epilogue also writes the sign image and
-    STE mask of the output for the next binary block (attached to the
-    returned tensor as ``_zk_sign``; a block with the same clip value reuses
-    them instead of re-reading its input).
+    With ``quantize_output`` the BN epilogue also writes the sign images
+    (bf16 and e2m1) and STE mask of the output for the next binary block
+    (attached to the returned tensor as ``_zk_sign`` = (clip, sx, mask, sx4);
+    a block with the same clip value reuses them instead of re-reading its
+    input).
     """
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)

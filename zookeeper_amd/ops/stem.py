@@ -10,8 +10,9 @@ forward   pack (zero-padded 4-channel image, bf16 [KH][Cout][32] kernel) →
           BN-1 + ReLU + max-pool (+ argmax tap, BN-2 partial sums) in one
           pass → BN-2 finalize → BN-2 apply;
 backward  BN-2 backward (bf16 kernels of ``norm_pool``) → BN-1 sums from
-          the pooled side (sparse) → dense dy1 in one pass → MFMA weight
-          gradient straight into the flat gradient buffer.
+          the pooled side (the pooled value is BN-1's output at the argmax
+          tap: no gather) → dense dy1 in one pass → MFMA weight gradient
+          straight into the flat gradient buffer.
 
 The image itself never needs a gradient; the op is only used when it does
 not (``x.requires_grad`` is False).
@@ -146,12 +147,18 @@ class _StemFn(torch.autograd.Function):
             out = torch.empty_like(p)
             if holder is not None and Cout % 32 == 0:
                 # also quantise the output for the first binary block
+                from zookeeper_amd.ops.binary import FP4
+
                 sx = torch.empty_like(p)
                 mask = torch.empty(P2 * Cout // 32, dtype=torch.int32, device=dev)
+                sx4 = (torch.empty((B, H2, W2, Cout // 2), dtype=torch.uint8, device=dev)
+                       if FP4 else None)
                 check(L.zk_bn_apply_bf16_sign(p.data_ptr(), coef2.data_ptr(), out.data_ptr(),
-                                              sx.data_ptr(), mask.data_ptr(), sign_clip, P2,
-                                              Cout, 0, st), "zk_bn_apply_bf16_sign")
-                holder[:] = [sign_clip, sx, mask]
+                                              sx.data_ptr(), mask.data_ptr(),
+                                              sx4.data_ptr() if sx4 is not None else None,
+                                              sign_clip, P2, Cout, 0, st),
+                      "zk_bn_apply_bf16_sign")
+                holder[:] = [sign_clip, sx, mask, sx4]
             else:
                 check(L.zk_bn_apply_bf16(p.data_ptr(), coef2.data_ptr(), out.data_ptr(), P2,
                                          Cout, 0, st), "zk_bn_apply_bf16")
@@ -186,7 +193,7 @@ class _StemFn(torch.autograd.Function):
         part = torch.empty((L.zk_stem_max_pool_parts(), 2, Cout), dtype=torch.float32,
                            device=dev)
         nb = ctypes.c_int(0)
-        check(L.zk_stem_pool_bwd_sums(dp.data_ptr(), arg.data_ptr(), y1.data_ptr(),
+        check(L.zk_stem_pool_bwd_sums(dp.data_ptr(), arg.data_ptr(), y1.data_ptr(), p.data_ptr(),
                                       coef1.data_ptr(), part.data_ptr(), B, Ho, Wo, Cout, H2, W2,
                                       pk, ps, pt2, pl2, ctypes.byref(nb), st),
               "zk_stem_pool_bwd_sums")
