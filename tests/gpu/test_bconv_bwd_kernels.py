@@ -71,7 +71,7 @@ def test_dgrad_wgrad(cin, cout, stride, hw, pad_ones):
 @pytest.mark.parametrize("variant", list(range(15)) + list(range(20, 28)))
 @pytest.mark.parametrize("cin,cout,stride,hw", [
     (64, 64, 1, 12), (64, 128, 2, 12), (128, 128, 1, 7), (256, 512, 2, 8), (128, 64, 1, 9),
-    (128, 256, 2, 15)])
+    (128, 256, 2, 15), (64, 64, 1, 28)])
 def test_igemm_dgrad_matches_reference(variant, cin, cout, stride, hw):
     """LDS-DMA ring implicit-GEMM dgrad (igemm.hip), every tile variant, vs
     the fp64 ±1 conv gradient (STE mask + residual gradient fused)."""

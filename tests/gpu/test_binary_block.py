@@ -167,3 +167,43 @@ def test_chained_blocks_reuse_fused_quantisation():
     torch.testing.assert_close(o1, o2, atol=0, rtol=0)  # forward is deterministic
     for a, b in zip(g1, g2):  # fp32 atomics in the reductions: order-dependent
         assert ((a - b).norm() / b.norm()).item() < 1e-3
+
+
+@pytest.mark.parametrize("second_consumer", [False, True])
+def test_fused_bn_backward_sums_match_separate_reduce(monkeypatch, second_consumer):
+    """A block whose output feeds only the next block (identity shortcut)
+    gets its BN-backward sums from that block's dgrad epilogue
+    (zk_igemm_dgrad_bnsum).  Gradients must match the separate reduce; with
+    a second consumer of the output (gradient accumulated after the dgrad)
+    the block must detect it and fall back."""
+    _setup()
+    from zookeeper_amd import ops
+    from zookeeper_amd.ops import binary
+
+    torch.manual_seed(11)
+    blocks = [BinaryResBlock(64, 64, 1).cuda().to(memory_format=torch.channels_last)
+              for _ in range(3)]
+    with torch.no_grad():
+        for b in blocks:
+            b.bn.weight.uniform_(0.5, 1.5)
+            b.bn.bias.uniform_(-0.5, 0.5)
+    x = (torch.randn(4, 64, 28, 28, device="cuda") * 1.5).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    g = torch.randn(4, 64, 28, 28, device="cuda").to(torch.bfloat16)
+    res = []
+    for fuse in (True, False):
+        monkeypatch.setattr(binary, "FUSE_BNSUM", fuse)
+        bs = [copy.deepcopy(b) for b in blocks]
+        xx = x.clone().requires_grad_(True)
+        h = xx
+        outs = []
+        for b in bs:
+            h = ops.binary_block(h, h, b.conv, b.bn)
+            outs.append(h)
+        loss = (h.float() * g.float()).sum()
+        if second_consumer:
+            loss = loss + (outs[0].float() * 0.5).sum()
+        loss.backward()
+        res.append([xx.grad.float()] + [p.grad.clone() for b in bs for p in b.parameters()])
+    for a, b in zip(*res):
+        assert ((a - b).norm() / b.norm().clamp_min(1e-12)).item() < 2e-3

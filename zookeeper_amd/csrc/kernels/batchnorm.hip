@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
                                                             float* __restrict__ sums,
-                                                            long long P) {
+                                                            long long P, int stripes) {
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;  // rows per block iteration
   const int cg = threadIdx.x % CG;
@@ -184,6 +184,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     red[1][threadIdx.x][k] = sgy[k];
   }
   __syncthreads();
+  float* out = sums + (long long)(blockIdx.x % stripes) * 2 * C;  // striped copies
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const int gcg = c / 8, k = c % 8;
     float a = 0.f, b = 0.f;
@@ -191,8 +192,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       a += red[0][rr * CG + gcg][k];
       b += red[1][rr * CG + gcg][k];
     }
-    atomicAdd(sums + c, a);
-    atomicAdd(sums + C + c, b);
+    atomicAdd(out + c, a);
+    atomicAdd(out + C + c, b);
   }
 }
 
@@ -240,18 +241,33 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint16_t* __restri
 // Per-channel backward coefficients from the reductions (one tiny launch
 // instead of a chain of framework ops), plus gamma/beta gradients
 // accumulated straight into the parameters' gradient buffers:
-//   sums = [sum g, sum g*yhat];  coef = [k1, k0, k3]
-//   dgamma += sum g*yhat,  dbeta += sum g
-__global__ void bn_bwd_coef_kernel(float* __restrict__ sums, const float* __restrict__ mean,
-                                   const float* __restrict__ rstd,
-                                   const float* __restrict__ gamma, double P, int C,
-                                   float* __restrict__ coef, float* __restrict__ dgamma,
-                                   float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const float sg = sums[c], sgy = sums[C + c];
-  sums[c] = 0.f;
-  sums[C + c] = 0.f;
+//   sums = [stripes][sum g, sum g*yhat] (copies summed and re-zeroed here);
+//   coef = [k1, k0, k3];  dgamma += sum g*yhat,  dbeta += sum g.
+// A group of 32 lanes owns one channel (lane k reads copies k, k+32, ...).
+__global__ __launch_bounds__(256) void bn_bwd_coef_kernel(float* __restrict__ sums,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          const float* __restrict__ gamma,
+                                                          double P, int C, int stripes,
+                                                          float* __restrict__ coef,
+                                                          float* __restrict__ dgamma,
+                                                          float* __restrict__ dbeta) {
+  const int k = threadIdx.x & 31;
+  const int c = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (c >= C) return;  // uniform over the 32-lane group
+  float sg = 0.f, sgy = 0.f;
+  for (int j = k; j < stripes; j += 32) {
+    sg += sums[(2LL * j) * C + c];
+    sgy += sums[(2LL * j + 1) * C + c];
+    sums[(2LL * j) * C + c] = 0.f;
+    sums[(2LL * j + 1) * C + c] = 0.f;
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    sg += __shfl_xor(sg, o, 32);
+    sgy += __shfl_xor(sgy, o, 32);
+  }
+  if (k != 0) return;
   const float rs = rstd[c];
   const float k1 = (gamma ? gamma[c] : 1.f) * rs;
   const float k3 = k1 * rs * (float)(sgy / P);
@@ -370,8 +386,10 @@ ZK_EXPORT int zk_bn_apply_sign(const void* y, const void* scale, const void* shi
   return 0;
 }
 
+// sums: [stripes][2][C] fp32 copies (block b adds into copy b % stripes).
 ZK_EXPORT int zk_bn_bwd_reduce(const void* g, const void* y, const void* mean, const void* rstd,
-                               void* sums, long long P, int C, hipStream_t stream) {
+                               void* sums, long long P, int C, int stripes, hipStream_t stream) {
+  if (stripes < 1) stripes = 1;
   // 512 blocks x 4 rows in flight per thread: enough bytes in flight for
   // HBM, few enough per-block atomics into the 2*C sums
   const int blocks = 512;
@@ -379,7 +397,7 @@ ZK_EXPORT int zk_bn_bwd_reduce(const void* g, const void* y, const void* mean, c
   case cg:                                                                                \
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<cg>, dim3(blocks), dim3(256), 0, stream,      \
                        (const uint16_t*)g, (const int16_t*)y, (const float*)mean,         \
-                       (const float*)rstd, (float*)sums, P);                              \
+                       (const float*)rstd, (float*)sums, P, stripes);                     \
     break;
   switch (C / 8) {
     ZK_RED_CASE(4)
@@ -411,11 +429,11 @@ ZK_EXPORT int zk_bn_bwd_dx(const void* g, const void* y, const void* coef, void*
 }
 
 ZK_EXPORT int zk_bn_bwd_coef(const void* sums, const void* mean, const void* rstd,
-                             const void* gamma, double P, int C, void* coef, void* dgamma,
-                             void* dbeta, hipStream_t stream) {
-  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, stream,
-                     (float*)sums, (const float*)mean, (const float*)rstd,
-                     (const float*)gamma, P, C, (float*)coef, (float*)dgamma, (float*)dbeta);
+                             const void* gamma, double P, int C, int stripes, void* coef,
+                             void* dgamma, void* dbeta, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 7) / 8), dim3(256), 0, stream, (float*)sums,
+                     (const float*)mean, (const float*)rstd, (const float*)gamma, P, C,
+                     stripes < 1 ? 1 : stripes, (float*)coef, (float*)dgamma, (float*)dbeta);
   ZK_CHECK_LAUNCH();
   return 0;
 }

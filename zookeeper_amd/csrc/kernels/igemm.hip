@@ -53,8 +53,102 @@ struct ConvArgs {
   void* out;             // dgrad: dx bf16 / fwd: y int16
   unsigned long long* stats;  // fwd: [stripes][2][Cout] int64 (sum, sum of squares)
   int pad_ones, relu;    // fwd
-  int stripes;           // fwd: copies of the statistics; block b adds into copy b % stripes
+  int stripes;           // copies of stats / psums; block b adds into copy b % stripes
+  // dgrad (optional): fused BN-backward reduction of the PREVIOUS block, whose
+  // output gradient is exactly the dx this kernel writes (identity shortcut,
+  // single consumer): psums[stripe][0][c] += sum dx, [1][c] += sum dx * yhat,
+  // yhat = (ypred - pmean[c]) * prstd[c] -- the zk_bn_bwd_reduce of that block.
+  const int16_t* ypred;
+  const float* pmean;
+  const float* prstd;
+  float* psums;
 };
+
+// Reduce-scatter of 32 values over the 32 lanes of each wave half: after
+// the 5 butterfly steps lane r holds the half's total of value r (31
+// exchanges per lane instead of 32 full 5-step reductions).
+template <int N>
+__device__ __forceinline__ void rs_step(float (&v)[32], int r32) {
+  constexpr int OFF = N;  // exchange distance == values kept
+  const bool upper = (r32 & OFF) != 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float send = upper ? v[i] : v[i + N];
+    const float keep = upper ? v[i + N] : v[i];
+    v[i] = keep + __shfl_xor(send, OFF, 64);
+  }
+}
+
+// dgrad epilogue for one 32-channel block of a wave's tile (lane = pixel,
+// 4 consecutive channels per register group): STE mask, + residual
+// gradient, bf16 dx, and (args.psums) the fused BN-backward sums of the
+// stored values.  pix[a] < 0: no pixel for this lane in row-group a.
+template <int TM>
+__device__ __forceinline__ void dgrad_store_block(const ConvArgs& args, const IGeom& g,
+                                                  const f32x16 (&acc)[TM], const long long (&pix)[TM],
+                                                  int nb, int h, int r32) {
+  uint16_t* dx = reinterpret_cast<uint16_t*>(args.out);
+  const int CW = g.Cin >> 5;
+  uint32_t mw[TM];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+    mw[a] = (args.mask && pix[a] >= 0) ? args.mask[pix[a] * CW + (nb >> 5)] : 0xFFFFFFFFu;
+  float* ps = nullptr;
+  if (args.psums)
+    ps = args.psums + (long long)(args.stripes > 1 ? blockIdx.x % args.stripes : 0) * 2 * g.Cin;
+  float vals[32];  // value j = s*16 + q*4 + e: sum (s = 0) / sum * yhat (s = 1) of channel (q, e)
+#pragma unroll
+  for (int j = 0; j < 32; ++j) vals[j] = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int nl = 8 * q + 4 * h;
+    float mu[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {0.f, 0.f, 0.f, 0.f};
+    if (ps) {
+      const float4 m4 = *reinterpret_cast<const float4*>(args.pmean + nb + nl);
+      const float4 r4 = *reinterpret_cast<const float4*>(args.prstd + nb + nl);
+      mu[0] = m4.x; mu[1] = m4.y; mu[2] = m4.z; mu[3] = m4.w;
+      rs[0] = r4.x; rs[1] = r4.y; rs[2] = r4.z; rs[3] = r4.w;
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      if (pix[a] < 0) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = ((mw[a] >> (nl + e)) & 1u) ? acc[a][4 * q + e] : 0.f;
+      const long long off = pix[a] * g.Cin + nb + nl;
+      if (args.dres) {
+        const uint2 d = *reinterpret_cast<const uint2*>(args.dres + off);
+        v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
+        v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
+        v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
+        v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
+      }
+      const uint2 o = make_uint2(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]));
+      *reinterpret_cast<uint2*>(dx + off) = o;
+      if (ps) {
+        const uint2 yv = *reinterpret_cast<const uint2*>(args.ypred + off);
+        const int16_t* yy = reinterpret_cast<const int16_t*>(&yv);
+        const uint32_t ow[2] = {o.x, o.y};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gv = zk::bf16_to_f32((uint16_t)(ow[e >> 1] >> (16 * (e & 1))));  // as stored
+          vals[q * 4 + e] += gv;
+          vals[16 + q * 4 + e] += gv * ((float)yy[e] - mu[e]) * rs[e];
+        }
+      }
+    }
+  }
+  if (ps) {
+    // the 32 lanes of a wave half hold the same 16 channels (other pixels)
+    rs_step<16>(vals, r32);
+    rs_step<8>(vals, r32);
+    rs_step<4>(vals, r32);
+    rs_step<2>(vals, r32);
+    rs_step<1>(vals, r32);
+    const int c = nb + 8 * ((r32 >> 2) & 3) + 4 * h + (r32 & 3);
+    atomicAdd(ps + (r32 >> 4) * g.Cin + c, vals[0]);
+  }
+}
 
 template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB, bool F4 = false>
 __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs args, IGeom g,
@@ -329,39 +423,61 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
     }
   } else {
     // ---- dgrad epilogue: lane = pixel, 4 consecutive channels per group
-    uint16_t* dx = reinterpret_cast<uint16_t*>(args.out);
-    const uint32_t* mask = args.mask;
-    const uint16_t* dres = args.dres;
-    const int CW = g.Cin >> 5;
+    if (args.psums) {
+      // + the previous block's fused BN-backward sums (dgrad_store_block)
+      long long pix[TM];
 #pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      const long long mc = m0 + wm * WTM + a * 32 + r32;
-      if (mc >= M) continue;
-      const int jw = (int)(mc % Wc);
-      const long long rr = mc / Wc;
-      const long long m =
-          ((rr / Hc) * g.H + (long long)(rr % Hc) * s + ph) * g.W + (long long)jw * s + pw;
+      for (int a = 0; a < TM; ++a) {
+        const long long mc = m0 + wm * WTM + a * 32 + r32;
+        pix[a] = -1;
+        if (mc < M) {
+          const int jw = (int)(mc % Wc);
+          const long long rr = mc / Wc;
+          pix[a] = ((rr / Hc) * g.H + (long long)(rr % Hc) * s + ph) * g.W + (long long)jw * s + pw;
+        }
+      }
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
-        const int nb = n0 + wn * WTN + b * 32;
-        const uint32_t mw = mask ? mask[m * CW + (nb >> 5)] : 0xFFFFFFFFu;
+        f32x16 ab[TM];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int nl = 8 * q + 4 * h;
-          float v[4];
+        for (int a = 0; a < TM; ++a) ab[a] = acc[a][b];
+        dgrad_store_block<TM>(args, g, ab, pix, n0 + wn * WTN + b * 32, h, r32);
+      }
+    } else {
+      uint16_t* dx = reinterpret_cast<uint16_t*>(args.out);
+      const uint32_t* mask = args.mask;
+      const uint16_t* dres = args.dres;
+      const int CW = g.Cin >> 5;
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            v[e] = ((mw >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
-          const long long off = m * g.Cin + nb + nl;
-          if (dres) {
-            const uint2 d = *reinterpret_cast<const uint2*>(dres + off);
-            v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
-            v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
-            v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
-            v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
+      for (int a = 0; a < TM; ++a) {
+        const long long mc = m0 + wm * WTM + a * 32 + r32;
+        if (mc >= M) continue;
+        const int jw = (int)(mc % Wc);
+        const long long rr = mc / Wc;
+        const long long m =
+            ((rr / Hc) * g.H + (long long)(rr % Hc) * s + ph) * g.W + (long long)jw * s + pw;
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int nb = n0 + wn * WTN + b * 32;
+          const uint32_t mw = mask ? mask[m * CW + (nb >> 5)] : 0xFFFFFFFFu;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int nl = 8 * q + 4 * h;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              v[e] = ((mw >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
+            const long long off = m * g.Cin + nb + nl;
+            if (dres) {
+              const uint2 d = *reinterpret_cast<const uint2*>(dres + off);
+              v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
+              v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
+              v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
+              v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
+            }
+            *reinterpret_cast<uint2*>(dx + off) =
+                make_uint2(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]));
           }
-          *reinterpret_cast<uint2*>(dx + off) =
-              make_uint2(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]));
         }
       }
     }
@@ -579,35 +695,52 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
     }
   } else {
     // ---- dgrad epilogue (stride 1: the pixel index is the row index)
-    uint16_t* dx = reinterpret_cast<uint16_t*>(args.out);
-    const uint32_t* mask = args.mask;
-    const uint16_t* dres = args.dres;
-    const int CW = g.Cin >> 5;
+    if (args.psums) {
+      // + the previous block's fused BN-backward sums (dgrad_store_block)
+      long long pix[TM];
 #pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      const long long m = m0 + wm * WTM + a * 32 + r32;
-      if (m >= M) continue;
+      for (int a = 0; a < TM; ++a) {
+        const long long m = m0 + wm * WTM + a * 32 + r32;
+        pix[a] = m < M ? m : -1;
+      }
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
-        const int nb = n0 + wn * WTN + b * 32;
-        const uint32_t mw = mask ? mask[m * CW + (nb >> 5)] : 0xFFFFFFFFu;
+        f32x16 ab[TM];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int nl = 8 * q + 4 * h;
-          float v[4];
+        for (int a = 0; a < TM; ++a) ab[a] = acc[a][b];
+        dgrad_store_block<TM>(args, g, ab, pix, n0 + wn * WTN + b * 32, h, r32);
+      }
+    } else {
+      uint16_t* dx = reinterpret_cast<uint16_t*>(args.out);
+      const uint32_t* mask = args.mask;
+      const uint16_t* dres = args.dres;
+      const int CW = g.Cin >> 5;
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            v[e] = ((mw >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
-          const long long off = m * g.Cin + nb + nl;
-          if (dres) {
-            const uint2 d = *reinterpret_cast<const uint2*>(dres + off);
-            v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
-            v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
-            v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
-            v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
+      for (int a = 0; a < TM; ++a) {
+        const long long m = m0 + wm * WTM + a * 32 + r32;
+        if (m >= M) continue;
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int nb = n0 + wn * WTN + b * 32;
+          const uint32_t mw = mask ? mask[m * CW + (nb >> 5)] : 0xFFFFFFFFu;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int nl = 8 * q + 4 * h;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              v[e] = ((mw >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
+            const long long off = m * g.Cin + nb + nl;
+            if (dres) {
+              const uint2 d = *reinterpret_cast<const uint2*>(dres + off);
+              v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
+              v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
+              v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
+              v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
+            }
+            *reinterpret_cast<uint2*>(dx + off) =
+                make_uint2(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]));
           }
-          *reinterpret_cast<uint2*>(dx + off) =
-              make_uint2(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]));
         }
       }
     }
@@ -644,9 +777,18 @@ int launch_conv3(const ConvArgs& args, const IGeom& g, hipStream_t stream) {
   return 0;
 }
 
+// Optional fused BN-backward reduction of the previous block (ConvArgs::psums).
+struct BnSum {
+  const void* ypred;
+  const void* mean;
+  const void* rstd;
+  void* sums;
+  int stripes;
+};
+
 template <int BM, int BN, int WM, int WN, int NS, int CB = 128>
 int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const void* dres,
-                       void* dx, const IGeom& g, hipStream_t stream) {
+                       void* dx, const IGeom& g, const BnSum& bs, hipStream_t stream) {
   if ((g.Cout * 2) % CB || g.Cin % BN || g.s > 2 || g.kh > 4 || g.kw > 4)
     return (int)hipErrorInvalidValue;
   constexpr int LDS = NS * (BM + BN) * CB;
@@ -664,7 +806,9 @@ int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const v
   const int m_tiles = (int)((Mc + BM - 1) / BM);
   const long long blocks = (long long)m_tiles * (g.Cin / BN);
   ConvArgs args{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
-                (const uint16_t*)dres, dx, nullptr, 0, 0, 1};
+                (const uint16_t*)dres, dx, nullptr, 0, 0, bs.stripes,
+                (const int16_t*)bs.ypred, (const float*)bs.mean, (const float*)bs.rstd,
+                (float*)bs.sums};
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, g.s * g.s), dim3(WM * WN * 64), LDS, stream,
                      args, g, m_tiles);
   return 0;
@@ -777,8 +921,9 @@ int igemm_fwd4_variant(int v, const void* sx, const void* wf, void* y, void* sta
 }
 
 int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
-                        const void* dres, void* dx, const IGeom& g, hipStream_t st) {
-#define ZK_IGD(...) return launch_igemm_dgrad<__VA_ARGS__>(dy, wt, mask, dres, dx, g, st)
+                        const void* dres, void* dx, const IGeom& g, const BnSum& bs,
+                        hipStream_t st) {
+#define ZK_IGD(...) return launch_igemm_dgrad<__VA_ARGS__>(dy, wt, mask, dres, dx, g, bs, st)
   switch (v) {
     case 0: ZK_IGD(128, 128, 2, 2, 2);        // 64 KB: 2 WG/CU
     case 1: ZK_IGD(128, 128, 2, 2, 4, 64);    // 64 KB, 3 K-steps of 32 in flight
@@ -798,7 +943,9 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
 #define ZK_IGD3(...)                                                                    \
   {                                                                                     \
     ConvArgs a{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,         \
-               (const uint16_t*)dres, dx, nullptr, 0, 0, 1};                            \
+               (const uint16_t*)dres, dx, nullptr, 0, 0, bs.stripes,                    \
+               (const int16_t*)bs.ypred, (const float*)bs.mean, (const float*)bs.rstd,  \
+               (float*)bs.sums};                                                        \
     return launch_conv3<false, __VA_ARGS__>(a, g, st);                                  \
   }
     case 20: ZK_IGD3(256, 64, 4, 1, 2, 128)
@@ -1111,13 +1258,9 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
 
 }  // namespace
 
-// Same contract as zk_bconv_dgrad (binary_conv_bwd.hip): wt ±1 bf16
-// [T][Cin][Cout], mask / dres optional, Cout % 64 == 0, Cin % BN == 0.
-ZK_EXPORT int zk_igemm_dgrad(const void* dy, const void* wt, const void* mask, const void* dres,
-                             void* dx, int B, int H, int W, int Cin, int Ho, int Wo, int Cout,
-                             int kh, int kw, int stride, int pt, int pl, int variant,
-                             hipStream_t stream) {
-  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+namespace {
+int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
+                     const IGeom& g, const BnSum& bs, int variant, hipStream_t stream) {
   if (variant < 0) {
     // Tuned on MI355X (tools/tune_bconv.py --only igemm, E18 shapes, batch
     // 256): 128x128 at 2 WG/CU for Cin >= 128 (8-wave 256x128 for the
@@ -1125,6 +1268,7 @@ ZK_EXPORT int zk_igemm_dgrad(const void* dy, const void* wt, const void* mask, c
     // 256x256 (v14) halves the LDS-fill bytes per FLOP; it pays where the
     // grid still has ~200 tiles (the 256-channel stride-1 layers).  conv3
     // (20+: horizontal tap reuse) for the other stride-1 3x3 layers.
+    const int Cin = g.Cin, stride = g.s;
     const bool c3 = conv3_ok(g, 0);
     if (Cin == 256 && stride == 1)
       variant = 14;
@@ -1139,10 +1283,38 @@ ZK_EXPORT int zk_igemm_dgrad(const void* dy, const void* wt, const void* mask, c
     else
       variant = 7;
   }
-  const int rc = igemm_dgrad_variant(variant, dy, wt, mask, dres, dx, g, stream);
+  const int rc = igemm_dgrad_variant(variant, dy, wt, mask, dres, dx, g, bs, stream);
   if (rc) return rc;
   ZK_CHECK_LAUNCH();
   return 0;
+}
+}  // namespace
+
+// Same contract as zk_bconv_dgrad (binary_conv_bwd.hip): wt ±1 bf16
+// [T][Cin][Cout], mask / dres optional, Cout % 64 == 0, Cin % BN == 0.
+ZK_EXPORT int zk_igemm_dgrad(const void* dy, const void* wt, const void* mask, const void* dres,
+                             void* dx, int B, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                             int kh, int kw, int stride, int pt, int pl, int variant,
+                             hipStream_t stream) {
+  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+  return igemm_dgrad_impl(dy, wt, mask, dres, dx, g, BnSum{nullptr, nullptr, nullptr, nullptr, 1},
+                          variant, stream);
+}
+
+// zk_igemm_dgrad + the previous block's BN-backward reduction fused into the
+// epilogue: sums [stripes][2][Cin] fp32 += (sum dx, sum dx * (ypred - mean) *
+// rstd) over the stored bf16 dx (ypred int16 [B][H][W][Cin]; mean / rstd
+// [Cin]).  Valid when dx is that block's whole output gradient.
+ZK_EXPORT int zk_igemm_dgrad_bnsum(const void* dy, const void* wt, const void* mask,
+                                   const void* dres, void* dx, const void* ypred, const void* mean,
+                                   const void* rstd, void* sums, int stripes, int B, int H, int W,
+                                   int Cin, int Ho, int Wo, int Cout, int kh, int kw, int stride,
+                                   int pt, int pl, int variant, hipStream_t stream) {
+  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+  if (!ypred || !mean || !rstd || !sums || Cin % 32) return (int)hipErrorInvalidValue;
+  return igemm_dgrad_impl(dy, wt, mask, dres, dx, g,
+                          BnSum{ypred, mean, rstd, sums, stripes < 1 ? 1 : stripes}, variant,
+                          stream);
 }
 
 namespace {

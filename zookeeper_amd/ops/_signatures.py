@@ -27,6 +27,7 @@ SIGNATURES = {
     "zk_bconv_fwd": (I32, [P, P, P, P, P] + [I32] * 14 + [P]),
     "zk_bconv_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
     "zk_igemm_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
+    "zk_igemm_dgrad_bnsum": (I32, [P] * 9 + [I32] * 14 + [P]),
     "zk_igemm_fwd": (I32, [P, P, P, P] + [I32] * 16 + [P]),
     "zk_igemm_fwd_fp4": (I32, [P, P, P, P] + [I32] * 16 + [P]),
     "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),
@@ -36,10 +37,10 @@ SIGNATURES = {
     "zk_bn_finalize": (I32, [P, I32, I32, C.c_double, P, P, F32, F32, P, P, P, P, P, P, P]),
     "zk_bn_apply": (I32, [P, P, P, P, P, I64, I32, P]),
     "zk_bn_apply_sign": (I32, [P, P, P, P, P, P, P, P, F32, I64, I32, P]),
-    "zk_bn_bwd_reduce": (I32, [P, P, P, P, P, I64, I32, P]),
+    "zk_bn_bwd_reduce": (I32, [P, P, P, P, P, I64, I32, I32, P]),
     "zk_bn_bwd_dx": (I32, [P, P, P, P, I64, I32, I32, P]),
     "zk_ste_combine": (I32, [P, P, P, P, I64, P]),
-    "zk_bn_bwd_coef": (I32, [P, P, P, P, C.c_double, I32, P, P, P, P]),
+    "zk_bn_bwd_coef": (I32, [P, P, P, P, C.c_double, I32, I32, P, P, P, P]),
     # batch norm (bf16) and pooling
     "zk_bn_stats_bf16": (I32, [P, P, I64, I32, P]),
     "zk_bn_finalize_f64": (I32, [P, I32, C.c_double, P, P, F32, F32, P, P, P, P]),

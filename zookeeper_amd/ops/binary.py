@@ -47,6 +47,36 @@ FP4 = os.environ.get("ZK_BCONV_FP4", "1") != "0"
 # copy b % STAT_STRIPES; zk_bn_finalize sums them): one [2][Cout] array took
 # thousands of serialised int64 atomics per cache line on the 56x56 layers.
 STAT_STRIPES = 32
+# ZK_FUSE_BNSUM=1: the BN-backward reduction (sum g, sum g*yhat) of a block
+# whose output only feeds the next block's identity shortcut + conv is done
+# in that block's dgrad epilogue, which writes exactly this gradient
+# (zk_igemm_dgrad_bnsum).  Off by default: measured on MI355X (E18, batch
+# 256) the extra epilogue work on the latency-bound dgrad tiles cost more
+# (33.4k -> 31.0k img/s) than the separate reduce kernels it removes.
+FUSE_BNSUM = os.environ.get("ZK_FUSE_BNSUM", "0") == "1"
+
+
+class _BnSum:
+    """What the successor's dgrad needs to reduce this block's BN gradient:
+    the int16 conv output, BN mean / rstd, the striped sums buffer, and (set
+    by the successor's backward) the dx it reduced and its version."""
+
+    __slots__ = ("y", "mean", "rstd", "sums", "dx", "dx_version")
+
+    def __init__(self, y, mean, rstd, sums):
+        self.y, self.mean, self.rstd, self.sums = y, mean, rstd, sums
+        self.dx = self.dx_version = None
+
+    def reduced(self, dout: torch.Tensor) -> bool:
+        """True if the successor's epilogue reduced exactly ``dout``: the
+        same storage (``self.dx`` holds it, so no other tensor can reuse the
+        address), not modified since (autograd accumulates a second
+        consumer's gradient in place, bumping the version counter, or into
+        a new tensor)."""
+        ok = (self.dx is not None and dout.data_ptr() == self.dx.data_ptr()
+              and dout._version == self.dx_version)
+        self.dx = None
+        return ok
 
 
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
@@ -57,7 +87,7 @@ def _nhwc(t: torch.Tensor) -> torch.Tensor:
 class _BinaryBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, gamma, beta, bn, meta):
-        (stride, act_relu, clip, pad_ones, identity, will_backward, next_sign) = meta
+        (stride, act_relu, clip, pad_ones, identity, will_backward, next_sign, side) = meta
         B, Cin, H, W = x.shape
         Cout, _, kh, kw = weight.shape
         T = kh * kw
@@ -174,6 +204,16 @@ class _BinaryBlockFn(torch.autograd.Function):
                                 res.data_ptr() if res is not None else None, out.data_ptr(), P,
                                 Cout, st), "zk_bn_apply")
 
+        # BN-backward fusion hand-off (see FUSE_BNSUM): this block's reduction
+        # may be done by its successor; the predecessor's by this block.
+        ctx.bnsum = None
+        if FUSE_BNSUM and will_backward and bn.training:
+            sums_buf = zeroed_scratch(bn, "bwd_sums", (STAT_STRIPES, 2, Cout), torch.float32, dev)
+            ctx.bnsum = _BnSum(y, mean, rstd, sums_buf)
+            side["bnsum"] = ctx.bnsum
+        pred = side.get("pred")
+        ctx.pred = (pred if (pred is not None and identity and mfma
+                             and tuple(pred.y.shape) == (B, H, W, Cin)) else None)
         ctx.save_for_backward(bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx)
         ctx.params = (weight, gamma, beta)
         ctx.geom = (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo)
@@ -187,7 +227,7 @@ class _BinaryBlockFn(torch.autograd.Function):
     def backward(ctx, dout):
         bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx = ctx.saved_tensors
         (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
-        (_, act_relu, clip, pad_ones, identity, _, _) = ctx.meta
+        (_, act_relu, clip, pad_ones, identity, _, _, _) = ctx.meta
         dev = dout.device
         st = stream_ptr(dev)
         L = lib()
@@ -195,9 +235,16 @@ class _BinaryBlockFn(torch.autograd.Function):
 
         g = _nhwc(dout.to(torch.bfloat16))
         weight_p, gamma_p, beta_p = ctx.params
-        sums = zeroed_scratch(ctx.bn, "bwd_sums", (2, Cout), torch.float32, dev)
-        check(L.zk_bn_bwd_reduce(g.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                                 sums.data_ptr(), P, Cout, st), "zk_bn_bwd_reduce")
+        sums = zeroed_scratch(ctx.bn, "bwd_sums", (STAT_STRIPES, 2, Cout), torch.float32, dev)
+        bs = ctx.bnsum
+        fused = bs is not None and bs.dx is not None
+        if not (fused and bs.reduced(dout)):
+            if fused:
+                sums.zero_()  # the successor reduced a gradient that was accumulated later
+            check(L.zk_bn_bwd_reduce(g.data_ptr(), y.data_ptr(), mean.data_ptr(),
+                                     rstd.data_ptr(), sums.data_ptr(), P, Cout, STAT_STRIPES, st),
+                  "zk_bn_bwd_reduce")
+        # else: the successor's dgrad epilogue reduced exactly this gradient
         # BN coefficients + gamma/beta gradients in one launch; gradients go
         # straight into the flat gradient buffer when the trainer manages it.
         dg_direct = direct_grad(gamma_p) if ctx.has_gamma else None
@@ -209,7 +256,8 @@ class _BinaryBlockFn(torch.autograd.Function):
         coef = torch.empty((3, Cout), dtype=torch.float32, device=dev)
         check(L.zk_bn_bwd_coef(sums.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                                gamma.data_ptr() if gamma is not None else None, float(P), Cout,
-                               coef.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
+                               STAT_STRIPES, coef.data_ptr(),
+                               dgamma.data_ptr() if dgamma is not None else None,
                                dbeta.data_ptr() if dbeta is not None else None, st),
               "zk_bn_bwd_coef")
         if dg_direct is not None:
@@ -230,10 +278,22 @@ class _BinaryBlockFn(torch.autograd.Function):
             if need_dx:
                 dx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
                 dres = g if identity else None
-                check(L.zk_igemm_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(),
-                                       dres.data_ptr() if dres is not None else None,
-                                       dx.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
-                                       stride, pt, pl, -1, st), "zk_igemm_dgrad")
+                pred = ctx.pred
+                if pred is not None:
+                    # + the predecessor's BN-backward sums over this dx
+                    check(L.zk_igemm_dgrad_bnsum(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(),
+                                                 dres.data_ptr() if dres is not None else None,
+                                                 dx.data_ptr(), pred.y.data_ptr(),
+                                                 pred.mean.data_ptr(), pred.rstd.data_ptr(),
+                                                 pred.sums.data_ptr(), STAT_STRIPES, B, H, W, Cin,
+                                                 Ho, Wo, Cout, kh, kw, stride, pt, pl, -1, st),
+                          "zk_igemm_dgrad_bnsum")
+                    pred.dx, pred.dx_version = dx, dx._version
+                else:
+                    check(L.zk_igemm_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(),
+                                           dres.data_ptr() if dres is not None else None,
+                                           dx.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
+                                           stride, pt, pl, -1, st), "zk_igemm_dgrad")
                 dx = dx.permute(0, 3, 1, 2)
             w_direct = direct_grad(weight_p, channels_last=True)
             if w_direct is not None:
@@ -334,11 +394,14 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
     will_backward = torch.is_grad_enabled() and (
         x.requires_grad or conv.weight.requires_grad or bn.training)
     holder: list = [] if quantize_output else None
+    side = {"pred": getattr(x, "_zk_bnsum", None)}
     meta = (conv.stride[0], act == "relu", float(clip_value), pad_value == 1.0, identity,
-            will_backward, holder)
+            will_backward, holder, side)
     out = _BinaryBlockFn.apply(x, None if identity else residual, conv.weight, bn.weight,
                                bn.bias, bn, meta)
     if holder:
         # consumed by the next binary block (same clip) instead of re-reading out
         out._zk_sign = tuple(holder)
+    if side.get("bnsum") is not None:
+        out._zk_bnsum = side["bnsum"]
     return out

@@ -87,7 +87,7 @@ class _BatchNormFn(torch.autograd.Function):
             torch.zeros(C, device=dev) if ctx.has_beta else None)
         bcoef = torch.empty((3, C), dtype=torch.float32, device=dev)
         check(L.zk_bn_bwd_coef(sums.data_ptr(), coef[2].data_ptr(), coef[3].data_ptr(),
-                               gamma.data_ptr() if gamma is not None else None, float(P), C,
+                               gamma.data_ptr() if gamma is not None else None, float(P), C, 1,
                                bcoef.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
                                dbeta.data_ptr() if dbeta is not None else None, st),
               "zk_bn_bwd_coef")

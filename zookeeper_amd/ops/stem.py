@@ -60,7 +60,7 @@ def _bn_bwd_coef(L, st, sums, coef, gamma_p, beta_p, P, C, dev):
     dbeta = db if db is not None else (torch.zeros(C, device=dev) if beta_p is not None else None)
     bcoef = torch.empty((3, C), dtype=torch.float32, device=dev)
     check(L.zk_bn_bwd_coef(sums.data_ptr(), coef[2].data_ptr(), coef[3].data_ptr(),
-                           gamma_p.data_ptr() if gamma_p is not None else None, float(P), C,
+                           gamma_p.data_ptr() if gamma_p is not None else None, float(P), C, 1,
                            bcoef.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
                            dbeta.data_ptr() if dbeta is not None else None, st), "zk_bn_bwd_coef")
     if dg is not None:
