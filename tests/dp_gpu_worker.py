@@ -1,0 +1,59 @@
+"""Worker for the data-parallel GPU test: two ranks share the box's GPU and
+talk over gloo (RCCL needs one GPU per rank), so the GPU training path --
+HIP kernels writing gradients straight into the flat buffer, post-accumulate
+hooks and direct-grad readiness driving the bucketed all-reduce, initial
+broadcast -- runs multi-rank.
+
+    python tests/dp_gpu_worker.py <same|split> <outdir>
+
+``same``: every rank trains on the same batches, so the averaged gradients
+equal a single process's and the result must match a world-size-1 run
+(``world=1`` when launched without the env contract).  ``split``: disjoint
+batches; ranks must stay bit-identical."""
+
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def run(mode: str, out: str) -> None:
+    from zookeeper_amd.core import configure
+    from zookeeper_amd.models.binary_resnet import BinaryResNetE
+    from zookeeper_amd.parallel import dist as zdist
+    from zookeeper_amd.train import Adam, Trainer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    info = zdist.init("gloo") if world > 1 else zdist.init()
+    torch.manual_seed(1234)
+    model = BinaryResNetE((64, 64, 3), 10, 18, backend="hip")
+    if info.rank == 1:  # different init on rank 1: the broadcast must fix it
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_(0.5)
+    spec = Adam()
+    configure(spec, {"learning_rate": 1e-3})
+    tr = Trainer(model, "sparse_categorical_crossentropy", spec, info, bucket_mb=2.0,
+                 first_bucket_mb=0.25)
+    g = torch.Generator().manual_seed(99)
+    steps, per = 3, 4
+    # the same tensors for every world size (at most 2 ranks)
+    xs = torch.randn(steps, 2 * per, 3, 64, 64, generator=g)
+    ys = torch.randint(0, 10, (steps, 2 * per), generator=g)
+    for s in range(steps):
+        lo = 0 if mode == "same" else info.rank * per
+        x = xs[s, lo:lo + per].to(info.device, torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        y = ys[s, lo:lo + per].to(info.device)
+        loss, _ = tr.train_step(x, y)
+    torch.cuda.synchronize()
+    torch.save({"params": tr.flat.data.cpu(), "loss": float(loss),
+                "buckets": tr.bucketer.num_buckets},
+               os.path.join(out, f"{mode}_w{world}_r{info.rank}.pt"))
+    zdist.shutdown()
+
+
+if __name__ == "__main__":
+    run(sys.argv[1], sys.argv[2])
