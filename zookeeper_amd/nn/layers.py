@@ -165,6 +165,13 @@ class QuantConv2d(nn.Module):
 
             if pointwise.supported(x, self.weight, self.stride, self.groups, self.bias):
                 return pointwise.conv1x1(x, self.weight)
+        if (self.input_quantizer is None and self.kernel_quantizer is None
+                and self.kernel_size == (3, 3) and _use_native(x)):
+            from zookeeper_amd.ops import conv3x3
+
+            if conv3x3.supported(x, self.weight, self.stride, self.padding, self.groups,
+                                 self.bias, self.pad_values):
+                return conv3x3.conv3x3(x, self.weight)
         if self.input_quantizer is not None:
             x = self.input_quantizer(x)
         if self.padding == "same":

@@ -67,6 +67,11 @@ class GradBucketer:
         self._hooks = []
         self._seen = [False] * len(flat.slots)
         self.enabled = world > 1
+        # gloo on GPU tensors (tests, 1-GPU rehearsals) stages through host
+        # copies on its own streams; order them with a host sync instead of
+        # relying on its stream events (RCCL orders on the device).
+        self._host_sync = (self.enabled and flat.grad.is_cuda
+                           and dist.get_backend(group) != "nccl")
         if self.enabled:
             for i, s in enumerate(flat.slots):
                 hook = self._make_hook(i)
@@ -94,6 +99,8 @@ class GradBucketer:
     def _launch(self, b: int) -> None:
         lo, hi = self.ranges[b]
         view = self.flat.grad[lo:hi]
+        if self._host_sync:
+            torch.cuda.current_stream(view.device).synchronize()
         if self.grad_dtype is not None and self.grad_dtype != view.dtype:
             tmp = view.to(self.grad_dtype)
             work = dist.all_reduce(tmp, group=self.group, async_op=True)
@@ -113,6 +120,8 @@ class GradBucketer:
             work.wait()
             if view is not None:
                 view.copy_(tmp)
+        if self._host_sync:
+            torch.cuda.synchronize(self.flat.grad.device)
         self._works.clear()
         self._pending = [len(b) for b in self.buckets]
         self._launched = [False] * len(self.buckets)
