@@ -1,0 +1,53 @@
+"""Binary-conv weight gradients on the side stream (ops/streams.py): the
+same gradients as the single-stream backward, and every deferred readiness
+signalled (each direct-gradient parameter reported ready exactly once)."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from zookeeper_amd import ops
+
+    assert ops.available(), ops.load_error()
+
+
+def _grads(side: bool, monkeypatch):
+    from zookeeper_amd.models.binary_resnet import BinaryResNetE
+    from zookeeper_amd.ops import streams
+    from zookeeper_amd.parallel.flat import FlatParams
+    from zookeeper_amd.train.losses import get_loss
+    from zookeeper_amd.train.trainer import prepare_model
+
+    monkeypatch.setattr(streams, "ENABLED", side)
+    torch.manual_seed(1234)
+    dev = torch.device("cuda", 0)
+    model = prepare_model(BinaryResNetE((64, 64, 3), 10, 18, backend="hip"), dev).train()
+    flat = FlatParams(model, dev)
+    ready = []
+    for s in flat.slots:
+        s.param._zk_grad_ready = (lambda n=s.name: ready.append(n))
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(8, 3, 64, 64, generator=g).to(dev, torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), generator=g).to(dev)
+    loss, _ = get_loss("sparse_categorical_crossentropy")(model(x), y)
+    with streams.session(dev):
+        loss.backward()
+    torch.cuda.synchronize()
+    return flat.grad.clone(), ready, flat
+
+
+def test_side_stream_wgrad_matches_single_stream(monkeypatch):
+    g_side, ready_side, flat = _grads(True, monkeypatch)
+    g_one, ready_one, _ = _grads(False, monkeypatch)
+    assert ((g_side - g_one).norm() / g_one.norm()).item() < 1e-5
+    # every binary conv weight reported ready once, in both modes
+    convs = [s.name for s in flat.slots if s.name.endswith("conv.weight")]
+    for name in convs:
+        assert ready_side.count(name) == 1 and ready_one.count(name) == 1, name

@@ -36,6 +36,7 @@ from typing import Optional
 import torch
 
 from zookeeper_amd.nn.layers import same_padding
+from zookeeper_amd.ops import streams
 from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
                                         zeroed_scratch)
 
@@ -274,6 +275,34 @@ class _BinaryBlockFn(torch.autograd.Function):
         native = Cout % 64 == 0 and Cin % 64 == 0 and stride <= 2 and kh <= 4 and kw <= 4
         dx = None
         if native:
+            # weight gradient first: on the side stream (ops/streams.py) it
+            # then overlaps this block's dgrad and the next block's backward
+            w_direct = direct_grad(weight_p, channels_last=True)
+            dweight = None
+            side = streams.active() and w_direct is not None and sx is not None
+            if side:
+                sstream = streams.side_stream(dev)
+                ready = torch.cuda.Event()
+                ready.record()  # dy written (compute stream)
+                sstream.wait_event(ready)
+                with torch.cuda.stream(sstream):
+                    _wgrad(L, dy, sx, w_ohwi, w_direct.permute(0, 2, 3, 1), ctx, sstream.cuda_stream)
+                    done = torch.cuda.Event()
+                    done.record(sstream)
+                for t in (dy, sx, w_ohwi):
+                    t.record_stream(sstream)
+            else:
+                dw = (w_direct.permute(0, 2, 3, 1) if w_direct is not None  # OHWI view
+                      else torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev))
+                if sx is not None:
+                    _wgrad(L, dy, sx, w_ohwi, dw, ctx, st)
+                else:
+                    check(L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w_ohwi.data_ptr(),
+                                           dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
+                                           stride, pt, pl, int(pad_ones), clip, 0, -1, st),
+                          "zk_bconv_wgrad")
+                if w_direct is None:
+                    dweight = dw.permute(0, 3, 1, 2)
             # MFMA implicit GEMMs; STE mask + residual gradient fused in dgrad.
             if need_dx:
                 dx = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
@@ -295,35 +324,32 @@ class _BinaryBlockFn(torch.autograd.Function):
                                            dx.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
                                            stride, pt, pl, -1, st), "zk_igemm_dgrad")
                 dx = dx.permute(0, 3, 1, 2)
-            w_direct = direct_grad(weight_p, channels_last=True)
-            if w_direct is not None:
-                dw = w_direct.permute(0, 2, 3, 1)  # OHWI view of the flat gradient
-            else:
-                dw = torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev)
-            if sx is not None:
-                # split-K partial sums go to a workspace slab (plain stores)
-                # and one reduce kernel adds them, masked, into dw
-                ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, Ho, Wo, Cout, kh, kw, stride, 0, -1)
-                ws = (torch.empty(max(ws_bytes, 0) // 4, dtype=torch.float32, device=dev)
-                      if ws_bytes > 0 else None)
-                check(L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w_ohwi.data_ptr(),
-                                       dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride,
-                                       pt, pl, int(pad_ones), clip, 0, -1,
-                                       ws.data_ptr() if ws is not None else None,
-                                       max(ws_bytes, 0), st), "zk_igemm_wgrad")
-            else:
-                check(L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w_ohwi.data_ptr(),
-                                       dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride,
-                                       pt, pl, int(pad_ones), clip, 0, -1, st), "zk_bconv_wgrad")
-            if w_direct is not None:
+            if side:
+                # earlier blocks' side-stream wgrads: order the compute stream
+                # after them (they overlapped this block) and signal readiness
+                streams.flush()
+                streams.defer_ready(done, weight_p)
+            elif w_direct is not None:
                 grad_ready(weight_p)
-                dweight = None
-            else:
-                dweight = dw.permute(0, 3, 1, 2)
         else:
             dx, dweight = _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx)
         dres_out = dout if ctx.has_residual else None
         return dx, dres_out, dweight, dgamma, dbeta, None, None
+
+
+def _wgrad(L, dy, sx, w_ohwi, dw, ctx, st) -> None:
+    """Binary-conv weight gradient (dyᵀ ⊛ sign(x), kernel STE mask) added
+    into ``dw`` (OHWI fp32) on stream ``st``: split-K partial sums go to a
+    workspace slab (plain stores) and one reduce kernel adds them, masked."""
+    (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
+    (_, _, clip, pad_ones) = ctx.meta[:4]
+    ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, Ho, Wo, Cout, kh, kw, stride, 0, -1)
+    ws = (torch.empty(max(ws_bytes, 0) // 4, dtype=torch.float32, device=dy.device)
+          if ws_bytes > 0 else None)
+    check(L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w_ohwi.data_ptr(), dw.data_ptr(), B, H,
+                           W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl, int(pad_ones), clip, 0,
+                           -1, ws.data_ptr() if ws is not None else None, max(ws_bytes, 0), st),
+          "zk_igemm_wgrad")
 
 
 def _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx):
@@ -331,7 +357,7 @@ def _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx):
     not a multiple of 64): bf16 library convolution backward on unpacked ±1
     operands, then the fused STE/residual kernel."""
     (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
-    (_, _, clip, pad_ones, identity, _, _) = ctx.meta
+    (_, _, clip, pad_ones, identity) = ctx.meta[:5]
     dev = dy.device
     st = stream_ptr(dev)
     L = lib()

@@ -1,0 +1,89 @@
+"""Weight-gradient side stream: binary-conv weight gradients run
+concurrently with the data-gradient chain.
+
+In a backward pass only the data gradients are on the critical path: block
+``k``'s BN backward and dgrad feed block ``k-1``, while its weight gradient is
+consumed by nobody until the optimizer (or the bucket all-reduce).  With the
+side stream on, ``ops.binary_block``'s backward enqueues the split-K wgrad
+on a second HIP stream right after ``dy`` is ready, so it overlaps the dgrad
+of the same block and the BN backward / dgrad of the next one — filling the
+CUs that the small deep-stage grids leave idle and pairing memory-bound BN
+passes with MFMA-bound GEMMs.
+
+Ordering is explicit with HIP events:
+
+* the side stream waits for an event recorded on the compute stream once
+  ``dy`` is written;
+* the gradient's readiness (``grad_ready`` → the data-parallel bucketer's
+  RCCL all-reduce) is *deferred*: the next block's backward (or the trainer
+  after ``backward()``) makes the compute stream wait for the wgrad's event
+  and only then signals readiness, so the all-reduce is ordered after it.
+
+Only active inside :func:`session` (the trainer opens one per step and
+flushes at its end), so direct callers of the ops keep single-stream
+semantics.  ``ZK_WGRAD_SIDE=0`` disables it.
+"""
+
+from __future__ import annotations
+
+import contextlib
+import os
+from typing import Dict, List, Tuple
+
+import torch
+
+from zookeeper_amd.ops._native import grad_ready
+
+ENABLED = os.environ.get("ZK_WGRAD_SIDE", "1") != "0"
+
+_active = False
+_streams: Dict[int, torch.cuda.Stream] = {}
+_pending: List[Tuple[torch.cuda.Event, object]] = []
+
+
+def active() -> bool:
+    return _active
+
+
+def side_stream(device: torch.device) -> torch.cuda.Stream:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _streams.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _streams[idx] = s
+    return s
+
+
+def defer_ready(event: torch.cuda.Event, param) -> None:
+    """``param``'s gradient is complete once ``event`` (side stream) fires."""
+    _pending.append((event, param))
+
+
+def flush() -> None:
+    """Order the compute stream after every deferred weight gradient and
+    signal their readiness (bucketed all-reduce)."""
+    if not _pending:
+        return
+    cur = torch.cuda.current_stream()
+    items = list(_pending)
+    _pending.clear()
+    for ev, _ in items:
+        cur.wait_event(ev)
+    for _, p in items:
+        grad_ready(p)
+
+
+@contextlib.contextmanager
+def session(device: torch.device):
+    """Enable the side stream for one training step's backward; everything
+    deferred is flushed (compute stream ordered after it) on exit."""
+    global _active
+    use = ENABLED and device.type == "cuda"
+    _pending.clear()
+    _active = use
+    try:
+        yield
+    finally:
+        _active = False
+        if use:
+            flush()

@@ -15,6 +15,7 @@ from typing import Callable, Optional, Tuple
 import torch
 import torch.nn as nn
 
+from zookeeper_amd.ops import streams
 from zookeeper_amd.parallel import dist as zdist
 from zookeeper_amd.parallel.ddp import GradBucketer
 from zookeeper_amd.parallel.flat import FlatParams
@@ -55,7 +56,9 @@ class Trainer:
         self.flat.zero_grad()
         logits = self.model(x)
         loss, correct = self.loss_fn(logits, y)
-        loss.backward()
+        # binary-conv weight gradients on a side stream, ordered by events
+        with streams.session(self.device):
+            loss.backward()
         self.bucketer.finish()
         self.optimizer.step()
         return loss.detach(), correct
