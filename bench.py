@@ -10,7 +10,10 @@ random-init weights), data parallel over RCCL with one process per GPU.
 A timed step is the complete training step: uint8→bf16 normalisation/flip
 of the batch, forward, softmax-CE, backward with bucketed all-reduce, fused
 Adam + weight_clip.  Input batches come from a device-resident pool of
-synthetic batches (no host work per step).  ``--steps`` steps are timed
+synthetic batches (no host work per step).  On one GPU, when the warmup
+shows the step host-bound (small ``--batch``), zero-grad + forward + loss +
+backward are replayed as one HIP graph (``--graph auto``); the optimizer
+still runs every step.  ``--steps`` steps are timed
 between a barrier + ``torch.cuda.synchronize()`` on both sides; the reported
 time is the MAX over ranks.  Rank 0 prints one JSON line.
 
@@ -41,6 +44,9 @@ def parse():
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     ap.add_argument("--pool", type=int, default=4, help="device-resident synthetic batches")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--graph", default="auto", choices=["0", "1", "auto"],
+                    help="replay forward+backward as a HIP graph (1 GPU; eager when distributed); "
+                         "auto: when the warmup shows the step host-bound")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -76,7 +82,9 @@ def main() -> int:
     backend = base_getattr(cfg, "model").resolved_backend()
     torch.manual_seed(1234)
     trainer = Trainer(model, "sparse_categorical_crossentropy", base_getattr(cfg, "optimizer"),
-                      info, bucket_mb=args.bucket_mb)
+                      info, bucket_mb=args.bucket_mb,
+                      graph="auto" if args.graph == "auto" else args.graph == "1",
+                      graph_warmup=max(1, min(3, args.warmup - 1)))  # capture inside the warmup
     pool = make_device_pool_batches(args.pool, args.batch, (224, 224, 3), 1000, info.device,
                                     seed=info.rank)
     prep = cfg.preprocessing
@@ -101,6 +109,7 @@ def main() -> int:
         loss, _ = step(args.warmup + i)
         if info.is_main and (i + 1) % 50 == 0:
             print(f"[bench] step {i + 1}/{args.steps}", file=sys.stderr, flush=True)
+    t_enq = time.perf_counter() - t0  # host time to enqueue (no sync yet)
     sync()
     zdist.barrier()
     elapsed = time.perf_counter() - t0
@@ -108,6 +117,14 @@ def main() -> int:
     final_loss = float(loss.item())
 
     ms = 1000.0 * elapsed / args.steps
+    if info.is_main and trainer.graph_probe is not None:
+        th, tg = trainer.graph_probe
+        print(f"[bench] graph probe: host {1e3 * th:.2f} ms, GPU {1e3 * tg:.2f} ms -> "
+              f"{'graph' if trainer.graph else 'eager'}", file=sys.stderr, flush=True)
+    if info.is_main:
+        # enqueue ~ total: host-bound; enqueue << total: the GPU is the limit
+        print(f"[bench] host enqueue {1000.0 * t_enq / args.steps:.2f} ms/step of {ms:.2f}",
+              file=sys.stderr, flush=True)
     global_batch = args.batch * info.world
     value = global_batch * args.steps / elapsed
     out = {
@@ -132,6 +149,7 @@ def main() -> int:
             "parallelism": f"dp{info.world}",
             "backend": backend,
             "optimizer": "adam+weight_clip (fused)",
+            "hip_graph": trainer.graph,
             "final_loss": round(final_loss, 4),
         },
     }

@@ -58,3 +58,20 @@ def test_resume_is_bit_exact(tmp_path):
     for x, y in data[3:]:
         b.train_step(x, y)
     torch.testing.assert_close(b.flat.data, ref.flat.data, atol=0, rtol=0)
+
+
+def test_graph_mode_is_gpu_single_process_only():
+    import pytest
+
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Linear(6, 8), nn.ReLU(), nn.Linear(8, 3))
+    spec = Adam()
+    configure(spec, {"learning_rate": 0.05})
+    for mode in (True, "auto"):
+        tr = Trainer(model, "sparse_categorical_crossentropy", spec, DistInfo(), graph=mode)
+        assert not tr.graph  # CPU device: always eager
+        x, y = _batches(1)[0]
+        loss, _ = tr.train_step(x, y)
+        assert torch.isfinite(loss)
+    with pytest.raises(ValueError):
+        Trainer(model, "sparse_categorical_crossentropy", spec, DistInfo(), graph="yes")

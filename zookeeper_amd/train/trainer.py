@@ -10,7 +10,8 @@ the device until the metrics logger flushes.
 
 from __future__ import annotations
 
-from typing import Callable, Optional, Tuple
+import time
+from typing import Callable, Optional, Tuple, Union
 
 import torch
 import torch.nn as nn
@@ -36,7 +37,8 @@ def prepare_model(model: nn.Module, device: torch.device) -> nn.Module:
 class Trainer:
     def __init__(self, model: nn.Module, loss, optimizer: OptimizerSpec,
                  info: Optional[zdist.DistInfo] = None, bucket_mb: float = 25.0,
-                 first_bucket_mb: float = 1.0, grad_dtype: Optional[torch.dtype] = None):
+                 first_bucket_mb: float = 1.0, grad_dtype: Optional[torch.dtype] = None,
+                 graph: Union[bool, str] = False, graph_warmup: int = 3):
         self.info = info or zdist.info()
         self.device = self.info.device
         self.model = prepare_model(model, self.device)
@@ -51,17 +53,71 @@ class Trainer:
         self.bucketer = GradBucketer(self.flat, self.info.world, bucket_mb, first_bucket_mb,
                                      grad_dtype=grad_dtype)
         self.optimizer = optimizer.create(self.flat, grad_scale=1.0 / self.info.world)
+        # HIP-graph replay of zero-grad + forward + loss + backward (single
+        # process): one graph launch instead of ~300 kernel launches and the
+        # Python / autograd work behind them.  The optimizer (host-side step
+        # count and learning-rate schedule) runs eagerly after each replay.
+        # ``graph="auto"`` decides on the last warmup step: replay only when
+        # the host cannot enqueue a step faster than the GPU runs it (small
+        # per-GPU batches); a GPU-bound step keeps the eager path, whose
+        # side-stream weight gradients overlap better than the replayed graph.
+        auto = isinstance(graph, str) and graph == "auto"
+        if isinstance(graph, str) and not auto:
+            raise ValueError(f"graph must be a bool or 'auto', got {graph!r}")
+        self.graph = (auto or bool(graph)) and self.device.type == "cuda" and self.info.world == 1
+        self._graph_auto = auto and self.graph
+        self.graph_probe: Optional[Tuple[float, float]] = None  # (host s, GPU s) of the probe
+        self.graph_warmup = max(1, graph_warmup)
+        self._eager_steps = 0
+        self._graph = None
+        self._static_in = None
+        self._static_out = None
 
-    def train_step(self, x: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    def _forward_backward(self, x: torch.Tensor, y: torch.Tensor):
         self.flat.zero_grad()
         logits = self.model(x)
         loss, correct = self.loss_fn(logits, y)
         # binary-conv weight gradients on a side stream, ordered by events
         with streams.session(self.device):
             loss.backward()
-        self.bucketer.finish()
-        self.optimizer.step()
         return loss.detach(), correct
+
+    def train_step(self, x: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """One training step.  In graph mode the returned tensors are the
+        graph's static outputs: overwritten by the next step (consume or
+        clone them before)."""
+        if not self.graph or self._eager_steps < self.graph_warmup:
+            probe = self._graph_auto and self._eager_steps == self.graph_warmup - 1
+            if probe:
+                # empty queue, then one step: the events' span is max(host
+                # enqueue, GPU time)
+                torch.cuda.synchronize(self.device)
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+                t0 = time.perf_counter()
+            self._eager_steps += 1  # eager warmup initialises lazy state (kernel attributes, scratch)
+            out = self._forward_backward(x, y)
+            self.bucketer.finish()
+            self.optimizer.step()
+            if probe:
+                t_host = time.perf_counter() - t0
+                ev[1].record()
+                ev[1].synchronize()
+                t_gpu = ev[0].elapsed_time(ev[1]) / 1e3
+                self.graph_probe = (t_host, t_gpu)
+                self.graph = t_host > 0.85 * t_gpu  # host-bound: replay
+            return out
+        if self._graph is None:
+            self._static_in = (x.clone(), y.clone())  # clone keeps x's channels_last strides
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph):
+                self._static_out = self._forward_backward(*self._static_in)
+        else:
+            self._static_in[0].copy_(x)
+            self._static_in[1].copy_(y)
+        self._graph.replay()
+        self.optimizer.step()
+        return self._static_out
 
     @torch.no_grad()
     def eval_step(self, x: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
