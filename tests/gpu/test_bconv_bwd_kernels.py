@@ -120,15 +120,16 @@ def test_igemm_dgrad_matches_reference(variant, cin, cout, stride, hw):
 
 
 @pytest.mark.parametrize("slab", [False, True])
-@pytest.mark.parametrize("variant", list(range(13)))
+@pytest.mark.parametrize("variant", list(range(13)) + list(range(20, 35)))
 @pytest.mark.parametrize("cin,cout,stride,hw,pad_ones", [
     (64, 64, 1, 12, 0), (64, 128, 2, 12, 0), (128, 128, 1, 7, 1), (256, 512, 2, 8, 0),
-    (128, 64, 1, 9, 1), (64, 192, 1, 5, 1)])
+    (128, 64, 1, 9, 1), (64, 192, 1, 5, 1), (64, 64, 1, 28, 1), (128, 256, 1, 14, 0)])
 def test_igemm_wgrad_matches_reference(variant, cin, cout, stride, hw, pad_ones, slab):
     """LDS-DMA ring implicit-GEMM wgrad (igemm.hip) on the bf16 sign(x)
-    image, every tile variant, split-K by fp32 atomics or by workspace slabs
-    + reduce kernel, accumulating into dw, vs the fp64 ±1 conv weight
-    gradient."""
+    image, every tile variant (20+: the conv3 kernel, all taps of a kernel
+    row per block over halo-extended rows; 3x3 stride-1 only), split-K by
+    fp32 atomics or by workspace slabs + reduce kernel, accumulating into dw,
+    vs the fp64 ±1 conv weight gradient."""
     from zookeeper_amd.nn.layers import pad_same_nhwc, same_padding
     from zookeeper_amd.nn.quantizers import sign_pm1
     from zookeeper_amd.ops._native import lib, stream_ptr
@@ -149,7 +150,8 @@ def test_igemm_wgrad_matches_reference(variant, cin, cout, stride, hw, pad_ones,
     dw = torch.full((cout, 3, 3, cin), 0.25, device="cuda")  # accumulates into dw
     ws = None
     if slab:
-        nbytes = L.zk_igemm_wgrad_ws_bytes(B, cin, ho, ho, cout, 3, 3, stride, 256, variant)
+        nbytes = L.zk_igemm_wgrad_ws_bytes(B, cin, hw, hw, ho, ho, cout, 3, 3, stride, pt, pt,
+                                            256, variant)
         if nbytes <= 0:
             pytest.skip("tile does not divide this shape")
         ws = torch.empty(nbytes // 4, device="cuda")

@@ -21,7 +21,7 @@ from zookeeper_amd.ops._native import lib, stream_ptr  # noqa: E402
 DG_VARIANTS = 8
 WG_VARIANTS = 8
 IG_VARIANTS = list(range(15)) + list(range(20, 28))
-IGW_VARIANTS = 13
+IGW_VARIANTS = list(range(13)) + list(range(20, 35))  # 20+: conv3 (3x3 s1)
 IGF_VARIANTS = list(range(15)) + list(range(20, 28))
 IGF4_VARIANTS = [-1] + list(range(10)) + list(range(20, 29))
 
@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default=None)
     ap.add_argument("--slab", type=int, default=1, help="wgrad split-K via workspace slabs")
+    ap.add_argument("--igw", default=None, help="comma list of igemm wgrad variants (default all)")
+    ap.add_argument("--tbs", default="512,1024,2048", help="wgrad target block counts")
     ap.add_argument("--only", default="fwd,dgrad,igemm,wgrad,miopen",
                     help="comma list of kernel families to time")
     args = ap.parse_args()
@@ -177,10 +179,11 @@ def main():
                                      B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v, st)
                     torch.cuda.synchronize()
                     ref_dw = dw.clone()
-        for v in (range(IGW_VARIANTS) if "igw" in fam else ()):
-            for tb in (512, 1024, 2048):
+        igw = [int(v) for v in args.igw.split(",")] if args.igw else IGW_VARIANTS
+        for v in (igw if "igw" in fam else ()):
+            for tb in [int(t) for t in args.tbs.split(",")]:
                 dw.zero_()
-                nb = L.zk_igemm_wgrad_ws_bytes(B, cin, Ho, Ho, cout, 3, 3, s, tb, v)
+                nb = L.zk_igemm_wgrad_ws_bytes(B, cin, H, W, Ho, Ho, cout, 3, 3, s, pt, pt, tb, v)
                 wsb = torch.empty(max(nb, 4) // 4, device="cuda") if args.slab else None
                 wsp = wsb.data_ptr() if wsb is not None else None
                 wsn = wsb.numel() * 4 if wsb is not None else 0
@@ -191,7 +194,9 @@ def main():
                 if rc != 0:
                     row[f"igw_v{v}_tb{tb}_us"] = None
                     continue
-                if ref_dw is not None:
+                if ref_dw is None:
+                    ref_dw = dw.clone()  # first variant that ran: the reference
+                else:
                     row[f"igw_v{v}_tb{tb}_relerr"] = ((dw - ref_dw).abs().max() /
                                                       ref_dw.abs().max()).item()
                 row[f"igw_v{v}_tb{tb}_us"] = timeit(lambda: L.zk_igemm_wgrad(

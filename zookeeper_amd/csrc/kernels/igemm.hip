@@ -1232,12 +1232,267 @@ int launch_igemm_wgrad(const void* dy, const void* sx, const void* w, void* dw, 
   return 0;
 }
 
+// ===========================================================================
+// conv3 weight gradient (3x3, stride 1, 'same'): the three taps of TH kernel
+// rows per block, one dy load per K-step for all of them.
+//
+// K runs over "extended" pixel positions e = (b*H + h)*(W+2) + w + 1: every
+// image row carries a halo column on both sides.  Tap (th, tw) of output e
+// reads sx at extended position e + tw - 1 of image row h + th - 1, i.e. LDS
+// row k + tw of kernel row th's staged segment (BK + 2 rows from e0 - 1).
+// Halo / out-of-image sx rows are loaded from the zero (+1) page and the dy
+// rows of halo positions from the zero page, so no fragment is masked.
+// Per K-step: BK dy rows + TH segments of BK + 2 sx rows feed 3*TH taps:
+// dy is read 3/TH times per layer instead of 9, sx 3 times instead of 9.
+// The halo costs 2/(W+2) of the K-steps.  Output as igemm_wgrad_kernel.
+// ===========================================================================
+template <int BM, int BN, int WM, int WN, int BK, int NS, int TH, int OCC>
+__global__ __launch_bounds__(WM * WN * 64, OCC) void igemm_wgrad3_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ sx,
+    const float* __restrict__ w, float* __restrict__ dw, float* __restrict__ slab, IGeom g,
+    int pad_ones, float clip, int k_per_split, int m_tiles, int n_tiles) {
+  constexpr int NWAVES = WM * WN, NT = 3 * TH, TG = 3 / TH;
+  static_assert(TH == 1 || TH == 3, "kernel rows per block");
+  constexpr int RA = BM * 2, RBB = BN * 2;
+  constexpr int SA = BK * RA;
+  static_assert(SA % (1024 * NWAVES) == 0, "A stage / waves");
+  constexpr int A_INS = SA / 1024 / NWAVES;
+  constexpr int SEG = (BK + 2) * RBB;  // one kernel row's sx segment
+  static_assert(SEG % 256 == 0, "segments keep the swizzle period");
+  constexpr int B_KB = (TH * SEG + 1023) / 1024;
+  constexpr int B_INS = (B_KB + NWAVES - 1) / NWAVES;  // tail lanes load the zero page
+  constexpr int SB = B_INS * NWAVES * 1024;
+  constexpr int LPS = A_INS + B_INS, STAGE = SA + SB;
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
+
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave / WN, wn = wave % WN;
+
+  // consecutive logical ids: the tiles (and kernel-row groups) of one split
+  const int L = xcd_linear(blockIdx.x, gridDim.x);
+  const int tiles = m_tiles * n_tiles * TG;
+  const int split = L / tiles, tile = L % tiles;
+  const int thg = tile % TG, mn = tile / TG;
+  const int m0 = (mn % m_tiles) * BM;  // co
+  const int n0 = (mn / m_tiles) * BN;  // ci
+  const int WE = g.W + 2;
+  const int E = g.B * g.H * WE;
+  const int kbeg = split * k_per_split;
+  if (kbeg >= E) return;
+  const int kend = min(E, kbeg + k_per_split);
+  const int NK = (kend - kbeg + BK - 1) / BK;
+
+  const unsigned char* dyb = reinterpret_cast<const unsigned char*>(dy);
+  const unsigned char* sxb = reinterpret_cast<const unsigned char*>(sx);
+  const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
+  const unsigned char* pp = pad_ones ? reinterpret_cast<const unsigned char*>(g_ones_page_bf16)
+                                     : zp;
+  const float invWE = 1.0f / (float)WE, invH = 1.0f / (float)g.H;
+
+  int a_row[A_INS], a_byte[A_INS];
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int off = ((j * NWAVES + wave) * 64 + lane) * 16;
+    a_row[j] = off / RA;
+    const int slot = (off % RA) >> 4;
+    a_byte[j] = m0 * 2 + ((slot ^ tr_swz<RA>(a_row[j])) << 4);
+  }
+  int b_row[B_INS], b_th[B_INS], b_byte[B_INS];  // b_th < 0: tail lane
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int off = ((j * NWAVES + wave) * 64 + lane) * 16;
+    b_th[j] = -1;
+    b_row[j] = b_byte[j] = 0;
+    if (off < TH * SEG) {
+      const int t = off / SEG, o = off % SEG;
+      b_th[j] = thg * TH + t;
+      b_row[j] = o / RBB;
+      b_byte[j] = n0 * 2 + ((((o % RBB) >> 4) ^ tr_swz<RBB>(b_row[j])) << 4);
+    }
+  }
+
+  auto issue = [&](int ks) {
+    unsigned char* st = smem + (ks % NS) * STAGE;
+    const int e0 = kbeg + ks * BK;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      const int e = e0 + a_row[j];
+      const unsigned char* src = zp;  // halo column / past the split: no contribution
+      if (e < kend) {
+        const int q = fdiv(e, WE, invWE);
+        const int c = e - q * WE - 1;
+        if (c >= 0 && c < g.W) src = dyb + ((long long)q * g.W + c) * (g.Cout * 2) + a_byte[j];
+      }
+      ZK_GLDS16(src, st + (j * NWAVES + wave) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const unsigned char* src = zp;
+      if (b_th[j] >= 0) {
+        src = pp;  // padding tap
+        const int e = e0 - 1 + b_row[j];
+        if (e >= 0 && e < E) {
+          const int q = fdiv(e, WE, invWE);  // b*H + h
+          const int c = e - q * WE - 1;
+          const int hh = q - fdiv(q, g.H, invH) * g.H + b_th[j] - 1;
+          if (c >= 0 && c < g.W && hh >= 0 && hh < g.H)
+            src = sxb + ((long long)(q + b_th[j] - 1) * g.W + c) * (g.Cin * 2) + b_byte[j];
+        }
+      }
+      ZK_GLDS16(src, st + SA + (j * NWAVES + wave) * 1024);
+    }
+  };
+
+  f32x16 acc[NT][TM][TN];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][a][b][r] = 0.f;
+
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < NK) issue(p);
+  for (int ks = 0; ks < NK; ++ks) {
+    if (ks + NS - 2 < NK)
+      wait_vmcnt<LPS * (NS - 2)>();
+    else
+      wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (ks + NS - 1 < NK) issue(ks + NS - 1);
+    const unsigned char* st = smem + (ks % NS) * STAGE;
+#pragma unroll
+    for (int sub = 0; sub < BK / 16; ++sub) {
+      uint4 af[TM];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) af[a] = tr_frag_swz<RA>(st, sub * 16, wm * WTM + a * 32, lane);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        // tap (t / 3, tw = t % 3): segment t / 3 shifted by tw rows
+        uint4 bfr[TN];
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          bfr[b] = tr_frag_swz<RBB>(st + SA + (t / 3) * SEG, sub * 16 + t % 3,
+                                    wn * WTN + b * 32, lane);
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b) acc[t][a][b] = mfma_bf16(af[a], bfr[b], acc[t][a][b]);
+      }
+    }
+  }
+
+  const int h = lane >> 5, r32 = lane & 31;
+  const int NTOT = 9 * g.Cin;
+  float* sl = slab ? slab + (long long)split * g.Cout * NTOT : nullptr;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int tap = (thg * TH + t / 3) * 3 + t % 3;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const long long idx =
+              (long long)co * NTOT + tap * g.Cin + n0 + wn * WTN + b * 32 + r32;
+          if (sl)
+            sl[idx] = acc[t][a][b][r];
+          else if (fabsf(w[idx]) <= clip)
+            atomicAdd(dw + idx, acc[t][a][b][r]);
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int BK, int TH>
+bool plan_wgrad3(const IGeom& g, int target_blocks, WgradPlan& p) {
+  if (!conv3_ok(g, 0) || g.Cout % BM || g.Cin % BN) return false;
+  const long long E = (long long)g.B * g.H * (g.W + 2);
+  if (E >= (1 << 24)) return false;  // fdiv range
+  p.m_tiles = g.Cout / BM;
+  p.n_tiles = g.Cin / BN;
+  const long long tiles = (long long)p.m_tiles * p.n_tiles * (3 / TH);
+  long long splits = (target_blocks + tiles - 1) / tiles;
+  const long long max_splits = (E + 4 * BK - 1) / (4 * BK);
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  long long kps = (E + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  p.splits = (int)((E + kps - 1) / kps);
+  p.kps = (int)kps;
+  return true;
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int NS, int TH, int OCC>
+int launch_igemm_wgrad3(const void* dy, const void* sx, const void* w, void* dw, const IGeom& g,
+                        int pad_ones, float clip, int target_blocks, void* ws, long long ws_bytes,
+                        long long* ws_needed, hipStream_t stream) {
+  WgradPlan p;
+  if (!plan_wgrad3<BM, BN, BK, TH>(g, target_blocks, p)) return (int)hipErrorInvalidValue;
+  const int NTOT = 9 * g.Cin;
+  const long long slab_bytes = (long long)p.splits * g.Cout * NTOT * 4;
+  if (ws_needed) {
+    *ws_needed = slab_bytes;
+    return 0;
+  }
+  constexpr int NW = WM * WN;
+  constexpr int SB = ((TH * (BK + 2) * BN * 2 + 1023) / 1024 + NW - 1) / NW * NW * 1024;
+  constexpr int LDS = NS * (BK * BM * 2 + SB);
+  static_assert(LDS <= 160 * 1024, "LDS");
+  auto kern = igemm_wgrad3_kernel<BM, BN, WM, WN, BK, NS, TH, OCC>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  float* slab = (ws && ws_bytes >= slab_bytes && NTOT % 4 == 0) ? (float*)ws : nullptr;
+  const long long tiles = (long long)p.m_tiles * p.n_tiles * (3 / TH);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * p.splits)), dim3(NW * 64), LDS, stream,
+                     (const uint16_t*)dy, (const uint16_t*)sx, (const float*)w, (float*)dw, slab,
+                     g, pad_ones, clip, p.kps, p.m_tiles, p.n_tiles);
+  if (slab) {
+    const long long n4 = (long long)g.Cout * NTOT / 4;
+    const long long blocks = (n4 + 15) / 16;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                       (const float4*)slab, p.splits, n4, (const float4*)w, clip, (float4*)dw);
+  }
+  return 0;
+}
+
 int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, void* dw,
                         const IGeom& g, int po, float clip, int tb, void* ws, long long wsb,
                         long long* need, hipStream_t st) {
 #define ZK_IGW(...) \
   return launch_igemm_wgrad<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, ws, wsb, need, st)
+#define ZK_IGW3(...) \
+  return launch_igemm_wgrad3<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, ws, wsb, need, st)
   switch (v) {
+    // conv3 family <BM, BN, WM, WN, BK, NS, TH, OCC>
+    case 20: ZK_IGW3(64, 64, 2, 2, 32, 4, 3, 1);
+    case 21: ZK_IGW3(64, 64, 2, 2, 32, 4, 1, 2);
+    case 22: ZK_IGW3(128, 64, 2, 2, 32, 3, 1, 2);
+    case 23: ZK_IGW3(128, 128, 2, 2, 32, 2, 1, 1);
+    case 24: ZK_IGW3(64, 128, 2, 2, 32, 3, 1, 2);
+    case 25: ZK_IGW3(64, 64, 2, 2, 64, 3, 3, 1);
+    case 26: ZK_IGW3(128, 128, 2, 2, 32, 3, 1, 1);
+    case 27: ZK_IGW3(64, 64, 2, 2, 32, 3, 3, 2);
+    case 28: ZK_IGW3(128, 64, 2, 2, 64, 2, 1, 2);
+    // two waves of 64 x 32 (the dy fragment feeds two MFMAs per sx fragment)
+    case 29: ZK_IGW3(64, 64, 1, 2, 32, 4, 3, 1);
+    case 30: ZK_IGW3(64, 64, 1, 2, 32, 3, 3, 1);
+    case 32: ZK_IGW3(128, 64, 2, 2, 32, 3, 3, 1);
+    case 33: ZK_IGW3(64, 64, 1, 2, 32, 4, 1, 2);
+    case 34: ZK_IGW3(128, 64, 1, 2, 32, 3, 1, 2);
     case 0: ZK_IGW(128, 128, 2, 2, 32, 2);
     case 1: ZK_IGW(128, 128, 2, 2, 32, 4);
     case 2: ZK_IGW(128, 192, 2, 2, 32, 3);
@@ -1254,6 +1509,7 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
     default: return (int)hipErrorInvalidValue;
   }
 #undef ZK_IGW
+#undef ZK_IGW3
 }
 
 }  // namespace
@@ -1321,8 +1577,18 @@ namespace {
 void wgrad_defaults(const IGeom& g, int& variant, int& target_blocks) {
   if (variant < 0) {
     // Tuned on MI355X (tools/tune_bconv.py --only igw, E18 shapes, batch 256)
-    // (slab split-K reduction)
-    if (g.Cin == 64 && g.s == 2 && g.Cout % 128 == 0 && (9 * g.Cin) % 192 == 0) {
+    // (slab split-K reduction).  3x3 stride-1 'same' layers with 64 / 128
+    // input channels: the conv3 kernel (profiles/r1at_wgrad3_tuning.md:
+    // 56x56x64 145 -> 107 us, 28x28x128 102 -> 96 us at batch 256); the
+    // 256 / 512-channel layers stay on 128x128 tiles (no gain there).
+    const bool c3 = conv3_ok(g, 0);
+    if (c3 && g.Cin == 64 && g.Cout % 64 == 0) {
+      variant = 20;
+      if (target_blocks <= 0) target_blocks = 512;
+    } else if (c3 && g.Cin == 128 && g.Cout % 128 == 0) {
+      variant = 28;
+      if (target_blocks <= 0) target_blocks = 512;
+    } else if (g.Cin == 64 && g.s == 2 && g.Cout % 128 == 0 && (9 * g.Cin) % 192 == 0) {
       variant = 2;
       if (target_blocks <= 0) target_blocks = 512;
     } else if (g.Cin == 64 || g.Cout % 128 != 0) {
@@ -1358,10 +1624,10 @@ ZK_EXPORT int zk_igemm_wgrad(const void* dy, const void* sx, const void* w, void
 }
 
 // Workspace bytes zk_igemm_wgrad needs for slab mode (-1: shape unsupported).
-ZK_EXPORT long long zk_igemm_wgrad_ws_bytes(int B, int Cin, int Ho, int Wo, int Cout, int kh,
-                                            int kw, int stride, int target_blocks,
-                                            int variant) {
-  IGeom g{B, 0, 0, Cin, Ho, Wo, Cout, kh, kw, stride, 0, 0};
+ZK_EXPORT long long zk_igemm_wgrad_ws_bytes(int B, int Cin, int H, int W, int Ho, int Wo,
+                                            int Cout, int kh, int kw, int stride, int pt, int pl,
+                                            int target_blocks, int variant) {
+  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
   wgrad_defaults(g, variant, target_blocks);
   long long need = -1;
   if (igemm_wgrad_variant(variant, nullptr, nullptr, nullptr, nullptr, g, 0, 0.f,

@@ -343,7 +343,8 @@ def _wgrad(L, dy, sx, w_ohwi, dw, ctx, st) -> None:
     workspace slab (plain stores) and one reduce kernel adds them, masked."""
     (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
     (_, _, clip, pad_ones) = ctx.meta[:4]
-    ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, Ho, Wo, Cout, kh, kw, stride, 0, -1)
+    ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Ho, Wo, Cout, kh, kw, stride, pt, pl,
+                                         0, -1)
     ws = (torch.empty(max(ws_bytes, 0) // 4, dtype=torch.float32, device=dy.device)
           if ws_bytes > 0 else None)
     check(L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w_ohwi.data_ptr(), dw.data_ptr(), B, H,

@@ -94,7 +94,7 @@ class _Conv3x3Fn(torch.autograd.Function):
             wf = weight.detach().permute(0, 2, 3, 1)
             if wf.dtype != torch.float32 or not wf.is_contiguous():
                 wf = wf.float().contiguous()
-            ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Cout, 3, 3, 1, 0, -1)
+            ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, H, W, Cout, 3, 3, 1, 1, 1, 0, -1)
             ws = (torch.empty(ws_bytes // 4, dtype=torch.float32, device=dev)
                   if ws_bytes > 0 else None)
             # clip = +inf: the kernel's |w| <= clip gradient mask is all-pass

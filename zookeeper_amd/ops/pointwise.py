@@ -89,7 +89,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             target = direct_grad(weight)
             dw = target.view(Cout, Cin) if target is not None else torch.zeros(
                 (Cout, Cin), dtype=torch.float32, device=dev)
-            ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Cout, 1, 1, 1, 0, -1)
+            ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, H, W, Cout, 1, 1, 1, 0, 0, 0, -1)
             ws = (torch.empty(ws_bytes // 4, dtype=torch.float32, device=dev)
                   if ws_bytes > 0 else None)
             wf = weight.detach().reshape(Cout, Cin)
