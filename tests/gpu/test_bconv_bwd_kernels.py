@@ -68,7 +68,7 @@ def test_dgrad_wgrad(cin, cout, stride, hw, pad_ones):
     assert err_dw <= 1e-4 * ref_dw.abs().max().item() + 1e-3, err_dw
 
 
-@pytest.mark.parametrize("variant", list(range(15)) + list(range(20, 28)))
+@pytest.mark.parametrize("variant", list(range(15)) + list(range(20, 35)))
 @pytest.mark.parametrize("cin,cout,stride,hw", [
     (64, 64, 1, 12), (64, 128, 2, 12), (128, 128, 1, 7), (256, 512, 2, 8), (128, 64, 1, 9),
     (128, 256, 2, 15), (64, 64, 1, 28)])

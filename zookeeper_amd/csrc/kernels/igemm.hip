@@ -448,34 +448,52 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
       const uint32_t* mask = args.mask;
       const uint16_t* dres = args.dres;
       const int CW = g.Cin >> 5;
+      // all mask / residual loads of the tile before the stores (see the
+      // conv3 epilogue)
+      long long pix[TM];
+      uint32_t mw[TM][TN];
+      uint2 dv[TM][TN][4];
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
         const long long mc = m0 + wm * WTM + a * 32 + r32;
-        if (mc >= M) continue;
-        const int jw = (int)(mc % Wc);
-        const long long rr = mc / Wc;
-        const long long m =
-            ((rr / Hc) * g.H + (long long)(rr % Hc) * s + ph) * g.W + (long long)jw * s + pw;
+        pix[a] = -1;
+        if (mc < M) {
+          const int jw = (int)(mc % Wc);
+          const long long rr = mc / Wc;
+          pix[a] = ((rr / Hc) * g.H + (long long)(rr % Hc) * s + ph) * g.W + (long long)jw * s + pw;
+        }
+        const long long m = pix[a];
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
           const int nb = n0 + wn * WTN + b * 32;
-          const uint32_t mw = mask ? mask[m * CW + (nb >> 5)] : 0xFFFFFFFFu;
+          mw[a][b] = !mask ? 0xFFFFFFFFu : m >= 0 ? mask[m * CW + (nb >> 5)] : 0u;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            dv[a][b][q] = (dres && m >= 0)
+                              ? *reinterpret_cast<const uint2*>(dres + m * g.Cin + nb + 8 * q + 4 * h)
+                              : make_uint2(0u, 0u);
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const long long m = pix[a];
+        if (m < 0) continue;
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int nb = n0 + wn * WTN + b * 32;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int nl = 8 * q + 4 * h;
             float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              v[e] = ((mw >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
-            const long long off = m * g.Cin + nb + nl;
-            if (dres) {
-              const uint2 d = *reinterpret_cast<const uint2*>(dres + off);
-              v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
-              v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
-              v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
-              v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
-            }
-            *reinterpret_cast<uint2*>(dx + off) =
+              v[e] = ((mw[a][b] >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
+            const uint2 d = dv[a][b][q];  // zero without a residual
+            v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
+            v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
+            v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
+            v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
+            *reinterpret_cast<uint2*>(dx + m * g.Cin + nb + nl) =
                 make_uint2(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]));
           }
         }
@@ -505,10 +523,12 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
   static_assert(!F4 || FWD, "e2m1 operands: the +-1 x +-1 forward only");
   constexpr int A_INS = (BM + 2 + RPI * NWAVES - 1) / (RPI * NWAVES);  // glds per wave
   constexpr int AR = A_INS * RPI * NWAVES;                             // A rows staged
-  constexpr int B_INS = 3 * BN / RPI / NWAVES;
-  static_assert(B_INS >= 1 && (3 * BN) % (RPI * NWAVES) == 0, "tile / wave mismatch");
+  // weight rows of the three taps, padded to whole load instructions (the
+  // tail lanes load the zero page into the pad rows)
+  constexpr int B_INS = (3 * BN + RPI * NWAVES - 1) / (RPI * NWAVES);
+  constexpr int BR = B_INS * RPI * NWAVES;
   constexpr int LPS = A_INS + B_INS;
-  constexpr int STAGE = (AR + 3 * BN) * CB;
+  constexpr int STAGE = (AR + BR) * CB;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   static_assert(!FWD || TM <= 4, "in-wave int32 sums of squares need TM <= 4");
@@ -570,11 +590,12 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
     }
 #pragma unroll
     for (int j = 0; j < B_INS; ++j) {
-      const int r = (j * NWAVES + wave) * RPI + lrow;  // 0 .. 3*BN-1
+      const int r = (j * NWAVES + wave) * RPI + lrow;  // 0 .. BR-1
       const int tw = r / BN, n = r % BN;
       const int t = th * 3 + tw;
       const int sw = lslot ^ ((n >> SH) & (SPR - 1));
-      ZK_GLDS16(wtb + ((long long)t * NCH + n0 + n) * RB + kc * CB + sw * 16,
+      ZK_GLDS16(r < 3 * BN ? wtb + ((long long)t * NCH + n0 + n) * RB + kc * CB + sw * 16
+                           : zp + sw * 16,
                 st + AR * CB + (j * NWAVES + wave) * 1024);
     }
   };
@@ -715,6 +736,26 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
       const uint32_t* mask = args.mask;
       const uint16_t* dres = args.dres;
       const int CW = g.Cin >> 5;
+      // every mask word / residual-gradient load of the tile first, then the
+      // stores: the loads overlap instead of each waiting behind the
+      // previous (possibly aliasing) store
+      uint32_t mw[TM][TN];
+      uint2 dv[TM][TN][4];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const long long m = m0 + wm * WTM + a * 32 + r32;
+        const bool live = m < M;
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int nb = n0 + wn * WTN + b * 32;
+          mw[a][b] = !mask ? 0xFFFFFFFFu : live ? mask[m * CW + (nb >> 5)] : 0u;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            dv[a][b][q] = (dres && live)
+                              ? *reinterpret_cast<const uint2*>(dres + m * g.Cin + nb + 8 * q + 4 * h)
+                              : make_uint2(0u, 0u);
+        }
+      }
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
         const long long m = m0 + wm * WTM + a * 32 + r32;
@@ -722,23 +763,19 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
           const int nb = n0 + wn * WTN + b * 32;
-          const uint32_t mw = mask ? mask[m * CW + (nb >> 5)] : 0xFFFFFFFFu;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int nl = 8 * q + 4 * h;
             float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              v[e] = ((mw >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
-            const long long off = m * g.Cin + nb + nl;
-            if (dres) {
-              const uint2 d = *reinterpret_cast<const uint2*>(dres + off);
-              v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
-              v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
-              v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
-              v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
-            }
-            *reinterpret_cast<uint2*>(dx + off) =
+              v[e] = ((mw[a][b] >> (nl + e)) & 1u) ? acc[a][b][4 * q + e] : 0.f;
+            const uint2 d = dv[a][b][q];  // zero without a residual
+            v[0] += zk::bf16_to_f32((uint16_t)(d.x & 0xffff));
+            v[1] += zk::bf16_to_f32((uint16_t)(d.x >> 16));
+            v[2] += zk::bf16_to_f32((uint16_t)(d.y & 0xffff));
+            v[3] += zk::bf16_to_f32((uint16_t)(d.y >> 16));
+            *reinterpret_cast<uint2*>(dx + m * g.Cin + nb + nl) =
                 make_uint2(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]));
           }
         }
@@ -760,7 +797,8 @@ int launch_conv3(const ConvArgs& args, const IGeom& g, hipStream_t stream) {
   if (RB % CB || NCH % BN || !conv3_ok(g, args.pad_ones)) return (int)hipErrorInvalidValue;
   constexpr int NW = WM * WN, RPI = 1024 / CB;
   constexpr int AR = (BM + 2 + RPI * NW - 1) / (RPI * NW) * RPI * NW;
-  constexpr int LDS = NS * (AR + 3 * BN) * CB;
+  constexpr int BR = (3 * BN + RPI * NW - 1) / (RPI * NW) * RPI * NW;
+  constexpr int LDS = NS * (AR + BR) * CB;
   static_assert(LDS <= 160 * 1024, "LDS");
   auto kern = igemm_conv3_kernel<FWD, BM, BN, WM, WN, NS, CB, F4>;
   static bool attr = false;
@@ -956,6 +994,14 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
     case 25: ZK_IGD3(256, 256, 4, 2, 2, 64)
     case 26: ZK_IGD3(128, 128, 2, 2, 3, 64)
     case 27: ZK_IGD3(256, 64, 4, 1, 2, 64)
+    // deeper rings with 32-B channel chunks (padded weight rows)
+    case 28: ZK_IGD3(256, 64, 4, 1, 4, 32)
+    case 29: ZK_IGD3(256, 64, 4, 1, 3, 32)
+    case 30: ZK_IGD3(128, 64, 2, 2, 4, 32)
+    case 31: ZK_IGD3(512, 64, 8, 1, 2, 64)
+    case 32: ZK_IGD3(256, 64, 4, 1, 4, 64)
+    case 33: ZK_IGD3(128, 128, 2, 2, 4, 32)
+    case 34: ZK_IGD3(256, 128, 4, 2, 3, 32)
 #undef ZK_IGD3
     default: return (int)hipErrorInvalidValue;
   }
