@@ -1570,9 +1570,14 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     // 256x256 (v14) halves the LDS-fill bytes per FLOP; it pays where the
     // grid still has ~200 tiles (the 256-channel stride-1 layers).  conv3
     // (20+: horizontal tap reuse) for the other stride-1 3x3 layers.
+    // Batch >= 512 (profiles/r1av_bconv_tuning_b512.md): 256x256 also wins
+    // for the 512-channel stride-1 and 256-channel stride-2 layers (7x7 x 512
+    // images: 154 -> 121 us); smaller batches keep the batch-256 choices.
     const int Cin = g.Cin, stride = g.s;
     const bool c3 = conv3_ok(g, 0);
     if (Cin == 256 && stride == 1)
+      variant = 14;
+    else if (Cin >= 256 && Cin % 256 == 0 && g.B >= 512)
       variant = 14;
     else if (c3 && Cin == 512)
       variant = 24;
@@ -1627,12 +1632,20 @@ void wgrad_defaults(const IGeom& g, int& variant, int& target_blocks) {
     // input channels: the conv3 kernel (profiles/r1at_wgrad3_tuning.md:
     // 56x56x64 145 -> 107 us, 28x28x128 102 -> 96 us at batch 256); the
     // 256 / 512-channel layers stay on 128x128 tiles (no gain there).
+    // Batch >= 512 (profiles/r1av_bconv_tuning_b512.md): twice the blocks for
+    // the 128-channel layers (28x28x128: 262 -> 183 us), and 256x256 tiles
+    // with 512 blocks for the 256-input-channel 3x3 layers (14x14x256:
+    // 235 -> 168 us; 256 -> 512 stride 2: 130 -> 106 us).
     const bool c3 = conv3_ok(g, 0);
+    const bool big = g.B >= 512;
     if (c3 && g.Cin == 64 && g.Cout % 64 == 0) {
       variant = 20;
       if (target_blocks <= 0) target_blocks = 512;
     } else if (c3 && g.Cin == 128 && g.Cout % 128 == 0) {
       variant = 28;
+      if (target_blocks <= 0) target_blocks = big ? 1024 : 512;
+    } else if (big && g.kh == 3 && g.kw == 3 && g.Cin == 256 && g.Cout % 256 == 0) {
+      variant = 8;
       if (target_blocks <= 0) target_blocks = 512;
     } else if (g.Cin == 64 && g.s == 2 && g.Cout % 128 == 0 && (9 * g.Cin) % 192 == 0) {
       variant = 2;
@@ -1644,7 +1657,7 @@ void wgrad_defaults(const IGeom& g, int& variant, int& target_blocks) {
       variant = 4;  // 128x128, 64-pixel K-steps
       if (target_blocks <= 0)
         target_blocks = (g.Cout >= 512 && g.s == 1) ? 2048
-                        : (g.Cin >= 256 || g.Cout >= 512) ? 1024 : 512;
+                        : (g.Cin >= 256 || g.Cout >= 512 || big) ? 1024 : 512;
     }
   }
   if (target_blocks <= 0) target_blocks = 1024;
@@ -1728,11 +1741,20 @@ ZK_EXPORT int zk_igemm_fwd_fp4(const void* sx4, const void* wf4, void* y, void* 
   if (Cin % 64 || Cout % 64) return (int)hipErrorInvalidValue;
   if (variant < 0) {
     const bool c3 = conv3_ok(g, pad_ones);
-    // Tuned on MI355X (tools/tune_bconv.py --only igf4, E18 shapes, batch 256)
+    // Tuned on MI355X (tools/tune_bconv.py --only igf4, E18 shapes, batch 256);
+    // at batch 512 the 256x256 tiles also win for Cin >= 256 once the output
+    // image has >= 25088 pixels (7x7x512: 47 -> 38 us; 256 -> 512 stride 2:
+    // 37 -> 27 us; profiles/r1av_bconv_tuning_b512.md).
+    const long long Po = (long long)g.B * g.Ho * g.Wo;
+    const bool wide = Cin % 256 == 0 && Cout % 256 == 0 && Po >= 25088;
     if (c3 && Cin == 64)
       variant = 20;
     else if (c3 && Cin == 256 && Cout % 256 == 0)
       variant = 26;
+    else if (c3 && wide)
+      variant = 26;
+    else if (!c3 && wide)
+      variant = 5;
     else if (c3 && Cin >= 256 && Cout % 128 == 0)
       variant = 23;
     else if (c3)
