@@ -97,6 +97,14 @@ def main() -> int:
         x, y = prep(pool[i % len(pool)], training=True)
         return trainer.train_step(x, y)
 
+    # ZK_MAIN_PRIORITY (experiment): run the step on a compute stream of that
+    # HIP priority (negative = above the side stream of the weight gradients)
+    main_prio = os.environ.get("ZK_MAIN_PRIORITY")
+    if main_prio and torch.cuda.is_available():
+        main_stream = torch.cuda.Stream(priority=int(main_prio))
+        main_stream.wait_stream(torch.cuda.current_stream())
+        torch.cuda.set_stream(main_stream)
+
     t_w = time.perf_counter()
     for i in range(args.warmup):
         loss, _ = step(i)

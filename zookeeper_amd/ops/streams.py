@@ -35,6 +35,7 @@ import torch
 from zookeeper_amd.ops._native import grad_ready
 
 ENABLED = os.environ.get("ZK_WGRAD_SIDE", "1") != "0"
+_PRIORITY = int(os.environ.get("ZK_WGRAD_PRIORITY", "0"))
 
 _active = False
 _streams: Dict[int, torch.cuda.Stream] = {}
@@ -49,7 +50,9 @@ def side_stream(device: torch.device) -> torch.cuda.Stream:
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _streams.get(idx)
     if s is None:
-        s = torch.cuda.Stream(device=idx)
+        # ZK_WGRAD_PRIORITY: HIP stream priority of the side stream (0 = the
+        # default / lowest, negative = higher than the compute stream)
+        s = torch.cuda.Stream(device=idx, priority=_PRIORITY)
         _streams[idx] = s
     return s
 
