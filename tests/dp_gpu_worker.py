@@ -43,6 +43,7 @@ def run(mode: str, out: str) -> None:
     configure(spec, {"learning_rate": 1e-2})
     tr = Trainer(model, "sparse_categorical_crossentropy", spec, info, bucket_mb=2.0,
                  first_bucket_mb=0.25)
+    init = tr.flat.data.detach().cpu().clone()  # after the initial broadcast
     g = torch.Generator().manual_seed(99)
     steps, per = 2, 4
     # the same tensors for every world size (at most 2 ranks)
@@ -55,7 +56,7 @@ def run(mode: str, out: str) -> None:
         y = ys[s, lo:lo + per].to(info.device)
         loss, _ = tr.train_step(x, y)
     torch.cuda.synchronize()
-    torch.save({"params": tr.flat.data.cpu(), "loss": float(loss),
+    torch.save({"params": tr.flat.data.cpu(), "init": init, "loss": float(loss),
                 "buckets": tr.bucketer.num_buckets},
                os.path.join(out, f"{mode}_w{world}_r{info.rank}.pt"))
     zdist.shutdown()

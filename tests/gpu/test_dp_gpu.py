@@ -45,8 +45,16 @@ def test_two_ranks_match_single_process_on_same_data(tmp_path):
     r1 = torch.load(tmp_path / "same_w2_r1.pt", weights_only=True)
     assert r0["buckets"] > 1
     torch.testing.assert_close(r0["params"], r1["params"], atol=0, rtol=0)
-    err = ((r0["params"] - ref["params"]).norm() / ref["params"].norm()).item()
-    assert err < 1e-5, err
+    torch.testing.assert_close(r0["init"], ref["init"], atol=0, rtol=0)
+    # Measured against the size of the update itself: fp32-atomics noise in
+    # the split-K weight gradients (~1e-7) plus a binary activation flipping
+    # sign in step 2 leaves run-to-run differences of ~1e-4 of the update
+    # (single-process runs differ from each other the same way), while a
+    # wrong gradient average (sum instead of mean, a bucket missed) is O(1).
+    update = (ref["params"] - ref["init"]).norm().item()
+    assert update > 0
+    err = (r0["params"] - ref["params"]).norm().item() / update
+    assert err < 1e-2, err
 
 
 @pytest.mark.timeout(300)
