@@ -55,7 +55,9 @@ def init(backend: str = "auto", timeout_s: float = 600.0) -> DistInfo:
     else:
         device = torch.device("cpu")
     if backend == "auto":
-        backend = "nccl" if use_gpu else "gloo"
+        # ZK_DIST_BACKEND=gloo rehearses a multi-rank GPU run with several
+        # ranks sharing one GPU (RCCL wants a distinct GPU per rank)
+        backend = os.environ.get("ZK_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
