@@ -48,6 +48,47 @@ def test_sweep_runs_grid_concurrently(tmp_path):
 
 
 @pytest.mark.timeout(300)
+def test_sweep_packs_runs_per_gpu(tmp_path):
+    out = tmp_path / "out"
+    out.mkdir()
+    cmd = [sys.executable, TASK, "RecordConfig", f"out_dir={str(out)!r}",
+           "--grid", "lr=[0.1,0.2]", "--grid", "wd=[0.0,0.5]", "--runs-per-gpu", "2"]
+    env = _env(ZK_SWEEP_DIR=str(tmp_path / "sweep"), HIP_VISIBLE_DEVICES="4,5")
+    res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stdout + res.stderr
+    recs = [json.load(open(out / f)) for f in sorted(os.listdir(out))]
+    assert len(recs) == 4
+    # two GPUs x two runs each: every run on one GPU, each GPU used twice
+    assert sorted(r["hip_visible"] for r in recs) == ["4", "4", "5", "5"]
+    assert res.stdout.count("[sweep] start") == 4
+    # all four slots filled before any run finished
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("[sweep]")]
+    assert all(ln.startswith("[sweep] start") for ln in lines[:4]), lines
+
+
+def test_sweep_slots_round_robin(monkeypatch, tmp_path):
+    from zookeeper_amd import sweep
+
+    started, run_ids = [], []
+
+    class FakeProc:
+        def __init__(self, argv, env, stdout, stderr):
+            started.append(env.get("HIP_VISIBLE_DEVICES"))
+            run_ids.append(env["ZK_RUN_ID"])
+
+        def poll(self):
+            return 0
+
+    monkeypatch.setattr(sweep.subprocess, "Popen", FakeProc)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3")
+    rc = sweep.run_sweep(["x"], [("lr", [1, 2, 3, 4, 5, 6])], gpus_per_run=2,
+                         sweep_dir=str(tmp_path), poll_s=0.0, runs_per_gpu=3)
+    assert rc == 0
+    assert started == ["0,1", "2,3", "0,1", "2,3", "0,1", "2,3"]
+    assert run_ids == [f"lr_{i}" for i in range(1, 7)]
+
+
+@pytest.mark.timeout(300)
 def test_sweep_reports_failed_runs(tmp_path):
     cmd = [sys.executable, TASK, "RecordConfig", f"out_dir={str(tmp_path)!r}", "fail_if_lr=0.2",
            "--grid", "lr=[0.1,0.2]"]

@@ -84,6 +84,13 @@ def task(cls: type) -> type:
         default=0,
         help="Concurrent sweep runs (default: all GPUs / gpus-per-run).",
     )
+    @click.option(
+        "--runs-per-gpu",
+        type=int,
+        default=1,
+        show_default=True,
+        help="Concurrent sweep runs sharing each GPU set.",
+    )
     @click.argument("config", type=ConfigParam(), nargs=-1)
     def command(
         config: Tuple[Tuple[str, Any], ...],
@@ -92,13 +99,15 @@ def task(cls: type) -> type:
         grid: Tuple[str, ...],
         gpus_per_run: int,
         max_parallel: int,
+        runs_per_gpu: int,
     ):
         conf = {k: v for k, v in config}
         if grid:
             from zookeeper_amd.sweep import run_sweep_from_cli
 
             raise SystemExit(
-                run_sweep_from_cli(cls.__name__, grid, gpus_per_run, max_parallel)
+                run_sweep_from_cli(cls.__name__, grid, gpus_per_run, max_parallel,
+                                   runs_per_gpu)
             )
         if nproc > 1:
             from zookeeper_amd.parallel.launch import maybe_relaunch

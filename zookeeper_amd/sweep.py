@@ -17,6 +17,12 @@ CLI (added to every @task command)::
   ``gpus_per_run``); each run gets ``HIP_VISIBLE_DEVICES`` restricted to its
   own GPUs and, if ``gpus_per_run > 1``, is launched data-parallel with
   ``--nproc gpus_per_run``;
+* ``--runs-per-gpu k`` packs k concurrent runs onto every GPU set (small
+  models that leave most of a 288 GB MI355X idle): the slots are the GPU
+  sets repeated k times, filled set by set round-robin;
+* every run gets ``ZK_RUN_ID=<run_name>``, the default ``run_id`` of a
+  training experiment, so runs sharing ``output_dir`` checkpoint into their
+  own ``<output_dir>/<Task>/<run_name>/``;
 * every run writes ``<sweep_dir>/<run_name>/stdout.log``, and the sweep writes
   ``<sweep_dir>/sweep.json`` (config, exit code, wall time per run); a failing
   run does not stop the others, the sweep exits non-zero if any run failed.
@@ -105,7 +111,8 @@ def _token(k: str, v: Any) -> str:
 
 def run_sweep(base_argv: Sequence[str], axes, gpus_per_run: int = 1,
               max_parallel: int = 0, sweep_dir: str = "sweeps/latest",
-              poll_s: float = 0.5, env: Optional[Dict[str, str]] = None) -> int:
+              poll_s: float = 0.5, env: Optional[Dict[str, str]] = None,
+              runs_per_gpu: int = 1) -> int:
     """Run the grid.  ``base_argv`` is the full command of one run *without*
     the grid values (e.g. ``[python, train.py, TrainImageNet, epochs=1]``)."""
     combos = expand(axes)
@@ -115,6 +122,9 @@ def run_sweep(base_argv: Sequence[str], axes, gpus_per_run: int = 1,
         per = max(gpus_per_run, 1)
         for i in range(0, len(devices) - per + 1, per):
             slots.append(devices[i:i + per])
+        # k runs per GPU set: one pass over the sets per k, so the first
+        # len(sets) runs still land on distinct GPUs
+        slots = [list(sl) for _ in range(max(runs_per_gpu, 1)) for sl in slots]
     if not slots:  # CPU-only: concurrency without device partitioning
         slots = [[] for _ in range(max(max_parallel, 1))]
     if max_parallel > 0:
@@ -135,6 +145,7 @@ def run_sweep(base_argv: Sequence[str], axes, gpus_per_run: int = 1,
             e = dict(base_env)
             if run.devices:
                 e["HIP_VISIBLE_DEVICES"] = ",".join(run.devices)
+            e["ZK_RUN_ID"] = run.name  # default run_id: separate checkpoint dirs
             for var in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT"):
                 e.pop(var, None)
             argv = list(run.argv)
@@ -175,20 +186,21 @@ def _strip_sweep_args(argv: Sequence[str]) -> List[str]:
         if skip:
             skip = False
             continue
-        if a in ("--grid", "--gpus-per-run", "--max-parallel"):
+        if a in ("--grid", "--gpus-per-run", "--max-parallel", "--runs-per-gpu"):
             skip = True
             continue
-        if a.startswith(("--grid=", "--gpus-per-run=", "--max-parallel=")):
+        if a.startswith(("--grid=", "--gpus-per-run=", "--max-parallel=", "--runs-per-gpu=")):
             continue
         out.append(a)
     return out
 
 
 def run_sweep_from_cli(task_name: str, grid: Sequence[str], gpus_per_run: int,
-                       max_parallel: int) -> int:
+                       max_parallel: int, runs_per_gpu: int = 1) -> int:
     """Entry point used by the @task command when ``--grid`` is given."""
     axes = parse_grid(grid)
     base = [sys.executable] + _strip_sweep_args(sys.argv)
     stamp = time.strftime("%Y%m%d-%H%M%S")
     sweep_dir = os.environ.get("ZK_SWEEP_DIR", os.path.join("sweeps", f"{task_name}-{stamp}"))
-    return run_sweep(base, axes, gpus_per_run, max_parallel, sweep_dir)
+    return run_sweep(base, axes, gpus_per_run, max_parallel, sweep_dir,
+                     runs_per_gpu=runs_per_gpu)

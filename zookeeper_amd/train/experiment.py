@@ -58,7 +58,9 @@ class TrainingExperiment(Experiment):
     log_every: int = Field(50)
     # Checkpointing: every N steps (0 = only at the end); output_dir None = off.
     output_dir: Optional[str] = Field(None)
-    run_id: str = Field("run")
+    # A sweep (zookeeper_amd/sweep.py) sets ZK_RUN_ID to each run's name so
+    # concurrent runs sharing output_dir keep separate run directories.
+    run_id: str = Field(lambda: os.environ.get("ZK_RUN_ID", "run"))
     checkpoint_every: int = Field(0)
     keep_checkpoints: int = Field(3)
     resume: bool = Field(True)
