@@ -31,7 +31,7 @@ import collections.abc as cabc
 import inspect
 import types
 import typing
-from typing import Any
+from typing import Any, Tuple
 
 __all__ = ["check_type"]
 
@@ -75,8 +75,31 @@ def _check_class(value: Any, cls: type) -> bool:
         return True
 
 
+_ORIGIN_ARGS: dict = {}
+
+
+def _origin_args(expected: Any) -> Tuple[Any, Tuple[Any, ...]]:
+    """``typing.get_origin`` / ``get_args``, memoised per annotation (the
+    same few annotations are checked on every configure / first access)."""
+    try:
+        return _ORIGIN_ARGS[expected]
+    except KeyError:
+        pass
+    except TypeError:  # unhashable annotation (e.g. Annotated metadata)
+        return typing.get_origin(expected), typing.get_args(expected)
+    r = (typing.get_origin(expected), typing.get_args(expected))
+    _ORIGIN_ARGS[expected] = r
+    return r
+
+
 def check_type(value: Any, expected: Any) -> bool:  # noqa: C901 - a dispatcher
     """Return True if ``value`` satisfies the annotation ``expected``."""
+    if type(expected) is type:  # a plain class (int, str, a component, ...)
+        if expected is float:
+            return isinstance(value, (float, int))
+        if expected is complex:
+            return isinstance(value, (complex, float, int))
+        return isinstance(value, expected)
     if expected is Any or expected is object or expected is inspect.Parameter.empty:
         return True
     if expected is None or expected is _NoneType:
@@ -94,8 +117,7 @@ def check_type(value: Any, expected: Any) -> bool:  # noqa: C901 - a dispatcher
     if supertype is not None:
         return check_type(value, supertype)
 
-    origin = typing.get_origin(expected)
-    args = typing.get_args(expected)
+    origin, args = _origin_args(expected)
 
     if origin is None:
         if inspect.isclass(expected):
