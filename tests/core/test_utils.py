@@ -4,7 +4,7 @@ cover the predicates and the version string; the extra cases pin the
 naming, CLI-value parsing, immutability and type-checking helpers that the
 rest of the config system relies on)."""
 
-from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple, Type, Union
+from typing import Annotated, Any, Callable, Dict, List, Optional, Sequence, Tuple, Type, Union
 
 import pytest
 
@@ -143,7 +143,11 @@ def test_ancestors_with_field_closest_first():
     ({"a": "b"}, Dict[str, int], False), (1, Union[str, int], True),
     (int, Type[int], True), (bool, Type[int], True), (str, Type[int], False),
     (len, Callable[..., int], True), (3, Callable, False), ([1.0], Sequence[float], True),
-    ("x", Any, True), (object(), object, True)])
+    ("x", Any, True), (object(), object, True),
+    # plain-class fast path and memoised / unhashable typing annotations
+    (1, complex, True), (2.5, complex, True), (None, type(None), True), (0, type(None), False),
+    ((1, 2), Tuple[int, int], True), ((1, 2), Tuple[int, int], True),
+    (1, Annotated[int, []], True), ("1", Annotated[int, []], False)])
 def test_check_type(value, tp, ok):
     assert check_type(value, tp) is ok
 
