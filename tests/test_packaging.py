@@ -29,3 +29,20 @@ def test_package_data_covers_native_sources():
     headers = glob.glob(os.path.join(pkg, "csrc", "**", "*.h"), recursive=True)
     for src in list(sources()) + headers:
         assert os.path.abspath(src) in covered, src
+
+
+def test_config_layer_microbenchmark_runs(tmp_path):
+    """tools/bench_config.py (profiles/config_layer_overheads.md) keeps working."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "cfg.json"
+    subprocess.run([sys.executable, os.path.join(root, "tools", "bench_config.py"),
+                    "--json", str(out)], check=True, capture_output=True, timeout=300)
+    res = json.loads(out.read_text())
+    for key in ("import_ms", "configure_tree_plus_first_touches_us", "cached_field_access_us",
+                "first_field_access_inherited_us", "cached_factory_field_access_us"):
+        assert res[key] > 0, key
