@@ -4,18 +4,29 @@ BinaryResNet-E18 on ImageNet-shape synthetic data (224×224×3, 1000 classes,
 random-init weights), data parallel over RCCL with one process per GPU.
 
     python bench.py --gpus 1 --steps 30 --warmup 10
+    python bench.py --gpus 8                      # spawns 8 ranks itself
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
         --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
 
+``--gpus N`` with N > 1 and no ``WORLD_SIZE`` in the environment starts N
+rank processes itself (``zookeeper_amd.parallel.launch.spawn``: subprocesses,
+before anything touches the GPU, never exec) and returns their exit code.
+Inside a launched job ``WORLD_SIZE`` must equal ``--gpus``: a mismatch is an
+error, never a silent 1-GPU run.
+
 A timed step is the complete training step: uint8→bf16 normalisation/flip
-of the batch, forward, softmax-CE, backward with bucketed all-reduce, fused
-Adam + weight_clip.  Input batches come from a device-resident pool of
-synthetic batches (no host work per step).  On one GPU, when the warmup
-shows the step host-bound (small ``--batch``), zero-grad + forward + loss +
-backward are replayed as one HIP graph (``--graph auto``); the optimizer
-still runs every step.  ``--steps`` steps are timed
-between a barrier + ``torch.cuda.synchronize()`` on both sides; the reported
-time is the MAX over ranks.  Rank 0 prints one JSON line.
+of the batch, forward, softmax-CE, backward with bucketed all-reduce on a
+comm stream, fused Adam + weight_clip.  ``--data pool`` (default) cycles a
+few device-resident synthetic batches; ``--data stream`` feeds the synthetic
+source through the host input pipeline (native row gather into pinned
+slots, side-stream H2D, event hand-off), so the host→device path is inside
+the timed region.  When the warmup shows the step host-bound (small
+``--batch``), zero-grad + forward + loss + backward are replayed as one HIP
+graph (``--graph auto``; under DP the all-reduce runs after the replay).
+``--steps`` steps are timed between a barrier + ``torch.cuda.synchronize()``
+on both sides; the reported time is the MAX over ranks.  Per-step GPU times
+(events between consecutive steps) give the median / p10 / p90.  Rank 0
+prints one JSON line.
 
 Weak scaling: the per-GPU batch (``--batch``, default 512) is fixed, the
 global batch is ``batch × N``.  512 images per GPU use a few GB of the 288 GB
@@ -36,30 +47,67 @@ METRIC = "images/sec (whole node) BinaryResNet-E18 ImageNet at 1/2/4/8 MI355X"
 OTHER_METRIC = "images/sec (whole node) {model} ImageNet-shape training"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=512, help="per-GPU batch")
     ap.add_argument("--model", default="BinaryResNetE18")
+    ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    ap.add_argument("--data", default="pool", choices=["pool", "stream"],
+                    help="pool: device-resident synthetic batches; stream: host pipeline "
+                         "(pinned ring + side-stream H2D) inside the timed region")
     ap.add_argument("--pool", type=int, default=4, help="device-resident synthetic batches")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--graph", default="auto", choices=["0", "1", "auto"],
-                    help="replay forward+backward as a HIP graph (1 GPU; eager when distributed); "
-                         "auto: when the warmup shows the step host-bound")
+                    help="replay forward+backward as a HIP graph; auto: when the warmup "
+                         "shows the step host-bound")
+    ap.add_argument("--allow-shared-gpu", action="store_true",
+                    help="(rehearsal) let several ranks share a GPU (ZK_DIST_BACKEND=gloo)")
     ap.add_argument("--json-out", default=None)
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _percentile(xs, q):
+    xs = sorted(xs)
+    if not xs:
+        return None
+    k = (len(xs) - 1) * q
+    lo, hi = int(k), min(int(k) + 1, len(xs) - 1)
+    return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
+
+
+def self_launch(args) -> int:
+    """Start ``--gpus`` ranks of this script (subprocesses; the parent never
+    initialises the GPU) and return the first non-zero exit code."""
+    from zookeeper_amd.parallel.launch import spawn
+
+    if not args.allow_shared_gpu:
+        import torch  # device_count() does not initialise the GPU on this image
+
+        have = torch.cuda.device_count()
+        if have and have < args.gpus:
+            print(f"error: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    return spawn([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], args.gpus)
 
 
 def main() -> int:
     args = parse()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args)
+    if world_env != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+        return 2
+
     import torch
 
     from zookeeper_amd import ComponentField, Field, component, configure
     from zookeeper_amd.core.component import base_getattr
-    from zookeeper_amd.data import (Dataset, ImageNetPreprocessing, Preprocessing,
+    from zookeeper_amd.data import (DeviceLoader, Dataset, ImageNetPreprocessing, Preprocessing,
                                     SyntheticImageNet, make_device_pool_batches)
     from zookeeper_amd import models
     from zookeeper_amd.parallel import dist as zdist
@@ -67,43 +115,52 @@ def main() -> int:
 
     info = zdist.init()
     if info.world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={info.world}", file=sys.stderr)
+        print(f"error: --gpus {args.gpus} but the job has {info.world} rank(s)", file=sys.stderr)
+        return 2
+    if (info.world > 1 and torch.cuda.is_available() and not args.allow_shared_gpu
+            and torch.cuda.device_count() < info.world):
+        print(f"error: {info.world} ranks but {torch.cuda.device_count()} GPU(s)", file=sys.stderr)
+        return 2
+    S = args.image_size
 
     @component
     class BenchConfig:
         dataset: Dataset = ComponentField(SyntheticImageNet)
-        input_shape: Tuple[int, int, int] = Field((224, 224, 3))
+        input_shape: Tuple[int, int, int] = Field((S, S, 3))
         preprocessing: Preprocessing = ComponentField(ImageNetPreprocessing)
         model: torch.nn.Module = ComponentField(getattr(models, args.model))
         optimizer: OptimizerSpec = ComponentField(Adam)
         learning_rate: float = Field(2e-3)
 
     cfg = BenchConfig()
-    configure(cfg, {"model.backend": args.backend})
+    configure(cfg, {"model.backend": args.backend, "dataset.image_shape": (S, S, 3)})
     model = cfg.model
     backend = base_getattr(cfg, "model").resolved_backend()
     torch.manual_seed(1234)
     trainer = Trainer(model, "sparse_categorical_crossentropy", base_getattr(cfg, "optimizer"),
                       info, bucket_mb=args.bucket_mb,
                       graph="auto" if args.graph == "auto" else args.graph == "1",
-                      graph_warmup=max(1, min(3, args.warmup - 1)))  # capture inside the warmup
-    pool = make_device_pool_batches(args.pool, args.batch, (224, 224, 3), 1000, info.device,
-                                    seed=info.rank)
+                      graph_warmup=max(1, min(3, args.warmup - 1)),  # capture inside the warmup
+                      comm_timing=info.world > 1 and torch.cuda.is_available())
     prep = cfg.preprocessing
+    loader = None
+    if args.data == "stream":
+        src, _ = cfg.dataset.train()
+        loader = DeviceLoader(src, args.batch, info.device, shuffle=True, seed=0,
+                              rank=info.rank, world=info.world, slots=4)
+        it = iter(loader)
+        next_batch = lambda i: next(it)  # noqa: E731
+    else:
+        pool = make_device_pool_batches(args.pool, args.batch, (S, S, 3), 1000, info.device,
+                                        seed=info.rank)
+        next_batch = lambda i: pool[i % len(pool)]  # noqa: E731
 
-    sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    cuda = torch.cuda.is_available()
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
 
     def step(i):
-        x, y = prep(pool[i % len(pool)], training=True)
+        x, y = prep(next_batch(i), training=True)
         return trainer.train_step(x, y)
-
-    # ZK_MAIN_PRIORITY (experiment): run the step on a compute stream of that
-    # HIP priority (negative = above the side stream of the weight gradients)
-    main_prio = os.environ.get("ZK_MAIN_PRIORITY")
-    if main_prio and torch.cuda.is_available():
-        main_stream = torch.cuda.Stream(priority=int(main_prio))
-        main_stream.wait_stream(torch.cuda.current_stream())
-        torch.cuda.set_stream(main_stream)
 
     t_w = time.perf_counter()
     for i in range(args.warmup):
@@ -112,11 +169,17 @@ def main() -> int:
             sync()
             print(f"[bench] warmup {i + 1}/{args.warmup} loss={loss.item():.4f} "
                   f"t={time.perf_counter() - t_w:.1f}s", file=sys.stderr, flush=True)
+    trainer.bucketer.pop_timings()  # discard warmup comm timings
     zdist.barrier()
     sync()
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if cuda else []
     t0 = time.perf_counter()
+    if marks:
+        marks[0].record()
     for i in range(args.steps):
         loss, _ = step(args.warmup + i)
+        if marks:
+            marks[i + 1].record()
         if info.is_main and (i + 1) % 50 == 0:
             print(f"[bench] step {i + 1}/{args.steps}", file=sys.stderr, flush=True)
     t_enq = time.perf_counter() - t0  # host time to enqueue (no sync yet)
@@ -125,6 +188,10 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     elapsed = zdist.all_reduce_max(elapsed)
     final_loss = float(loss.item())
+    step_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)] if marks else []
+    comm = trainer.bucketer.pop_timings()
+    if loader is not None:
+        loader.close()
 
     ms = 1000.0 * elapsed / args.steps
     if info.is_main and trainer.graph_probe is not None:
@@ -137,32 +204,50 @@ def main() -> int:
               file=sys.stderr, flush=True)
     global_batch = args.batch * info.world
     value = global_batch * args.steps / elapsed
+    r3 = lambda v: None if v is None else round(v, 3)  # noqa: E731
+    data_desc = (f"synthetic (ImageNet-shape uint8 {S}x{S}x3, 1000 classes, "
+                 + ("device-resident pool" if args.data == "pool" else
+                    "host source streamed: native gather into pinned slots + side-stream H2D")
+                 + "; random-init weights)")
     out = {
-        "metric": METRIC if args.model == "BinaryResNetE18" else OTHER_METRIC.format(model=args.model),
+        "metric": METRIC if (args.model == "BinaryResNetE18" and S == 224)
+        else OTHER_METRIC.format(model=args.model),
         "value": round(value, 2),
         "unit": "images/sec",
         "n_gpus": info.world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms, 3),
+        "ms_per_step_median": r3(_percentile(step_ms, 0.5)),
+        "ms_per_step_p10": r3(_percentile(step_ms, 0.1)),
+        "ms_per_step_p90": r3(_percentile(step_ms, 0.9)),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (ImageNet-shape uint8 224x224x3, 1000 classes, device-resident pool; random-init weights)",
+        "data": data_desc,
         "config": {
             "model": args.model,
             "global_batch": global_batch,
             "per_gpu_batch": args.batch,
             "seq_len": None,
-            "image_shape": [224, 224, 3],
+            "image_shape": [S, S, 3],
             "parallelism": f"dp{info.world}",
             "backend": backend,
             "optimizer": "adam+weight_clip (fused)",
             "hip_graph": trainer.graph,
+            "data_path": args.data,
+            "buckets": trainer.bucketer.num_buckets if info.world > 1 else 0,
             "final_loss": round(final_loss, 4),
         },
     }
+    if comm:
+        out["comm"] = {
+            "comm_ms_median": r3(_percentile([c["comm_ms"] for c in comm], 0.5)),
+            "bucket_sum_ms_median": r3(_percentile([c["bucket_sum_ms"] for c in comm], 0.5)),
+            "exposed_ms_median": r3(_percentile([c["exposed_ms"] for c in comm], 0.5)),
+            "exposed_ms_max": r3(max(c["exposed_ms"] for c in comm)),
+        }
     if info.is_main:
         line = json.dumps(out)
         print(line, flush=True)

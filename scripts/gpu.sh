@@ -1,0 +1,81 @@
+#!/bin/bash
+# One parameterised GPU-box driver (replaces the per-experiment one-liners).
+#
+#   gpurun --timeout 900 -- bash scripts/gpu.sh <step> [<step> ...]
+#
+# Steps (each runs under its own time limit, output under gpurun_out/):
+#   tests            python -m pytest tests -m gpu
+#   tests:<expr>     python -m pytest tests -m gpu -k <expr>
+#   bench[:model[:batch[:steps]]]      bench.py on 1 GPU (default E18 b512 60 steps)
+#   stream[:model]   bench.py --data stream (pinned ring + side-stream H2D)
+#   prof[:model[:batch]]               rocprofv3 --kernel-trace --stats of bench.py
+#   tune[:args]      tools/tune_bconv.py with the given (comma-separated) args
+#   py:<module>      python -m <module>  (tools, one-off diagnostics)
+#   dpgloo:<n>       bench.py with n gloo ranks sharing the GPU (ordering rehearsal)
+#
+# A step that times out, aborts or faults ends the script (no GPU work after).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+PROG="$OUT/progress.txt"
+
+gpu_step() {
+  local t=$1; shift
+  local log=$1; shift
+  echo "start '$*' $(date +%T)" >> "$PROG"
+  timeout -k 10 "$t" "$@" > "$log" 2>&1
+  local rc=$?
+  echo "step '$*' rc=$rc $(date +%T)" >> "$PROG"
+  if [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -ge 128 ]; then
+    echo "fatal rc=$rc in: $*" >> "$PROG"
+    exit $rc
+  fi
+  return $rc
+}
+
+n=0
+for spec in "$@"; do
+  n=$((n + 1))
+  IFS=':' read -r kind a1 a2 a3 <<< "$spec"
+  case "$kind" in
+    tests)
+      if [ -n "${a1:-}" ]; then
+        gpu_step 600 "$OUT/pytest_$n.log" python -u -m pytest tests -m gpu -x -q \
+          --timeout 120 --timeout-method thread -k "$a1" || exit $?
+      else
+        gpu_step 900 "$OUT/pytest_$n.log" python -u -m pytest tests -m gpu -x -q \
+          --timeout 120 --timeout-method thread || exit $?
+      fi
+      ;;
+    bench)
+      gpu_step 420 "$OUT/bench_${n}_${a1:-E18}.log" python -u bench.py \
+        --model "${a1:-BinaryResNetE18}" --batch "${a2:-512}" --steps "${a3:-60}" \
+        --warmup 10 --json-out "$OUT/bench_${n}.json" || exit $?
+      ;;
+    stream)
+      gpu_step 420 "$OUT/stream_${n}.log" python -u bench.py --data stream \
+        --model "${a1:-BinaryResNetE18}" --steps 60 --warmup 10 \
+        --json-out "$OUT/stream_${n}.json" || exit $?
+      ;;
+    prof)
+      gpu_step 600 "$OUT/prof_${n}.log" rocprofv3 --kernel-trace --stats \
+        -d "$OUT/prof_$n" -o run -- python3 bench.py --model "${a1:-BinaryResNetE18}" \
+        --batch "${a2:-512}" --steps 20 --warmup 10 --graph 0 || exit $?
+      ;;
+    tune)
+      gpu_step 600 "$OUT/tune_${n}.log" python -u tools/tune_bconv.py ${a1//,/ } || exit $?
+      ;;
+    py)
+      gpu_step 600 "$OUT/py_${n}.log" python -u -m "$a1" ${a2//,/ } || exit $?
+      ;;
+    dpgloo)
+      ZK_DIST_BACKEND=gloo gpu_step 600 "$OUT/dpgloo_${n}.log" python -u bench.py \
+        --gpus "${a1:-2}" --allow-shared-gpu --batch 64 --steps 10 --warmup 3 || exit $?
+      ;;
+    *)
+      echo "unknown step $spec" >> "$PROG"; exit 2 ;;
+  esac
+done
+echo "all steps done $(date +%T)" >> "$PROG"

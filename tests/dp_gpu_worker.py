@@ -6,6 +6,11 @@ broadcast -- runs multi-rank.
 
     python tests/dp_gpu_worker.py <same|split> <outdir>
 
+Environment: ``ZK_WGRAD_SIDE=0|1`` (side-stream weight gradients),
+``ZK_TEST_GRAPH=0|1`` (HIP-graph replay under DP).  The bucketer never
+synchronises the host: ordering is carried by events alone
+(compute → comm stream at bucket-ready, comm → compute before the optimizer).
+
 ``same``: every rank trains on the same batches, so the averaged gradients
 equal a single process's and the result must match a world-size-1 run
 (``world=1`` when launched without the env contract).  ``split``: disjoint
@@ -41,11 +46,15 @@ def run(mode: str, out: str) -> None:
                 p.add_(0.5)
     spec = SGD()
     configure(spec, {"learning_rate": 1e-2})
+    # ZK_TEST_GRAPH=1: forward+backward replayed as a HIP graph (the
+    # all-reduce issued on the comm stream after each replay)
+    graph = os.environ.get("ZK_TEST_GRAPH", "0") == "1"
     tr = Trainer(model, "sparse_categorical_crossentropy", spec, info, bucket_mb=2.0,
-                 first_bucket_mb=0.25)
+                 first_bucket_mb=0.25, graph=graph, graph_warmup=1,
+                 comm_timing=world > 1)
     init = tr.flat.data.detach().cpu().clone()  # after the initial broadcast
     g = torch.Generator().manual_seed(99)
-    steps, per = 2, 4
+    steps, per = int(os.environ.get("ZK_TEST_STEPS", "2")), 4
     # the same tensors for every world size (at most 2 ranks)
     xs = torch.randn(steps, 2 * per, 3, 64, 64, generator=g)
     ys = torch.randint(0, 10, (steps, 2 * per), generator=g)
@@ -56,8 +65,12 @@ def run(mode: str, out: str) -> None:
         y = ys[s, lo:lo + per].to(info.device)
         loss, _ = tr.train_step(x, y)
     torch.cuda.synchronize()
+    timings = tr.bucketer.pop_timings()
     torch.save({"params": tr.flat.data.cpu(), "init": init, "loss": float(loss),
-                "buckets": tr.bucketer.num_buckets},
+                "buckets": tr.bucketer.num_buckets, "graph": tr.graph,
+                "comm_steps": len(timings),
+                "slots": [(sl.name, sl.offset, sl.numel) for sl in tr.flat.slots],
+                "ranges": list(tr.bucketer.ranges)},
                os.path.join(out, f"{mode}_w{world}_r{info.rank}.pt"))
     zdist.shutdown()
 

@@ -65,6 +65,25 @@ if __name__ == "__main__":
 
         time.sleep(60)  # would hang; the launcher must terminate us
         sys.exit(0)
+    if mode == "bnsync":
+        # BN running statistics drift apart per rank; all_reduce_buffers
+        # must leave every rank with the cross-rank mean
+        from zookeeper_amd.parallel import dist as zdist
+        from zookeeper_amd.parallel.ddp import all_reduce_buffers
+
+        zdist.init("gloo")
+        torch.manual_seed(0)
+        bn = nn.BatchNorm1d(6)
+        bn.train()
+        g = torch.Generator().manual_seed(100 + rank)
+        for _ in range(3):
+            bn(torch.randn(16, 6, generator=g) * (rank + 1) + rank)
+        before = {k: v.clone() for k, v in bn.state_dict().items()}
+        all_reduce_buffers(bn)
+        torch.save({"before": before, "after": bn.state_dict()},
+                   os.path.join(out, f"bn{rank}.pt"))
+        zdist.shutdown()
+        sys.exit(0)
     tr = train(rank, world, bucket_mb=0.001)
     torch.save({"params": tr.flat.data.clone(), "buckets": tr.bucketer.num_buckets},
                os.path.join(out, f"rank{rank}.pt"))

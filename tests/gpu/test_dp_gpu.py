@@ -18,8 +18,9 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 WORKER = os.path.join(os.path.dirname(HERE), "dp_gpu_worker.py")
 
 
-def _run(mode, out, nproc):
-    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+def _run(mode, out, nproc, side="1", graph="0"):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4", ZK_WGRAD_SIDE=side,
+               ZK_TEST_GRAPH=graph)
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     if nproc == 1:
@@ -37,13 +38,17 @@ def _gpu():
 
 
 @pytest.mark.timeout(300)
-def test_two_ranks_match_single_process_on_same_data(tmp_path):
-    assert _run("same", tmp_path, 1) == 0
-    assert _run("same", tmp_path, 2) == 0
+@pytest.mark.parametrize("side,graph", [("1", "0"), ("0", "0"), ("1", "1")],
+                         ids=["side-stream", "single-stream", "graph"])
+def test_two_ranks_match_single_process_on_same_data(tmp_path, side, graph):
+    assert _run("same", tmp_path, 1, side, graph) == 0
+    assert _run("same", tmp_path, 2, side, graph) == 0
     ref = torch.load(tmp_path / "same_w1_r0.pt", weights_only=True)
     r0 = torch.load(tmp_path / "same_w2_r0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "same_w2_r1.pt", weights_only=True)
     assert r0["buckets"] > 1
+    assert r0["graph"] == (graph == "1") and ref["graph"] == (graph == "1")
+    assert r0["comm_steps"] == 2  # every step's collectives were timed
     torch.testing.assert_close(r0["params"], r1["params"], atol=0, rtol=0)
     torch.testing.assert_close(r0["init"], ref["init"], atol=0, rtol=0)
     # Measured against the size of the update itself: fp32-atomics noise in

@@ -116,3 +116,25 @@ def test_native_gather_rows():
     dst = torch.empty(100, 64, 3, dtype=torch.uint8)
     _native.gather_rows(src, idx, dst)
     assert (dst.numpy() == src[idx]).all()
+
+
+def test_stream_gather_plan_matches_get_batch():
+    """The streaming loader gathers rows natively through ``gather_plan``;
+    its batches must be bit-identical to ``get_batch`` of the sampler's
+    indices (synthetic, array and sliced sources), over several epochs."""
+    from zookeeper_amd.data.dataset import SyntheticSource, _SubsetSource
+    from zookeeper_amd.data.loader import IndexSampler
+
+    arr = np.random.default_rng(3).integers(0, 255, (48, 5, 5, 3), dtype=np.uint8)
+    for src in (SyntheticSource(40, (6, 6, 3), 10, seed=5, pool=7),
+                ArraySource(arr, np.arange(48) % 9),
+                _SubsetSource(ArraySource(arr, np.arange(48)), 8, 40)):
+        loader = DeviceLoader(src, 8, torch.device("cpu"), shuffle=True, seed=11)
+        sampler = IndexSampler(len(src), 8, True, 11)
+        it, ref = iter(loader), sampler.batches()
+        for _ in range(11):  # wraps past an epoch boundary
+            got, idx = next(it), next(ref)
+            want = src.get_batch(idx)
+            assert torch.equal(got["image"], torch.from_numpy(np.ascontiguousarray(want["image"])))
+            assert torch.equal(got["label"], torch.from_numpy(want["label"]))
+        loader.close()

@@ -60,3 +60,16 @@ def test_bucketer_layout():
     # grads are views into the flat buffer
     for s in flat.slots:
         assert s.param.grad.data_ptr() == flat.grad.data_ptr() + 4 * s.offset
+
+
+@pytest.mark.timeout(120)
+def test_bn_buffers_all_reduced(tmp_path):
+    assert _launch("bnsync", tmp_path) == 0
+    r = [torch.load(tmp_path / f"bn{i}.pt", weights_only=True) for i in range(2)]
+    for key in ("running_mean", "running_var"):
+        assert not torch.equal(r[0]["before"][key], r[1]["before"][key])
+        mean = (r[0]["before"][key] + r[1]["before"][key]) / 2
+        torch.testing.assert_close(r[0]["after"][key], mean)
+        torch.testing.assert_close(r[1]["after"][key], mean)
+    # integer buffers are left alone
+    assert int(r[0]["after"]["num_batches_tracked"]) == 3

@@ -130,7 +130,16 @@ def test_training_checkpoint_and_resume(tmp_path):
     assert res.returncode == 0, res.stderr[-2000:]
     run_dir = tmp_path / "BinaryNetMnist" / "run"
     assert (run_dir / "checkpoints" / "step_00000002" / "model.pt").exists()
-    assert (run_dir / "config.json").exists()
+    rec = json.load(open(run_dir / "config.json"))
+    cfg = rec["config"]
+    # the resolved dotted-key config, replayable through configure / the CLI
+    assert rec["task"] == "BinaryNetMnist"
+    assert cfg["batch_size"] == 8 and cfg["steps_per_epoch"] == 2
+    assert cfg["model"] == "BinaryNet" and cfg["model.filters"] == 32
+    assert cfg["dataset"] == "SyntheticMNIST" and cfg["dataset.num_train_examples"] == 64
+    assert cfg["preprocessing.pad_size"] == 32
+    assert cfg["metrics"] == ["accuracy"]
+    assert "BinaryNetMnist(" in rec["tree"]
     lines = open(run_dir / "metrics.jsonl").read().strip().splitlines()
     assert json.loads(lines[-1])["step"] == 2
     res = subprocess.run(base + ["epochs=2"], env=_env(), capture_output=True, text=True,
@@ -147,11 +156,16 @@ def test_cifar10_binarynet_task_runs_on_cpu(tmp_path):
     cmd = [sys.executable, os.path.join(ROOT, "examples", "larq_experiment.py"), "BinaryNetCifar10",
            "epochs=1", "batch_size=8", "steps_per_epoch=3", "print_summary=False",
            f"output_dir={str(tmp_path)!r}", "model.filters=32", "model.dense_units=64",
-           "dataset.num_train_examples=64", "dataset.num_validation_examples=16"]
+           "dataset.num_train_examples=64", "dataset.num_validation_examples=16",
+           "metrics=['accuracy','sparse_top_k_categorical_accuracy']"]
     res = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=800)
     assert res.returncode == 0, res.stderr[-2000:]
     run_dir = tmp_path / "BinaryNetCifar10" / "run"
     lines = open(run_dir / "metrics.jsonl").read().strip().splitlines()
     recs = [json.loads(line) for line in lines]
     assert any(r.get("step") == 3 for r in recs)
+    # configured Keras-style metrics: top-1 and top-5 logged per flush
+    assert all("top1" in r and "top5" in r for r in recs)
+    assert all(r["top5"] >= r["top1"] for r in recs)
+    assert "val_top5=" in res.stdout
     assert (run_dir / "checkpoints" / "step_00000003" / "model.pt").exists()

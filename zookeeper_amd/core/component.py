@@ -256,6 +256,41 @@ def _field_strings(instance: Any, single_line: bool) -> Iterator[str]:
         yield f"{name}={text}"
 
 
+def flatten_config(instance: Any, prefix: str = "") -> Dict[str, Any]:
+    """The resolved configuration of a configured component tree as a flat
+    dotted-key dict — the same key syntax ``configure`` and the CLI accept,
+    so a run record (``config.json``) can be replayed.  A sub-component
+    contributes ``key: ClassName`` plus its own fields under ``key.``; values
+    a child inherits from an ancestor are recorded once, at the ancestor;
+    missing ``allow_missing`` fields are omitted; callables are recorded by
+    name.  Not in the reference (its only record is ``str(task)``,
+    zookeeper/core/component.py:331-337)."""
+    out: Dict[str, Any] = {}
+    for name, field in type(instance).__component_fields__.items():
+        try:
+            value = base_getattr(instance, name)
+        except AttributeError:
+            continue
+        parent = next(utils.generate_component_ancestors_with_field(instance, name), None)
+        if parent is not None:
+            try:
+                if base_getattr(parent, name) is value:
+                    continue
+            except AttributeError:
+                pass
+        key = prefix + name
+        if utils.is_component_instance(value):
+            out[key] = type(value).__name__
+            out.update(flatten_config(value, key + "."))
+        elif callable(value) and not isinstance(value, type):
+            out[key] = f"<callable {getattr(value, '__qualname__', type(value).__name__)}>"
+        elif isinstance(value, type):
+            out[key] = value.__name__
+        else:
+            out[key] = value
+    return out
+
+
 def _unconfigured(instance: Any) -> str:
     return f"<Unconfigured component '{instance.__component_name__}' instance>"
 

@@ -60,6 +60,14 @@ class Source(abc.ABC):
     def image_shape(self) -> Optional[Tuple[int, ...]]:
         return None
 
+    def gather_plan(self, indices: np.ndarray) -> Optional[Tuple[np.ndarray, np.ndarray, np.ndarray]]:
+        """``(rows, row_index, labels)`` when the batch's images are whole
+        rows of one C-contiguous array: the loader then gathers them with the
+        native multi-threaded row gather straight into a pinned slot
+        (``zk_gather_rows``) instead of materialising ``get_batch``.  None
+        (default) → ``get_batch``."""
+        return None
+
 
 class ArraySource(Source):
     """Examples held in (possibly memory-mapped) numpy arrays."""
@@ -75,6 +83,12 @@ class ArraySource(Source):
     def get_batch(self, indices: np.ndarray) -> Batch:
         idx = np.asarray(indices)
         return {"image": self.images[idx], "label": self.labels[idx].astype(np.int64)}
+
+    def gather_plan(self, indices: np.ndarray):
+        if not (isinstance(self.images, np.ndarray) and self.images.flags.c_contiguous):
+            return None
+        idx = np.asarray(indices, dtype=np.int64)
+        return self.images, idx, self.labels[idx].astype(np.int64)
 
     @property
     def image_shape(self):
@@ -152,8 +166,17 @@ class SyntheticSource(Source):
         idx = np.asarray(indices, dtype=np.int64)
         if idx.size and (idx.min() < 0 or idx.max() >= self.num_examples):
             raise IndexError("synthetic index out of range")
-        pick = _mix64(idx.astype(np.uint64) ^ np.uint64(0xA5A5A5A5)) % np.uint64(len(self.pool))
-        return {"image": self.pool[pick.astype(np.int64)], "label": self.labels_for(idx)}
+        return {"image": self.pool[self._pick(idx)], "label": self.labels_for(idx)}
+
+    def _pick(self, idx: np.ndarray) -> np.ndarray:
+        h = _mix64(idx.astype(np.uint64) ^ np.uint64(0xA5A5A5A5)) % np.uint64(len(self.pool))
+        return h.astype(np.int64)
+
+    def gather_plan(self, indices: np.ndarray):
+        idx = np.asarray(indices, dtype=np.int64)
+        if idx.size and (idx.min() < 0 or idx.max() >= self.num_examples):
+            raise IndexError("synthetic index out of range")
+        return self.pool, self._pick(idx), self.labels_for(idx)
 
     @property
     def image_shape(self):
@@ -205,6 +228,9 @@ class _SubsetSource(Source):
 
     def get_batch(self, indices: np.ndarray) -> Batch:
         return self.inner.get_batch(np.asarray(indices) + self.lo)
+
+    def gather_plan(self, indices: np.ndarray):
+        return self.inner.gather_plan(np.asarray(indices, dtype=np.int64) + self.lo)
 
     @property
     def image_shape(self):

@@ -15,6 +15,9 @@ Design (MI355X-first):
   stream** and published with an event; the compute stream waits on the
   event only when it consumes the batch, so the copy of batch *i+1* overlaps
   compute on batch *i* (double/triple buffering);
+* slots are recycled through an event-carrying free list: the consumer never
+  blocks on a copy — the producer thread waits for a slot's last copy event
+  before it refills that slot;
 * ``device_pool`` mode keeps a few batches resident on the GPU and cycles
   them — the benchmark mode for synthetic data (zero host work per step).
 """
@@ -88,11 +91,13 @@ class DeviceLoader:
 
     def __init__(self, source: Source, batch_size: int, device: torch.device,
                  shuffle: bool = True, seed: int = 0, rank: int = 0, world: int = 1,
-                 slots: int = 3, device_pool: int = 0, start_step: int = 0):
+                 slots: int = 4, device_pool: int = 0, start_step: int = 0,
+                 gather_threads: int = 8):
         self.source, self.batch_size, self.device = source, batch_size, torch.device(device)
         self.sampler = IndexSampler(len(source), batch_size, shuffle, seed, rank, world)
         self.steps_per_epoch = self.sampler.steps_per_epoch
-        self.slots, self.device_pool = max(2, slots), device_pool
+        self.slots, self.device_pool = max(3, slots), device_pool
+        self.gather_threads = gather_threads
         self._start_step = start_step
         self._pool = None
         self._thread: Optional[threading.Thread] = None
@@ -112,23 +117,30 @@ class DeviceLoader:
 
     # -- streaming path ----------------------------------------------------- #
 
-    def _producer(self, free_q: "queue.Queue[int]", full_q: "queue.Queue", pinned, idx_iter):
+    def _producer(self, free_q: "queue.Queue", full_q: "queue.Queue", pinned, idx_iter):
         native = _native_ring()
         try:
             while not self._stop.is_set():
-                slot = free_q.get()
-                if slot < 0:
+                item = free_q.get()
+                if item is None:
                     break
+                slot, copied = item
+                if copied is not None:
+                    # the slot's previous H2D copy must have landed before it
+                    # is overwritten (waits in this thread, not the consumer)
+                    copied.synchronize()
                 idx = next(idx_iter)
-                host = self.source.get_batch(idx) if native is None or not hasattr(
-                    self.source, "images") else None
-                if host is None:
-                    # Native multi-threaded gather of whole rows into pinned memory.
+                plan = self.source.gather_plan(idx) if native is not None else None
+                if plan is not None:
+                    # native multi-threaded gather of whole rows into pinned memory
                     from zookeeper_amd.ops import _native
 
-                    _native.gather_rows(self.source.images, idx, pinned[slot]["image"])
-                    pinned[slot]["label"].numpy()[:] = self.source.labels[idx]
+                    rows, row_idx, labels = plan
+                    _native.gather_rows(rows, row_idx, pinned[slot]["image"],
+                                        threads=self.gather_threads)
+                    pinned[slot]["label"].numpy()[:] = labels
                 else:
+                    host = self.source.get_batch(idx)
                     for k, v in host.items():
                         pinned[slot][k].numpy()[...] = v
                 full_q.put(slot)
@@ -154,23 +166,24 @@ class DeviceLoader:
                                 dtype=torch.from_numpy(v[:1]).dtype, pin_memory=use_pin)
                 slot[k] = t
             pinned.append(slot)
-        free_q: "queue.Queue[int]" = queue.Queue()
+        free_q: "queue.Queue" = queue.Queue()
         full_q: "queue.Queue" = queue.Queue()
         self._free_q = free_q
         for s in range(self.slots):
-            free_q.put(s)
+            free_q.put((s, None))
         idx_iter = self.sampler.batches(self._start_step)
+        self._stop.clear()
         self._thread = threading.Thread(
             target=self._producer, args=(free_q, full_q, pinned, idx_iter), daemon=True
         )
         self._thread.start()
 
         copy_stream = torch.cuda.Stream(self.device) if use_pin else None
+        ahead = max(1, self.slots - 2)  # H2D copies kept in flight ahead of the consumer
         in_flight: list = []  # (slot, device batch, event)
         try:
             while True:
-                # Keep up to 2 H2D copies in flight ahead of the consumer.
-                while len(in_flight) < 2:
+                while len(in_flight) < ahead:
                     item = full_q.get()
                     if isinstance(item, Exception):
                         raise item
@@ -187,12 +200,14 @@ class DeviceLoader:
                     in_flight.append((slot, dev, ev))
                 slot, dev, ev = in_flight.pop(0)
                 if ev is not None:
-                    torch.cuda.current_stream(self.device).wait_event(ev)
+                    # the compute stream (not the host) waits for the copy
+                    cur = torch.cuda.current_stream(self.device)
+                    cur.wait_event(ev)
                     for v in dev.values():
-                        v.record_stream(torch.cuda.current_stream(self.device))
-                    # The pinned slot may be refilled once the copy has landed.
-                    ev.synchronize()
-                free_q.put(slot)
+                        v.record_stream(cur)
+                # recycled through the free list with its copy event: the
+                # producer thread waits on it before refilling the slot
+                free_q.put((slot, ev))
                 yield dev
         finally:
             self.close()
@@ -202,7 +217,7 @@ class DeviceLoader:
         self._stop.set()
         q = getattr(self, "_free_q", None)
         if q is not None:
-            q.put(-1)
+            q.put(None)
         if self._thread is not None and self._thread.is_alive():
             self._thread.join(timeout=10)
         self._thread = None

@@ -6,14 +6,29 @@ Mechanism:
   order (:class:`~zookeeper_amd.parallel.flat.FlatParams`);
 * the buffer is cut into contiguous **buckets** (``bucket_mb``, the first —
   holding the last layers — kept small so communication starts early);
-* a ``post_accumulate_grad`` hook on every parameter counts arrivals; when a
-  bucket's last gradient lands, its range is all-reduced asynchronously.
-  With the ``nccl`` (= RCCL) backend the collective runs on RCCL's own HIP
-  stream, ordered after the producing backward kernels by an event, so it
-  overlaps the rest of backward on the compute stream;
-* :meth:`finish` waits for the outstanding work before the optimizer reads
-  the buffer.  The ``1/world`` averaging is folded into the optimizer's
-  gradient scale (no extra pass over the gradients).
+* a ``post_accumulate_grad`` hook on every parameter (and the ``grad_ready``
+  callback of the fused kernels that write gradients in place) counts
+  arrivals; when a bucket's last gradient lands, its range is all-reduced
+  asynchronously.
+
+Stream ordering is explicit and backend-independent (no host
+synchronisation anywhere on the GPU path):
+
+* at bucket-ready an event is recorded on the **compute** stream;
+* a dedicated **comm** HIP stream waits on that event and issues the
+  collective under itself (``torch.distributed`` — backend ``"nccl"`` is
+  RCCL — orders its internal stream after the comm stream; gloo's CUDA work
+  orders its staging copies the same way);
+* :meth:`GradBucketer.finish` makes the comm stream wait on every
+  outstanding work, then the compute stream waits on the comm stream once,
+  before the optimizer reads the buffer.  The ``1/world`` averaging is folded
+  into the optimizer's gradient scale (no extra pass over the gradients).
+
+With ``timing=True`` each bucket's collective is bracketed by timing events
+on the comm stream, and an event marks the end of backward on the compute
+stream; :meth:`GradBucketer.pop_timings` returns per step the comm span, the
+sum of per-bucket times and the **exposed** communication (how long the last
+collective ran past the end of backward).
 
 xGMI sizing: on MI355X every GPU has 7 point-to-point links of ≈153 GB/s, a
 ring uses one link per hop, so a bucket of S bytes costs ≈ 2·(N-1)/N · S /
@@ -24,7 +39,11 @@ far below the backward pass they hide under.
 
 from __future__ import annotations
 
-from typing import List, Optional
+import contextlib
+import os
+import queue
+import threading
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -34,7 +53,8 @@ from zookeeper_amd.parallel.flat import FlatParams
 
 class GradBucketer:
     def __init__(self, flat: FlatParams, world: int, bucket_mb: float = 25.0,
-                 first_bucket_mb: float = 1.0, group=None, grad_dtype: Optional[torch.dtype] = None):
+                 first_bucket_mb: float = 1.0, group=None, grad_dtype: Optional[torch.dtype] = None,
+                 timing: bool = False):
         self.flat, self.world, self.group = flat, world, group
         self.grad_dtype = grad_dtype
         limit0 = int(first_bucket_mb * 2**20 / 4)
@@ -66,12 +86,25 @@ class GradBucketer:
         self._launched = [False] * len(buckets)
         self._hooks = []
         self._seen = [False] * len(flat.slots)
+        self._suspended = False
         self.enabled = world > 1
-        # gloo on GPU tensors (tests, 1-GPU rehearsals) stages through host
-        # copies on its own streams; order them with a host sync instead of
-        # relying on its stream events (RCCL orders on the device).
-        self._host_sync = (self.enabled and flat.grad.is_cuda
-                           and dist.get_backend(group) != "nccl")
+        self.cuda = flat.grad.is_cuda
+        self.comm_stream = torch.cuda.Stream(flat.grad.device) if (self.enabled and self.cuda) else None
+        self.timing = bool(timing) and self.comm_stream is not None
+        # diagnostics only: ZK_COMM_HOST_SYNC=1 synchronises the device before
+        # each collective and after the last (isolates stream-ordering bugs)
+        hs = os.environ.get("ZK_COMM_HOST_SYNC", "0") if self.cuda else "0"
+        self._sync_launch = hs in ("1", "launch")
+        self._sync_finish = hs in ("1", "finish")
+        self._step_events: Optional[Dict] = None
+        self._timings: List[Dict] = []
+        # gloo with GPU tensors (rehearsals on one GPU): explicit host
+        # staging instead of handing device tensors to gloo (its internal
+        # staging streams raced with the compute stream on this ROCm build,
+        # tools/dp_order_diag.py)
+        self._stager = None
+        if self.enabled and self.cuda and dist.get_backend(group) != "nccl":
+            self._stager = _HostStager(flat.total, group)
         if self.enabled:
             for i, s in enumerate(flat.slots):
                 hook = self._make_hook(i)
@@ -84,9 +117,22 @@ class GradBucketer:
     def num_buckets(self) -> int:
         return len(self.buckets)
 
+    @contextlib.contextmanager
+    def suspended(self):
+        """Ignore readiness signals (HIP-graph capture of forward+backward:
+        the collectives are issued eagerly after the replay instead)."""
+        old = self._suspended
+        self._suspended = True
+        try:
+            yield
+        finally:
+            self._suspended = old
+            self._seen = [False] * len(self.flat.slots)
+            self._pending = [len(b) for b in self.buckets]
+
     def _make_hook(self, slot_index: int):
         def hook(_param):
-            if self._seen[slot_index]:
+            if self._suspended or self._seen[slot_index]:
                 return
             self._seen[slot_index] = True
             b = self.slot_bucket[slot_index]
@@ -96,36 +142,105 @@ class GradBucketer:
 
         return hook
 
+    def _events(self) -> Dict:
+        if self._step_events is None:
+            mk = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+            self._step_events = {"start": {}, "end": {}, "bwd_end": mk(), "mk": mk}
+        return self._step_events
+
     def _launch(self, b: int) -> None:
         lo, hi = self.ranges[b]
         view = self.flat.grad[lo:hi]
-        if self._host_sync:
-            torch.cuda.current_stream(view.device).synchronize()
-        if self.grad_dtype is not None and self.grad_dtype != view.dtype:
-            tmp = view.to(self.grad_dtype)
-            work = dist.all_reduce(tmp, group=self.group, async_op=True)
-            self._works.append((work, view, tmp))
-        else:
-            self._works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
+        if self.comm_stream is None:  # CPU tensors (gloo): plain async collective
+            self._works.append((self._issue(view), view, b))
+            self._launched[b] = True
+            return
+        if self._sync_launch:
+            torch.cuda.synchronize(view.device)
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(view.device))
+        self.comm_stream.wait_event(ready)
+        with torch.cuda.stream(self.comm_stream):
+            if self.timing:
+                ev = self._events()
+                ev["start"][b] = ev["mk"]()
+                ev["start"][b].record(self.comm_stream)
+            if self._stager is not None:
+                self._works.append((self._stager.submit(b, lo, hi, view, self.comm_stream),
+                                    view, b))
+            else:
+                self._works.append((self._issue(view), view, b))
         self._launched[b] = True
 
-    def finish(self) -> None:
-        """Launch any bucket whose hooks did not fire (unused params) and wait."""
+    def _issue(self, view: torch.Tensor):
+        if self.grad_dtype is not None and self.grad_dtype != view.dtype:
+            tmp = view.to(self.grad_dtype)
+            return (dist.all_reduce(tmp, group=self.group, async_op=True), tmp)
+        return (dist.all_reduce(view, group=self.group, async_op=True), None)
+
+    def launch_all(self) -> None:
+        """Issue every bucket not yet launched (after a graph replay, or for
+        parameters whose hooks never fired)."""
         if not self.enabled:
             return
         for b, done in enumerate(self._launched):
             if not done:
                 self._launch(b)
-        for work, view, tmp in self._works:
-            work.wait()
-            if view is not None:
-                view.copy_(tmp)
-        if self._host_sync:
-            torch.cuda.synchronize(self.flat.grad.device)
+
+    def finish(self) -> None:
+        """Launch any bucket whose hooks did not fire (unused params) and make
+        the compute stream wait for every collective."""
+        if not self.enabled:
+            return
+        if self.timing:
+            self._events()["bwd_end"].record(torch.cuda.current_stream(self.flat.grad.device))
+        self.launch_all()
+        if self.comm_stream is None:
+            for (work, tmp), view, _ in self._works:
+                work.wait()
+                if tmp is not None:
+                    view.copy_(tmp)
+        else:
+            with torch.cuda.stream(self.comm_stream):
+                for (work, tmp), view, b in self._works:
+                    work.wait()  # comm stream waits on the collective's stream
+                    if tmp is not None:
+                        view.copy_(tmp, non_blocking=True)
+                    if self.timing:
+                        ev = self._events()
+                        ev["end"][b] = ev["mk"]()
+                        ev["end"][b].record(self.comm_stream)
+            torch.cuda.current_stream(self.flat.grad.device).wait_stream(self.comm_stream)
+            if self._sync_finish:
+                torch.cuda.synchronize(self.flat.grad.device)
+        if self.timing and self._step_events is not None:
+            self._timings.append(self._step_events)
+            self._step_events = None
         self._works.clear()
         self._pending = [len(b) for b in self.buckets]
         self._launched = [False] * len(self.buckets)
         self._seen = [False] * len(self.flat.slots)
+
+    def pop_timings(self) -> List[Dict[str, float]]:
+        """Per recorded step: ``comm_ms`` (first collective start → last end),
+        ``bucket_sum_ms`` and ``exposed_ms`` (last end − backward end, ≥0).
+        Synchronises on the recorded events; call outside timed regions."""
+        out = []
+        for ev in self._timings:
+            starts, ends = ev["start"], ev["end"]
+            if not ends:
+                continue
+            for e in ends.values():
+                e.synchronize()
+            first = min(starts.values(), key=lambda e: ev["bwd_end"].elapsed_time(e))
+            last = max(ends.values(), key=lambda e: ev["bwd_end"].elapsed_time(e))
+            out.append({
+                "comm_ms": first.elapsed_time(last),
+                "bucket_sum_ms": sum(starts[b].elapsed_time(ends[b]) for b in ends if b in starts),
+                "exposed_ms": max(0.0, ev["bwd_end"].elapsed_time(last)),
+            })
+        self._timings.clear()
+        return out
 
     def remove(self) -> None:
         for h in self._hooks:
@@ -134,6 +249,57 @@ class GradBucketer:
         for s in self.flat.slots:
             if hasattr(s.param, "_zk_grad_ready"):
                 del s.param._zk_grad_ready
+
+
+class _StagedWork:
+    def __init__(self, done: threading.Event, box: list):
+        self.done, self.box = done, box
+
+    def wait(self):
+        self.done.wait()
+        if self.box:
+            raise self.box[0]
+
+
+class _HostStager:
+    """gloo all-reduce of GPU gradient ranges through a pinned host mirror.
+
+    On the comm stream: D2H of the range into the mirror (after the
+    bucket-ready event), then an event.  A worker thread waits for that
+    event (the compute stream never blocks), all-reduces the host range over
+    gloo — one thread, so every rank issues the collectives in the same
+    bucket order — and signals.  :meth:`GradBucketer.finish` then copies the
+    result back H2D on the comm stream, which the compute stream waits on.
+    The mirror range is reused next step only after this H2D (same stream)."""
+
+    def __init__(self, total: int, group):
+        self.host = torch.empty(total, dtype=torch.float32, pin_memory=True)
+        self.group = group
+        self.q: "queue.Queue" = queue.Queue()
+        self.thread = threading.Thread(target=self._run, daemon=True)
+        self.thread.start()
+
+    def _run(self):
+        while True:
+            item = self.q.get()
+            if item is None:
+                return
+            lo, hi, ev, done, box = item
+            try:
+                ev.synchronize()
+                dist.all_reduce(self.host[lo:hi], group=self.group)
+            except Exception as e:  # surfaced by wait()
+                box.append(e)
+            done.set()
+
+    def submit(self, b: int, lo: int, hi: int, view: torch.Tensor, stream) -> tuple:
+        host = self.host[lo:hi]
+        host.copy_(view, non_blocking=True)  # on the comm stream (current)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        done, box = threading.Event(), []
+        self.q.put((lo, hi, ev, done, box))
+        return _StagedWork(done, box), host
 
 
 def broadcast_module(module: torch.nn.Module, src: int = 0, group=None) -> None:
@@ -146,14 +312,25 @@ def broadcast_module(module: torch.nn.Module, src: int = 0, group=None) -> None:
 
 
 def all_reduce_buffers(module: torch.nn.Module, group=None) -> None:
-    """Average floating-point buffers (BN running statistics) across ranks."""
+    """Average the floating-point buffers (BN running statistics) across
+    ranks with ONE coalesced all-reduce.  Called before evaluation and before
+    every checkpoint so eval and the saved model use the cross-rank mean
+    (each rank's statistics otherwise drift apart after the initial
+    broadcast)."""
     if not (dist.is_available() and dist.is_initialized()):
         return
     world = dist.get_world_size(group)
     if world == 1:
         return
+    bufs = [b for b in module.buffers() if b.is_floating_point()]
+    if not bufs:
+        return
     with torch.no_grad():
-        for b in module.buffers():
-            if b.is_floating_point():
-                dist.all_reduce(b, group=group)
-                b.div_(world)
+        flat = torch.cat([b.detach().reshape(-1).float() for b in bufs])
+        dist.all_reduce(flat, group=group)
+        flat.div_(world)
+        off = 0
+        for b in bufs:
+            n = b.numel()
+            b.copy_(flat[off:off + n].view_as(b))
+            off += n

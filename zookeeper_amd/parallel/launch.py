@@ -56,6 +56,8 @@ def spawn(argv: Sequence[str], nproc: int, env: Optional[Dict[str, str]] = None,
     base["MASTER_PORT"] = str(master_port or free_port())
     base["WORLD_SIZE"] = str(nproc)
     base["LOCAL_WORLD_SIZE"] = str(nproc)
+    # CPU ranks (gloo) would each start one OpenMP thread per core
+    base.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // nproc)))
     procs: List[subprocess.Popen] = []
     files = []
     for r in range(nproc):

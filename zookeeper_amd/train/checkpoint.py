@@ -117,8 +117,26 @@ def load(path: str, model: torch.nn.Module, optimizer=None, rank: int = 0) -> Di
         return json.load(f)
 
 
+def _jsonable(v: Any) -> Any:
+    if v is None or isinstance(v, (bool, int, float, str)):
+        return v
+    if isinstance(v, (list, tuple)):
+        return [_jsonable(x) for x in v]
+    if isinstance(v, dict):
+        return {str(k): _jsonable(x) for k, x in v.items()}
+    return repr(v)
+
+
 def write_config(root: str, task: Any, config: Dict[str, Any]) -> None:
+    """``config.json``: the resolved dotted-key config (``flatten_config``
+    of the task) and the ``str(task)`` tree."""
     os.makedirs(root, exist_ok=True)
     with open(os.path.join(root, "config.json"), "w") as f:
-        json.dump({"config": {k: repr(v) for k, v in config.items()}, "tree": str(task)},
-                  f, indent=2)
+        json.dump({"task": type(task).__name__,
+                   "config": {k: _jsonable(v) for k, v in config.items()},
+                   "tree": str(task)}, f, indent=2)
+
+
+def read_config(root: str) -> Dict[str, Any]:
+    with open(os.path.join(root, "config.json")) as f:
+        return json.load(f)

@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import os
 import time
-from typing import Any, Callable, Optional, Union
+from typing import Any, Callable, Optional, Sequence, Union
 
 import torch
 import torch.nn as nn
@@ -49,6 +49,9 @@ class TrainingExperiment(Experiment):
     ``@task``)."""
 
     loss: Union[str, Callable] = Field("sparse_categorical_crossentropy")
+    # Keras-style metric names (``compile(metrics=...)``,
+    # examples/larq_experiment.py:118,142): accuracy, top5, top<k>, ...
+    metrics: Sequence[str] = Field(lambda: ["accuracy"])
     learning_rate: float = Field(1e-3)
     seed: int = Field(0)
     # None → examples // global batch.
@@ -76,12 +79,15 @@ class TrainingExperiment(Experiment):
         return os.path.join(self.output_dir, type(self).__name__, self.run_id)
 
     def run(self) -> dict:
+        from zookeeper_amd.core.component import flatten_config
         from zookeeper_amd.models.base import summary
         from zookeeper_amd.parallel import dist as zdist
+        from zookeeper_amd.parallel.ddp import all_reduce_buffers
         from zookeeper_amd.train import checkpoint as ckpt
-        from zookeeper_amd.train.metrics import MetricsLogger
+        from zookeeper_amd.train.metrics import MetricsLogger, resolve_metrics
         from zookeeper_amd.train.trainer import Trainer
 
+        logit_metrics = {k: f for k, f in resolve_metrics(self.metrics).items() if f is not None}
         info = zdist.init()
         torch.manual_seed(self.seed)
         if info.is_main:
@@ -96,14 +102,14 @@ class TrainingExperiment(Experiment):
         if info.is_main and self.print_summary:
             print(summary(model), flush=True)
         trainer = Trainer(model, self.loss, base_getattr(self, "optimizer"), info,
-                          bucket_mb=self.bucket_mb)
+                          bucket_mb=self.bucket_mb, metric_fns=logit_metrics)
         trainer.optimizer.total_steps = total_steps
 
         run_dir = self.run_dir()
         start_step = 0
         if run_dir is not None:
             if info.is_main:
-                ckpt.write_config(run_dir, self, {})
+                ckpt.write_config(run_dir, self, flatten_config(self))
             last = ckpt.latest(run_dir) if self.resume else None
             if last is not None:
                 meta = ckpt.load(last, trainer.model, trainer.optimizer, info.rank)
@@ -120,7 +126,7 @@ class TrainingExperiment(Experiment):
                               device_pool=self.device_pool, start_step=start_step)
         metrics = MetricsLogger(info.device,
                                 os.path.join(run_dir, "metrics.jsonl") if run_dir else None,
-                                info.rank, info.world)
+                                info.rank, info.world, metrics=self.metrics)
         it = iter(loader)
         step = start_step
         t_start = time.perf_counter()
@@ -129,17 +135,21 @@ class TrainingExperiment(Experiment):
             batch = next(it)
             x, y = self.preprocessing(batch, training=True)
             loss, correct = trainer.train_step(x, y)
-            metrics.update(loss, correct, x.shape[0])
+            metrics.update(loss, correct, x.shape[0], trainer.last_metrics)
             step += 1
             epoch_end = step % steps_per_epoch == 0
             if step % self.log_every == 0 or epoch_end or step == total_steps:
                 last_rec = metrics.flush(step, {"epoch": step / steps_per_epoch,
                                                 "lr": trainer.optimizer.spec.lr_at(
                                                     step - 1, total_steps)})
-            if run_dir is not None and (
+            save_now = run_dir is not None and (
                 (self.checkpoint_every and step % self.checkpoint_every == 0)
-                or step == total_steps
-            ):
+                or step == total_steps)
+            if save_now or (epoch_end and self.validate):
+                # BN running statistics: cross-rank mean before they are
+                # evaluated or saved (each rank's drift apart otherwise)
+                all_reduce_buffers(trainer.model)
+            if save_now:
                 ckpt.save(run_dir, step, trainer.model, trainer.optimizer, info.rank,
                           {"epoch": step / steps_per_epoch, "world": info.world},
                           keep=self.keep_checkpoints, barrier=zdist.barrier)
@@ -165,20 +175,27 @@ class TrainingExperiment(Experiment):
         loader = DeviceLoader(src, self.batch_size, info.device, shuffle=False,
                               rank=info.rank, world=info.world)
         it = iter(loader)
+        from zookeeper_amd.train.metrics import resolve_metrics
+
+        keys = list(resolve_metrics(self.metrics))
         tot_loss = torch.zeros((), device=info.device)
-        tot_hits = torch.zeros((), device=info.device)
+        tot_hits = {k: torch.zeros((), device=info.device) for k in keys}
         for _ in range(steps):
             batch = next(it)
             x, y = self.preprocessing(batch, training=False)
             loss, hits = trainer.eval_step(x, y)
             tot_loss += loss.float()
-            tot_hits += hits.float()
+            for k in keys:
+                tot_hits[k] += (trainer.last_metrics[k] if k in trainer.last_metrics
+                                else hits).float()
         loader.close()
-        vals = torch.stack([tot_loss, tot_hits]).double()
+        vals = torch.stack([tot_loss] + [tot_hits[k] for k in keys]).double()
         if info.world > 1:
             import torch.distributed as dist
 
             dist.all_reduce(vals)
-        loss_sum, hits = vals.tolist()
-        return {"val_loss": loss_sum / (steps * info.world),
-                "val_top1": hits / (steps * self.batch_size * info.world)}
+        vals = vals.tolist()
+        out = {"val_loss": vals[0] / (steps * info.world)}
+        for k, v in zip(keys, vals[1:]):
+            out[f"val_{k}"] = v / (steps * self.batch_size * info.world)
+        return out

@@ -38,12 +38,17 @@ class Trainer:
     def __init__(self, model: nn.Module, loss, optimizer: OptimizerSpec,
                  info: Optional[zdist.DistInfo] = None, bucket_mb: float = 25.0,
                  first_bucket_mb: float = 1.0, grad_dtype: Optional[torch.dtype] = None,
-                 graph: Union[bool, str] = False, graph_warmup: int = 3):
+                 graph: Union[bool, str] = False, graph_warmup: int = 3,
+                 comm_timing: bool = False, metric_fns: Optional[dict] = None):
         self.info = info or zdist.info()
         self.device = self.info.device
         self.model = prepare_model(model, self.device)
         self.model.train()
         self.loss_fn: Callable = get_loss(loss)
+        # metrics that need the logits (top-k): device hit counts per step,
+        # exposed as ``last_metrics`` (graph mode: static graph outputs)
+        self.metric_fns = dict(metric_fns or {})
+        self.last_metrics: dict = {}
         self.flat = FlatParams(self.model, self.device)
         if self.info.world > 1:
             # One broadcast of the flat parameter buffer + the BN buffers.
@@ -51,20 +56,25 @@ class Trainer:
             for b in self.model.buffers():
                 zdist.broadcast_(b)
         self.bucketer = GradBucketer(self.flat, self.info.world, bucket_mb, first_bucket_mb,
-                                     grad_dtype=grad_dtype)
+                                     grad_dtype=grad_dtype, timing=comm_timing)
         self.optimizer = optimizer.create(self.flat, grad_scale=1.0 / self.info.world)
-        # HIP-graph replay of zero-grad + forward + loss + backward (single
-        # process): one graph launch instead of ~300 kernel launches and the
-        # Python / autograd work behind them.  The optimizer (host-side step
-        # count and learning-rate schedule) runs eagerly after each replay.
+        # HIP-graph replay of zero-grad + forward + loss + backward: one graph
+        # launch instead of ~300 kernel launches and the Python / autograd
+        # work behind them.  The optimizer (host-side step count and
+        # learning-rate schedule) runs eagerly after each replay.  Under data
+        # parallelism the collectives stay OUTSIDE the graph: readiness
+        # signals are ignored during capture and every bucket is all-reduced
+        # on the comm stream right after the replay (no overlap with
+        # backward, but no host enqueue cost either — the trade is only worth
+        # it when the step is host-bound).
         # ``graph="auto"`` decides on the last warmup step: replay only when
         # the host cannot enqueue a step faster than the GPU runs it (small
         # per-GPU batches); a GPU-bound step keeps the eager path, whose
-        # side-stream weight gradients overlap better than the replayed graph.
+        # side-stream weight gradients and overlapped all-reduce win.
         auto = isinstance(graph, str) and graph == "auto"
         if isinstance(graph, str) and not auto:
             raise ValueError(f"graph must be a bool or 'auto', got {graph!r}")
-        self.graph = (auto or bool(graph)) and self.device.type == "cuda" and self.info.world == 1
+        self.graph = (auto or bool(graph)) and self.device.type == "cuda"
         self._graph_auto = auto and self.graph
         self.graph_probe: Optional[Tuple[float, float]] = None  # (host s, GPU s) of the probe
         self.graph_warmup = max(1, graph_warmup)
@@ -77,6 +87,9 @@ class Trainer:
         self.flat.zero_grad()
         logits = self.model(x)
         loss, correct = self.loss_fn(logits, y)
+        if self.metric_fns:
+            with torch.no_grad():
+                self.last_metrics = {k: f(logits.detach(), y) for k, f in self.metric_fns.items()}
         # binary-conv weight gradients on a side stream, ordered by events
         with streams.session(self.device):
             loss.backward()
@@ -110,12 +123,13 @@ class Trainer:
         if self._graph is None:
             self._static_in = (x.clone(), y.clone())  # clone keeps x's channels_last strides
             self._graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._graph):
+            with self.bucketer.suspended(), torch.cuda.graph(self._graph):
                 self._static_out = self._forward_backward(*self._static_in)
         else:
             self._static_in[0].copy_(x)
             self._static_in[1].copy_(y)
         self._graph.replay()
+        self.bucketer.finish()  # DP: all buckets all-reduced after the replay
         self.optimizer.step()
         return self._static_out
 
@@ -125,6 +139,8 @@ class Trainer:
         self.model.eval()
         try:
             logits = self.model(x)
+            if self.metric_fns:
+                self.last_metrics = {k: f(logits, y) for k, f in self.metric_fns.items()}
             return self.loss_fn(logits, y)
         finally:
             self.model.train(was)
