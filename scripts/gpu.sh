@@ -9,6 +9,10 @@
 #   bench[:model[:batch[:steps]]]      bench.py on 1 GPU (default E18 b512 60 steps)
 #   stream[:model]   bench.py --data stream (pinned ring + side-stream H2D)
 #   prof[:model[:batch]]               rocprofv3 --kernel-trace --stats of bench.py
+#   pmc[:model]      three rocprofv3 PMC passes over 2 training steps (SQ MFMA/LDS,
+#                    FETCH_SIZE, WRITE_SIZE; one counter group per run)
+#   pmcconv:op:shape PMC passes over one conv kernel (tools/one_conv.py), e.g.
+#                    pmcconv:dgrad:56,56,64,64,1
 #   tune[:args]      tools/tune_bconv.py with the given (comma-separated) args
 #   py:<module>      python -m <module>  (tools, one-off diagnostics)
 #   dpgloo:<n>       bench.py with n gloo ranks sharing the GPU (ordering rehearsal)
@@ -19,7 +23,7 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 OUT=gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-PROG="$OUT/progress.txt"
+PROG="$(pwd)/$OUT/progress.txt"
 
 gpu_step() {
   local t=$1; shift
@@ -61,8 +65,30 @@ for spec in "$@"; do
       ;;
     prof)
       gpu_step 600 "$OUT/prof_${n}.log" rocprofv3 --kernel-trace --stats \
-        -d "$OUT/prof_$n" -o run -- python3 bench.py --model "${a1:-BinaryResNetE18}" \
+        -d "$OUT/prof_$n" -o run --output-format csv -- python3 bench.py --model "${a1:-BinaryResNetE18}" \
         --batch "${a2:-512}" --steps 20 --warmup 10 --graph 0 || exit $?
+      ;;
+    pmc)
+      R="$(pwd)"
+      for pass in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS" \
+                  "FETCH_SIZE" "WRITE_SIZE"; do
+        tag=$(echo "$pass" | cut -d' ' -f1)
+        (cd /tmp && gpu_step 150 "$R/$OUT/pmc_${n}_${tag}.log" timeout -s KILL 140 rocprofv3 --pmc $pass \
+          -d "$R/$OUT/pmc_${n}_${tag}" -o run --output-format csv -- python3 "$R/bench.py" \
+          --model "${a1:-BinaryResNetE18}" --steps 2 --warmup 2 --graph 0) || exit $?
+      done
+      ;;
+    pmcconv)
+      R="$(pwd)"
+      nm="${a1}_${a2//,/_}"
+      gpu_step 120 "$OUT/pmcconv_${nm}_time.log" python tools/one_conv.py --op "$a1" --shape "$a2" --reps 50 || exit $?
+      for pass in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT" \
+                  "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"; do
+        tag=$(echo "$pass" | cut -d' ' -f1)
+        (cd /tmp && gpu_step 90 "$R/$OUT/pmcconv_${nm}_${tag}.log" timeout -s KILL 80 rocprofv3 --pmc $pass \
+          -d "$R/$OUT/pmcconv_${nm}_${tag}" -o run --output-format csv -- python3 "$R/tools/one_conv.py" \
+          --op "$a1" --shape "$a2" --reps 5) || exit $?
+      done
       ;;
     tune)
       gpu_step 600 "$OUT/tune_${n}.log" python -u tools/tune_bconv.py ${a1//,/ } || exit $?

@@ -1,11 +1,26 @@
 """MFMA dgrad / wgrad kernels of the binary conv vs fp64 references (the ±1
 operand is exact; dy is bf16, so errors come only from fp32 accumulation)."""
 
+import os
+import sys
+
 import pytest
 import torch
 import torch.nn.functional as F
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import tile_support as ts  # noqa: E402
+
 pytestmark = pytest.mark.gpu
+
+# (variant, shape) pairs generated at collection: only those the launcher
+# accepts (tests/test_tile_support.py pins the rule to the native queries)
+DGRAD_SHAPES = [(64, 64, 1, 12), (64, 128, 2, 12), (128, 128, 1, 7), (256, 512, 2, 8),
+                (128, 64, 1, 9), (128, 256, 2, 15), (64, 64, 1, 28), (256, 256, 1, 6)]
+WGRAD_SHAPES = [(64, 64, 1, 12, 0), (64, 128, 2, 12, 0), (128, 128, 1, 7, 1), (256, 512, 2, 8, 0),
+                (128, 64, 1, 9, 1), (64, 192, 1, 5, 1), (64, 64, 1, 28, 1), (128, 256, 1, 14, 0)]
+FWD_SHAPES = [(64, 64, 1, 12, 0, 0), (64, 128, 2, 12, 0, 1), (128, 128, 1, 7, 1, 1),
+              (256, 512, 2, 8, 0, 0), (128, 64, 1, 9, 1, 0), (512, 128, 1, 5, 0, 1)]
 
 
 @pytest.fixture(autouse=True)
@@ -68,10 +83,7 @@ def test_dgrad_wgrad(cin, cout, stride, hw, pad_ones):
     assert err_dw <= 1e-4 * ref_dw.abs().max().item() + 1e-3, err_dw
 
 
-@pytest.mark.parametrize("variant", list(range(15)) + list(range(20, 35)))
-@pytest.mark.parametrize("cin,cout,stride,hw", [
-    (64, 64, 1, 12), (64, 128, 2, 12), (128, 128, 1, 7), (256, 512, 2, 8), (128, 64, 1, 9),
-    (128, 256, 2, 15), (64, 64, 1, 28)])
+@pytest.mark.parametrize("variant,cin,cout,stride,hw", ts.pairs(ts.dgrad_ok, ts.DGRAD, DGRAD_SHAPES))
 def test_igemm_dgrad_matches_reference(variant, cin, cout, stride, hw):
     """LDS-DMA ring implicit-GEMM dgrad (igemm.hip), every tile variant, vs
     the fp64 ±1 conv gradient (STE mask + residual gradient fused)."""
@@ -104,11 +116,7 @@ def test_igemm_dgrad_matches_reference(variant, cin, cout, stride, hw):
     rc = L.zk_igemm_dgrad(dy.data_ptr(), wt.data_ptr(), mask.data_ptr(), dres.data_ptr(),
                           dx.data_ptr(), B, hw, hw, cin, ho, ho, cout, 3, 3, stride, pt, pt,
                           variant, st)
-    if rc != 0:
-        # 256-wide tiles need Cin % 256; conv3 (20+) needs stride 1
-        assert cin % 128 != 0 or variant in (3, 12, 13, 14, 25) or variant >= 20, \
-            f"variant {variant} rejected a supported shape"
-        pytest.skip("tile does not divide Cin")
+    assert rc == 0, f"variant {variant} rejected a supported shape"
     torch.cuda.synchronize()
     xs = sign_pm1(x.double()).permute(0, 3, 1, 2).requires_grad_(True)
     ws = sign_pm1(w.double()).permute(0, 3, 1, 2)
@@ -120,10 +128,8 @@ def test_igemm_dgrad_matches_reference(variant, cin, cout, stride, hw):
 
 
 @pytest.mark.parametrize("slab", [False, True])
-@pytest.mark.parametrize("variant", list(range(13)) + list(range(20, 35)))
-@pytest.mark.parametrize("cin,cout,stride,hw,pad_ones", [
-    (64, 64, 1, 12, 0), (64, 128, 2, 12, 0), (128, 128, 1, 7, 1), (256, 512, 2, 8, 0),
-    (128, 64, 1, 9, 1), (64, 192, 1, 5, 1), (64, 64, 1, 28, 1), (128, 256, 1, 14, 0)])
+@pytest.mark.parametrize("variant,cin,cout,stride,hw,pad_ones",
+                         ts.pairs(ts.wgrad_ok, ts.WGRAD, WGRAD_SHAPES))
 def test_igemm_wgrad_matches_reference(variant, cin, cout, stride, hw, pad_ones, slab):
     """LDS-DMA ring implicit-GEMM wgrad (igemm.hip) on the bf16 sign(x)
     image, every tile variant (20+: the conv3 kernel, all taps of a kernel
@@ -152,15 +158,13 @@ def test_igemm_wgrad_matches_reference(variant, cin, cout, stride, hw, pad_ones,
     if slab:
         nbytes = L.zk_igemm_wgrad_ws_bytes(B, cin, hw, hw, ho, ho, cout, 3, 3, stride, pt, pt,
                                             256, variant)
-        if nbytes <= 0:
-            pytest.skip("tile does not divide this shape")
+        assert nbytes > 0, f"variant {variant} rejected a supported shape"
         ws = torch.empty(nbytes // 4, device="cuda")
     rc = L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w.data_ptr(), dw.data_ptr(), B, hw, hw,
                           cin, ho, ho, cout, 3, 3, stride, pt, pt, pad_ones, 1.0, 256, variant,
                           ws.data_ptr() if ws is not None else None,
                           ws.numel() * 4 if ws is not None else 0, st)
-    if rc != 0:
-        pytest.skip("tile does not divide this shape")
+    assert rc == 0, f"variant {variant} rejected a supported shape"
     torch.cuda.synchronize()
     xs = sign_pm1(x.double()).permute(0, 3, 1, 2)
     wsgn = sign_pm1(w.double()).permute(0, 3, 1, 2).requires_grad_(True)
@@ -171,10 +175,8 @@ def test_igemm_wgrad_matches_reference(variant, cin, cout, stride, hw, pad_ones,
     assert err <= 1e-4 * ref.abs().max().item() + 1e-3, err
 
 
-@pytest.mark.parametrize("variant", list(range(15)) + list(range(20, 28)))
-@pytest.mark.parametrize("cin,cout,stride,hw,pad_ones,relu", [
-    (64, 64, 1, 12, 0, 0), (64, 128, 2, 12, 0, 1), (128, 128, 1, 7, 1, 1),
-    (256, 512, 2, 8, 0, 0), (128, 64, 1, 9, 1, 0), (512, 128, 1, 5, 0, 1)])
+@pytest.mark.parametrize("variant,cin,cout,stride,hw,pad_ones,relu",
+                         ts.pairs(ts.fwd_ok, ts.FWD, FWD_SHAPES))
 def test_igemm_fwd_matches_reference(variant, cin, cout, stride, hw, pad_ones, relu):
     """MFMA forward (igemm.hip) on the sign image: exact int16 output and
     exact int64 (sum, sum of squares) per channel, every tile variant."""
@@ -200,8 +202,7 @@ def test_igemm_fwd_matches_reference(variant, cin, cout, stride, hw, pad_ones, r
     stats = torch.zeros(2, cout, dtype=torch.int64, device="cuda")
     rc = L.zk_igemm_fwd(sx.data_ptr(), wf.data_ptr(), y.data_ptr(), stats.data_ptr(), B, hw, hw,
                         cin, cout, 3, 3, stride, pt, pt, ho, ho, pad_ones, relu, variant, 1, st)
-    if rc != 0:
-        pytest.skip("tile does not divide this shape")
+    assert rc == 0, f"variant {variant} rejected a supported shape"
     torch.cuda.synchronize()
     xs = sign_pm1(x.double()).permute(0, 3, 1, 2)
     ws = sign_pm1(w.double()).permute(0, 3, 1, 2)

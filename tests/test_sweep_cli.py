@@ -169,3 +169,22 @@ def test_cifar10_binarynet_task_runs_on_cpu(tmp_path):
     assert all(r["top5"] >= r["top1"] for r in recs)
     assert "val_top5=" in res.stdout
     assert (run_dir / "checkpoints" / "step_00000003" / "model.pt").exists()
+
+
+@pytest.mark.timeout(600)
+def test_sweep_records_throughput_and_loss(tmp_path):
+    """BASELINE config 5's record: each run of a training sweep reports its
+    images/sec and final loss in sweep.json (via ZK_RESULT_JSON)."""
+    cmd = [sys.executable, os.path.join(ROOT, "examples", "larq_experiment.py"), "BinaryNetCifar10",
+           "epochs=1", "batch_size=8", "steps_per_epoch=2", "print_summary=False", "validate=False",
+           "model.filters=32", "model.dense_units=64", "dataset.num_train_examples=64",
+           "--grid", "learning_rate=[0.001,0.01]"]
+    env = _env(ZK_SWEEP_DIR=str(tmp_path / "sweep"))
+    res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=560)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
+    summary = json.load(open(tmp_path / "sweep" / "sweep.json"))
+    assert sorted(s["name"] for s in summary) == ["learning_rate_0.001", "learning_rate_0.01"]
+    for s in summary:
+        assert s["exit_code"] == 0 and s["steps"] == 2
+        assert s["images_per_sec"] > 0
+        assert s["final_loss"] == s["final_loss"] and s["final_loss"] > 0  # finite

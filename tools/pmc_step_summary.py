@@ -1,5 +1,5 @@
 """Per-kernel PMC summary of a training step from three rocprofv3 --pmc runs
-(scripts/gpu_r1bc.sh): pass 1 SQ counters (MFMA busy, LDS), pass 2
+(scripts/gpu.sh pmc): pass 1 SQ counters (MFMA busy, LDS), pass 2
 FETCH_SIZE, pass 3 WRITE_SIZE.  Only the last ``--last`` dispatches of each
 kernel name are kept (the timed steps, not warmup/MIOpen find trials).
 

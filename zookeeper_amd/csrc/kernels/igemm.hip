@@ -30,6 +30,12 @@
 
 namespace {
 
+// Support queries (zk_igemm_*_supported): every launcher validates the
+// geometry for its tile, then returns 0 WITHOUT launching while this is set.
+// Host-only; lets the test suite enumerate the valid (variant, shape) pairs
+// on a machine without a GPU.
+thread_local bool g_dry_run = false;
+
 struct IGeom {
   int B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl;
 };
@@ -795,6 +801,7 @@ int launch_conv3(const ConvArgs& args, const IGeom& g, hipStream_t stream) {
   const int NCH = FWD ? g.Cout : g.Cin, KCH = FWD ? g.Cin : g.Cout;
   const int RB = F4 ? KCH / 2 : KCH * 2;
   if (RB % CB || NCH % BN || !conv3_ok(g, args.pad_ones)) return (int)hipErrorInvalidValue;
+  if (g_dry_run) return 0;
   constexpr int NW = WM * WN, RPI = 1024 / CB;
   constexpr int AR = (BM + 2 + RPI * NW - 1) / (RPI * NW) * RPI * NW;
   constexpr int BR = (3 * BN + RPI * NW - 1) / (RPI * NW) * RPI * NW;
@@ -829,6 +836,7 @@ int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const v
                        void* dx, const IGeom& g, const BnSum& bs, hipStream_t stream) {
   if ((g.Cout * 2) % CB || g.Cin % BN || g.s > 2 || g.kh > 4 || g.kw > 4)
     return (int)hipErrorInvalidValue;
+  if (g_dry_run) return 0;
   constexpr int LDS = NS * (BM + BN) * CB;
   static_assert(LDS <= 160 * 1024, "LDS");
   auto kern = igemm_conv_kernel<false, BM, BN, WM, WN, NS, CB>;
@@ -857,6 +865,7 @@ int launch_igemm_fwd(const void* sx, const void* wf, void* y, void* stats, const
                      int pad_ones, int relu, int stripes, hipStream_t stream) {
   const int RB = F4 ? g.Cin / 2 : g.Cin * 2;
   if (RB % CB || g.Cout % BN) return (int)hipErrorInvalidValue;
+  if (g_dry_run) return 0;
   constexpr int LDS = NS * (BM + BN) * CB;
   static_assert(LDS <= 160 * 1024, "LDS");
   auto kern = igemm_conv_kernel<true, BM, BN, WM, WN, NS, CB, F4>;
@@ -1592,7 +1601,7 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
   }
   const int rc = igemm_dgrad_variant(variant, dy, wt, mask, dres, dx, g, bs, stream);
   if (rc) return rc;
-  ZK_CHECK_LAUNCH();
+  if (!g_dry_run) ZK_CHECK_LAUNCH();
   return 0;
 }
 }  // namespace
@@ -1678,7 +1687,7 @@ ZK_EXPORT int zk_igemm_wgrad(const void* dy, const void* sx, const void* w, void
   const int rc = igemm_wgrad_variant(variant, dy, sx, w, dw, g, pad_ones, clip, target_blocks,
                                      workspace, ws_bytes, nullptr, stream);
   if (rc) return rc;
-  ZK_CHECK_LAUNCH();
+  if (!g_dry_run) ZK_CHECK_LAUNCH();
   return 0;
 }
 
@@ -1723,7 +1732,7 @@ ZK_EXPORT int zk_igemm_fwd(const void* sx, const void* wf, void* y, void* stats,
   const int rc =
       igemm_fwd_variant(variant, sx, wf, y, stats, g, pad_ones, relu, stat_stripes, stream);
   if (rc) return rc;
-  ZK_CHECK_LAUNCH();
+  if (!g_dry_run) ZK_CHECK_LAUNCH();
   return 0;
 }
 
@@ -1769,6 +1778,34 @@ ZK_EXPORT int zk_igemm_fwd_fp4(const void* sx4, const void* wf4, void* y, void* 
   const int rc =
       igemm_fwd4_variant(variant, sx4, wf4, y, stats, g, pad_ones, relu, stat_stripes, stream);
   if (rc) return rc;
-  ZK_CHECK_LAUNCH();
+  if (!g_dry_run) ZK_CHECK_LAUNCH();
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Support queries: 1 if the tile variant accepts the geometry, 0 if not
+// (nothing is launched; no GPU needed).  variant -1 = the tuned default.
+namespace {
+struct DryRun {
+  DryRun() { g_dry_run = true; }
+  ~DryRun() { g_dry_run = false; }
+};
+}  // namespace
+
+ZK_EXPORT int zk_igemm_dgrad_supported(int B, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                                       int kh, int kw, int stride, int pt, int pl, int variant) {
+  DryRun dr;
+  return zk_igemm_dgrad(nullptr, nullptr, nullptr, nullptr, nullptr, B, H, W, Cin, Ho, Wo, Cout,
+                        kh, kw, stride, pt, pl, variant, nullptr) == 0;
+}
+
+ZK_EXPORT int zk_igemm_fwd_supported(int B, int H, int W, int Cin, int Cout, int kh, int kw,
+                                     int stride, int pt, int pl, int Ho, int Wo, int pad_ones,
+                                     int variant, int fp4) {
+  DryRun dr;
+  if (fp4)
+    return zk_igemm_fwd_fp4(nullptr, nullptr, nullptr, nullptr, B, H, W, Cin, Cout, kh, kw, stride,
+                            pt, pl, Ho, Wo, pad_ones, 0, variant, 1, nullptr) == 0;
+  return zk_igemm_fwd(nullptr, nullptr, nullptr, nullptr, B, H, W, Cin, Cout, kh, kw, stride, pt,
+                      pl, Ho, Wo, pad_ones, 0, variant, 1, nullptr) == 0;
 }

@@ -351,15 +351,36 @@ class HFDataset(SplitDataset):
     label_key: str = Field("label")
 
     def _load_hf(self, split: Optional[str] = None):
+        """The whole dataset (``split=None``) or one split.  ``download=False``
+        loads strictly offline (a ``save_to_disk`` directory under
+        ``data_dir`` or an already-prepared cache): a missing dataset raises
+        instead of being fetched, like TFDS' ``download=False``
+        (zookeeper/tf/dataset.py:119-138)."""
         import datasets as hf
 
+        if "_hf" in self.__dict__:
+            ds = self.__dict__["_hf"]
+            return ds[split] if split is not None else ds
         try:
             if self.data_dir is not None and os.path.isdir(os.path.join(self.data_dir, self.name)):
                 ds = hf.load_from_disk(os.path.join(self.data_dir, self.name))
+                self.__dict__["_hf"] = ds
                 return ds[split] if split is not None else ds
-            mode = None if self.download else "reuse_cache_if_exists"
-            return hf.load_dataset(self.name, split=split, cache_dir=self.data_dir,
-                                   download_mode=mode)
+            if self.download:
+                return hf.load_dataset(self.name, split=split, cache_dir=self.data_dir)
+            old_env = os.environ.get("HF_DATASETS_OFFLINE")
+            old_cfg = getattr(hf.config, "HF_DATASETS_OFFLINE", None)
+            os.environ["HF_DATASETS_OFFLINE"] = "1"
+            hf.config.HF_DATASETS_OFFLINE = True
+            try:
+                return hf.load_dataset(self.name, split=split, cache_dir=self.data_dir,
+                                       download_mode="reuse_cache_if_exists")
+            finally:
+                if old_env is None:
+                    os.environ.pop("HF_DATASETS_OFFLINE", None)
+                else:
+                    os.environ["HF_DATASETS_OFFLINE"] = old_env
+                hf.config.HF_DATASETS_OFFLINE = old_cfg
         except Exception:
             if not self.download:
                 utils.warn(

@@ -16,10 +16,14 @@ repo, which only ships BinaryNet; see SURVEY §2.4:
 convs at 64/128/256/512 channels.
 
 Execution: the ``hip`` backend runs each binary block as ONE fused autograd
-op (:func:`zookeeper_amd.ops.binary_block`): bit-packing of the input signs
-and STE mask, XNOR-popcount implicit-GEMM conv with the BN statistics fused
-into its epilogue, BN-apply + residual add, and a matching fused backward on
-MFMA.  The ``torch`` backend is the pure-PyTorch oracle used by the tests.
+op (:func:`zookeeper_amd.ops.binary_block`): the previous BN epilogue writes
+the input signs as MX-FP4 (e2m1 ±1) nibbles plus the STE mask bits, the
+forward conv is an MX-FP4 MFMA implicit GEMM (``v_mfma_scale_f32_32x32x64_f8f6f4``,
+exact integer outputs; measured faster than the XNOR-popcount kernel, which
+remains as ``zk_bconv_fwd``) with the BN statistics fused into its epilogue,
+then BN-apply + residual add, and a matching fused backward (bf16 MFMA
+dgrad / wgrad, BN backward).  The ``torch`` backend is the pure-PyTorch
+oracle used by the tests.
 """
 
 from __future__ import annotations

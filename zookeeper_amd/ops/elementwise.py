@@ -61,7 +61,7 @@ def fused_optimizer_step(opt, lr: float) -> None:
         t = opt.step_count
         check(lib().zk_adam_step(flat.data.data_ptr(), flat.grad.data_ptr(), opt.m.data_ptr(),
                                  opt.v.data_ptr(), ch.data_ptr(), ch.shape[0], lr, sp.beta_1,
-                                 sp.beta_2, sp.epsilon, sp.weight_decay, 1 - sp.beta_1**t,
+                                 sp.beta_2, sp.eps_effective(t), sp.weight_decay, 1 - sp.beta_1**t,
                                  1 - sp.beta_2**t, opt.grad_scale, st), "zk_adam_step")
     else:
         check(lib().zk_sgd_step(flat.data.data_ptr(), flat.grad.data_ptr(), opt.m.data_ptr(),

@@ -23,8 +23,10 @@ CLI (added to every @task command)::
 * every run gets ``ZK_RUN_ID=<run_name>``, the default ``run_id`` of a
   training experiment, so runs sharing ``output_dir`` checkpoint into their
   own ``<output_dir>/<Task>/<run_name>/``;
-* every run writes ``<sweep_dir>/<run_name>/stdout.log``, and the sweep writes
-  ``<sweep_dir>/sweep.json`` (config, exit code, wall time per run); a failing
+* every run writes ``<sweep_dir>/<run_name>/stdout.log`` and (training
+  experiments, via ``ZK_RESULT_JSON``) ``result.json``; the sweep writes
+  ``<sweep_dir>/sweep.json`` (config, exit code, wall time, images/sec, final
+  loss and validation metrics per run); a failing
   run does not stop the others, the sweep exits non-zero if any run failed.
 
 The parent process never touches the GPU (device counting only reads the
@@ -153,6 +155,7 @@ def run_sweep(base_argv: Sequence[str], axes, gpus_per_run: int = 1,
                 argv.append(f"--nproc={gpus_per_run}")
             rdir = os.path.join(sweep_dir, run.name)
             os.makedirs(rdir, exist_ok=True)
+            e["ZK_RESULT_JSON"] = os.path.abspath(os.path.join(rdir, "result.json"))
             out = open(os.path.join(rdir, "stdout.log"), "w")
             run.start = time.time()
             run.proc = subprocess.Popen(argv, env=e, stdout=out, stderr=subprocess.STDOUT)
@@ -171,13 +174,27 @@ def run_sweep(base_argv: Sequence[str], axes, gpus_per_run: int = 1,
             done.append(run)
             print(f"[sweep] done  {run.name} rc={rc} ({run.end - run.start:.1f}s)", flush=True)
         time.sleep(poll_s)
-    summary = [{"name": r.name, "overrides": {k: repr(v) for k, v in r.overrides.items()},
-                "devices": r.devices, "exit_code": r.code, "wall_s": round(r.end - r.start, 3)}
-               for r in done]
+    summary = []
+    for r in done:
+        rec = {"name": r.name, "overrides": {k: repr(v) for k, v in r.overrides.items()},
+               "devices": r.devices, "exit_code": r.code, "wall_s": round(r.end - r.start, 3)}
+        res = _read_result(os.path.join(sweep_dir, r.name, "result.json"))
+        for key in ("images_per_sec", "final_loss", "steps", "validation"):
+            if key in res:
+                rec[key] = res[key]
+        summary.append(rec)
     with open(os.path.join(sweep_dir, "sweep.json"), "w") as f:
         json.dump(summary, f, indent=2)
     failed = [r for r in done if r.code != 0]
     return 1 if failed else 0
+
+
+def _read_result(path: str) -> Dict[str, Any]:
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
 
 
 def _strip_sweep_args(argv: Sequence[str]) -> List[str]:

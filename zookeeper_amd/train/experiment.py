@@ -160,8 +160,17 @@ class TrainingExperiment(Experiment):
                           " ".join(f"{k}={v:.5g}" for k, v in val.items()), flush=True)
                     result["validation"] = val
         loader.close()
-        result.update(steps=step, train=last_rec,
-                      wall_s=time.perf_counter() - t_start)
+        wall = time.perf_counter() - t_start
+        result.update(steps=step, train=last_rec, wall_s=wall,
+                      final_loss=last_rec.get("loss"),
+                      images_per_sec=(step - start_step) * global_batch / max(wall, 1e-9))
+        # a sweep (zookeeper_amd/sweep.py) collects every run's result here
+        out = os.environ.get("ZK_RESULT_JSON")
+        if out and info.is_main:
+            import json
+
+            with open(out, "w") as f:
+                json.dump(result, f, indent=2, default=repr)
         return result
 
     def evaluate(self, trainer, info) -> dict:

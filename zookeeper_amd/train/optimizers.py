@@ -70,13 +70,33 @@ class OptimizerSpec:
 
 @component
 class Adam(OptimizerSpec):
-    """Adam (decoupled weight decay ⇒ AdamW when ``weight_decay > 0``)."""
+    """Adam (decoupled weight decay ⇒ AdamW when ``weight_decay > 0``).
+
+    ``epsilon_form="keras"`` (default) is the update of the reference's
+    ``tf.keras.optimizers.Adam`` (examples/larq_experiment.py:120-122):
+    ``p -= lr·√(1-β₂ᵗ)/(1-β₁ᵗ) · m/(√v + ε)``, i.e. ε is added to the raw
+    √v ("epsilon hat").  ``"textbook"`` is Kingma & Ba's / PyTorch's
+    ``p -= lr · m̂/(√v̂ + ε)`` with bias-corrected moments.  The two differ
+    only in how large ε acts during the first steps (by √(1-β₂ᵗ)), which
+    matters for binary networks with tiny latent-weight gradients.  The
+    fused kernel computes the textbook form; the Keras form is the same
+    kernel with ε/√(1-β₂ᵗ)."""
 
     beta_1: float = Field(0.9)
     beta_2: float = Field(0.999)
     epsilon: float = Field(1e-7)  # Keras' default
+    epsilon_form: str = Field("keras")
 
     kind = "adam"
+
+    def eps_effective(self, t: int) -> float:
+        """ε to use in the textbook form at step ``t`` so that it equals the
+        configured form."""
+        if self.epsilon_form == "textbook":
+            return self.epsilon
+        if self.epsilon_form == "keras":
+            return self.epsilon / math.sqrt(1.0 - self.beta_2 ** t)
+        raise ValueError(f"epsilon_form must be 'keras' or 'textbook', got {self.epsilon_form!r}")
 
 
 @component
@@ -128,7 +148,7 @@ class FlatOptimizer:
                 self.v.mul_(b2).addcmul_(g, g, value=1 - b2)
                 mhat = self.m / (1 - b1**t)
                 vhat = self.v / (1 - b2**t)
-                upd = mhat / (vhat.sqrt() + sp.epsilon)
+                upd = mhat / (vhat.sqrt() + sp.eps_effective(t))
                 if sp.weight_decay:
                     upd = upd + sp.weight_decay * decay * p
                 p.sub_(lr * upd)
