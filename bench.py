@@ -55,6 +55,7 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=512, help="per-GPU batch")
     ap.add_argument("--model", default="BinaryResNetE18")
     ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--num-classes", type=int, default=1000)
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     ap.add_argument("--data", default="pool", choices=["pool", "stream"],
                     help="pool: device-resident synthetic batches; stream: host pipeline "
@@ -133,7 +134,8 @@ def main() -> int:
         learning_rate: float = Field(2e-3)
 
     cfg = BenchConfig()
-    configure(cfg, {"model.backend": args.backend, "dataset.image_shape": (S, S, 3)})
+    configure(cfg, {"dataset.image_shape": (S, S, 3), "dataset.num_classes": args.num_classes,
+                    "model.backend": args.backend})
     model = cfg.model
     backend = base_getattr(cfg, "model").resolved_backend()
     torch.manual_seed(1234)
@@ -151,8 +153,8 @@ def main() -> int:
         it = iter(loader)
         next_batch = lambda i: next(it)  # noqa: E731
     else:
-        pool = make_device_pool_batches(args.pool, args.batch, (S, S, 3), 1000, info.device,
-                                        seed=info.rank)
+        pool = make_device_pool_batches(args.pool, args.batch, (S, S, 3), args.num_classes,
+                                        info.device, seed=info.rank)
         next_batch = lambda i: pool[i % len(pool)]  # noqa: E731
 
     cuda = torch.cuda.is_available()
@@ -205,12 +207,13 @@ def main() -> int:
     global_batch = args.batch * info.world
     value = global_batch * args.steps / elapsed
     r3 = lambda v: None if v is None else round(v, 3)  # noqa: E731
-    data_desc = (f"synthetic (ImageNet-shape uint8 {S}x{S}x3, 1000 classes, "
+    data_desc = (f"synthetic (ImageNet-shape uint8 {S}x{S}x3, {args.num_classes} classes, "
                  + ("device-resident pool" if args.data == "pool" else
                     "host source streamed: native gather into pinned slots + side-stream H2D")
                  + "; random-init weights)")
     out = {
-        "metric": METRIC if (args.model == "BinaryResNetE18" and S == 224)
+        "metric": METRIC if (args.model == "BinaryResNetE18" and S == 224
+                             and args.num_classes == 1000)
         else OTHER_METRIC.format(model=args.model),
         "value": round(value, 2),
         "unit": "images/sec",

@@ -13,6 +13,8 @@
 #                    FETCH_SIZE, WRITE_SIZE; one counter group per run)
 #   pmcconv:op:shape PMC passes over one conv kernel (tools/one_conv.py), e.g.
 #                    pmcconv:dgrad:56,56,64,64,1
+#   benchargs:<a,b>  bench.py with arbitrary comma-separated arguments
+#   profargs:<a,b>   rocprofv3 --kernel-trace --stats of bench.py with those arguments
 #   tune[:args]      tools/tune_bconv.py with the given (comma-separated) args
 #   py:<module>      python -m <module>  (tools, one-off diagnostics)
 #   dpgloo:<n>       bench.py with n gloo ranks sharing the GPU (ordering rehearsal)
@@ -67,6 +69,14 @@ for spec in "$@"; do
       gpu_step 600 "$OUT/prof_${n}.log" rocprofv3 --kernel-trace --stats \
         -d "$OUT/prof_$n" -o run --output-format csv -- python3 bench.py --model "${a1:-BinaryResNetE18}" \
         --batch "${a2:-512}" --steps 20 --warmup 10 --graph 0 || exit $?
+      ;;
+    benchargs)
+      gpu_step 420 "$OUT/benchargs_${n}.log" python -u bench.py ${a1//,/ } \
+        --json-out "$OUT/benchargs_${n}.json" || exit $?
+      ;;
+    profargs)
+      gpu_step 600 "$OUT/profargs_${n}.log" rocprofv3 --kernel-trace --stats \
+        -d "$OUT/profargs_$n" -o run --output-format csv -- python3 bench.py ${a1//,/ } || exit $?
       ;;
     pmc)
       R="$(pwd)"

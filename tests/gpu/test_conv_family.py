@@ -1,0 +1,183 @@
+"""The native conv family beyond the fused binary blocks, each vs an fp64
+oracle of the same op (autograd through ``F.conv2d`` / ``F.linear``):
+
+* ``ops.conv``     float conv, stride 1/2, 1×1 and 3×3, ``same`` / ``valid``
+                   (ResNet-50's strided convs) — bf16 MFMA forward epilogue,
+                   strided dgrad, split-K wgrad;
+* ``ops.bconv``    stand-alone binary conv (BinaryNet: conv → pool → BN) and
+                   binary dense (BinaryNet's three ``QuantDense``), STE masks on
+                   input and kernel, zero / one padding, padded 10-way output;
+* ``ops.smallconv`` small-K convs (K ≤ 64): BinaryNet's float-input ±1-kernel
+                   first layer, QuickNet's 3→16 stem conv and 16→64 1×1 conv
+                   (with its data gradient).
+"""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+def _pad(x, k, s, padding, value=0.0):
+    from zookeeper_amd.nn.layers import pad_same_nhwc
+
+    return pad_same_nhwc(x, (k, k), (s, s), value) if padding == "same" else x
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _close(got, ref, rel):
+    err = (got.double() - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err <= rel * scale, (err, scale)
+
+
+@pytest.mark.parametrize("cin,cout,k,s,padding,hw", [
+    (64, 128, 3, 2, "same", 14), (64, 64, 3, 2, "same", 13), (128, 64, 1, 2, "valid", 15),
+    (256, 512, 1, 2, "valid", 14), (64, 128, 3, 1, "valid", 9), (128, 128, 3, 2, "valid", 12)])
+def test_float_conv_matches_fp64(cin, cout, k, s, padding, hw):
+    from zookeeper_amd.ops import conv as conv_op
+
+    torch.manual_seed(0)
+    B = 4
+    x = _cl(torch.randn(B, cin, hw, hw, device="cuda").to(torch.bfloat16)).requires_grad_(True)
+    w = _cl(torch.randn(cout, cin, k, k, device="cuda") * 0.1).requires_grad_(True)
+    assert conv_op.supported(x, w, (s, s), padding, 1)
+    y = conv_op.conv2d(x, w, s, padding)
+    g = torch.randn_like(y.float()).to(torch.bfloat16)
+    y.backward(g)
+
+    xd = x.detach().double().requires_grad_(True)
+    wd = w.detach().to(torch.bfloat16).double().requires_grad_(True)
+    ref = F.conv2d(_pad(xd, k, s, padding), wd, stride=s)
+    ref.backward(g.double())
+    assert y.shape == ref.shape
+    _close(y, ref, 1e-2)
+    _close(x.grad, xd.grad, 2e-2)
+    _close(w.grad, wd.grad, 2e-3)
+
+
+def _sign(t):
+    return torch.where(t >= 0, 1.0, -1.0).to(t.dtype)
+
+
+@pytest.mark.parametrize("cin,cout,s,padding,hw,pad_value", [
+    (128, 128, 1, "same", 13, 0.0), (64, 128, 2, "same", 12, 0.0), (128, 256, 1, "valid", 10, 0.0),
+    (64, 64, 1, "same", 9, 1.0)])
+def test_binary_conv_matches_fp64(cin, cout, s, padding, hw, pad_value):
+    from zookeeper_amd.ops import bconv
+
+    torch.manual_seed(1)
+    B = 3
+    x = _cl(torch.randn(B, cin, hw, hw, device="cuda").to(torch.bfloat16)).requires_grad_(True)
+    w = _cl(torch.empty(cout, cin, 3, 3, device="cuda").uniform_(-1.3, 1.3)).requires_grad_(True)
+    y = bconv.binary_conv(x, w, s, padding, 1.0, 1.0, pad_value)
+    g = torch.randn_like(y.float()).to(torch.bfloat16)
+    y.backward(g)
+
+    xd = x.detach().double()
+    wd = w.detach().double()
+    xs = _sign(xd).requires_grad_(True)
+    ws = _sign(wd).requires_grad_(True)
+    ref = F.conv2d(_pad(xs, 3, s, padding, pad_value), ws, stride=s)
+    ref.backward(g.double())
+    # the int16 conv output is exact; bf16 rounds |y| > 256 only
+    _close(y, ref, 4e-3)
+    _close(x.grad, xs.grad * (xd.abs() <= 1.0), 1e-2)
+    _close(w.grad, ws.grad * (wd.abs() <= 1.0), 1e-4)
+
+
+@pytest.mark.parametrize("B,K,N", [(128, 4608, 1024), (37, 1024, 10), (64, 1024, 1024)])
+def test_binary_dense_matches_fp64(B, K, N):
+    from zookeeper_amd.ops import bconv
+
+    torch.manual_seed(2)
+    x = torch.randn(B, K, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    w = torch.empty(N, K, device="cuda").uniform_(-1.2, 1.2).requires_grad_(True)
+    y = bconv.binary_dense(x, w)
+    g = torch.randn(B, N, device="cuda").to(torch.bfloat16)
+    y.backward(g)
+    xd, wd = x.detach().double(), w.detach().double()
+    xs, ws = _sign(xd).requires_grad_(True), _sign(wd).requires_grad_(True)
+    ref = F.linear(xs, ws)
+    ref.backward(g.double())
+    assert y.shape == (B, N)
+    _close(y, ref, 4e-3)
+    _close(x.grad, xs.grad * (xd.abs() <= 1.0), 1e-2)
+    _close(w.grad, ws.grad * (wd.abs() <= 1.0), 1e-4)
+
+
+@pytest.mark.parametrize("cin,cout,k,s,padding,hw,binary_kernel,need_dx", [
+    (3, 128, 3, 1, "valid", 30, True, False),    # BinaryNet layer 1 (CIFAR)
+    (1, 128, 3, 1, "valid", 28, True, False),    # BinaryNet layer 1 (MNIST)
+    (3, 16, 3, 2, "same", 33, False, False),     # QuickNet stem conv
+    (16, 64, 1, 1, "valid", 14, False, True),    # QuickNet stem 1x1 (+ dgrad)
+    (4, 32, 3, 2, "same", 16, False, False)])
+def test_small_conv_matches_fp64(cin, cout, k, s, padding, hw, binary_kernel, need_dx):
+    from zookeeper_amd.ops import smallconv
+
+    torch.manual_seed(3)
+    B = 5
+    x = _cl(torch.randn(B, cin, hw, hw, device="cuda").to(torch.bfloat16)).requires_grad_(need_dx)
+    w = _cl(torch.empty(cout, cin, k, k, device="cuda").uniform_(-1.3, 1.3) * (1 if binary_kernel else 0.2))
+    w.requires_grad_(True)
+    assert smallconv.supported(x, w, (s, s), padding, 1)
+    y = smallconv.small_conv(x, w, s, padding, 1.0 if binary_kernel else None)
+    g = torch.randn_like(y.float()).to(torch.bfloat16)
+    y.backward(g)
+    xd = x.detach().double().requires_grad_(need_dx)
+    wd = w.detach().double()
+    wq = (_sign(wd) if binary_kernel else wd.to(torch.bfloat16).double()).requires_grad_(True)
+    ref = F.conv2d(_pad(xd, k, s, padding), wq, stride=s)
+    ref.backward(g.double())
+    assert y.shape == ref.shape
+    _close(y, ref, 1e-2)
+    mask = (wd.abs() <= 1.0) if binary_kernel else torch.ones_like(wd, dtype=torch.bool)
+    _close(w.grad, wq.grad * mask, 2e-3)
+    if need_dx:
+        _close(x.grad, xd.grad, 2e-2)
+
+
+@pytest.mark.timeout(120)
+def test_binarynet_runs_native_and_matches_fp32_oracle():
+    """A whole BinaryNet (CIFAR shape) training step on the native path
+    (every conv / dense / BN / pool a HIP kernel) vs the same weights run
+    as the fp32 torch oracle on the same (bf16-rounded) input: the losses
+    agree and every gradient is finite and non-zero.  (Per-parameter
+    gradient directions are NOT comparable at model level: in a binary
+    network a perturbation as small as rounding the input to bf16 flips
+    activation signs and moves the fp32 oracle's own gradients to cosine
+    ~0.05 — measured on CPU; each layer's gradients are pinned to fp64 by
+    the tests above.)"""
+    import copy
+
+    from zookeeper_amd.models.binarynet import BinaryNetModule
+    from zookeeper_amd.train.losses import softmax_cross_entropy
+
+    torch.manual_seed(4)
+    m = BinaryNetModule((32, 32, 3), 10, filters=64, dense_units=256).cuda()
+    for mod in m.modules():
+        for name, p in mod.named_parameters(recurse=False):
+            if p.dim() == 4:
+                p.data = p.data.contiguous(memory_format=torch.channels_last)
+    ref = copy.deepcopy(m)
+    x = torch.randn(32, 3, 32, 32, device="cuda").to(torch.bfloat16)
+    y = torch.randint(0, 10, (32,), device="cuda")
+    out = m(_cl(x))
+    loss, _ = softmax_cross_entropy(out, y)
+    loss.backward()
+    out_r = ref(_cl(x.float()))
+    loss_r = F.cross_entropy(out_r, y)
+    loss_r.backward()
+    assert abs(loss.item() - loss_r.item()) < 0.1 * abs(loss_r.item()) + 0.05
+    for p in m.parameters():
+        assert torch.isfinite(p.grad).all() and p.grad.abs().sum() > 0

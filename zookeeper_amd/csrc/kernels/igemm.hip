@@ -156,7 +156,8 @@ __device__ __forceinline__ void dgrad_store_block(const ConvArgs& args, const IG
   }
 }
 
-template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB, bool F4 = false>
+template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB, bool F4 = false,
+          bool OB = false>
 __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs args, IGeom g,
                                                                      int m_tiles) {
   constexpr int NWAVES = WM * WN;
@@ -165,6 +166,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
   constexpr int RPI = 1024 / CB;          // rows per wave-instruction
   constexpr int SH = (CB == 128) ? 1 : (CB == 64) ? 2 : 3;  // swizzle shift (see header)
   static_assert(!F4 || FWD, "e2m1 operands: the +-1 x +-1 forward only");
+  static_assert(!OB || (FWD && !F4), "bf16 output: the float (bf16 x bf16) forward");
   constexpr int A_INS = BM / RPI / NWAVES;  // glds per wave per stage
   constexpr int B_INS = BN / RPI / NWAVES;
   static_assert(A_INS >= 1 && B_INS >= 1 && BM % (RPI * NWAVES) == 0 &&
@@ -374,7 +376,25 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
     }
   }
 
-  if constexpr (FWD) {
+  if constexpr (FWD && OB) {
+    // ---- float forward epilogue: bf16 y (+ReLU), lane = output channel,
+    // registers = pixels (64-B contiguous per wave half and register)
+    uint16_t* y = reinterpret_cast<uint16_t*>(args.out);
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long mc = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (mc >= M) continue;
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          float v = acc[a][b][r];
+          if (args.relu) v = fmaxf(v, 0.f);
+          y[mc * g.Cout + n0 + wn * WTN + b * 32 + r32] = zk::f32_to_bf16(v);
+        }
+      }
+    }
+  } else if constexpr (FWD) {
     // ---- forward epilogue: lane = output channel, registers = pixels;
     // the fp32 accumulators hold exact integers (|v| <= K)
     int16_t* y = reinterpret_cast<int16_t*>(args.out);
@@ -884,6 +904,49 @@ int launch_igemm_fwd(const void* sx, const void* wf, void* y, void* stats, const
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, 1), dim3(WM * WN * 64), LDS, stream, args, g,
                      m_tiles);
   return 0;
+}
+
+// Float forward (bf16 x bf16 -> bf16 y), any stride <= 2 / kernel <= 4x4:
+// the binary-forward kernel with the bf16 epilogue.
+template <int BM, int BN, int WM, int WN, int NS, int CB = 128>
+int launch_igemm_fwd_bf16(const void* x, const void* wf, void* y, const IGeom& g, int relu,
+                          hipStream_t stream) {
+  if ((g.Cin * 2) % CB || g.Cout % BN || g.s > 2 || g.kh > 4 || g.kw > 4)
+    return (int)hipErrorInvalidValue;
+  if (g_dry_run) return 0;
+  constexpr int LDS = NS * (BM + BN) * CB;
+  static_assert(LDS <= 160 * 1024, "LDS");
+  auto kern = igemm_conv_kernel<true, BM, BN, WM, WN, NS, CB, false, true>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  const long long Mo = (long long)g.B * g.Ho * g.Wo;
+  const int m_tiles = (int)((Mo + BM - 1) / BM);
+  const long long blocks = (long long)m_tiles * (g.Cout / BN);
+  ConvArgs args{(const uint16_t*)x, (const uint16_t*)wf, nullptr, nullptr, y, nullptr, 0, relu,
+                1};
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks, 1), dim3(WM * WN * 64), LDS, stream, args, g,
+                     m_tiles);
+  return 0;
+}
+
+int igemm_fwd_bf16_variant(int v, const void* x, const void* wf, void* y, const IGeom& g,
+                           int relu, hipStream_t st) {
+#define ZK_IGB(...) return launch_igemm_fwd_bf16<__VA_ARGS__>(x, wf, y, g, relu, st)
+  switch (v) {
+    case 0: ZK_IGB(128, 128, 2, 2, 2);
+    case 1: ZK_IGB(256, 128, 4, 2, 2);
+    case 2: ZK_IGB(128, 64, 2, 2, 2);
+    case 3: ZK_IGB(256, 256, 4, 2, 2, 128);
+    case 4: ZK_IGB(128, 64, 2, 2, 4, 64);
+    case 5: ZK_IGB(256, 64, 4, 1, 2);
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef ZK_IGB
 }
 
 int igemm_fwd_variant(int v, const void* sx, const void* wf, void* y, void* stats,
@@ -1782,6 +1845,29 @@ ZK_EXPORT int zk_igemm_fwd_fp4(const void* sx4, const void* wf4, void* y, void* 
   return 0;
 }
 
+// Float forward convolution on MFMA: y bf16 [B][Ho][Wo][Cout] = x ⊛ W (+ReLU);
+// x bf16 [B][H][W][Cin], wf bf16 [T][Cout][Cin] (T = kh*kw, tap-major).
+// Any stride <= 2 and kernel <= 4x4 (ResNet-50's strided 3x3 / 1x1 convs);
+// Cin % 64 == 0, Cout % 64 == 0.
+ZK_EXPORT int zk_igemm_fwd_bf16(const void* x, const void* wf, void* y, int B, int H, int W,
+                                int Cin, int Cout, int kh, int kw, int stride, int pt, int pl,
+                                int Ho, int Wo, int relu, int variant, hipStream_t stream) {
+  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+  if (variant < 0) {
+    const long long Mo = (long long)B * Ho * Wo;
+    if (Cout % 256 == 0 && Cin % 64 == 0 && Mo * (Cout / 256) >= 256 * 256)
+      variant = 3;  // 256x256: half the LDS-fill bytes per FLOP when the grid stays full
+    else if (Cout % 128 == 0)
+      variant = Mo >= 65536 ? 1 : 0;
+    else
+      variant = 2;
+  }
+  const int rc = igemm_fwd_bf16_variant(variant, x, wf, y, g, relu, stream);
+  if (rc) return rc;
+  if (!g_dry_run) ZK_CHECK_LAUNCH();
+  return 0;
+}
+
 // ---------------------------------------------------------------------------
 // Support queries: 1 if the tile variant accepts the geometry, 0 if not
 // (nothing is launched; no GPU needed).  variant -1 = the tuned default.
@@ -1797,6 +1883,14 @@ ZK_EXPORT int zk_igemm_dgrad_supported(int B, int H, int W, int Cin, int Ho, int
   DryRun dr;
   return zk_igemm_dgrad(nullptr, nullptr, nullptr, nullptr, nullptr, B, H, W, Cin, Ho, Wo, Cout,
                         kh, kw, stride, pt, pl, variant, nullptr) == 0;
+}
+
+ZK_EXPORT int zk_igemm_fwd_bf16_supported(int B, int H, int W, int Cin, int Cout, int kh,
+                                          int kw, int stride, int pt, int pl, int Ho, int Wo,
+                                          int variant) {
+  DryRun dr;
+  return zk_igemm_fwd_bf16(nullptr, nullptr, nullptr, B, H, W, Cin, Cout, kh, kw, stride, pt, pl,
+                           Ho, Wo, 0, variant, nullptr) == 0;
 }
 
 ZK_EXPORT int zk_igemm_fwd_supported(int B, int H, int W, int Cin, int Cout, int kh, int kw,

@@ -172,6 +172,30 @@ class QuantConv2d(nn.Module):
             if conv3x3.supported(x, self.weight, self.stride, self.padding, self.groups,
                                  self.bias, self.pad_values):
                 return conv3x3.conv3x3(x, self.weight)
+        if self._binary() and _use_native(x):
+            from zookeeper_amd.ops import bconv
+
+            if bconv.conv_supported(x, self.weight, self.stride, self.padding, self.groups,
+                                    self.bias, self.pad_values):
+                clip = getattr(self, "clip_value", 1.0)
+                return bconv.binary_conv(x, self.weight, self.stride[0], self.padding, clip,
+                                         clip, self.pad_values, owner=self)
+        if (self.input_quantizer is None and self.kernel_quantizer is None
+                and _use_native(x)):
+            from zookeeper_amd.ops import conv as conv_op
+
+            if conv_op.supported(x, self.weight, self.stride, self.padding, self.groups,
+                                 self.bias, self.pad_values):
+                return conv_op.conv2d(x, self.weight, self.stride[0], self.padding)
+        if (self.input_quantizer is None and self.kernel_quantizer_name in (None, "ste_sign")
+                and (self.kernel_quantizer is None or self.kernel_quantizer_name == "ste_sign")
+                and _use_native(x)):
+            from zookeeper_amd.ops import smallconv
+
+            if smallconv.supported(x, self.weight, self.stride, self.padding, self.groups,
+                                   self.bias, self.pad_values):
+                kclip = getattr(self, "clip_value", 1.0) if self.kernel_quantizer else None
+                return smallconv.small_conv(x, self.weight, self.stride[0], self.padding, kclip)
         if self.input_quantizer is not None:
             x = self.input_quantizer(x)
         if self.padding == "same":
@@ -179,6 +203,10 @@ class QuantConv2d(nn.Module):
         w = self.quantized_weight().to(x.dtype)
         b = self.bias.to(x.dtype) if self.bias is not None else None
         return F.conv2d(x, w, b, self.stride, 0, 1, self.groups)
+
+    def _binary(self) -> bool:
+        """ste_sign on both the input and the kernel (Larq's binary layer)."""
+        return self.input_quantizer_name == "ste_sign" and self.kernel_quantizer_name == "ste_sign"
 
     def apply_constraints(self) -> None:
         if self.kernel_constraint is not None:
@@ -200,6 +228,8 @@ class QuantDense(nn.Module):
     ):
         super().__init__()
         self.in_features, self.out_features = in_features, out_features
+        self.input_quantizer_name = input_quantizer if isinstance(input_quantizer, str) else None
+        self.kernel_quantizer_name = kernel_quantizer if isinstance(kernel_quantizer, str) else None
         self.input_quantizer = get_quantizer(input_quantizer)
         self.kernel_quantizer = get_quantizer(kernel_quantizer)
         self.kernel_constraint = kernel_constraint
@@ -209,6 +239,13 @@ class QuantDense(nn.Module):
         self.bias = nn.Parameter(torch.zeros(out_features)) if use_bias else None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if (self.input_quantizer_name == "ste_sign" and self.kernel_quantizer_name == "ste_sign"
+                and _use_native(x)):
+            from zookeeper_amd.ops import bconv
+
+            if bconv.dense_supported(x, self.weight, self.bias):
+                clip = getattr(self, "clip_value", 1.0)
+                return bconv.binary_dense(x, self.weight, clip, clip, owner=self)
         if self.input_quantizer is not None:
             x = self.input_quantizer(x)
         w = self.weight
@@ -253,6 +290,13 @@ class BatchNorm(nn.Module):
 
             if norm_pool.supported(x):
                 return norm_pool.batch_norm(x, self, relu)
+            y = self._formula(x.float())  # e.g. a 10-way classifier's BN: tiny
+            return (F.relu(y) if relu else y).to(x.dtype)
+        if x.is_cuda:
+            # the fp32 oracle on the GPU: explicit arithmetic, not the library
+            # BN (MIOpen's backward mis-shapes the bias gradient when scale=False)
+            y = self._formula(x.float()).to(x.dtype)
+            return F.relu(y) if relu else y
         w = self.weight
         b = self.bias
         if x.dtype != torch.float32:
@@ -264,6 +308,28 @@ class BatchNorm(nn.Module):
             y = F.batch_norm(x, self.running_mean, self.running_var, w, b, self.training,
                              1.0 - self.momentum, self.eps)
         return F.relu(y) if relu else y
+
+
+    def _formula(self, x: torch.Tensor) -> torch.Tensor:
+        """Batch norm as plain fp32 tensor arithmetic (no library BN kernel)."""
+        dims = [0] + list(range(2, x.dim()))
+        shape = [1, -1] + [1] * (x.dim() - 2)
+        if self.training:
+            mean = x.mean(dim=dims)
+            var = x.var(dim=dims, unbiased=False)
+            n = x.numel() // x.shape[1]
+            with torch.no_grad():
+                m = 1.0 - self.momentum
+                self.running_mean.mul_(1 - m).add_(mean.detach(), alpha=m)
+                self.running_var.mul_(1 - m).add_(var.detach() * n / max(n - 1, 1), alpha=m)
+        else:
+            mean, var = self.running_mean, self.running_var
+        y = (x - mean.view(shape)) * torch.rsqrt(var.view(shape) + self.eps)
+        if self.weight is not None:
+            y = y * self.weight.view(shape)
+        if self.bias is not None:
+            y = y + self.bias.view(shape)
+        return y
 
 
 class MaxPool2d(nn.Module):

@@ -33,8 +33,13 @@ SIGNATURES = {
     "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),
     "zk_igemm_wgrad_ws_bytes": (I64, [I32] * 14),
     "zk_igemm_dgrad_supported": (I32, [I32] * 13),
+    "zk_igemm_fwd_bf16": (I32, [P, P, P] + [I32] * 14 + [P]),
+    "zk_igemm_fwd_bf16_supported": (I32, [I32] * 13),
     "zk_igemm_fwd_supported": (I32, [I32] * 15),
     "zk_bconv_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P]),
+    # small-K convolutions (smallconv.hip)
+    "zk_smallk_conv_fwd": (I32, [P, P, P] + [I32] * 12 + [P]),
+    "zk_smallk_conv_wgrad": (I32, [P, P, P, P] + [I32] * 12 + [F32, I32, P]),
     # batch norm
     "zk_bn_finalize": (I32, [P, I32, I32, C.c_double, P, P, F32, F32, P, P, P, P, P, P, P]),
     "zk_bn_apply": (I32, [P, P, P, P, P, I64, I32, P]),

@@ -1,0 +1,122 @@
+"""Small-K convolutions on MFMA (``csrc/kernels/smallconv.hip``): convs whose
+reduction ``K = KH·KW·Cin`` is at most 64 — the layers that read the image
+or a thin feature map, where the 64-channel-chunked implicit GEMMs of
+``igemm.hip`` do not apply:
+
+* BinaryNet's first layer: float input, ``ste_sign`` ±1 kernel, 3×3
+  ``valid`` (examples/larq_experiment.py:62-69) — the kernel's sign is taken
+  when packing, its STE mask (``|w| ≤ 1``) applied in the weight gradient;
+* QuickNet's stem conv (3×3/2 over the image) and its 16→64 1×1 conv.
+
+forward   im2col of a 128-pixel tile built in LDS, ``v_mfma_f32_16x16x32_bf16``
+          over the whole K (padded to 32 / 64), bf16 NHWC out;
+backward  weight gradient: split-K over pixels, fp32 atomics straight into the
+          flat gradient buffer; data gradient (only the 1×1 stride-1 case
+          needs one) = the same forward kernel on dY with Wᵀ (K = Cout ≤ 64).
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
+
+_INF = float("inf")
+
+
+def _geometry(H, W, kh, kw, s, padding):
+    from zookeeper_amd.ops.conv import geometry
+
+    return geometry(H, W, kh, kw, s, padding)
+
+
+def supported(x: torch.Tensor, weight: torch.Tensor, stride, padding: str, groups: int,
+              bias: Optional[torch.Tensor] = None, pad_value: float = 0.0) -> bool:
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and weight.dim() == 4
+            and groups == 1 and bias is None and pad_value == 0.0 and padding in ("same", "valid")):
+        return False
+    Cout, Cin, kh, kw = weight.shape
+    s = tuple(stride)
+    if not (s[0] == s[1] and x.shape[1] == Cin and Cout % 16 == 0 and Cout <= 128
+            and kh * kw * Cin <= 64):
+        return False
+    # a data gradient is only available for 1x1 stride-1 convs with Cout <= 64
+    needs_dx = x.requires_grad and torch.is_grad_enabled()
+    return not needs_dx or (kh == kw == 1 and s[0] == 1 and Cout <= 64 and Cin % 16 == 0)
+
+
+def _pack(w2: torch.Tensor, KP: int) -> torch.Tensor:
+    """[N][K] float → bf16 [N][KP], zero beyond K."""
+    out = torch.zeros((w2.shape[0], KP), dtype=torch.bfloat16, device=w2.device)
+    out[:, :w2.shape[1]] = w2.to(torch.bfloat16)
+    return out
+
+
+class _SmallConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding, kclip):
+        B, Cin, H, W = x.shape
+        Cout, _, kh, kw = weight.shape
+        pt, pl, Ho, Wo = _geometry(H, W, kh, kw, stride, padding)
+        K = kh * kw * Cin
+        KP = 32 if K <= 32 else 64
+        w2 = weight.detach().permute(0, 2, 3, 1).reshape(Cout, K).float()
+        if kclip is not None:  # ste_sign kernel: ±1 (sign(0) = +1)
+            w2 = torch.where(w2 >= 0, 1.0, -1.0)
+        wp = _pack(w2, KP)
+        xn = x.permute(0, 2, 3, 1).contiguous()
+        y = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x.device)
+        check(lib().zk_smallk_conv_fwd(xn.data_ptr(), wp.data_ptr(), y.data_ptr(), B, H, W, Cin,
+                                       Ho, Wo, Cout, kh, kw, stride, pt, pl,
+                                       stream_ptr(x.device)), "zk_smallk_conv_fwd")
+        ctx.save_for_backward(xn)
+        ctx.weight, ctx.kclip = weight, kclip
+        ctx.geom = (B, Cin, H, W, Cout, kh, kw, stride, pt, pl, Ho, Wo)
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (xn,) = ctx.saved_tensors
+        weight, kclip = ctx.weight, ctx.kclip
+        B, Cin, H, W, Cout, kh, kw, s, pt, pl, Ho, Wo = ctx.geom
+        g = dout.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+        dev = g.device
+        L = lib()
+        st = stream_ptr(dev)
+        dx = dweight = None
+        if ctx.needs_input_grad[0]:
+            # 1x1 stride 1: dx = dY · W  (a K = Cout conv with Cin outputs)
+            w2 = weight.detach().reshape(Cout, Cin).float()
+            if kclip is not None:
+                w2 = torch.where(w2 >= 0, 1.0, -1.0)
+            wpT = _pack(w2.t(), 32 if Cout <= 32 else 64)
+            dxn = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
+            check(L.zk_smallk_conv_fwd(g.data_ptr(), wpT.data_ptr(), dxn.data_ptr(), B, H, W, Cout,
+                                       H, W, Cin, 1, 1, 1, 0, 0, st), "zk_smallk_conv_fwd(dgrad)")
+            dx = dxn.permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            target = direct_grad(weight, channels_last=True)
+            dw = (target.permute(0, 2, 3, 1) if target is not None
+                  else torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev))
+            wf = weight.detach().permute(0, 2, 3, 1)
+            if wf.dtype != torch.float32 or not wf.is_contiguous():
+                wf = wf.float().contiguous()
+            check(L.zk_smallk_conv_wgrad(g.data_ptr(), xn.data_ptr(), wf.data_ptr(), dw.data_ptr(),
+                                         B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl,
+                                         _INF if kclip is None else float(kclip), 0, st),
+                  "zk_smallk_conv_wgrad")
+            if target is not None:
+                grad_ready(weight)
+            else:
+                dweight = dw.permute(0, 3, 1, 2)
+        return dx, dweight, None, None, None
+
+
+def small_conv(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: str,
+               kernel_clip: Optional[float] = None) -> torch.Tensor:
+    """Convolution with ``K = KH·KW·Cin ≤ 64`` (see ``supported``).  With
+    ``kernel_clip`` the kernel is ``ste_sign``-quantised: ±1 forward, gradient
+    masked by ``|w| ≤ kernel_clip``."""
+    return _SmallConvFn.apply(x, weight, int(stride), padding, kernel_clip)
