@@ -1,0 +1,148 @@
+"""Whole-model checks on the native path against the fp32 torch oracle
+(same weights, same bf16-rounded input), at reduced size:
+
+* ResNet-50 (float network, bottleneck tail as ONE fused BN + residual +
+  ReLU pass): loss and every parameter gradient agree with the oracle;
+* QuickNet-Large / BinaryResNet-E18 (binary networks): the loss agrees and
+  every gradient is finite and non-zero.  Binary networks' per-parameter
+  gradients are not comparable at model level (a bf16 rounding of the
+  input already flips activation signs; see test_conv_family), their
+  layers are pinned to fp64 by the kernel tests.
+"""
+
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _prep(m):
+    m = m.cuda()
+    for mod in m.modules():
+        for _, p in mod.named_parameters(recurse=False):
+            if p.dim() == 4:
+                p.data = p.data.contiguous(memory_format=torch.channels_last)
+    return m
+
+
+@pytest.mark.parametrize("C,relu", [(64, True), (256, True), (128, False)])
+def test_bn_residual_relu_matches_fp64(C, relu):
+    from zookeeper_amd.nn.layers import BatchNorm
+    from zookeeper_amd.ops import norm_pool
+
+    torch.manual_seed(0)
+    bn = BatchNorm(C, 0.9, 1e-5).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    x = _cl(torch.randn(4, C, 9, 9, device="cuda").to(torch.bfloat16)).requires_grad_(True)
+    r = _cl(torch.randn(4, C, 9, 9, device="cuda").to(torch.bfloat16)).requires_grad_(True)
+    y = norm_pool.batch_norm(x, bn, relu=relu, residual=r)
+    g = torch.randn_like(y.float()).to(torch.bfloat16)
+    y.backward(g)
+    xd = x.detach().double().requires_grad_(True)
+    rd = r.detach().double().requires_grad_(True)
+    w = bn.weight.detach().double().requires_grad_(True)
+    b = bn.bias.detach().double().requires_grad_(True)
+    ref = F.batch_norm(xd, None, None, w, b, True, 0.0, 1e-5) + rd
+    if relu:
+        ref = F.relu(ref)
+    ref.backward(g.double())
+    for got, want, tol in ((y, ref, 2e-2), (x.grad, xd.grad, 3e-2), (r.grad, rd.grad, 1e-2),
+                           (bn.weight.grad, w.grad, 2e-2), (bn.bias.grad, b.grad, 2e-2)):
+        err = (got.double() - want).abs().max().item()
+        assert err <= tol * (want.abs().max().item() + 1e-3), (err, want.abs().max().item())
+
+
+def _step(m, x, y):
+    from zookeeper_amd.train.losses import softmax_cross_entropy
+
+    out = m(x)
+    loss, _ = softmax_cross_entropy(out, y) if x.dtype == torch.bfloat16 else (
+        F.cross_entropy(out.float(), y), None)
+    loss.backward()
+    return loss.item()
+
+
+def _cosines(m, ref):
+    out = {}
+    for (n, p), (_, pr) in zip(m.named_parameters(), ref.named_parameters()):
+        a, b = p.grad.flatten().double(), pr.grad.flatten().double()
+        assert torch.isfinite(a).all(), n
+        if b.norm() > 1e-8:
+            out[n] = (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+    return out
+
+
+@pytest.mark.timeout(120)
+def test_resnet50_step_matches_fp32_oracle(monkeypatch):
+    """Native bf16 ResNet-50 step vs the fp32 oracle, measured against what
+    bf16 itself costs: the same model through the library bf16 path (torch
+    ops, MIOpen / hipBLASLt) vs the same fp32 oracle.  The native path must
+    be at least as close to fp32 as library bf16 is."""
+    from zookeeper_amd.models import resnet
+    from zookeeper_amd.models.resnet import ResNetModule
+    from zookeeper_amd.nn import layers
+
+    torch.manual_seed(1)
+    m = _prep(ResNetModule((64, 64, 3), 10, blocks=(1, 1, 2, 1)))
+    with torch.no_grad():  # non-zero last-BN gammas so every branch carries gradient
+        for mod in m.modules():
+            if hasattr(mod, "bn3"):
+                mod.bn3.weight.fill_(0.5)
+    ref = copy.deepcopy(m)
+    lib16 = copy.deepcopy(m)
+    x = _cl(torch.randn(8, 3, 64, 64, device="cuda").to(torch.bfloat16))
+    y = torch.randint(0, 10, (8,), device="cuda")
+    loss = _step(m, x, y)
+    loss_r = _step(ref, x.float(), y)
+    monkeypatch.setattr(layers, "_use_native", lambda t: False)
+    monkeypatch.setattr(resnet, "_use_native", lambda t: False)
+    out16 = lib16(x)
+    F.cross_entropy(out16.float(), y).backward()
+    assert abs(loss - loss_r) < 0.02 * abs(loss_r) + 0.02, (loss, loss_r)
+    cn, cl = _cosines(m, ref), _cosines(lib16, ref)
+    mean_n, mean_l = sum(cn.values()) / len(cn), sum(cl.values()) / len(cl)
+    assert mean_n > 0.9 and mean_n >= mean_l - 0.02, (mean_n, mean_l)
+    assert min(cn.values()) >= min(cl.values()) - 0.05, (
+        sorted(cn.items(), key=lambda t: t[1])[:4], sorted(cl.items(), key=lambda t: t[1])[:4])
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("name", ["QuickNetLarge", "BinaryResNetE18"])
+def test_binary_models_step_loss_matches_fp32_oracle(name):
+    from zookeeper_amd.models.binary_resnet import BinaryResNetE
+    from zookeeper_amd.models.quicknet import QuickNetModule
+
+    torch.manual_seed(2)
+    if name == "QuickNetLarge":
+        m = QuickNetModule((64, 64, 3), 10, (2, 2, 2, 2), (64, 128, 256, 512), backend="hip")
+        r = QuickNetModule((64, 64, 3), 10, (2, 2, 2, 2), (64, 128, 256, 512), backend="torch")
+    else:
+        m = BinaryResNetE((64, 64, 3), 10, 18, backend="hip")
+        r = BinaryResNetE((64, 64, 3), 10, 18, backend="torch")
+    r.load_state_dict(m.state_dict())
+    m, r = _prep(m), _prep(r)
+    # batch 32: at random init a binary network's loss moves by ~+-15% under
+    # a 1e-3 input perturbation even in fp32 (measured on CPU, batch 8), so
+    # the bound is loose; the learning test pins convergence instead
+    x = _cl(torch.randn(32, 3, 64, 64, device="cuda").to(torch.bfloat16))
+    y = torch.randint(0, 10, (32,), device="cuda")
+    loss = _step(m, x, y)
+    loss_r = _step(r, x.float(), y)
+    assert abs(loss - loss_r) < 0.15 * abs(loss_r) + 0.1, (loss, loss_r)
+    for n, p in m.named_parameters():
+        assert torch.isfinite(p.grad).all() and p.grad.abs().sum() > 0, n

@@ -113,7 +113,8 @@ __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __re
                                                             uint16_t* __restrict__ sx = nullptr,
                                                             uint8_t* __restrict__ smask = nullptr,
                                                             float clip = 1.f,
-                                                            uint32_t* __restrict__ sx4 = nullptr) {
+                                                            uint32_t* __restrict__ sx4 = nullptr,
+                                                            const uint16_t* __restrict__ res = nullptr) {
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;
   const int cg = threadIdx.x % CG;
@@ -127,9 +128,11 @@ __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __re
        r += (long long)gridDim.x * RB) {
     float v[8];
     load8_bf16(x + r * C + cg * 8, v);
+    float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (res) load8_bf16(res + r * C + cg * 8, rv);  // residual added before the ReLU
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      v[k] = sc[k] * v[k] + sh[k];
+      v[k] = sc[k] * v[k] + sh[k] + rv[k];
       if (relu) v[k] = fmaxf(v[k], 0.f);
     }
     const uint32_t ow[4] = {zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
@@ -226,7 +229,7 @@ template <int CG>
 __global__ __launch_bounds__(256) void bn_bwd_dx_bf16_kernel(
     const uint16_t* __restrict__ g, const uint16_t* __restrict__ x,
     const uint16_t* __restrict__ y, const float* __restrict__ bcoef, uint16_t* __restrict__ dx,
-    long long P) {
+    long long P, uint16_t* __restrict__ dres = nullptr) {
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;
   const int cg = threadIdx.x % CG;
@@ -248,6 +251,8 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_bf16_kernel(
 #pragma unroll
       for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
     }
+    // gradient of a residual added before the ReLU: the masked output gradient
+    if (dres) store8_bf16(dres + r * C + cg * 8, gv);
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = k1[k] * gv[k] + k0[k] - k3[k] * xv[k];
     store8_bf16(dx + r * C + cg * 8, o);
@@ -512,6 +517,41 @@ ZK_EXPORT int zk_bn_bwd_dx_bf16(const void* g, const void* x, const void* y, con
     hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,   \
                        (const uint16_t*)g, (const uint16_t*)x, (const uint16_t*)y,           \
                        (const float*)bcoef, (uint16_t*)dx, P);                               \
+    break;
+  ZK_CG_CASES(C, CASE)
+#undef CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// y = act(scale * x + shift + res): BN apply with a residual added before
+// the optional ReLU (a ResNet bottleneck's tail: relu(bn3(conv3) + shortcut)).
+ZK_EXPORT int zk_bn_apply_res_bf16(const void* x, const void* coef, const void* res, void* y,
+                                   long long P, int C, int relu, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+#define CASE(cg)                                                                           \
+  case cg:                                                                                 \
+    hipLaunchKernelGGL(bn_apply_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,  \
+                       (const uint16_t*)x, (const float*)coef, (uint16_t*)y, P, relu,      \
+                       nullptr, nullptr, 1.f, nullptr, (const uint16_t*)res);              \
+    break;
+  ZK_CG_CASES(C, CASE)
+#undef CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// zk_bn_bwd_dx_bf16 + the residual's gradient (the ReLU-masked output
+// gradient) written to dres in the same pass.
+ZK_EXPORT int zk_bn_bwd_dx_res_bf16(const void* g, const void* x, const void* y,
+                                    const void* bcoef, void* dx, void* dres, long long P, int C,
+                                    hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+#define CASE(cg)                                                                             \
+  case cg:                                                                                   \
+    hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,   \
+                       (const uint16_t*)g, (const uint16_t*)x, (const uint16_t*)y,           \
+                       (const float*)bcoef, (uint16_t*)dx, P, (uint16_t*)dres);              \
     break;
   ZK_CG_CASES(C, CASE)
 #undef CASE

@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from zookeeper_amd.core import Field, factory
 from zookeeper_amd.models.base import ModelFactory
 from zookeeper_amd.nn.layers import (BatchNorm, GlobalAvgPool, ImageStem, MaxPool2d, QuantConv2d,
-                                     glorot_normal_)
+                                     _use_native, glorot_normal_)
 
 
 class Bottleneck(nn.Module):
@@ -41,8 +41,14 @@ class Bottleneck(nn.Module):
         idt = self.down(x) if self.down is not None else x
         y = self.bn1(self.conv1(x))
         y = self.bn2(self.conv2(y))
-        y = self.bn3(self.conv3(y))
-        return F.relu(y + idt)
+        y = self.conv3(y)
+        if _use_native(y):
+            from zookeeper_amd.ops import norm_pool
+
+            if norm_pool.supported(y):
+                # relu(bn3(y) + shortcut) in one pass (and one pass back)
+                return norm_pool.batch_norm(y, self.bn3, relu=True, residual=idt)
+        return F.relu(self.bn3(y) + idt)
 
 
 class ResNetModule(nn.Module):

@@ -37,6 +37,8 @@ SIGNATURES = {
     "zk_igemm_fwd_bf16_supported": (I32, [I32] * 13),
     "zk_igemm_fwd_supported": (I32, [I32] * 15),
     "zk_bconv_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P]),
+    "zk_bn_apply_res_bf16": (I32, [P, P, P, P, I64, I32, I32, P]),
+    "zk_bn_bwd_dx_res_bf16": (I32, [P, P, P, P, P, P, I64, I32, P]),
     # small-K convolutions (smallconv.hip)
     "zk_smallk_conv_fwd": (I32, [P, P, P] + [I32] * 12 + [P]),
     "zk_smallk_conv_wgrad": (I32, [P, P, P, P] + [I32] * 12 + [F32, I32, P]),

@@ -29,7 +29,7 @@ def supported(x: torch.Tensor) -> bool:
 
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, bn, relu):
+    def forward(ctx, x, gamma, beta, residual, bn, relu):
         dim = x.dim()
         C = x.shape[1]
         xn = _nhwc(x)
@@ -56,8 +56,14 @@ class _BatchNormFn(torch.autograd.Function):
             coef[2] = bn.running_mean
             coef[3] = rstd
         y = torch.empty_like(xn)
-        check(L.zk_bn_apply_bf16(xn.data_ptr(), coef.data_ptr(), y.data_ptr(), P, C, int(relu), st),
-              "zk_bn_apply_bf16")
+        if residual is not None:
+            rn = _nhwc(residual.to(torch.bfloat16))
+            check(L.zk_bn_apply_res_bf16(xn.data_ptr(), coef.data_ptr(), rn.data_ptr(),
+                                         y.data_ptr(), P, C, int(relu), st), "zk_bn_apply_res_bf16")
+        else:
+            check(L.zk_bn_apply_bf16(xn.data_ptr(), coef.data_ptr(), y.data_ptr(), P, C, int(relu),
+                                     st), "zk_bn_apply_bf16")
+        ctx.has_res = residual is not None
         ctx.save_for_backward(xn, y if relu else None, coef, gamma)
         ctx.params = (gamma, beta)
         ctx.dim, ctx.P, ctx.C = dim, P, C
@@ -98,14 +104,26 @@ class _BatchNormFn(torch.autograd.Function):
             grad_ready(beta_p)
             dbeta = None
         dx = torch.empty_like(g)
-        check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), xn.data_ptr(),
-                                  y.data_ptr() if y is not None else None, bcoef.data_ptr(),
-                                  dx.data_ptr(), P, C, st), "zk_bn_bwd_dx_bf16")
-        return _back(dx, ctx.dim), dgamma, dbeta, None, None
+        dres = None
+        if ctx.has_res and ctx.needs_input_grad[3]:
+            dres = torch.empty_like(g)
+            check(L.zk_bn_bwd_dx_res_bf16(g.data_ptr(), xn.data_ptr(),
+                                          y.data_ptr() if y is not None else None,
+                                          bcoef.data_ptr(), dx.data_ptr(), dres.data_ptr(), P, C,
+                                          st), "zk_bn_bwd_dx_res_bf16")
+            dres = _back(dres, ctx.dim)
+        else:
+            check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), xn.data_ptr(),
+                                      y.data_ptr() if y is not None else None, bcoef.data_ptr(),
+                                      dx.data_ptr(), P, C, st), "zk_bn_bwd_dx_bf16")
+        return _back(dx, ctx.dim), dgamma, dbeta, dres, None, None
 
 
-def batch_norm(x: torch.Tensor, bn, relu: bool = False) -> torch.Tensor:
-    return _BatchNormFn.apply(x, bn.weight, bn.bias, bn, relu)
+def batch_norm(x: torch.Tensor, bn, relu: bool = False,
+               residual: torch.Tensor = None) -> torch.Tensor:
+    """``act(bn(x) [+ residual])`` in one pass (forward) / one pass (the
+    data gradient, plus the residual's gradient when given)."""
+    return _BatchNormFn.apply(x, bn.weight, bn.bias, residual, bn, relu)
 
 
 class _MaxPoolFn(torch.autograd.Function):
