@@ -114,3 +114,46 @@ def test_fused_stem_sign_handoff_matches_sign_pack():
     assert torch.equal(mask, ref_mask)
     if sx4 is not None:
         assert torch.equal(sx4, ref_sx4)
+
+
+@pytest.mark.parametrize("hw,B", [(64, 5), (56, 6), (224, 3), (50, 2)])
+def test_recompute_fused_stem_matches_materialising(hw, B, monkeypatch):
+    """stem_fused.hip (conv recomputed in the stats, pool and weight-gradient
+    passes; no y1 / dy1 tensors) against stem.hip's materialising kernels and
+    the fp32 oracle: the same y1 bf16 values by construction, so the outputs
+    agree to the BN-1 statistics' summation order; every gradient is at least
+    as close to fp32 as the materialising path's (whose BN-1 backward sums use
+    yhat reconstructed from the bf16 pooled value, the fused path the exact
+    y1 at the argmax)."""
+    import zookeeper_amd.ops.stem as stem_mod
+
+    torch.manual_seed(3)
+    base = _stem(True).cuda().to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        for m in base.modules():
+            if isinstance(m, BatchNorm):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.3, 0.3)
+    oracle = copy.deepcopy(base).float()
+    x = torch.randn(B, 3, hw, hw, device="cuda").to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y_ref = torch.nn.Sequential.forward(oracle, x.float())
+    g = torch.randn_like(y_ref).to(torch.bfloat16)
+    y_ref.backward(g.float())
+    ref = {n: p.grad for n, p in oracle.named_parameters()}
+    runs = {}
+    for fused in (False, True):
+        monkeypatch.setattr(stem_mod, "_FUSED", fused)
+        m = copy.deepcopy(base)
+        y = m(x)
+        y.backward(g)
+        torch.cuda.synchronize()
+        runs[fused] = (y.detach().float(), {n: p.grad.clone() for n, p in m.named_parameters()},
+                       {n: b.clone() for n, b in m.named_buffers()})
+    (y0, g0, b0), (y1, g1, b1) = runs[False], runs[True]
+    assert _rel(y1, y0) < 2e-3
+    for n in g0:
+        e1, e0 = _rel(g1[n], ref[n]), _rel(g0[n], ref[n])
+        assert e1 < max(1.5 * e0, 2e-2), (n, e1, e0)
+    for n in b0:
+        torch.testing.assert_close(b1[n], b0[n], atol=1e-4, rtol=1e-4)

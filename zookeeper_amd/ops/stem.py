@@ -21,6 +21,7 @@ not (``x.requires_grad`` is False).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -28,6 +29,9 @@ import torch
 from zookeeper_amd.nn.layers import same_padding
 from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
                                         zeroed_scratch)
+
+# ZK_STEM_FUSED=0 selects the materialising kernels of stem.hip (A/B runs).
+_FUSED = os.environ.get("ZK_STEM_FUSED", "1") != "0"
 
 
 def supported(x: torch.Tensor, conv, bn1, pool_k: int, pool_s: int) -> bool:
@@ -37,6 +41,14 @@ def supported(x: torch.Tensor, conv, bn1, pool_k: int, pool_s: int) -> bool:
             and conv.padding == "same" and conv.bias is None and conv.groups == 1
             and conv.input_quantizer is None and conv.kernel_quantizer is None
             and pool_k * pool_k <= 255)
+
+
+def _fused_ok(KH, Cout, Cin, KW, s, pk, ps, Ho, Wo, pt2, pl2, H2, W2) -> bool:
+    """Geometry the recompute-fused kernels (stem_fused.hip) cover: 7-row
+    kernels, 64 output channels, stride 2, 3x3/2 'same' max pool."""
+    return (_FUSED and KH == 7 and Cout == 64 and Cin <= 4 and KW <= 8 and s == 2 and pk == 3
+            and ps == 2 and pt2 in (0, 1) and pl2 in (0, 1) and H2 == (Ho + pt2 + 1) // 2
+            and W2 == (Wo + pl2 + 1) // 2)
 
 
 def _bn_eval_coef(bn, C, dev):
@@ -97,38 +109,62 @@ class _StemFn(torch.autograd.Function):
         ws = torch.empty((KH, Cout, 32), dtype=torch.bfloat16, device=dev)
         check(L.zk_stem_pack_weight(w_ohwi.data_ptr(), ws.data_ptr(), Cout, KH, KW, Cin, st),
               "zk_stem_pack_weight")
-        y1 = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=dev)
-        part = torch.empty((L.zk_stem_max_parts(B, Ho, Wo), 2, Cout), dtype=torch.float32,
-                           device=dev)
-        nb = ctypes.c_int(0)  # number of partial-sum rows, written by the launcher
-        check(L.zk_stem_conv_fwd(xp.data_ptr(), ws.data_ptr(), y1.data_ptr(), part.data_ptr(), B,
-                                 Cin, Cout, KH, KW, s, Ho, Wo, Hp, Wp, -1, ctypes.byref(nb), st),
-              "zk_stem_conv_fwd")
+        pt2, pb2 = same_padding(Ho, pk, ps)
+        pl2, pr2 = same_padding(Wo, pk, ps)
+        H2, W2 = (Ho + pt2 + pb2 - pk) // ps + 1, (Wo + pl2 + pr2 - pk) // ps + 1
+        fused = _fused_ok(KH, Cout, Cin, KW, s, pk, ps, Ho, Wo, pt2, pl2, H2, W2)
         P1 = B * Ho * Wo
-        if bn1.training:
+        geo = (B, Cin, KW, Ho, Wo, Hp, Wp, H2, W2, pt2, pl2)
+
+        def finalize1(part, nb):
             coef1 = torch.empty((4, Cout), dtype=torch.float32, device=dev)
-            check(L.zk_bn_finalize_partials(part.data_ptr(), nb.value, Cout, float(P1),
+            check(L.zk_bn_finalize_partials(part.data_ptr(), nb, Cout, float(P1),
                                             g1.data_ptr() if g1 is not None else None,
                                             b1.data_ptr() if b1 is not None else None, bn1.eps,
                                             bn1.momentum, bn1.running_mean.data_ptr(),
                                             bn1.running_var.data_ptr(), coef1.data_ptr(), st),
                   "zk_bn_finalize_partials")
-        else:
-            coef1 = _bn_eval_coef(bn1, Cout, dev)
+            return coef1
 
-        pt2, pb2 = same_padding(Ho, pk, ps)
-        pl2, pr2 = same_padding(Wo, pk, ps)
-        H2, W2 = (Ho + pt2 + pb2 - pk) // ps + 1, (Wo + pl2 + pr2 - pk) // ps + 1
         p = torch.empty((B, H2, W2, Cout), dtype=torch.bfloat16, device=dev)
         arg = torch.empty((B, H2, W2, Cout), dtype=torch.uint8, device=dev)
         want_part2 = bn2 is not None and bn2.training
-        part2 = torch.empty((L.zk_stem_max_pool_parts(), 2, Cout), dtype=torch.float32,
-                            device=dev) if want_part2 else None
         nb2 = ctypes.c_int(0)
-        check(L.zk_stem_pool_fwd(y1.data_ptr(), coef1.data_ptr(), p.data_ptr(), arg.data_ptr(),
-                                 part2.data_ptr() if part2 is not None else None, B, Ho, Wo, Cout,
-                                 H2, W2, pk, ps, pt2, pl2, ctypes.byref(nb2), st),
-              "zk_stem_pool_fwd")
+        y1 = ya = None
+        if fused:
+            # conv recomputed in every pass: y1 never exists (stem_fused.hip)
+            if bn1.training:
+                part = torch.empty((L.zk_stem_fused_blocks(0, B, Ho, Wo, H2, W2), 2, Cout),
+                                   dtype=torch.float32, device=dev)
+                nb = ctypes.c_int(0)
+                check(L.zk_stem_fwd_stats(xp.data_ptr(), ws.data_ptr(), part.data_ptr(), *geo,
+                                          ctypes.byref(nb), st), "zk_stem_fwd_stats")
+                coef1 = finalize1(part, nb.value)
+            else:
+                coef1 = _bn_eval_coef(bn1, Cout, dev)
+            ya = torch.empty_like(p)
+            part2 = torch.empty((L.zk_stem_fused_blocks(1, B, Ho, Wo, H2, W2), 2, Cout),
+                                dtype=torch.float32, device=dev) if want_part2 else None
+            check(L.zk_stem_fwd_pool(xp.data_ptr(), ws.data_ptr(), coef1.data_ptr(),
+                                     p.data_ptr(), arg.data_ptr(), ya.data_ptr(),
+                                     part2.data_ptr() if part2 is not None else None, *geo,
+                                     ctypes.byref(nb2), st), "zk_stem_fwd_pool")
+        else:
+            y1 = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=dev)
+            part = torch.empty((L.zk_stem_max_parts(B, Ho, Wo), 2, Cout), dtype=torch.float32,
+                               device=dev)
+            nb = ctypes.c_int(0)  # number of partial-sum rows, written by the launcher
+            check(L.zk_stem_conv_fwd(xp.data_ptr(), ws.data_ptr(), y1.data_ptr(),
+                                     part.data_ptr(), B, Cin, Cout, KH, KW, s, Ho, Wo, Hp, Wp, -1,
+                                     ctypes.byref(nb), st), "zk_stem_conv_fwd")
+            coef1 = finalize1(part, nb.value) if bn1.training else _bn_eval_coef(bn1, Cout, dev)
+            part2 = torch.empty((L.zk_stem_max_pool_parts(), 2, Cout), dtype=torch.float32,
+                                device=dev) if want_part2 else None
+            check(L.zk_stem_pool_fwd(y1.data_ptr(), coef1.data_ptr(), p.data_ptr(),
+                                     arg.data_ptr(),
+                                     part2.data_ptr() if part2 is not None else None, B, Ho, Wo,
+                                     Cout, H2, W2, pk, ps, pt2, pl2, ctypes.byref(nb2), st),
+                  "zk_stem_pool_fwd")
         P2 = B * H2 * W2
         coef2 = None
         out = p
@@ -162,7 +198,9 @@ class _StemFn(torch.autograd.Function):
             else:
                 check(L.zk_bn_apply_bf16(p.data_ptr(), coef2.data_ptr(), out.data_ptr(), P2,
                                          Cout, 0, st), "zk_bn_apply_bf16")
-        ctx.save_for_backward(xp, y1, arg, p, coef1, coef2, g1, g2)
+        ctx.save_for_backward(xp, ws, y1 if y1 is not None else ya, arg, p, coef1, coef2, g1,
+                              g2)
+        ctx.fused = fused
         ctx.params = (weight, g1, b1, g2, b2)
         ctx.geom = (B, Cin, Cout, KH, KW, s, Ho, Wo, Hp, Wp, H2, W2, pk, ps, pt2, pl2)
         ctx.has_bn2 = bn2 is not None
@@ -171,7 +209,7 @@ class _StemFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        xp, y1, arg, p, coef1, coef2, g1, g2 = ctx.saved_tensors
+        xp, ws, y1, arg, p, coef1, coef2, g1, g2 = ctx.saved_tensors  # fused: y1 = ya
         weight, g1p, b1p, g2p, b2p = ctx.params
         (B, Cin, Cout, KH, KW, s, Ho, Wo, Hp, Wp, H2, W2, pk, ps, pt2, pl2) = ctx.geom
         dev = dout.device
@@ -193,19 +231,20 @@ class _StemFn(torch.autograd.Function):
         part = torch.empty((L.zk_stem_max_pool_parts(), 2, Cout), dtype=torch.float32,
                            device=dev)
         nb = ctypes.c_int(0)
-        check(L.zk_stem_pool_bwd_sums(dp.data_ptr(), arg.data_ptr(), y1.data_ptr(), p.data_ptr(),
-                                      coef1.data_ptr(), part.data_ptr(), B, Ho, Wo, Cout, H2, W2,
-                                      pk, ps, pt2, pl2, ctypes.byref(nb), st),
-              "zk_stem_pool_bwd_sums")
+        if ctx.fused:
+            check(L.zk_stem_pool_bwd_sums_ya(dp.data_ptr(), y1.data_ptr(), coef1.data_ptr(),
+                                             part.data_ptr(), P2, ctypes.byref(nb), st),
+                  "zk_stem_pool_bwd_sums_ya")
+        else:
+            check(L.zk_stem_pool_bwd_sums(dp.data_ptr(), arg.data_ptr(), y1.data_ptr(),
+                                          p.data_ptr(), coef1.data_ptr(), part.data_ptr(), B, Ho,
+                                          Wo, Cout, H2, W2, pk, ps, pt2, pl2, ctypes.byref(nb),
+                                          st), "zk_stem_pool_bwd_sums")
         sums1 = torch.empty((2, Cout), dtype=torch.float32, device=dev)
         check(L.zk_reduce_partials(part.data_ptr(), nb.value, 2 * Cout, sums1.data_ptr(), st),
               "zk_reduce_partials")
         P1 = B * Ho * Wo
         bcoef1, dg1, db1 = _bn_bwd_coef(L, st, sums1, coef1, g1p, b1p, P1, Cout, dev)
-        dy1 = torch.empty_like(y1)
-        check(L.zk_stem_dy1(dp.data_ptr(), arg.data_ptr(), y1.data_ptr(), coef1.data_ptr(),
-                            bcoef1.data_ptr(), dy1.data_ptr(), B, Ho, Wo, Cout, H2, W2, pk, ps,
-                            pt2, pl2, st), "zk_stem_dy1")
         dweight = None
         if ctx.needs_input_grad[1]:
             target = direct_grad(weight, channels_last=True)
@@ -213,8 +252,21 @@ class _StemFn(torch.autograd.Function):
                 dw = target.permute(0, 2, 3, 1)  # OHWI view of the flat gradient
             else:
                 dw = torch.zeros((Cout, KH, KW, Cin), dtype=torch.float32, device=dev)
-            check(L.zk_stem_wgrad(dy1.data_ptr(), xp.data_ptr(), dw.data_ptr(), B, Cin, Cout, KH,
-                                  KW, s, Ho, Wo, Hp, Wp, 0, st), "zk_stem_wgrad")
+            if ctx.fused:
+                nblk = L.zk_stem_fused_blocks(0, B, Ho, Wo, H2, W2)
+                slab = torch.empty((nblk, L.zk_stem_fused_slab_floats()), dtype=torch.float32,
+                                   device=dev)
+                check(L.zk_stem_bwd_fused(xp.data_ptr(), ws.data_ptr(), dp.data_ptr(),
+                                          arg.data_ptr(), coef1.data_ptr(), bcoef1.data_ptr(),
+                                          slab.data_ptr(), dw.data_ptr(), B, Cin, KW, Ho, Wo, Hp,
+                                          Wp, H2, W2, pt2, pl2, st), "zk_stem_bwd_fused")
+            else:
+                dy1 = torch.empty_like(y1)
+                check(L.zk_stem_dy1(dp.data_ptr(), arg.data_ptr(), y1.data_ptr(),
+                                    coef1.data_ptr(), bcoef1.data_ptr(), dy1.data_ptr(), B, Ho,
+                                    Wo, Cout, H2, W2, pk, ps, pt2, pl2, st), "zk_stem_dy1")
+                check(L.zk_stem_wgrad(dy1.data_ptr(), xp.data_ptr(), dw.data_ptr(), B, Cin, Cout,
+                                      KH, KW, s, Ho, Wo, Hp, Wp, 0, st), "zk_stem_wgrad")
             if target is not None:
                 grad_ready(weight)
             else:
