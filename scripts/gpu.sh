@@ -17,6 +17,8 @@
 #   profargs:<a,b>   rocprofv3 --kernel-trace --stats of bench.py with those arguments
 #   tune[:args]      tools/tune_bconv.py with the given (comma-separated) args
 #   py:<module>      python -m <module>  (tools, one-off diagnostics)
+#   pmcpy:<script,args>  PMC passes (SQ timing, SQ instruction mix, FETCH, WRITE)
+#                    over python3 <script> <args> (commas -> spaces)
 #   dpgloo:<n>       bench.py with n gloo ranks sharing the GPU (ordering rehearsal)
 #
 # A step that times out, aborts or faults ends the script (no GPU work after).
@@ -98,6 +100,18 @@ for spec in "$@"; do
         (cd /tmp && gpu_step 90 "$R/$OUT/pmcconv_${nm}_${tag}.log" timeout -s KILL 80 rocprofv3 --pmc $pass \
           -d "$R/$OUT/pmcconv_${nm}_${tag}" -o run --output-format csv -- python3 "$R/tools/one_conv.py" \
           --op "$a1" --shape "$a2" --reps 5) || exit $?
+      done
+      ;;
+    pmcpy)
+      # three PMC passes over `python3 <a1 with commas as spaces>`
+      R="$(pwd)"
+      script="${a1%%,*}"; rest=""; [ "$script" != "$a1" ] && rest="${a1#*,}"; rest="${rest//,/ }"
+      for pass in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT" \
+                  "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_MFMA_MOPS_BF16" \
+                  "FETCH_SIZE" "WRITE_SIZE"; do
+        tag=$(echo "$pass" | cut -d' ' -f1)
+        (cd /tmp && gpu_step 150 "$R/$OUT/pmcpy_${n}_${tag}.log" timeout -s KILL 140 rocprofv3 --pmc $pass \
+          -d "$R/$OUT/pmcpy_${n}_${tag}" -o run --output-format csv -- python3 "$R/$script" $rest) || exit $?
       done
       ;;
     tune)

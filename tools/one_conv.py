@@ -27,7 +27,20 @@ def main() -> None:
     from zookeeper_amd.nn.layers import same_padding
     from zookeeper_amd.ops._native import lib, stream_ptr
 
-    H, W, cin, cout, s = (int(v) for v in args.shape.split(","))
+    if args.shape == "all":
+        from zookeeper_amd.models.binary_resnet import stage_shapes
+
+        for shp in sorted(set(stage_shapes((224, 224, 3)))):
+            run_one(args, ",".join(str(v) for v in shp))
+        return
+    run_one(args, args.shape)
+
+
+def run_one(args, shape: str) -> None:
+    from zookeeper_amd.nn.layers import same_padding
+    from zookeeper_amd.ops._native import lib, stream_ptr
+
+    H, W, cin, cout, s = (int(v) for v in shape.split(","))
     B = args.batch
     L, st = lib(), stream_ptr()
     pt, pb = same_padding(H, 3, s)
@@ -76,7 +89,10 @@ def main() -> None:
         run()
     torch.cuda.synchronize()
     us = (time.perf_counter() - t0) / args.reps * 1e6
-    print(f"{args.op} {args.shape} v{args.variant}: {us:.1f} us/call", flush=True)
+    flops = 2.0 * B * Ho * Ho * cout * 9 * cin
+    print(f"{args.op} {shape} b{B} v{args.variant}: {us:.1f} us/call "
+          f"({flops / us / 1e9:.3f} PF/s) ZK_KORDER={os.environ.get('ZK_KORDER', '0')}",
+          flush=True)
 
 
 if __name__ == "__main__":

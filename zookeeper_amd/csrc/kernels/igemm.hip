@@ -26,6 +26,8 @@
 //     pixel rows) so every lane owns one pixel and 4 consecutive channels
 //     per register group: the epilogue moves 8 B per access;
 //   * XCD-aware tile order: consecutive M tiles of one N tile share an XCD.
+#include <stdlib.h>
+
 #include "mfma_common.h"
 
 namespace {
@@ -68,7 +70,20 @@ struct ConvArgs {
   const float* pmean;
   const float* prstd;
   float* psums;
+  // K-step order: 0 = tap-major (all channel chunks of a tap, then the next
+  // tap), 1 = channel-chunk-major (all taps of a chunk): the shifted
+  // activation rows of the taps are re-read while still in L2.
+  int korder;
 };
+
+int korder_env() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ZK_KORDER");
+    v = (e && *e) ? atoi(e) : 0;
+  }
+  return v;
+}
 
 // Reduce-scatter of 32 values over the 32 lanes of each wave half: after
 // the 5 butterfly steps lane r holds the half's total of value r (31
@@ -288,8 +303,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
   };
   // Issue the glds of K-step ks into ring slot ks % NS.
   int cur_tap = -1;
+  const int korder = args.korder;
   auto issue = [&](int ks) {
-    const int ti = ks / kchunks, kc = ks % kchunks;
+    const int ti = korder ? ks % T : ks / kchunks, kc = korder ? ks / T : ks % kchunks;
     if (ti != cur_tap) {
       set_tap(ti);
       cur_tap = ti;
@@ -598,8 +614,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
     }
   }
 
+  const int korder = args.korder;
   auto issue = [&](int ks) {
-    const int th = ks / kchunks, kc = ks % kchunks;
+    const int th = korder ? ks % 3 : ks / kchunks, kc = korder ? ks / 3 : ks % kchunks;
     const int dh = FWD ? th - 1 : 1 - th;
     unsigned char* st = smem + (ks % NS) * STAGE;
     const long long base = m0 + (long long)dh * W - 1;  // LDS row 0
@@ -649,7 +666,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
     __builtin_amdgcn_s_barrier();
     if (ks + NS - 1 < NK) issue(ks + NS - 1);
     const unsigned char* st = smem + (ks % NS) * STAGE;
-    const int th = ks / kchunks;
+    const int th = korder ? ks % 3 : ks / kchunks;
     uint32_t okh[TM];
 #pragma unroll
     for (int a = 0; a < TM; ++a) okh[a] = (vh[a] >> th) & 1u;
@@ -828,6 +845,8 @@ int launch_conv3(const ConvArgs& args, const IGeom& g, hipStream_t stream) {
   constexpr int LDS = NS * (AR + BR) * CB;
   static_assert(LDS <= 160 * 1024, "LDS");
   auto kern = igemm_conv3_kernel<FWD, BM, BN, WM, WN, NS, CB, F4>;
+  ConvArgs ka = args;
+  ka.korder = korder_env();
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -838,7 +857,7 @@ int launch_conv3(const ConvArgs& args, const IGeom& g, hipStream_t stream) {
   const long long M = (long long)g.B * g.H * g.W;
   const int m_tiles = (int)((M + BM - 1) / BM);
   hipLaunchKernelGGL(kern, dim3((unsigned)((long long)m_tiles * (NCH / BN))), dim3(NW * 64), LDS,
-                     stream, args, g, m_tiles);
+                     stream, ka, g, m_tiles);
   return 0;
 }
 
@@ -875,6 +894,7 @@ int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const v
                 (const uint16_t*)dres, dx, nullptr, 0, 0, bs.stripes,
                 (const int16_t*)bs.ypred, (const float*)bs.mean, (const float*)bs.rstd,
                 (float*)bs.sums};
+  args.korder = korder_env();
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, g.s * g.s), dim3(WM * WN * 64), LDS, stream,
                      args, g, m_tiles);
   return 0;
@@ -901,6 +921,7 @@ int launch_igemm_fwd(const void* sx, const void* wf, void* y, void* stats, const
   const long long blocks = (long long)m_tiles * (g.Cout / BN);
   ConvArgs args{(const uint16_t*)sx, (const uint16_t*)wf, nullptr, nullptr, y,
                 (unsigned long long*)stats, pad_ones, relu, stripes};
+  args.korder = korder_env();
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, 1), dim3(WM * WN * 64), LDS, stream, args, g,
                      m_tiles);
   return 0;
@@ -929,6 +950,7 @@ int launch_igemm_fwd_bf16(const void* x, const void* wf, void* y, const IGeom& g
   const long long blocks = (long long)m_tiles * (g.Cout / BN);
   ConvArgs args{(const uint16_t*)x, (const uint16_t*)wf, nullptr, nullptr, y, nullptr, 0, relu,
                 1};
+  args.korder = korder_env();
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, 1), dim3(WM * WN * 64), LDS, stream, args, g,
                      m_tiles);
   return 0;

@@ -137,6 +137,48 @@ __device__ __forceinline__ void conv_tile(const unsigned char* wl, const unsigne
   }
 }
 
+// Weight fragments of all 64 channels for every K-substep, in registers
+// (112 VGPRs): w[kh][sub][a] = chunk 2 sub + h of row 32a + lane%32 of kernel
+// row kh.
+__device__ __forceinline__ void load_wfrags(const unsigned char* ws, int lane,
+                                            uint4 (&w)[SKH][2][2]) {
+  const int r32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int kh = 0; kh < SKH; ++kh)
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+        w[kh][sub][a] = *reinterpret_cast<const uint4*>(
+            ws + (kh * SC + 32 * a + r32) * 64 + (2 * sub + h) * 16);
+}
+
+// conv_tile with the A operand (weights) from registers: one LDS read per
+// two MFMAs.
+template <int TR, int TC>
+__device__ __forceinline__ void conv_tile_wreg(const uint4 (&w)[SKH][2][2],
+                                               const unsigned char* lb, int px0, int lane,
+                                               f32x16 (&acc)[2]) {
+  using L = LBuf<TR, TC>;
+  const int r32 = lane & 31, h = lane >> 5;
+  int px = px0 + r32;
+  if (px >= TR * TC) px = 0;
+  const int rr = px / TC, cc = px - rr * TC;
+  const int segb = 2 * rr * L::RB + 16 * cc + 16 * h;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
+#pragma unroll
+  for (int kh = 0; kh < SKH; ++kh)
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const uint4 bf = *reinterpret_cast<const uint4*>(lb + segb + kh * L::RB + 32 * sub);
+#pragma unroll
+      for (int a = 0; a < 2; ++a) acc[a] = mfma_bf16(w[kh][sub][a], bf, acc[a]);
+    }
+}
+
 __device__ __forceinline__ float bf16r(float v) { return zk::bf16_to_f32(zk::f32_to_bf16(v)); }
 
 __device__ __forceinline__ void unpack8(const uint4& q, float (&v)[8]) {
@@ -193,14 +235,13 @@ __device__ __forceinline__ float rs32(float (&v)[32], int r32) {
 // ===========================================================================
 constexpr int F1_TR = 8, F1_TC = 16;
 constexpr int F1_LB = LBuf<F1_TR, F1_TC>::BYTES;
-constexpr int F1_LDS = W_BYTES + 2 * F1_LB;
+constexpr int F1_LDS = 2 * F1_LB;
 
 __global__ __launch_bounds__(256, 2) void stem_fwd_stats_kernel(
     const unsigned char* __restrict__ xp, const unsigned char* __restrict__ ws,
     float* __restrict__ part, FGeom g, int tiles_w, int tiles_img, int ntiles) {
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
-  unsigned char* wl = smem;
-  unsigned char* lbuf0 = smem + W_BYTES;
+  unsigned char* lbuf0 = smem;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r32 = lane & 31, h = lane >> 5;
   const int blk = xcd_linear(blockIdx.x, gridDim.x), nblk = gridDim.x;
@@ -217,13 +258,13 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_stats_kernel(
     tile_pos(blk, b, r0, c0);
     issue_lbuf<F1_TR, F1_TC, 256>(lbuf0, xp, g, b, r0, c0, tid);
   }
-  load_weights<256>(wl, ws, tid);
+  uint4 wf[SKH][2][2];
+  load_wfrags(ws, lane, wf);
 
-  float cs[2][16], cq[2][16];
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  f32x2 cs[16], cq[16];  // value pairs (a = 0, 1) of register r: packed adds / FMAs
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) cs[a][r] = cq[a][r] = 0.f;
+  for (int r = 0; r < 16; ++r) cs[r] = cq[r] = (f32x2){0.f, 0.f};
 
   int it = 0;
   for (int T = blk; T < ntiles; T += nblk, ++it) {
@@ -236,32 +277,39 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_stats_kernel(
       tile_pos(T + nblk, bn, rn, cn);
       issue_lbuf<F1_TR, F1_TC, 256>(lbuf0 + (cur ^ 1) * F1_LB, xp, g, bn, rn, cn, tid);
     }
-    f32x16 acc[2][1];
-    conv_tile<F1_TR, F1_TC, 1>(wl, lbuf0 + cur * F1_LB, 32 * wave, lane, acc);
-    const int px = 32 * wave + r32;
-    const int ho = r0 + px / F1_TC, wo = c0 + px % F1_TC;
-    const bool live = ho < g.Ho && wo < g.Wo;
+    f32x16 acc[2];
+    conv_tile_wreg<F1_TR, F1_TC>(wf, lbuf0 + cur * F1_LB, 32 * wave, lane, acc);
+    // statistics of the fp32 accumulators (the stored-bf16 rounding of
+    // stem.hip is below the statistics' own summation error)
+    if (r0 + F1_TR > g.Ho || c0 + F1_TC > g.Wo) {  // partial tile (uniform)
+      const int px = 32 * wave + r32;
+      const bool live = r0 + px / F1_TC < g.Ho && c0 + px % F1_TC < g.Wo;
+      if (!live) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float v = live ? bf16r(acc[a][0][r]) : 0.f;
-        cs[a][r] += v;
-        cq[a][r] += v * v;
+        for (int r = 0; r < 16; ++r) acc[0][r] = acc[1][r] = 0.f;
       }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const f32x2 v = {acc[0][r], acc[1][r]};
+      cs[r] += v;
+      cq[r] += v * v;
+    }
   }
 
   // channel co = 32a + 8(r>>2) + 4h + (r&3): reduce over the 32 pixel lanes
   float v[32];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[a * 16 + r] = cs[a][r];
+  for (int r = 0; r < 16; ++r) {
+    v[r] = cs[r].x;
+    v[16 + r] = cs[r].y;
+  }
   const float s_sum = rs32(v, r32);
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[a * 16 + r] = cq[a][r];
+  for (int r = 0; r < 16; ++r) {
+    v[r] = cq[r].x;
+    v[16 + r] = cq[r].y;
+  }
   const float s_sq = rs32(v, r32);
   // lane r32 holds value index i = r32 = a*16 + r
   const int a = r32 >> 4, r = r32 & 15;
@@ -281,36 +329,57 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_stats_kernel(
 
 // ===========================================================================
 // F2: conv -> relu(BN-1) -> 3x3/2 max pool.  Tile = 8 x 7 pool outputs, whose
-// windows cover a 17 x 15 conv region (255 pixels + 1 dummy = 4 waves x 64).
+// windows cover a 17 x 15 conv region (255 pixels + 1 dummy = 8 waves x 32).
 // Writes p (pooled), arg (tap of the first maximum), ya (y1 there) and
 // per-block BN-2 partial sums of p.  y1 of the region is staged in LDS
-// ([pixel][channel] bf16, chunk slot ^ ((m >> 1) & 7)).
+// ([pixel][channel] bf16, chunk slot ^ ((m >> 1) & 7)).  One block per CU,
+// the line buffer double-buffered and issued a whole tile ahead; every wave
+// issues exactly three output stores per tile (pool outputs outside the
+// image store to a sink), so the next tile waits for its line buffer with
+// vmcnt(3) instead of draining the stores.
 // ===========================================================================
 constexpr int F2_PR = 8, F2_PC = 7;
 constexpr int F2_TR = 2 * F2_PR + 1, F2_TC = 2 * F2_PC + 1;
 constexpr int F2_LB = LBuf<F2_TR, F2_TC>::BYTES;
 constexpr int F2_YT = 256 * 128;
-constexpr int F2_LDS = W_BYTES + F2_LB + F2_YT;
+constexpr int F2_NT = 512;
+constexpr int F2_LDS = W_BYTES + 2 * F2_LB + F2_YT;
 static_assert(F2_TR * F2_TC <= 256, "F2 region");
+static_assert(F2_PR * F2_PC * 8 <= F2_NT, "one pool item per thread");
+static_assert(F2_LDS <= 160 * 1024, "F2 LDS");
 
-__global__ __launch_bounds__(256, 2) void stem_fwd_pool_kernel(
+__device__ __attribute__((aligned(16))) uint4 g_pool_sink[2];
+
+__global__ __launch_bounds__(F2_NT, 1) void stem_fwd_pool_kernel(
     const unsigned char* __restrict__ xp, const unsigned char* __restrict__ ws,
     const float* __restrict__ coef1, uint16_t* __restrict__ p, uint8_t* __restrict__ arg,
     uint16_t* __restrict__ ya, float* __restrict__ part, FGeom g, int tiles_w, int tiles_img,
     int ntiles) {
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   unsigned char* wl = smem;
-  unsigned char* lb = smem + W_BYTES;
-  unsigned char* yt = smem + W_BYTES + F2_LB;
+  unsigned char* lb0 = smem + W_BYTES;
+  unsigned char* yt = smem + W_BYTES + 2 * F2_LB;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r32 = lane & 31, h = lane >> 5;
   const int blk = xcd_linear(blockIdx.x, gridDim.x), nblk = gridDim.x;
-  const int cg = tid & 7;  // fixed channel group of this thread in the pool phase
-  float a1[8], s1[8];
+  const int cg = tid & 7;  // channel group of this thread in the pool phase
+  const int po = tid >> 3;
+  const int pi = po / F2_PC, pj = po - (po / F2_PC) * F2_PC;
+  const bool pitem = po < F2_PR * F2_PC;
+  float a1[8], s1[8], sg[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     a1[k] = coef1[cg * 8 + k];
     s1[k] = coef1[SC + cg * 8 + k];
+    sg[k] = a1[k] < 0.f ? -1.f : 1.f;
+  }
+  uint4 flip;  // bf16 sign bits of the channels with a < 0
+  {
+    uint32_t f[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      f[q] = (a1[2 * q] < 0.f ? 0x8000u : 0u) | (a1[2 * q + 1] < 0.f ? 0x80000000u : 0u);
+    flip = make_uint4(f[0], f[1], f[2], f[3]);
   }
   auto tile_pos = [&](int T, int& b, int& oh0, int& ow0) {
     b = T / tiles_img;
@@ -319,94 +388,125 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_pool_kernel(
     oh0 = th * F2_PR;
     ow0 = (rem - th * tiles_w) * F2_PC;
   };
+  load_weights<F2_NT>(wl, ws, tid);
   if (blk < ntiles) {
     int b, oh0, ow0;
     tile_pos(blk, b, oh0, ow0);
-    issue_lbuf<F2_TR, F2_TC, 256>(lb, xp, g, b, 2 * oh0 - g.pt2, 2 * ow0 - g.pl2, tid);
+    issue_lbuf<F2_TR, F2_TC, F2_NT>(lb0, xp, g, b, 2 * oh0 - g.pt2, 2 * ow0 - g.pl2, tid);
   }
-  load_weights<256>(wl, ws, tid);
 
   float bs1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bs2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int T = blk; T < ntiles; T += nblk) {
-    tile_barrier();  // line buffer of T ready; last tile's pool reads of yt done
+  int it = 0;
+  for (int T = blk; T < ntiles; T += nblk, ++it) {
+    const int cur = it & 1;
+    // line buffer of T retired (the previous tile's 3 stores may stay in
+    // flight); the barrier also ends the previous pool phase's reads of yt
+    if (it == 0)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     int b, oh0, ow0;
     tile_pos(T, b, oh0, ow0);
-    f32x16 acc[2][2];
-    conv_tile<F2_TR, F2_TC, 2>(wl, lb, 64 * wave, lane, acc);
-    lds_barrier();  // every wave is done with the line buffer
     if (T + nblk < ntiles) {
       int bn, on, wn;
       tile_pos(T + nblk, bn, on, wn);
-      issue_lbuf<F2_TR, F2_TC, 256>(lb, xp, g, bn, 2 * on - g.pt2, 2 * wn - g.pl2, tid);
+      issue_lbuf<F2_TR, F2_TC, F2_NT>(lb0 + (cur ^ 1) * F2_LB, xp, g, bn, 2 * on - g.pt2,
+                                      2 * wn - g.pl2, tid);
     }
+    f32x16 acc[2][1];
+    conv_tile<F2_TR, F2_TC, 1>(wl, lb0 + cur * F2_LB, 32 * wave, lane, acc);
     // y1 (bf16) -> yt[m][co]: 4 consecutive channels per 8-B store
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int m = 64 * wave + 32 * t + r32;
+    {
+      const int m = 32 * wave + r32;
       const int swz = (m >> 1) & 7;
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int chunk = 4 * a + q;
-          const uint2 v = make_uint2(zk::pack_bf16x2(acc[a][t][4 * q], acc[a][t][4 * q + 1]),
-                                     zk::pack_bf16x2(acc[a][t][4 * q + 2], acc[a][t][4 * q + 3]));
+          const uint2 v = make_uint2(zk::pack_bf16x2(acc[a][0][4 * q], acc[a][0][4 * q + 1]),
+                                     zk::pack_bf16x2(acc[a][0][4 * q + 2], acc[a][0][4 * q + 3]));
           *reinterpret_cast<uint2*>(yt + m * 128 + ((chunk ^ swz) << 4) + 8 * h) = v;
         }
     }
     lds_barrier();
-    // pool: item = (pool output, channel group)
-    const int hr0 = 2 * oh0 - g.pt2, wc0 = 2 * ow0 - g.pl2;  // conv coords of region (0, 0)
-    for (int item = tid; item < F2_PR * F2_PC * 8; item += 256) {
-      const int po = item >> 3;
-      const int i = po / F2_PC, j = po - (po / F2_PC) * F2_PC;
+    // pool: one (pool output, channel group) per thread, branch-free
+    {
+      const int hr0 = 2 * oh0 - g.pt2, wc0 = 2 * ow0 - g.pl2;  // conv coords of region (0, 0)
+      const int i = pitem ? pi : 0, j = pitem ? pj : 0;
       const int oh = oh0 + i, ow = ow0 + j;
-      if (oh >= g.H2 || ow >= g.W2) continue;
+      const bool live = pitem && oh < g.H2 && ow < g.W2;
+      // relu(a y + s) is monotone in y (increasing for a >= 0, else
+      // decreasing), so the first maximum of the window is the first maximum
+      // of y ^ sign(a) (a sign flip on the packed bf16); ties at relu's 0 do
+      // not matter (they route no gradient).  Out-of-image taps read -inf.
+      uint4 tv[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int m = (2 * i + t / 3) * F2_TC + 2 * j + t % 3;
+        tv[t] = *reinterpret_cast<const uint4*>(yt + m * 128 + ((cg ^ ((m >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {  // y -> y * sign(a) on the packed bf16
+        tv[t].x ^= flip.x;
+        tv[t].y ^= flip.y;
+        tv[t].z ^= flip.z;
+        tv[t].w ^= flip.w;
+      }
+      const bool interior = hr0 + 2 * i >= 0 && hr0 + 2 * i + 2 < g.Ho && wc0 + 2 * j >= 0 &&
+                            wc0 + 2 * j + 2 < g.Wo;
+      if (!interior) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int hc = hr0 + 2 * i + t / 3, wc = wc0 + 2 * j + t % 3;
+          if (!(hc >= 0 && hc < g.Ho && wc >= 0 && wc < g.Wo))
+            tv[t] = make_uint4(0xFF80FF80u, 0xFF80FF80u, 0xFF80FF80u, 0xFF80FF80u);  // -inf
+        }
+      }
       float best[8], yb[8];
       uint32_t bi[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        best[k] = -1.f;
-        yb[k] = 0.f;
-        bi[k] = 0;
-      }
+      for (int k = 0; k < 8; ++k) bi[k] = 0;
+      unpack8(tv[0], best);
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int ti = t / 3, tj = t % 3;
-        const int hc = hr0 + 2 * i + ti, wc = wc0 + 2 * j + tj;
-        if (hc < 0 || hc >= g.Ho || wc < 0 || wc >= g.Wo) continue;
-        const int m = (2 * i + ti) * F2_TC + 2 * j + tj;
-        float yv[8];
-        unpack8(*reinterpret_cast<const uint4*>(yt + m * 128 + ((cg ^ ((m >> 1) & 7)) << 4)), yv);
+      for (int t = 1; t < 9; ++t) {
+        float v[8];
+        unpack8(tv[t], v);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float u = fmaxf(fmaf(a1[k], yv[k], s1[k]), 0.f);
-          if (u > best[k]) {
-            best[k] = u;
-            bi[k] = t;
-            yb[k] = yv[k];
-          }
+          const bool gt = v[k] > best[k];
+          best[k] = gt ? v[k] : best[k];
+          bi[k] = gt ? (uint32_t)t : bi[k];
         }
       }
-      const long long off = (((long long)b * g.H2 + oh) * g.W2 + ow) * SC + cg * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        yb[k] = best[k] * sg[k];
+        best[k] = fmaxf(fmaf(a1[k], yb[k], s1[k]), 0.f);
+      }
       const uint4 pk = pack8f(best);
-      *reinterpret_cast<uint4*>(p + off) = pk;
-      *reinterpret_cast<uint4*>(ya + off) = pack8f(yb);
-      *reinterpret_cast<uint2*>(arg + off) =
-          make_uint2(bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
-                     bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
+      const long long off = (((long long)b * g.H2 + oh) * g.W2 + ow) * SC + cg * 8;
+      uint4* dp_ = live ? reinterpret_cast<uint4*>(p + off) : &g_pool_sink[0];
+      uint4* dy_ = live ? reinterpret_cast<uint4*>(ya + off) : &g_pool_sink[1];
+      uint2* da_ = live ? reinterpret_cast<uint2*>(arg + off) : reinterpret_cast<uint2*>(&g_pool_sink[0]);
+      *dp_ = pk;
+      *dy_ = pack8f(yb);
+      *da_ = make_uint2(bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
+                        bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
       float st[8];
       unpack8(pk, st);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        bs1[k] += st[k];
-        bs2[k] += st[k] * st[k];
+        const float v = live ? st[k] : 0.f;
+        bs1[k] += v;
+        bs2[k] += v * v;
       }
     }
   }
   if (!part) return;
   __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);  // [256][2][8]
+  float* red = reinterpret_cast<float*>(smem);  // [512][2][8]
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     red[(tid * 2 + 0) * 8 + k] = bs1[k];
@@ -416,7 +516,7 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_pool_kernel(
   if (tid < 2 * SC) {
     const int which = tid / SC, c = tid % SC, g8 = c >> 3, k = c & 7;
     float t = 0.f;
-    for (int r = g8; r < 256; r += 8) t += red[(r * 2 + which) * 8 + k];
+    for (int r = g8; r < F2_NT; r += 8) t += red[(r * 2 + which) * 8 + k];
     part[((long long)blockIdx.x * 2 + which) * SC + c] = t;
   }
 }
@@ -596,7 +696,31 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
           aw[i][j][1] = av.y;
           gq[i][j] = *reinterpret_cast<const uint4*>(rt + o * 128 + cgp * 16);
         }
-#pragma unroll 1
+      // the four pixels' y1 and the channel coefficients, loads up front
+      uint4 yq[4];
+#pragma unroll
+      for (int pq = 0; pq < 4; ++pq) {
+        const int m = (2 * cr + (pq >> 1)) * B2_TC + 2 * cc + (pq & 1);
+        yq[pq] = *reinterpret_cast<const uint4*>(yt + m * 128 + ((cgp ^ tr_swz<128>(m)) << 4));
+      }
+      const float4* c4 = reinterpret_cast<const float4*>(cf + cgp * 8);
+      float ca[8], cs[8], k1[8], k0[8], k3[8];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const float4 v0 = c4[hf], v1 = c4[SC / 4 + hf], v2 = c4[2 * SC / 4 + hf],
+                     v3 = c4[3 * SC / 4 + hf], v4 = c4[4 * SC / 4 + hf];
+        ca[4 * hf] = v0.x; ca[4 * hf + 1] = v0.y; ca[4 * hf + 2] = v0.z; ca[4 * hf + 3] = v0.w;
+        cs[4 * hf] = v1.x; cs[4 * hf + 1] = v1.y; cs[4 * hf + 2] = v1.z; cs[4 * hf + 3] = v1.w;
+        k1[4 * hf] = v2.x; k1[4 * hf + 1] = v2.y; k1[4 * hf + 2] = v2.z; k1[4 * hf + 3] = v2.w;
+        k0[4 * hf] = v3.x; k0[4 * hf + 1] = v3.y; k0[4 * hf + 2] = v3.z; k0[4 * hf + 3] = v3.w;
+        k3[4 * hf] = v4.x; k3[4 * hf + 1] = v4.y; k3[4 * hf + 2] = v4.z; k3[4 * hf + 3] = v4.w;
+      }
+      float gv[2][2][8];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) unpack8(gq[i][j], gv[i][j]);
+#pragma unroll
       for (int pq = 0; pq < 4; ++pq) {
         const int dy = pq >> 1, dx = pq & 1;
         const int hh = r0 + 2 * cr + dy, ww = c0 + 2 * cc + dx;
@@ -605,37 +729,29 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            // tap of this pixel in the window of pool output (ohb+cr+i, owb+cc+j)
+            // tap of this pixel in the window of pool output (ohb+cr+i, owb+cc+j);
+            // the range test is uniform (pt2, pl2), the candidate's validity not
             const int th = dy + 2 - g.pt2 - 2 * i, tw = dx + 2 - g.pl2 - 2 * j;
-            if (!cv[i][j] || th < 0 || th > 2 || tw < 0 || tw > 2) continue;
+            if (th < 0 || th > 2 || tw < 0 || tw > 2) continue;
             const uint32_t t = th * 3 + tw;
-            float gv[8];
-            unpack8(gq[i][j], gv);
+            const uint32_t tm = cv[i][j] ? t : 0xFFu;  // 0xFF never matches a tap
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-              if (((aw[i][j][k >> 2] >> (8 * (k & 3))) & 0xff) == t) du[k] += gv[k];
+            for (int k = 0; k < 8; ++k) {
+              const bool hit = ((aw[i][j][k >> 2] >> (8 * (k & 3))) & 0xff) == tm;
+              du[k] += hit ? gv[i][j][k] : 0.f;
+            }
           }
         const int m = (2 * cr + dy) * B2_TC + 2 * cc + dx;
-        unsigned char* yp = yt + m * 128 + ((cgp ^ tr_swz<128>(m)) << 4);
         float yv[8], o8[8];
-        unpack8(*reinterpret_cast<const uint4*>(yp), yv);
+        unpack8(yq[pq], yv);
         const bool live = hh < g.Ho && ww < g.Wo;
-        const float4* c4 = reinterpret_cast<const float4*>(cf + cgp * 8);
 #pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-          const float4 ca = c4[hf], cs = c4[SC / 4 + hf], k1 = c4[2 * SC / 4 + hf],
-                       k0 = c4[3 * SC / 4 + hf], k3 = c4[4 * SC / 4 + hf];
-          const float a_[4] = {ca.x, ca.y, ca.z, ca.w}, s_[4] = {cs.x, cs.y, cs.z, cs.w};
-          const float k1_[4] = {k1.x, k1.y, k1.z, k1.w}, k0_[4] = {k0.x, k0.y, k0.z, k0.w};
-          const float k3_[4] = {k3.x, k3.y, k3.z, k3.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int k = 4 * hf + e;
-            const float u = fmaf(a_[e], yv[k], s_[e]);
-            o8[k] = live ? k1_[e] * (u > 0.f ? du[k] : 0.f) + k0_[e] - k3_[e] * yv[k] : 0.f;
-          }
+        for (int k = 0; k < 8; ++k) {
+          const float u = fmaf(ca[k], yv[k], cs[k]);
+          const float v = k1[k] * (u > 0.f ? du[k] : 0.f) + k0[k] - k3[k] * yv[k];
+          o8[k] = live ? v : 0.f;
         }
-        *reinterpret_cast<uint4*>(yp) = pack8f(o8);
+        *reinterpret_cast<uint4*>(yt + m * 128 + ((cgp ^ tr_swz<128>(m)) << 4)) = pack8f(o8);
       }
     }
     lds_barrier();
@@ -676,7 +792,8 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
   }
 }
 
-// dw OHWI [64][KH][KW][Cin] += sum over blocks of slab[blk][co][kh*32 + kw*4 + c]
+// dw OHWI [64][KH][KW][Cin] += sum over blocks of slab[blk][co][kh*32 + kw*4 + c]:
+// blockIdx.y takes every gridDim.y-th slab, one fp32 atomic per output each.
 __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __restrict__ slab,
                                                                 int nblk, float* __restrict__ dw,
                                                                 int KW, int Cin) {
@@ -685,9 +802,14 @@ __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __r
   const int j = i & 31, kh = (i >> 5) % SKH, co = i / (SKH * 32);
   const int kw = j >> 2, c = j & 3;
   if (kw >= KW || c >= Cin) return;
-  float t = 0.f;
-  for (int s = 0; s < nblk; ++s) t += slab[(long long)s * B2_NSLAB + i];
-  dw[((co * SKH + kh) * KW + kw) * Cin + c] += t;
+  float t[4] = {0.f, 0.f, 0.f, 0.f};
+  int s = blockIdx.y;
+  for (; s + 3 * (int)gridDim.y < nblk; s += 4 * gridDim.y) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[u] += slab[(long long)(s + u * gridDim.y) * B2_NSLAB + i];
+  }
+  for (; s < nblk; s += gridDim.y) t[0] += slab[(long long)s * B2_NSLAB + i];
+  atomicAdd(dw + ((co * SKH + kh) * KW + kw) * Cin + c, (t[0] + t[1]) + (t[2] + t[3]));
 }
 
 // B1 from the pooled side with the exact y1 at the argmax (F2's ya):
@@ -774,11 +896,11 @@ int grid_for(long long ntiles, int per_cu) {
 // Number of per-block partial rows / slabs a pass writes (host-side sizing).
 ZK_EXPORT int zk_stem_fused_blocks(int which, int B, int Ho, int Wo, int H2, int W2) {
   long long nt;
-  if (which == 1) {  // F2: pool tiles
+  if (which == 1) {  // F2: pool tiles, one block per CU
     nt = (long long)B * ((H2 + F2_PR - 1) / F2_PR) * ((W2 + F2_PC - 1) / F2_PC);
-  } else {  // F1 / B2: conv tiles
-    nt = (long long)B * ((Ho + 7) / 8) * ((Wo + 15) / 16);
+    return grid_for(nt, 1);
   }
+  nt = (long long)B * ((Ho + 7) / 8) * ((Wo + 15) / 16);  // F1 / B2: conv tiles
   return grid_for(nt, 2);
 }
 
@@ -811,10 +933,10 @@ ZK_EXPORT int zk_stem_fwd_pool(const void* xp, const void* ws, const void* coef1
   const int tw = (W2 + F2_PC - 1) / F2_PC, th = (H2 + F2_PR - 1) / F2_PR;
   const long long nt = (long long)B * th * tw;
   if (nt >= (1LL << 31)) return (int)hipErrorInvalidValue;
-  const int grid = grid_for(nt, 2);
+  const int grid = grid_for(nt, 1);
   if (nparts) *nparts = grid;
   if (int e = set_lds_once(stem_fwd_pool_kernel, F2_LDS)) return e;
-  hipLaunchKernelGGL(stem_fwd_pool_kernel, dim3(grid), dim3(256), F2_LDS, st,
+  hipLaunchKernelGGL(stem_fwd_pool_kernel, dim3(grid), dim3(F2_NT), F2_LDS, st,
                      (const unsigned char*)xp, (const unsigned char*)ws, (const float*)coef1,
                      (uint16_t*)p, (uint8_t*)arg, (uint16_t*)ya, (float*)part, g, tw, th * tw,
                      (int)nt);
@@ -853,8 +975,9 @@ ZK_EXPORT int zk_stem_bwd_fused(const void* xp, const void* ws, const void* dp, 
                      (const uint8_t*)arg, (const float*)coef1, (const float*)bcoef1,
                      (float*)slab, g, tw, th * tw, (int)nt);
   ZK_CHECK_LAUNCH();
-  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3((B2_NSLAB + 255) / 256), dim3(256), 0, st,
-                     (const float*)slab, grid, (float*)dw, KW, Cin);
+  const int groups = grid < 32 ? grid : 32;
+  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3((B2_NSLAB + 255) / 256, groups), dim3(256), 0,
+                     st, (const float*)slab, grid, (float*)dw, KW, Cin);
   ZK_CHECK_LAUNCH();
   return 0;
 }
