@@ -19,6 +19,7 @@ DGRAD: Dict[int, Tuple[int, int, bool]] = {
     4: (64, 128, False), 5: (64, 128, False), 6: (64, 128, False), 7: (64, 64, False),
     8: (64, 64, False), 9: (64, 128, False), 10: (128, 128, False), 11: (128, 64, False),
     12: (256, 64, False), 13: (256, 64, False), 14: (256, 128, False),
+    15: (256, 64, False), 16: (128, 64, False), 17: (256, 64, False),
     20: (64, 128, True), 21: (64, 64, True), 22: (64, 128, True), 23: (128, 64, True),
     24: (128, 64, True), 25: (256, 64, True), 26: (128, 64, True), 27: (64, 64, True),
     28: (64, 32, True), 29: (64, 32, True), 30: (64, 32, True), 31: (64, 64, True),

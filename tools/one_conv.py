@@ -40,7 +40,7 @@ def run_one(args, shape: str) -> None:
     from zookeeper_amd.nn.layers import same_padding
     from zookeeper_amd.ops._native import lib, stream_ptr
 
-    H, W, cin, cout, s = (int(v) for v in shape.split(","))
+    H, W, cin, cout, s = (int(v) for v in shape.replace("x", ",").split(","))
     B = args.batch
     L, st = lib(), stream_ptr()
     pt, pb = same_padding(H, 3, s)

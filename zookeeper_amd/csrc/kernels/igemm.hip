@@ -1072,6 +1072,10 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
     case 12: ZK_IGD(256, 256, 4, 2, 3, 64);   // 8 waves, 96 KB: 2x bytes/FLOP of 128x128
     case 13: ZK_IGD(256, 256, 2, 4, 3, 64);
     case 14: ZK_IGD(256, 256, 4, 2, 2, 128);  // 128 KB
+    // three K-steps of 32 channels in flight
+    case 15: ZK_IGD(256, 256, 4, 2, 4, 64);   // 128 KB
+    case 16: ZK_IGD(256, 128, 4, 2, 4, 64);   // 96 KB
+    case 17: ZK_IGD(128, 256, 2, 4, 4, 64);   // 96 KB
 #define ZK_IGD3(...)                                                                    \
   {                                                                                     \
     ConvArgs a{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,         \

@@ -133,9 +133,23 @@ def grad_ready(p) -> None:
         cb()
 
 
+# ZK_DEBUG_SYNC=1: synchronise the device after every native launch so a
+# kernel fault is reported at the launch that caused it (debugging only).
+_DEBUG_SYNC = os.environ.get("ZK_DEBUG_SYNC", "0") not in ("", "0")
+
+
 def check(code: int, what: str = "kernel") -> None:
     if code != 0:
         raise RuntimeError(f"{what} failed with hipError {code}")
+    if _DEBUG_SYNC:
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:
+            raise RuntimeError(f"{what}: device error after the launch: {e}") from None
+        log = os.environ.get("ZK_DEBUG_SYNC_LOG")
+        if log:
+            with open(log, "a") as f:
+                f.write(f"ok {what}\n")
 
 
 def gather_rows(src: np.ndarray, idx: np.ndarray, dst: torch.Tensor, threads: int = 8) -> None:

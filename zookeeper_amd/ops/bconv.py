@@ -34,6 +34,7 @@ from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stre
 def conv_supported(x: torch.Tensor, weight: torch.Tensor, stride, padding: str, groups: int,
                    bias: Optional[torch.Tensor] = None, pad_value: float = 0.0) -> bool:
     if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and weight.dim() == 4
+            and weight.device == x.device
             and groups == 1 and bias is None and pad_value in (0.0, 1.0)
             and padding in ("same", "valid")):
         return False

@@ -415,6 +415,11 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
         raise ValueError("binary_block needs Cin % 32 == 0 and Cout % 8 == 0")
     if conv.stride[0] != conv.stride[1]:
         raise ValueError("binary_block needs a square stride")
+    for name, t in (("conv.weight", conv.weight), ("bn.weight", bn.weight),
+                    ("residual", residual)):
+        if t is not None and t.device != x.device:
+            # a host pointer handed to a kernel faults the GPU instead of raising
+            raise ValueError(f"binary_block: {name} is on {t.device}, the input on {x.device}")
     identity = residual is x
     if residual is not None and not identity and residual.dtype != torch.bfloat16:
         residual = residual.to(torch.bfloat16)

@@ -47,6 +47,7 @@ def geometry(H: int, W: int, kh: int, kw: int, stride: int, padding: str) -> Tup
 def supported(x: torch.Tensor, weight: torch.Tensor, stride, padding: str, groups: int,
               bias: Optional[torch.Tensor] = None, pad_value: float = 0.0) -> bool:
     if not (ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and weight.device == x.device
             and weight.dim() == 4 and groups == 1 and bias is None and pad_value == 0.0):
         return False
     Cout, Cin, kh, kw = weight.shape

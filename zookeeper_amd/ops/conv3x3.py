@@ -36,6 +36,7 @@ ENABLED = os.environ.get("ZK_CONV3_MFMA", "1") != "0"
 def supported(x: torch.Tensor, weight: torch.Tensor, stride, padding: str, groups: int,
               bias: Optional[torch.Tensor] = None, pad_value: float = 0.0) -> bool:
     return (ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and weight.device == x.device
             and weight.dim() == 4 and tuple(weight.shape[2:]) == (3, 3) and groups == 1
             and tuple(stride) == (1, 1) and padding == "same" and pad_value == 0.0
             and bias is None and x.shape[1] == weight.shape[1]

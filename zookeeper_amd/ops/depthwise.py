@@ -17,6 +17,7 @@ from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, strea
 def supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
     C = x.shape[1]
     return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and C % 8 == 0
+            and weight.device == x.device
             and 256 % (C // 8) == 0 and tuple(weight.shape) == (C, 1, 3, 3)
             and weight.dtype == torch.float32)
 

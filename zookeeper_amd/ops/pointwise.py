@@ -36,6 +36,7 @@ _INF = float("inf")
 def supported(x: torch.Tensor, weight: torch.Tensor, stride, groups: int,
               bias: Optional[torch.Tensor] = None) -> bool:
     return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and weight.device == x.device
             and weight.dim() == 4 and weight.shape[2:] == (1, 1) and groups == 1
             and tuple(stride) == (1, 1) and x.shape[1] == weight.shape[1]
             and bias is None and x.shape[1] % 64 == 0 and weight.shape[0] % 64 == 0

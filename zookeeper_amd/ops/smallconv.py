@@ -35,6 +35,7 @@ def _geometry(H, W, kh, kw, s, padding):
 def supported(x: torch.Tensor, weight: torch.Tensor, stride, padding: str, groups: int,
               bias: Optional[torch.Tensor] = None, pad_value: float = 0.0) -> bool:
     if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and weight.dim() == 4
+            and weight.device == x.device
             and groups == 1 and bias is None and pad_value == 0.0 and padding in ("same", "valid")):
         return False
     Cout, Cin, kh, kw = weight.shape

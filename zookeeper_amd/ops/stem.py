@@ -37,6 +37,7 @@ _FUSED = os.environ.get("ZK_STEM_FUSED", "1") != "0"
 def supported(x: torch.Tensor, conv, bn1, pool_k: int, pool_s: int) -> bool:
     Cout, Cin, KH, KW = conv.weight.shape
     return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and not x.requires_grad
+            and conv.weight.device == x.device
             and Cin <= 4 and Cout == 64 and KH <= 8 and KW <= 8 and conv.stride == (2, 2)
             and conv.padding == "same" and conv.bias is None and conv.groups == 1
             and conv.input_quantizer is None and conv.kernel_quantizer is None
@@ -107,6 +108,17 @@ class _StemFn(torch.autograd.Function):
                                    st), "zk_stem_pack_input")
         w_ohwi = weight.detach().permute(0, 2, 3, 1).contiguous()
         ws = torch.empty((KH, Cout, 32), dtype=torch.bfloat16, device=dev)
+        if os.environ.get("ZK_DEBUG_STEM"):
+            for nm, t in (("x", x), ("xn", xn), ("xp", xp), ("weight", weight),
+                          ("w_ohwi", w_ohwi), ("ws", ws)):
+                st_ = t.untyped_storage()
+                print(f"[stem] {nm}: shape {tuple(t.shape)} stride {t.stride()} {t.dtype} "
+                      f"{t.device} ptr {t.data_ptr():#x} storage {st_.data_ptr():#x}+"
+                      f"{st_.nbytes()} offset {t.storage_offset()}", flush=True)
+            print(f"[stem] geom B={B} Cin={Cin} H={H} W={W} Cout={Cout} KH={KH} KW={KW} "
+                  f"Ho={Ho} Wo={Wo} Hp={Hp} Wp={Wp} pt={pt} pl={pl} stream={st:#x}", flush=True)
+            if os.environ.get("ZK_DEBUG_STEM") == "dry":
+                raise RuntimeError("ZK_DEBUG_STEM=dry: stopping before the stem kernels")
         check(L.zk_stem_pack_weight(w_ohwi.data_ptr(), ws.data_ptr(), Cout, KH, KW, Cin, st),
               "zk_stem_pack_weight")
         pt2, pb2 = same_padding(Ho, pk, ps)

@@ -10,6 +10,7 @@ the device until the metrics logger flushes.
 
 from __future__ import annotations
 
+import dataclasses
 import time
 from typing import Callable, Optional, Tuple, Union
 
@@ -41,6 +42,12 @@ class Trainer:
                  graph: Union[bool, str] = False, graph_warmup: int = 3,
                  comm_timing: bool = False, metric_fns: Optional[dict] = None):
         self.info = info or zdist.info()
+        if info is None and self.info.world == 1 and self.info.device.type == "cpu" \
+                and torch.cuda.is_available():
+            # single process without zdist.init(): train on the current GPU
+            # rather than silently moving the model to the host
+            self.info = dataclasses.replace(
+                self.info, device=torch.device("cuda", torch.cuda.current_device()))
         self.device = self.info.device
         self.model = prepare_model(model, self.device)
         self.model.train()
