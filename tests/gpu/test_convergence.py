@@ -2,8 +2,8 @@
 against the pure-PyTorch fp32 path on a learnable synthetic task.
 
 Task: 10 classes, each a fixed smooth random image (a class template); a
-sample is its class template plus Gaussian noise of 1.5x the template's
-scale.  Both runs start from the same weights, see the same batches and use
+sample is 0.3x its class template plus Gaussian noise of 2.5x the template's
+scale (hard enough that neither path saturates in 150 steps).  Both runs start from the same weights, see the same batches and use
 the same Adam settings (the reference trains BinaryNet with Keras Adam,
 examples/larq_experiment.py:118-122).  After ~150 steps the native run's
 held-out accuracy must be well above chance and within a stated tolerance of
@@ -38,9 +38,9 @@ def _templates(n_cls, hw, seed=123):
     return t / t.std()
 
 
-def _batch(tpl, n, gen, noise=1.5):
+def _batch(tpl, n, gen, signal=0.3, noise=2.5):
     y = torch.randint(0, tpl.shape[0], (n,), generator=gen)
-    x = tpl[y] + noise * torch.randn((n,) + tpl.shape[1:], generator=gen)
+    x = signal * tpl[y] + noise * torch.randn((n,) + tpl.shape[1:], generator=gen)
     return x, y
 
 
@@ -107,7 +107,7 @@ def test_native_training_matches_fp32(name):
     c_hip, acc_hip = _run(hip, torch.bfloat16, tpl, steps, batch, lr, seed=7, tag=f"{name} bf16")
     c_ref, acc_ref = _run(ref, torch.float32, tpl, steps, batch, lr, seed=7, tag=f"{name} fp32")
     rec = {"model": name, "steps": steps, "batch": batch, "lr": lr, "input": [hw, hw, 3],
-           "task": "10 smooth class templates + N(0, 1.5^2) noise",
+           "task": "0.3 x one of 10 smooth class templates + N(0, 2.5^2) noise",
            "native_bf16": {"loss": c_hip, "heldout_acc": acc_hip},
            "torch_fp32": {"loss": c_ref, "heldout_acc": acc_ref}}
     out_dir = os.environ.get("ZK_CURVE_DIR")
@@ -119,7 +119,7 @@ def test_native_training_matches_fp32(name):
           f"fp32 acc {acc_ref:.3f} (loss {c_ref[0]:.3f} -> {c_ref[-1]:.3f})")
     assert all(map(lambda v: v == v, c_hip)), "NaN loss"
     # well above chance (0.1) and within 0.1 (absolute) of the fp32 run
-    assert acc_hip >= 0.5, (acc_hip, acc_ref)
+    assert acc_hip >= 0.3, (acc_hip, acc_ref)
     assert acc_hip >= acc_ref - 0.1, (acc_hip, acc_ref)
-    # the loss fell on both paths
-    assert sum(c_hip[-10:]) < 0.6 * sum(c_hip[:10]), c_hip[::15]
+    # the loss fell on the native path
+    assert sum(c_hip[-10:]) < 0.8 * sum(c_hip[:10]), c_hip[::15]

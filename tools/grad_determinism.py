@@ -21,6 +21,7 @@ def main() -> None:
     ap.add_argument("--hw", type=int, default=64)
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--freeze", default="", help="comma list of parameter names to freeze")
     args = ap.parse_args()
     from zookeeper_amd.models.binary_resnet import BinaryResNetE
     from zookeeper_amd.parallel.flat import FlatParams
@@ -31,19 +32,27 @@ def main() -> None:
     dev = torch.device("cuda", 0)
     model = prepare_model(BinaryResNetE((args.hw, args.hw, 3), 10, 18, backend="hip"), dev)
     model.train()
+    for n, p_ in model.named_parameters():
+        if n in args.freeze.split(","):
+            p_.requires_grad_(False)
     flat = FlatParams(model, dev)
     loss_fn = get_loss("sparse_categorical_crossentropy")
     g = torch.Generator().manual_seed(99)
     x = torch.randn(args.batch, 3, args.hw, args.hw, generator=g).to(dev, torch.bfloat16)
     x = x.contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (args.batch,), generator=g).to(dev)
-    grads = []
+    grads, logits = [], []
     for _ in range(args.reps):
         flat.zero_grad()
-        loss, _ = loss_fn(model(x), y)
+        out = model(x)
+        logits.append(out.detach().float().clone())
+        loss, _ = loss_fn(out, y)
         loss.backward()
         torch.cuda.synchronize()
         grads.append(flat.grad.clone())
+    for i in range(1, args.reps):
+        print(f"rep {i}: logits max |diff| vs rep 0: {(logits[i] - logits[0]).abs().max().item():.3g}",
+              flush=True)
     ref = grads[0]
     for i, gi in enumerate(grads[1:], 1):
         rows = []

@@ -21,6 +21,8 @@ def main() -> None:
     ap.add_argument("--hw", type=int, default=224)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--fused", type=int, default=1)
+    ap.add_argument("--check", type=int, default=0,
+                    help="run fwd+bwd N times from the same state, report bitwise differences")
     args = ap.parse_args()
     import zookeeper_amd.ops.stem as stem_mod
     from zookeeper_amd.nn.layers import BatchNorm, ImageStem, MaxPool2d, QuantConv2d
@@ -35,6 +37,32 @@ def main() -> None:
     g = torch.randn_like(y)
     y.backward(g)
     torch.cuda.synchronize()
+    if args.check:
+        import copy
+        base = copy.deepcopy(stem.state_dict())
+        ref = None
+        for rep in range(args.check):
+            stem.load_state_dict(base)
+            for p_ in stem.parameters():
+                p_.grad = None
+            out = stem(x)
+            out.backward(g)
+            torch.cuda.synchronize()
+            cur = {"out": out.detach().clone(), "running": [b.clone() for b in stem.buffers()],
+                   **{n: p_.grad.clone() for n, p_ in stem.named_parameters()}}
+            if ref is None:
+                ref = cur
+                continue
+            diffs = []
+            for k in cur:
+                a, b = cur[k], ref[k]
+                if isinstance(a, list):
+                    d = max(((u.float() - v.float()).abs().max().item() for u, v in zip(a, b)),
+                            default=0.0)
+                else:
+                    d = (a.float() - b.float()).abs().max().item()
+                diffs.append(f"{k}={d:.3g}")
+            print(f"rep {rep}: max |diff| vs rep 0: " + " ".join(diffs), flush=True)
     t0 = time.perf_counter()
     for _ in range(args.reps):
         y = stem(x)

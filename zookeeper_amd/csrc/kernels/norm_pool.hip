@@ -160,7 +160,10 @@ __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __re
   }
 }
 
-template <int CG>
+// PARTS: per-block partial sums [block][2][C] with plain stores (summed in a
+// fixed order by zk_bn_bwd_coef with stripes = blocks: run-to-run
+// deterministic) instead of fp32 atomics into one [2][C] row.
+template <int CG, bool PARTS = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
     const uint16_t* __restrict__ g, const uint16_t* __restrict__ x,
     const uint16_t* __restrict__ y, const float* __restrict__ coef, float* __restrict__ sums,
@@ -219,8 +222,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
       a += red[0][rr * CG + c / 8][c % 8];
       b += red[1][rr * CG + c / 8][c % 8];
     }
-    atomicAdd(sums + c, a);
-    atomicAdd(sums + C + c, b);
+    if (PARTS) {
+      sums[(2LL * blockIdx.x) * C + c] = a;
+      sums[(2LL * blockIdx.x + 1) * C + c] = b;
+    } else {
+      atomicAdd(sums + c, a);
+      atomicAdd(sums + C + c, b);
+    }
   }
 }
 
@@ -502,6 +510,29 @@ ZK_EXPORT int zk_bn_bwd_reduce_bf16(const void* g, const void* x, const void* y,
     hipLaunchKernelGGL(bn_bwd_reduce_bf16_kernel<cg>, dim3(red_grid(P, C)), dim3(256), 0, st, \
                        (const uint16_t*)g, (const uint16_t*)x, (const uint16_t*)y,            \
                        (const float*)coef, (float*)sums, P);                                  \
+    break;
+  ZK_CG_CASES(C, CASE)
+#undef CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// Deterministic form: parts [zk_bn_bwd_parts_max()][2][C] receives one row
+// pair per block (*nparts of them); pass parts and *nparts as sums / stripes
+// to zk_bn_bwd_coef.
+ZK_EXPORT int zk_bn_bwd_parts_max() { return 512; }
+
+ZK_EXPORT int zk_bn_bwd_reduce_bf16_parts(const void* g, const void* x, const void* y,
+                                          const void* coef, void* parts, long long P, int C,
+                                          int* nparts, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const int grid = red_grid(P, C);
+  if (nparts) *nparts = grid;
+#define CASE(cg)                                                                           \
+  case cg:                                                                                 \
+    hipLaunchKernelGGL((bn_bwd_reduce_bf16_kernel<cg, true>), dim3(grid), dim3(256), 0, st, \
+                       (const uint16_t*)g, (const uint16_t*)x, (const uint16_t*)y,         \
+                       (const float*)coef, (float*)parts, P);                              \
     break;
   ZK_CG_CASES(C, CASE)
 #undef CASE

@@ -792,16 +792,16 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
   }
 }
 
-// dw OHWI [64][KH][KW][Cin] += sum over blocks of slab[blk][co][kh*32 + kw*4 + c]:
-// blockIdx.y takes every gridDim.y-th slab, one fp32 atomic per output each.
+// dw OHWI [64][KH][KW][Cin] += sum over blocks of slab[blk][co][kh*32 + kw*4 + c],
+// in a fixed order (run-to-run identical): pass 1 sums every gridDim.y-th slab
+// into tmp[blockIdx.y], pass 2 sums the groups in order and adds into dW.
+constexpr int B2_GROUPS = 32;
+
 __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __restrict__ slab,
-                                                                int nblk, float* __restrict__ dw,
-                                                                int KW, int Cin) {
+                                                                int nblk,
+                                                                float* __restrict__ tmp) {
   const int i = blockIdx.x * 256 + threadIdx.x;  // over SC * SKH * 32
   if (i >= B2_NSLAB) return;
-  const int j = i & 31, kh = (i >> 5) % SKH, co = i / (SKH * 32);
-  const int kw = j >> 2, c = j & 3;
-  if (kw >= KW || c >= Cin) return;
   float t[4] = {0.f, 0.f, 0.f, 0.f};
   int s = blockIdx.y;
   for (; s + 3 * (int)gridDim.y < nblk; s += 4 * gridDim.y) {
@@ -809,7 +809,21 @@ __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __r
     for (int u = 0; u < 4; ++u) t[u] += slab[(long long)(s + u * gridDim.y) * B2_NSLAB + i];
   }
   for (; s < nblk; s += gridDim.y) t[0] += slab[(long long)s * B2_NSLAB + i];
-  atomicAdd(dw + ((co * SKH + kh) * KW + kw) * Cin + c, (t[0] + t[1]) + (t[2] + t[3]));
+  tmp[(long long)blockIdx.y * B2_NSLAB + i] = (t[0] + t[1]) + (t[2] + t[3]);
+}
+
+__global__ __launch_bounds__(256) void stem_wgrad_reduce2_kernel(const float* __restrict__ tmp,
+                                                                 int groups,
+                                                                 float* __restrict__ dw, int KW,
+                                                                 int Cin) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B2_NSLAB) return;
+  const int j = i & 31, kh = (i >> 5) % SKH, co = i / (SKH * 32);
+  const int kw = j >> 2, c = j & 3;
+  if (kw >= KW || c >= Cin) return;
+  float t = 0.f;
+  for (int g = 0; g < groups; ++g) t += tmp[(long long)g * B2_NSLAB + i];
+  dw[((co * SKH + kh) * KW + kw) * Cin + c] += t;
 }
 
 // B1 from the pooled side with the exact y1 at the argmax (F2's ya):
@@ -905,6 +919,8 @@ ZK_EXPORT int zk_stem_fused_blocks(int which, int B, int Ho, int Wo, int H2, int
 }
 
 ZK_EXPORT int zk_stem_fused_slab_floats() { return B2_NSLAB; }
+// extra slab rows zk_stem_bwd_fused needs beyond one per block (reduction groups)
+ZK_EXPORT int zk_stem_fused_slab_extra() { return B2_GROUPS; }
 
 ZK_EXPORT int zk_stem_fwd_stats(const void* xp, const void* ws, void* part, int B, int Cin,
                                 int KW, int Ho, int Wo, int Hp, int Wp, int H2, int W2, int pt2,
@@ -957,8 +973,9 @@ ZK_EXPORT int zk_stem_pool_bwd_sums_ya(const void* dp, const void* ya, const voi
   return 0;
 }
 
-// slab: [zk_stem_fused_blocks(0, ...)][zk_stem_fused_slab_floats()] fp32
-// scratch; dw: OHWI fp32 gradient, accumulated.
+// slab: [zk_stem_fused_blocks(0, ...) + zk_stem_fused_slab_extra()]
+// [zk_stem_fused_slab_floats()] fp32 scratch; dw: OHWI fp32 gradient,
+// accumulated.
 ZK_EXPORT int zk_stem_bwd_fused(const void* xp, const void* ws, const void* dp, const void* arg,
                                 const void* coef1, const void* bcoef1, void* slab, void* dw,
                                 int B, int Cin, int KW, int Ho, int Wo, int Hp, int Wp, int H2,
@@ -975,9 +992,13 @@ ZK_EXPORT int zk_stem_bwd_fused(const void* xp, const void* ws, const void* dp, 
                      (const uint8_t*)arg, (const float*)coef1, (const float*)bcoef1,
                      (float*)slab, g, tw, th * tw, (int)nt);
   ZK_CHECK_LAUNCH();
-  const int groups = grid < 32 ? grid : 32;
+  const int groups = grid < B2_GROUPS ? grid : B2_GROUPS;
+  float* tmp = (float*)slab + (long long)grid * B2_NSLAB;
   hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3((B2_NSLAB + 255) / 256, groups), dim3(256), 0,
-                     st, (const float*)slab, grid, (float*)dw, KW, Cin);
+                     st, (const float*)slab, grid, tmp);
+  ZK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(stem_wgrad_reduce2_kernel, dim3((B2_NSLAB + 255) / 256), dim3(256), 0, st,
+                     (const float*)tmp, groups, (float*)dw, KW, Cin);
   ZK_CHECK_LAUNCH();
   return 0;
 }

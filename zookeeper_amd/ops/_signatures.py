@@ -57,6 +57,8 @@ SIGNATURES = {
     "zk_bn_apply_bf16_sign": (I32, [P, P, P, P, P, P, F32, I64, I32, I32, P]),
     "zk_bn_bwd_reduce_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
     "zk_bn_bwd_dx_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
+    "zk_bn_bwd_parts_max": (I32, []),
+    "zk_bn_bwd_reduce_bf16_parts": (I32, [P, P, P, P, P, I64, I32, IP, P]),
     # depthwise convolution
     "zk_dw_fwd": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_dw_dgrad": (I32, [P, P, P] + [I32] * 10 + [P]),
@@ -79,6 +81,7 @@ SIGNATURES = {
     # recompute-fused stem (stem_fused.hip)
     "zk_stem_fused_blocks": (I32, [I32] * 6),
     "zk_stem_fused_slab_floats": (I32, []),
+    "zk_stem_fused_slab_extra": (I32, []),
     "zk_stem_fwd_stats": (I32, [P, P, P] + [I32] * 11 + [IP, P]),
     "zk_stem_fwd_pool": (I32, [P] * 7 + [I32] * 11 + [IP, P]),
     "zk_stem_pool_bwd_sums_ya": (I32, [P, P, P, P, I64, IP, P]),

@@ -64,7 +64,7 @@ def _bn_eval_coef(bn, C, dev):
     return coef
 
 
-def _bn_bwd_coef(L, st, sums, coef, gamma_p, beta_p, P, C, dev):
+def _bn_bwd_coef(L, st, sums, coef, gamma_p, beta_p, P, C, dev, stripes: int = 1):
     """BN backward coefficients [k1, k0, k3]; γ/β gradients go into the flat
     buffer when the trainer manages it, else are returned."""
     dg = direct_grad(gamma_p) if gamma_p is not None else None
@@ -73,7 +73,8 @@ def _bn_bwd_coef(L, st, sums, coef, gamma_p, beta_p, P, C, dev):
     dbeta = db if db is not None else (torch.zeros(C, device=dev) if beta_p is not None else None)
     bcoef = torch.empty((3, C), dtype=torch.float32, device=dev)
     check(L.zk_bn_bwd_coef(sums.data_ptr(), coef[2].data_ptr(), coef[3].data_ptr(),
-                           gamma_p.data_ptr() if gamma_p is not None else None, float(P), C, 1,
+                           gamma_p.data_ptr() if gamma_p is not None else None, float(P), C,
+                           stripes,
                            bcoef.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
                            dbeta.data_ptr() if dbeta is not None else None, st), "zk_bn_bwd_coef")
     if dg is not None:
@@ -231,10 +232,18 @@ class _StemFn(torch.autograd.Function):
         g = dout.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
         dg2 = db2 = None
         if ctx.has_bn2:
-            sums2 = zeroed_scratch(ctx.bn2, "bwd_sums", (2, Cout), torch.float32, dev)
-            check(L.zk_bn_bwd_reduce_bf16(g.data_ptr(), p.data_ptr(), None, coef2.data_ptr(),
-                                          sums2.data_ptr(), P2, Cout, st), "zk_bn_bwd_reduce_bf16")
-            bcoef2, dg2, db2 = _bn_bwd_coef(L, st, sums2, coef2, g2p, b2p, P2, Cout, dev)
+            # per-block partials summed in a fixed order: the stem's BN-1 / conv
+            # gradients amplify run-to-run noise of these sums (BN-2 makes
+            # dL/dgamma1 a near-total cancellation)
+            sums2 = torch.empty((L.zk_bn_bwd_parts_max(), 2, Cout), dtype=torch.float32,
+                                device=dev)
+            nb2 = ctypes.c_int(0)
+            check(L.zk_bn_bwd_reduce_bf16_parts(g.data_ptr(), p.data_ptr(), None,
+                                                coef2.data_ptr(), sums2.data_ptr(), P2, Cout,
+                                                ctypes.byref(nb2), st),
+                  "zk_bn_bwd_reduce_bf16_parts")
+            bcoef2, dg2, db2 = _bn_bwd_coef(L, st, sums2, coef2, g2p, b2p, P2, Cout, dev,
+                                            stripes=nb2.value)
             dp = torch.empty_like(g)
             check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), p.data_ptr(), None, bcoef2.data_ptr(),
                                       dp.data_ptr(), P2, Cout, st), "zk_bn_bwd_dx_bf16")
@@ -255,6 +264,14 @@ class _StemFn(torch.autograd.Function):
         sums1 = torch.empty((2, Cout), dtype=torch.float32, device=dev)
         check(L.zk_reduce_partials(part.data_ptr(), nb.value, 2 * Cout, sums1.data_ptr(), st),
               "zk_reduce_partials")
+        if os.environ.get("ZK_DEBUG_STEM"):
+            torch.cuda.synchronize()
+
+            def cs(t):
+                return f"{t.double().sum().item():.9e}/{t.double().abs().sum().item():.9e}"
+            print(f"[stem bwd] g {cs(g)} dp {cs(dp)} y1 {cs(y1)} arg {cs(arg)} p {cs(p)} "
+                  f"coef1 {cs(coef1)} nb {nb.value} part {cs(part[:nb.value])} "
+                  f"sums1 {sums1.tolist()[0][:3]}", flush=True)
         P1 = B * Ho * Wo
         bcoef1, dg1, db1 = _bn_bwd_coef(L, st, sums1, coef1, g1p, b1p, P1, Cout, dev)
         dweight = None
@@ -266,7 +283,8 @@ class _StemFn(torch.autograd.Function):
                 dw = torch.zeros((Cout, KH, KW, Cin), dtype=torch.float32, device=dev)
             if ctx.fused:
                 nblk = L.zk_stem_fused_blocks(0, B, Ho, Wo, H2, W2)
-                slab = torch.empty((nblk, L.zk_stem_fused_slab_floats()), dtype=torch.float32,
+                slab = torch.empty((nblk + L.zk_stem_fused_slab_extra(),
+                                    L.zk_stem_fused_slab_floats()), dtype=torch.float32,
                                    device=dev)
                 check(L.zk_stem_bwd_fused(xp.data_ptr(), ws.data_ptr(), dp.data_ptr(),
                                           arg.data_ptr(), coef1.data_ptr(), bcoef1.data_ptr(),
