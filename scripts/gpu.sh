@@ -108,7 +108,7 @@ for spec in "$@"; do
       script="${a1%%,*}"; rest=""; [ "$script" != "$a1" ] && rest="${a1#*,}"; rest="${rest//,/ }"
       for pass in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT" \
                   "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_MFMA_MOPS_BF16" \
-                  "FETCH_SIZE" "WRITE_SIZE"; do
+                  "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"; do
         tag=$(echo "$pass" | cut -d' ' -f1)
         (cd /tmp && gpu_step 150 "$R/$OUT/pmcpy_${n}_${tag}.log" timeout -s KILL 140 rocprofv3 --pmc $pass \
           -d "$R/$OUT/pmcpy_${n}_${tag}" -o run --output-format csv -- python3 "$R/$script" $rest) || exit $?

@@ -22,6 +22,8 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--freeze", default="", help="comma list of parameter names to freeze")
+    ap.add_argument("--no-handoff", action="store_true",
+                    help="stem does not hand its sign images to the first block")
     args = ap.parse_args()
     from zookeeper_amd.models.binary_resnet import BinaryResNetE
     from zookeeper_amd.parallel.flat import FlatParams
@@ -32,6 +34,8 @@ def main() -> None:
     dev = torch.device("cuda", 0)
     model = prepare_model(BinaryResNetE((args.hw, args.hw, 3), 10, 18, backend="hip"), dev)
     model.train()
+    if args.no_handoff:
+        model.stem.sign_clip = None
     for n, p_ in model.named_parameters():
         if n in args.freeze.split(","):
             p_.requires_grad_(False)
@@ -41,7 +45,8 @@ def main() -> None:
     x = torch.randn(args.batch, 3, args.hw, args.hw, generator=g).to(dev, torch.bfloat16)
     x = x.contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (args.batch,), generator=g).to(dev)
-    grads, logits = [], []
+    grads, logits, stem_out = [], [], []
+    model.stem.register_forward_hook(lambda m, i, o: stem_out.append(o.detach().clone()))
     for _ in range(args.reps):
         flat.zero_grad()
         out = model(x)
@@ -51,7 +56,8 @@ def main() -> None:
         torch.cuda.synchronize()
         grads.append(flat.grad.clone())
     for i in range(1, args.reps):
-        print(f"rep {i}: logits max |diff| vs rep 0: {(logits[i] - logits[0]).abs().max().item():.3g}",
+        print(f"rep {i}: logits max |diff| vs rep 0: {(logits[i] - logits[0]).abs().max().item():.3g}"
+              f"  stem output: {(stem_out[i].float() - stem_out[0].float()).abs().max().item():.3g}",
               flush=True)
     ref = grads[0]
     for i, gi in enumerate(grads[1:], 1):
