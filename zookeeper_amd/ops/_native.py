@@ -134,14 +134,18 @@ def grad_ready(p) -> None:
 
 
 # ZK_DEBUG_SYNC=1: synchronise the device after every native launch so a
-# kernel fault is reported at the launch that caused it (debugging only).
-_DEBUG_SYNC = os.environ.get("ZK_DEBUG_SYNC", "0") not in ("", "0")
+# kernel fault is reported at the launch that caused it (debugging only);
+# ZK_DEBUG_SYNC=a,b: only after launches whose name contains a or b.
+_DEBUG_SYNC_ENV = os.environ.get("ZK_DEBUG_SYNC", "0")
+_DEBUG_SYNC = _DEBUG_SYNC_ENV not in ("", "0")
+_DEBUG_SYNC_ONLY = (tuple(x for x in _DEBUG_SYNC_ENV.split(",") if x)
+                    if _DEBUG_SYNC_ENV not in ("", "0", "1") else ())
 
 
 def check(code: int, what: str = "kernel") -> None:
     if code != 0:
         raise RuntimeError(f"{what} failed with hipError {code}")
-    if _DEBUG_SYNC:
+    if _DEBUG_SYNC and (not _DEBUG_SYNC_ONLY or any(x in what for x in _DEBUG_SYNC_ONLY)):
         try:
             torch.cuda.synchronize()
         except RuntimeError as e:
