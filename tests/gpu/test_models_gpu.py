@@ -67,6 +67,79 @@ def test_bn_residual_relu_matches_fp64(C, relu):
         assert err <= tol * (want.abs().max().item() + 1e-3), (err, want.abs().max().item())
 
 
+@pytest.mark.parametrize("C", [64, 256])
+def test_bn_relu_backward_recomputes_the_stored_mask(C):
+    """BN + ReLU without a residual keeps no output for the backward: the
+    ReLU mask is recomputed from x.  Pinned against the fp64 BN backward
+    taken through the mask of the STORED forward output (a mask element
+    recomputed differently moves dx by ~|g|, far above the tolerance)."""
+    from zookeeper_amd.nn.layers import BatchNorm
+    from zookeeper_amd.ops import norm_pool
+
+    torch.manual_seed(3)
+    bn = BatchNorm(C, 0.9, 1e-5).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(-1.5, 1.5)  # negative scales too
+        bn.bias.uniform_(-0.5, 0.5)
+    x = _cl(torch.randn(8, C, 10, 10, device="cuda").to(torch.bfloat16)).requires_grad_(True)
+    y = norm_pool.batch_norm(x, bn, relu=True)
+    g = torch.randn_like(y.float()).to(torch.bfloat16)
+    y.backward(g)
+    xd = x.detach().double()
+    n = xd.numel() // C
+    mean = xd.mean(dim=(0, 2, 3), keepdim=True)
+    var = xd.var(dim=(0, 2, 3), unbiased=False, keepdim=True)
+    rstd = (var + 1e-5).rsqrt()
+    xhat = (xd - mean) * rstd
+    gm = g.double() * (y.detach() > 0)
+    dbeta = gm.sum(dim=(0, 2, 3), keepdim=True)
+    dgamma = (gm * xhat).sum(dim=(0, 2, 3), keepdim=True)
+    w = bn.weight.detach().double().view(1, C, 1, 1)
+    dx = w * rstd / n * (n * gm - dbeta - xhat * dgamma)
+    for got, want in ((x.grad, dx), (bn.bias.grad, dbeta.flatten()),
+                      (bn.weight.grad, dgamma.flatten())):
+        err = (got.double() - want).abs().max().item()
+        assert err <= 2e-2 * (want.abs().max().item() + 1e-3), (err, want.abs().max().item())
+
+
+def test_bottleneck_residual_handoff_matches_autograd_sum(monkeypatch):
+    """Identity bottleneck: x's shortcut gradient added in conv1's dgrad
+    epilogue (norm_pool.ResidualHandoff) equals autograd's separate sum."""
+    from zookeeper_amd.models.resnet import Bottleneck
+    from zookeeper_amd.ops import norm_pool
+
+    torch.manual_seed(4)
+    blk = _prep(Bottleneck(256, 64, 1))
+    with torch.no_grad():
+        blk.bn3.weight.fill_(0.5)
+    x = _cl(torch.randn(4, 256, 14, 14, device="cuda").to(torch.bfloat16))
+    g = torch.randn(4, 256, 14, 14, device="cuda").to(torch.bfloat16)
+
+    def run():
+        xi = x.clone().requires_grad_(True)
+        for p in blk.parameters():
+            p.grad = None
+        blk(xi).backward(g)
+        return xi.grad.double(), [p.grad.double().clone() for p in blk.parameters()]
+
+    made = []
+    real = norm_pool.ResidualHandoff
+
+    def spy():
+        made.append(real())
+        return made[-1]
+
+    monkeypatch.setattr(norm_pool, "ResidualHandoff", spy)
+    gx, gp = run()
+    assert made and made[-1].dres is None  # created, filled and consumed
+    monkeypatch.setattr(norm_pool, "ResidualHandoff", lambda: None)
+    gx0, gp0 = run()
+    # one bf16 rounding of (dgrad + dres) instead of two
+    assert (gx - gx0).abs().max().item() <= 1e-2 * gx0.abs().max().item()
+    for a, b in zip(gp, gp0):
+        assert (a - b).abs().max().item() <= 1e-2 * (b.abs().max().item() + 1e-6)
+
+
 def _step(m, x, y):
     from zookeeper_amd.train.losses import softmax_cross_entropy
 

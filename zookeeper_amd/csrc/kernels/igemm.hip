@@ -171,8 +171,95 @@ __device__ __forceinline__ void dgrad_store_block(const ConvArgs& args, const IG
   }
 }
 
+// Coalesced dgrad epilogue through LDS (LE variants; no fused BN sums).
+// The masked fp32 fragments (lane = pixel, 4 consecutive channels per
+// register group) are staged half a tile of pixel rows at a time (row
+// groups a < TM/2, then the rest: [BM/2][BN] fp32 = BM * BN * 2 bytes,
+// 16-B chunk k of staged row r at slot k ^ (r % (BN/4))); then each thread
+// moves 8 channels = one 16-B bf16 chunk, consecutive lanes along a pixel
+// row, so dx stores and residual-gradient loads are whole contiguous rows
+// instead of 8 B per lane spread over 32 rows.  Same arithmetic as the
+// register epilogue (masked fp32 + residual, one rounding).  pix(m) maps a
+// tile row to its pixel.  The ring is free once every wave is past its last
+// fragment read (first barrier).
+template <int BM, int BN, int WM, int NT, int TM, int TN, typename PixFn>
+__device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeom& g,
+                                                const f32x16 (&acc)[TM][TN], unsigned char* smem,
+                                                long long m0, long long M, int n0, int wm,
+                                                int wcol0, int h, int r32, int tid, PixFn pix) {
+  constexpr int WTM = BM / WM, HT = TM / 2;
+  constexpr int NCH = BN / 4;  // 16-B fp32 chunks per staged row
+  static_assert(TM % 2 == 0 && (NCH & (NCH - 1)) == 0 && NCH >= 8, "LDS epilogue tiling");
+  const uint32_t* mask = args.mask;
+  uint32_t mw[TM][TN];
+  if (mask) {
+    const int CW = g.Cin >> 5;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const long long m = m0 + wm * WTM + a * 32 + r32;
+      const bool live = m < M;
+      const long long pm = live ? pix(m) : 0;
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        mw[a][b] = live ? mask[pm * CW + ((n0 + wcol0 + b * 32) >> 5)] : 0u;
+    }
+  }
+  uint16_t* dx = reinterpret_cast<uint16_t*>(args.out);
+  const uint16_t* dres = args.dres;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    __syncthreads();  // the ring (p = 0) / the previous half's tile is free
+#pragma unroll
+    for (int aa = 0; aa < HT; ++aa) {
+      const int a = p * HT + aa;
+      const int lr = wm * (WTM / 2) + aa * 32 + r32;
+      unsigned char* rb = smem + lr * (BN * 4);
+      const int sw = lr & (NCH - 1);
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int nl = 8 * q + 4 * h;
+          float4 v;
+          float* vp = reinterpret_cast<float*>(&v);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            vp[e] = (!mask || ((mw[a][b] >> (nl + e)) & 1u)) ? acc[a][b][4 * q + e] : 0.f;
+          const int k = (wcol0 + b * 32 + nl) >> 2;
+          *reinterpret_cast<float4*>(rb + ((k ^ sw) << 4)) = v;
+        }
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < (BM / 2) * (BN / 8); i += NT) {
+      const int lr = i / (BN / 8), j = i % (BN / 8);
+      const int row = (lr / (WTM / 2)) * WTM + (p * HT + (lr % (WTM / 2)) / 32) * 32 + lr % 32;
+      const long long m = m0 + row;
+      if (m >= M) continue;
+      const unsigned char* rb = smem + lr * (BN * 4);
+      const int sw = lr & (NCH - 1);
+      const float4 f0 = *reinterpret_cast<const float4*>(rb + (((2 * j) ^ sw) << 4));
+      const float4 f1 = *reinterpret_cast<const float4*>(rb + (((2 * j + 1) ^ sw) << 4));
+      float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+      const long long off = pix(m) * g.Cin + n0 + 8 * j;
+      if (dres) {
+        const uint4 d = *reinterpret_cast<const uint4*>(dres + off);
+        const uint32_t dd[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] += zk::bf16_to_f32((uint16_t)(dd[k] & 0xffff));
+          v[2 * k + 1] += zk::bf16_to_f32((uint16_t)(dd[k] >> 16));
+        }
+      }
+      *reinterpret_cast<uint4*>(dx + off) =
+          make_uint4(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
+                     zk::pack_bf16x2(v[4], v[5]), zk::pack_bf16x2(v[6], v[7]));
+    }
+  }
+}
+
 template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB, bool F4 = false,
-          bool OB = false>
+          bool OB = false, bool LE = false>
 __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs args, IGeom g,
                                                                      int m_tiles) {
   constexpr int NWAVES = WM * WN;
@@ -485,6 +572,17 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
         for (int a = 0; a < TM; ++a) ab[a] = acc[a][b];
         dgrad_store_block<TM>(args, g, ab, pix, n0 + wn * WTN + b * 32, h, r32);
       }
+    } else if constexpr (LE) {
+      static_assert(BM * BN * 2 <= NS * STAGE, "LDS epilogue: the ring holds half the tile");
+      const int W = g.W, H = g.H;
+      dgrad_store_lds<BM, BN, WM, NWAVES * 64, TM, TN>(
+          args, g, acc, smem, m0, M, n0, wm, wn * WTN, h, r32, tid,
+          [=](long long mc) -> long long {
+            if (s == 1) return mc;
+            const int jw = (int)(mc % Wc);
+            const long long rr = mc / Wc;
+            return ((rr / Hc) * H + (long long)(rr % Hc) * s + ph) * W + (long long)jw * s + pw;
+          });
     } else {
       uint16_t* dx = reinterpret_cast<uint16_t*>(args.out);
       const uint32_t* mask = args.mask;
@@ -870,15 +968,16 @@ struct BnSum {
   int stripes;
 };
 
-template <int BM, int BN, int WM, int WN, int NS, int CB = 128>
+template <int BM, int BN, int WM, int WN, int NS, int CB = 128, bool LE = false>
 int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const void* dres,
                        void* dx, const IGeom& g, const BnSum& bs, hipStream_t stream) {
+  if (LE && bs.sums) return (int)hipErrorInvalidValue;  // fused BN sums: register epilogue
   if ((g.Cout * 2) % CB || g.Cin % BN || g.s > 2 || g.kh > 4 || g.kw > 4)
     return (int)hipErrorInvalidValue;
   if (g_dry_run) return 0;
   constexpr int LDS = NS * (BM + BN) * CB;
   static_assert(LDS <= 160 * 1024, "LDS");
-  auto kern = igemm_conv_kernel<false, BM, BN, WM, WN, NS, CB>;
+  auto kern = igemm_conv_kernel<false, BM, BN, WM, WN, NS, CB, false, false, LE>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -1076,6 +1175,16 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
     case 15: ZK_IGD(256, 256, 4, 2, 4, 64);   // 128 KB
     case 16: ZK_IGD(256, 128, 4, 2, 4, 64);   // 96 KB
     case 17: ZK_IGD(128, 256, 2, 4, 4, 64);   // 96 KB
+    // coalesced LDS-staged epilogue (dgrad_store_lds): whole-row dx stores
+    case 40: ZK_IGD(128, 128, 2, 2, 2, 128, true);
+    case 41: ZK_IGD(128, 128, 2, 2, 4, 64, true);
+    case 42: ZK_IGD(128, 64, 2, 2, 2, 128, true);
+    case 43: ZK_IGD(128, 64, 2, 2, 4, 64, true);
+    case 44: ZK_IGD(256, 128, 4, 2, 2, 128, true);
+    case 45: ZK_IGD(256, 256, 4, 2, 2, 128, true);
+    case 46: ZK_IGD(256, 128, 4, 2, 4, 64, true);
+    case 47: ZK_IGD(128, 256, 2, 4, 4, 64, true);
+    case 48: ZK_IGD(128, 64, 2, 2, 3, 128, true);
 #define ZK_IGD3(...)                                                                    \
   {                                                                                     \
     ConvArgs a{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,         \
@@ -1671,12 +1780,21 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     // Batch >= 512 (profiles/r1av_bconv_tuning_b512.md): 256x256 also wins
     // for the 512-channel stride-1 and 256-channel stride-2 layers (7x7 x 512
     // images: 154 -> 121 us); smaller batches keep the batch-256 choices.
+    // 1x1 GEMMs (ResNet-50's bottleneck convs: K = 64..2048, mostly bound
+    // by the output bytes) and the 256x256 tiles use the coalesced
+    // LDS-staged epilogue (40+) unless the fused BN sums need the register
+    // one (tools/tune_pw.py, batch 512: 56x56 N256 K64 387 -> 334 us,
+    // 14x14 N1024 K256 144 -> 127 us, 28x28 N128 K512 139 -> 120 us).
     const int Cin = g.Cin, stride = g.s;
     const bool c3 = conv3_ok(g, 0);
-    if (Cin == 256 && stride == 1)
-      variant = 14;
+    const bool le = bs.sums == nullptr;
+    const int v256 = le ? 45 : 14;
+    if (le && g.kh == 1 && g.kw == 1 && stride == 1 && Cin % 64 == 0)
+      variant = Cin % 256 == 0 ? 45 : Cin % 128 == 0 ? 41 : 43;
+    else if (Cin == 256 && stride == 1)
+      variant = v256;
     else if (Cin >= 256 && Cin % 256 == 0 && g.B >= 512)
-      variant = 14;
+      variant = v256;
     else if (c3 && Cin == 512)
       variant = 24;
     else if (c3 && Cin == 128)

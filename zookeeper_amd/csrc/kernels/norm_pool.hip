@@ -105,6 +105,19 @@ __global__ void bn_finalize_f64_kernel(double* __restrict__ sums, int C, double 
   }
 }
 
+// BN pre-activation sc * x + sh + r: one expression shared by the forward
+// apply and the backward kernels that recompute the ReLU mask from x (same
+// contraction, so the recomputed bf16 output, and its sign, are bit-identical
+// to the stored one).
+__device__ __forceinline__ float bn_pre(float sc, float x, float sh, float r) {
+  return sc * x + sh + r;
+}
+
+// ReLU mask of the stored output bf16(max(v, 0)) from v: bf16(v) > 0.
+__device__ __forceinline__ bool relu_live(float v) {
+  return (int16_t)zk::f32_to_bf16(v) > 0;
+}
+
 template <int CG>
 __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __restrict__ x,
                                                             const float* __restrict__ coef,
@@ -132,7 +145,7 @@ __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __re
     if (res) load8_bf16(res + r * C + cg * 8, rv);  // residual added before the ReLU
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      v[k] = sc[k] * v[k] + sh[k] + rv[k];
+      v[k] = bn_pre(sc[k], v[k], sh[k], rv[k]);
       if (relu) v[k] = fmaxf(v[k], 0.f);
     }
     const uint32_t ow[4] = {zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
@@ -163,7 +176,9 @@ __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __re
 // PARTS: per-block partial sums [block][2][C] with plain stores (summed in a
 // fixed order by zk_bn_bwd_coef with stripes = blocks: run-to-run
 // deterministic) instead of fp32 atomics into one [2][C] row.
-template <int CG, bool PARTS = false>
+// RC: BN + ReLU without a stored output: the ReLU mask is recomputed from x
+// and the forward coefficients (relu_live(bn_pre(...))), saving a read of y.
+template <int CG, bool PARTS = false, bool RC = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
     const uint16_t* __restrict__ g, const uint16_t* __restrict__ x,
     const uint16_t* __restrict__ y, const float* __restrict__ coef, float* __restrict__ sums,
@@ -171,11 +186,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;
   const int cg = threadIdx.x % CG;
-  float mu[8], rs[8], sg[8], sgx[8];
+  float mu[8], rs[8], sg[8], sgx[8], fa[8], fs[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     mu[k] = coef[2 * C + cg * 8 + k];
     rs[k] = coef[3 * C + cg * 8 + k];
+    fa[k] = RC ? coef[cg * 8 + k] : 0.f;
+    fs[k] = RC ? coef[C + cg * 8 + k] : 0.f;
     sg[k] = sgx[k] = 0.f;
   }
   constexpr int UR = 4;  // rows in flight per thread (loads first, then math)
@@ -190,8 +207,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
       gq[u] = in ? *reinterpret_cast<const uint4*>(g + off) : make_uint4(0, 0, 0, 0);
       xq[u] = in ? *reinterpret_cast<const uint4*>(x + off) : make_uint4(0, 0, 0, 0);
       // fused ReLU: gradient only where the output was positive
-      yq[u] = (in && y) ? *reinterpret_cast<const uint4*>(y + off)
-                        : make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+      yq[u] = (!RC && in && y)
+                  ? *reinterpret_cast<const uint4*>(y + off)
+                  : make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
     }
 #pragma unroll
     for (int u = 0; u < UR; ++u) {
@@ -203,7 +221,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
         const int sh = 16 * (k & 1);
         float gk = zk::bf16_to_f32((uint16_t)(g4[k >> 1] >> sh));
         const float xk = zk::bf16_to_f32((uint16_t)(x4[k >> 1] >> sh));
-        if (!(zk::bf16_to_f32((uint16_t)(y4[k >> 1] >> sh)) > 0.f)) gk = 0.f;
+        if (RC) {
+          if (!relu_live(bn_pre(fa[k], xk, fs[k], 0.f))) gk = 0.f;
+        } else if (!(zk::bf16_to_f32((uint16_t)(y4[k >> 1] >> sh)) > 0.f)) {
+          gk = 0.f;
+        }
         sg[k] += gk;
         sgx[k] += gk * (xk - mu[k]) * rs[k];
       }
@@ -233,20 +255,24 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
 }
 
 // bcoef: [k1, k0, k3] x C with dx = k1*g' + k0 - k3*x
+// fcoef (forward coefficients, scale / shift rows): BN + ReLU with the mask
+// recomputed from x instead of read from y (see bn_bwd_reduce_bf16_kernel).
 template <int CG>
 __global__ __launch_bounds__(256) void bn_bwd_dx_bf16_kernel(
     const uint16_t* __restrict__ g, const uint16_t* __restrict__ x,
     const uint16_t* __restrict__ y, const float* __restrict__ bcoef, uint16_t* __restrict__ dx,
-    long long P, uint16_t* __restrict__ dres = nullptr) {
+    long long P, uint16_t* __restrict__ dres = nullptr, const float* __restrict__ fcoef = nullptr) {
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;
   const int cg = threadIdx.x % CG;
-  float k1[8], k0[8], k3[8];
+  float k1[8], k0[8], k3[8], fa[8], fs[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     k1[k] = bcoef[cg * 8 + k];
     k0[k] = bcoef[C + cg * 8 + k];
     k3[k] = bcoef[2 * C + cg * 8 + k];
+    fa[k] = fcoef ? fcoef[cg * 8 + k] : 0.f;
+    fs[k] = fcoef ? fcoef[C + cg * 8 + k] : 0.f;
   }
   for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
        r += (long long)gridDim.x * RB) {
@@ -258,6 +284,10 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_bf16_kernel(
       load8_bf16(y + r * C + cg * 8, yv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+    } else if (fcoef) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        gv[k] = relu_live(bn_pre(fa[k], xv[k], fs[k], 0.f)) ? gv[k] : 0.f;
     }
     // gradient of a residual added before the ReLU: the masked output gradient
     if (dres) store8_bf16(dres + r * C + cg * 8, gv);
@@ -548,6 +578,39 @@ ZK_EXPORT int zk_bn_bwd_dx_bf16(const void* g, const void* x, const void* y, con
     hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,   \
                        (const uint16_t*)g, (const uint16_t*)x, (const uint16_t*)y,           \
                        (const float*)bcoef, (uint16_t*)dx, P);                               \
+    break;
+  ZK_CG_CASES(C, CASE)
+#undef CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// BN + ReLU backward without the stored output: the ReLU mask is recomputed
+// from x and the forward coefficients coef [4][C] (scale, shift, mean, rstd).
+ZK_EXPORT int zk_bn_bwd_reduce_relu_bf16(const void* g, const void* x, const void* coef,
+                                         void* sums, long long P, int C, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+#define CASE(cg)                                                                         \
+  case cg:                                                                               \
+    hipLaunchKernelGGL((bn_bwd_reduce_bf16_kernel<cg, false, true>), dim3(red_grid(P, C)), \
+                       dim3(256), 0, st, (const uint16_t*)g, (const uint16_t*)x, nullptr, \
+                       (const float*)coef, (float*)sums, P);                             \
+    break;
+  ZK_CG_CASES(C, CASE)
+#undef CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_bn_bwd_dx_relu_bf16(const void* g, const void* x, const void* coef,
+                                     const void* bcoef, void* dx, long long P, int C,
+                                     hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+#define CASE(cg)                                                                             \
+  case cg:                                                                                   \
+    hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,   \
+                       (const uint16_t*)g, (const uint16_t*)x, nullptr, (const float*)bcoef, \
+                       (uint16_t*)dx, P, nullptr, (const float*)coef);                       \
     break;
   ZK_CG_CASES(C, CASE)
 #undef CASE

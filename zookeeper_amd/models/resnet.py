@@ -39,7 +39,15 @@ class Bottleneck(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idt = self.down(x) if self.down is not None else x
-        y = self.bn1(self.conv1(x))
+        handoff = None
+        if self.down is None and self.conv1.uses_pointwise(x):
+            from zookeeper_amd.ops import norm_pool
+
+            if norm_pool.supported(x):  # the tail's channels = x's (identity)
+                # x's two gradients (shortcut + main path) summed in conv1's
+                # data-gradient epilogue instead of a separate add pass
+                handoff = norm_pool.ResidualHandoff()
+        y = self.bn1(self.conv1(x, handoff=handoff) if handoff is not None else self.conv1(x))
         y = self.bn2(self.conv2(y))
         y = self.conv3(y)
         if _use_native(y):
@@ -47,7 +55,10 @@ class Bottleneck(nn.Module):
 
             if norm_pool.supported(y):
                 # relu(bn3(y) + shortcut) in one pass (and one pass back)
-                return norm_pool.batch_norm(y, self.bn3, relu=True, residual=idt)
+                return norm_pool.batch_norm(y, self.bn3, relu=True, residual=idt,
+                                            handoff=handoff)
+        if handoff is not None:
+            raise RuntimeError("residual hand-off without the native BN tail")
         return F.relu(self.bn3(y) + idt)
 
 

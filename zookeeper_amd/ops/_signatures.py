@@ -57,6 +57,8 @@ SIGNATURES = {
     "zk_bn_apply_bf16_sign": (I32, [P, P, P, P, P, P, F32, I64, I32, I32, P]),
     "zk_bn_bwd_reduce_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
     "zk_bn_bwd_dx_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
+    "zk_bn_bwd_reduce_relu_bf16": (I32, [P, P, P, P, I64, I32, P]),
+    "zk_bn_bwd_dx_relu_bf16": (I32, [P, P, P, P, P, I64, I32, P]),
     "zk_bn_bwd_parts_max": (I32, []),
     "zk_bn_bwd_reduce_bf16_parts": (I32, [P, P, P, P, P, I64, I32, IP, P]),
     # depthwise convolution

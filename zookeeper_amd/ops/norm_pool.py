@@ -32,7 +32,7 @@ def supported(x: torch.Tensor) -> bool:
 
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, bn, relu):
+    def forward(ctx, x, gamma, beta, residual, bn, relu, handoff=None):
         dim = x.dim()
         C = x.shape[1]
         xn = _nhwc(x)
@@ -67,7 +67,11 @@ class _BatchNormFn(torch.autograd.Function):
             check(L.zk_bn_apply_bf16(xn.data_ptr(), coef.data_ptr(), y.data_ptr(), P, C, int(relu),
                                      st), "zk_bn_apply_bf16")
         ctx.has_res = residual is not None
-        ctx.save_for_backward(xn, y if relu else None, coef, gamma)
+        ctx.handoff = handoff if residual is not None else None
+        # BN + ReLU without a residual keeps no output: the backward kernels
+        # recompute the ReLU mask from x (one read less in each of them)
+        ctx.relu_rc = relu and residual is None
+        ctx.save_for_backward(xn, y if (relu and residual is not None) else None, coef, gamma)
         ctx.params = (gamma, beta)
         ctx.dim, ctx.P, ctx.C = dim, P, C
         ctx.bn = bn
@@ -83,10 +87,15 @@ class _BatchNormFn(torch.autograd.Function):
         L = lib()
         g = _nhwc(dy.to(torch.bfloat16))
         sums = zeroed_scratch(ctx.bn, "bwd_sums", (2, C), torch.float32, dev)
-        check(L.zk_bn_bwd_reduce_bf16(g.data_ptr(), xn.data_ptr(),
-                                      y.data_ptr() if y is not None else None,
-                                      coef.data_ptr(), sums.data_ptr(), P, C, st),
-              "zk_bn_bwd_reduce_bf16")
+        if ctx.relu_rc:
+            check(L.zk_bn_bwd_reduce_relu_bf16(g.data_ptr(), xn.data_ptr(), coef.data_ptr(),
+                                               sums.data_ptr(), P, C, st),
+                  "zk_bn_bwd_reduce_relu_bf16")
+        else:
+            check(L.zk_bn_bwd_reduce_bf16(g.data_ptr(), xn.data_ptr(),
+                                          y.data_ptr() if y is not None else None,
+                                          coef.data_ptr(), sums.data_ptr(), P, C, st),
+                  "zk_bn_bwd_reduce_bf16")
         gamma_p, beta_p = ctx.params
         dg_direct = direct_grad(gamma_p) if ctx.has_gamma else None
         db_direct = direct_grad(beta_p) if ctx.has_beta else None
@@ -114,19 +123,51 @@ class _BatchNormFn(torch.autograd.Function):
                                           y.data_ptr() if y is not None else None,
                                           bcoef.data_ptr(), dx.data_ptr(), dres.data_ptr(), P, C,
                                           st), "zk_bn_bwd_dx_res_bf16")
-            dres = _back(dres, ctx.dim)
+            if ctx.handoff is not None:
+                # the residual's consumer adds it in its data-gradient epilogue
+                # (see ResidualHandoff): no separate gradient-accumulation pass
+                ctx.handoff.dres = dres
+                dres = None
+            else:
+                dres = _back(dres, ctx.dim)
+        elif ctx.relu_rc:
+            check(L.zk_bn_bwd_dx_relu_bf16(g.data_ptr(), xn.data_ptr(), coef.data_ptr(),
+                                           bcoef.data_ptr(), dx.data_ptr(), P, C, st),
+                  "zk_bn_bwd_dx_relu_bf16")
         else:
             check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), xn.data_ptr(),
                                       y.data_ptr() if y is not None else None, bcoef.data_ptr(),
                                       dx.data_ptr(), P, C, st), "zk_bn_bwd_dx_bf16")
-        return _back(dx, ctx.dim), dgamma, dbeta, dres, None, None
+        return _back(dx, ctx.dim), dgamma, dbeta, dres, None, None, None
+
+
+class ResidualHandoff:
+    """Gradient hand-off between a residual block's tail and the first layer
+    of its main path when both read the same tensor ``x`` (an identity
+    shortcut).  Autograd would sum the two gradients of ``x`` in a separate
+    elementwise pass (read both, write the sum); instead the tail's backward
+    (which runs first: the main path feeds it) leaves the shortcut's gradient
+    here and returns none for it, and the first layer's data-gradient kernel
+    adds it in its epilogue (``zk_igemm_dgrad``'s ``dres``).  Only valid when
+    that first layer computes the full gradient of ``x`` — the caller pairs a
+    handoff with a native layer it knows consumes it."""
+
+    __slots__ = ("dres",)
+
+    def __init__(self):
+        self.dres = None
+
+    def take(self):
+        d, self.dres = self.dres, None
+        return d
 
 
 def batch_norm(x: torch.Tensor, bn, relu: bool = False,
-               residual: torch.Tensor = None) -> torch.Tensor:
+               residual: torch.Tensor = None, handoff: ResidualHandoff = None) -> torch.Tensor:
     """``act(bn(x) [+ residual])`` in one pass (forward) / one pass (the
-    data gradient, plus the residual's gradient when given)."""
-    return _BatchNormFn.apply(x, bn.weight, bn.bias, residual, bn, relu)
+    data gradient, plus the residual's gradient when given — or left in
+    ``handoff`` for the residual's other consumer)."""
+    return _BatchNormFn.apply(x, bn.weight, bn.bias, residual, bn, relu, handoff)
 
 
 class _MaxPoolFn(torch.autograd.Function):

@@ -54,7 +54,7 @@ def _rows(x: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, handoff=None):
         B, Cin, H, W = x.shape
         Cout = weight.shape[0]
         x2 = _rows(x)
@@ -66,6 +66,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                                    stream_ptr(x.device)), "zk_igemm_dgrad(1x1 fwd)")
         ctx.save_for_backward(x2, w2)
         ctx.weight = weight
+        ctx.handoff = handoff
         ctx.shape = (B, Cin, H, W, Cout)
         return y2.view(B, H, W, Cout).permute(0, 3, 1, 2)
 
@@ -79,11 +80,17 @@ class _Conv1x1Fn(torch.autograd.Function):
         L = lib()
         st = stream_ptr(dev)
         dx = dweight = None
+        # + the identity shortcut's gradient of x (norm_pool.ResidualHandoff)
+        dres = ctx.handoff.take() if ctx.handoff is not None else None
         if ctx.needs_input_grad[0]:
             dx2 = torch.empty((g2.shape[0], Cin), dtype=torch.bfloat16, device=dev)
             wt = w2.t().contiguous()  # [Cin][Cout]
-            check(L.zk_igemm_dgrad(g2.data_ptr(), wt.data_ptr(), None, None, dx2.data_ptr(), B,
-                                   H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0, -1, st),
+            if dres is not None and tuple(dres.shape) != (B, H, W, Cin):
+                raise RuntimeError(f"residual gradient {tuple(dres.shape)} does not match the "
+                                   f"1x1 conv input {(B, H, W, Cin)}")
+            check(L.zk_igemm_dgrad(g2.data_ptr(), wt.data_ptr(), None,
+                                   dres.data_ptr() if dres is not None else None, dx2.data_ptr(),
+                                   B, H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0, -1, st),
                   "zk_igemm_dgrad(1x1)")
             dx = dx2.view(B, H, W, Cin).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
@@ -105,10 +112,12 @@ class _Conv1x1Fn(torch.autograd.Function):
                 grad_ready(weight)
             else:
                 dweight = dw.view(Cout, Cin, 1, 1)
-        return dx, dweight
+        return dx, dweight, None
 
 
-def conv1x1(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+def conv1x1(x: torch.Tensor, weight: torch.Tensor, handoff=None) -> torch.Tensor:
     """``F.conv2d(x, weight)`` for a 1×1 stride-1 kernel (see ``supported``),
-    as MFMA implicit GEMMs.  Returns a channels_last bf16 tensor."""
-    return _Conv1x1Fn.apply(x, weight)
+    as MFMA implicit GEMMs.  Returns a channels_last bf16 tensor.  With a
+    ``norm_pool.ResidualHandoff`` the data gradient also adds the gradient a
+    residual tail left there for the same input."""
+    return _Conv1x1Fn.apply(x, weight, handoff)
