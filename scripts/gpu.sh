@@ -15,11 +15,13 @@
 #                    pmcconv:dgrad:56,56,64,64,1
 #   benchargs:<a,b>  bench.py with arbitrary comma-separated arguments
 #   profargs:<a,b>   rocprofv3 --kernel-trace --stats of bench.py with those arguments
-#   tune[:args]      tools/tune_bconv.py with the given (comma-separated) args
+#   tune[:args]      tools/tune_bconv.py with the given (comma-separated) args; '+'
+#                    is a comma inside one argument (--igw,20+120)
 #   py:<module>      python -m <module>  (tools, one-off diagnostics)
 #   pmcpy:<script,args>  PMC passes (SQ timing, SQ instruction mix, FETCH, WRITE)
 #                    over python3 <script> <args> (commas -> spaces)
 #   dpgloo:<n>       bench.py with n gloo ranks sharing the GPU (ordering rehearsal)
+#   env:<VAR=VAL>    export VAR=VAL for the following steps (A/B switches)
 #
 # A step that times out, aborts or faults ends the script (no GPU work after).
 set -u
@@ -115,7 +117,8 @@ for spec in "$@"; do
       done
       ;;
     tune)
-      gpu_step 600 "$OUT/tune_${n}.log" python -u tools/tune_bconv.py ${a1//,/ } || exit $?
+      targs="${a1//,/ }"  # '+' stands for a comma inside one argument (--igw 20+120)
+      gpu_step 600 "$OUT/tune_${n}.log" python -u tools/tune_bconv.py ${targs//+/,} || exit $?
       ;;
     py)
       gpu_step 600 "$OUT/py_${n}.log" python -u -m "$a1" ${a2//,/ } || exit $?
@@ -123,6 +126,10 @@ for spec in "$@"; do
     dpgloo)
       ZK_DIST_BACKEND=gloo gpu_step 600 "$OUT/dpgloo_${n}.log" python -u bench.py \
         --gpus "${a1:-2}" --allow-shared-gpu --batch 64 --steps 10 --warmup 3 || exit $?
+      ;;
+    env)
+      export "${spec#env:}"
+      echo "env ${spec#env:}" >> "$PROG"
       ;;
     *)
       echo "unknown step $spec" >> "$PROG"; exit 2 ;;

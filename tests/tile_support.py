@@ -53,6 +53,17 @@ WGRAD: Dict[int, Tuple[int, int, bool]] = {
     33: (64, 64, True), 34: (128, 64, True),
 }
 
+# wgrad on the e2m1 sign image (zk_igemm_wgrad_f4): variant -> same tuple;
+# the tile of variant v - 100 (or its >= 3-stage form).
+WGRAD_F4: Dict[int, Tuple[int, int, bool]] = {
+    101: (128, 128, False), 102: (128, 192, False), 104: (128, 128, False), 107: (64, 64, False),
+    108: (256, 256, False), 109: (256, 256, False), 110: (256, 128, False), 111: (128, 128, False),
+    114: (128, 128, False), 118: (256, 256, False),
+    120: (64, 64, True), 121: (64, 64, True), 122: (128, 64, True), 123: (128, 64, True),
+    125: (64, 64, True),
+    126: (128, 128, True), 127: (64, 64, True), 128: (128, 64, True), 132: (128, 64, True),
+}
+
 
 def same_pad(hw: int, stride: int) -> Tuple[int, int]:
     out = -(-hw // stride)
@@ -83,9 +94,12 @@ def fwd_ok(v: int, cin: int, cout: int, stride: int) -> bool:
 
 
 def wgrad_ok(v: int, cin: int, cout: int, stride: int) -> bool:
-    if v not in WGRAD:
+    table = WGRAD_F4 if v >= 100 else WGRAD
+    if v not in table:
         return False
-    bm, bn, c3 = WGRAD[v]
+    bm, bn, c3 = table[v]
+    if v >= 100 and cin % 32:
+        return False
     if c3:
         return conv3_ok(stride) and cout % bm == 0 and cin % bn == 0
     return cout % bm == 0 and (9 * cin) % bn == 0 and cin % 8 == 0

@@ -180,16 +180,23 @@ def main():
                     torch.cuda.synchronize()
                     ref_dw = dw.clone()
         igw = [int(v) for v in args.igw.split(",")] if args.igw else IGW_VARIANTS
+        if "igw" in fam and any(v >= 100 for v in igw):
+            # e2m1 sign image for the F4B variants (zk_igemm_wgrad_f4)
+            sx4w = torch.empty(B, H, W, cin // 2, dtype=torch.uint8, device="cuda")
+            L.zk_sign_pack(x.data_ptr(), None, None, None, sx4w.data_ptr(), nwords, 1.0, st)
         for v in (igw if "igw" in fam else ()):
+            f4 = v >= 100
+            fn = L.zk_igemm_wgrad_f4 if f4 else L.zk_igemm_wgrad
+            sxp = sx4w.data_ptr() if f4 else sx.data_ptr()
             for tb in [int(t) for t in args.tbs.split(",")]:
                 dw.zero_()
-                nb = L.zk_igemm_wgrad_ws_bytes(B, cin, H, W, Ho, Ho, cout, 3, 3, s, pt, pt, tb, v)
+                nb = (L.zk_igemm_wgrad_f4_ws_bytes if f4 else L.zk_igemm_wgrad_ws_bytes)(
+                    B, cin, H, W, Ho, Ho, cout, 3, 3, s, pt, pt, tb, v)
                 wsb = torch.empty(max(nb, 4) // 4, device="cuda") if args.slab else None
                 wsp = wsb.data_ptr() if wsb is not None else None
                 wsn = wsb.numel() * 4 if wsb is not None else 0
-                rc = L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w.data_ptr(), dw.data_ptr(),
-                                      B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v,
-                                      wsp, wsn, st)
+                rc = fn(dy.data_ptr(), sxp, w.data_ptr(), dw.data_ptr(),
+                        B, H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v, wsp, wsn, st)
                 torch.cuda.synchronize()
                 if rc != 0:
                     row[f"igw_v{v}_tb{tb}_us"] = None
@@ -199,8 +206,8 @@ def main():
                 else:
                     row[f"igw_v{v}_tb{tb}_relerr"] = ((dw - ref_dw).abs().max() /
                                                       ref_dw.abs().max()).item()
-                row[f"igw_v{v}_tb{tb}_us"] = timeit(lambda: L.zk_igemm_wgrad(
-                    dy.data_ptr(), sx.data_ptr(), w.data_ptr(), dw.data_ptr(), B, H, W, cin, Ho,
+                row[f"igw_v{v}_tb{tb}_us"] = timeit(lambda: fn(
+                    dy.data_ptr(), sxp, w.data_ptr(), dw.data_ptr(), B, H, W, cin, Ho,
                     Ho, cout, 3, 3, s, pt, pt, 0, 1.0, tb, v, wsp, wsn, st), args.reps)
         # library reference: bf16 conv backward on unpacked ±1 operands
         xs = torch.where(x >= 0, 1.0, -1.0).to(torch.bfloat16).permute(0, 3, 1, 2)

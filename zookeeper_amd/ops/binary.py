@@ -55,6 +55,20 @@ STAT_STRIPES = 32
 # 256) the extra epilogue work on the latency-bound dgrad tiles cost more
 # (33.4k -> 31.0k img/s) than the separate reduce kernels it removes.
 FUSE_BNSUM = os.environ.get("ZK_FUSE_BNSUM", "0") == "1"
+# ZK_WGRAD_F4=1: weight gradients read the e2m1 sign image the MX-FP4
+# forward already uses (zk_igemm_wgrad_f4: a quarter of the sx bytes, DMA'd
+# beside dy and expanded to bf16 +-1 in LDS), and no bf16 sign image is
+# written at all.  Off by default: measured on MI355X (E18, batch 512) the
+# in-LDS expansion costs more than the bytes it saves -- 128x128 tiles
+# 217 -> 352 us, 256x256 170 -> 183 us, conv3 64-channel 183 -> 203 us
+# (tools/tune_bconv.py), whole step 40.6k -> 40.1k img/s.
+WGRAD_F4 = FP4 and os.environ.get("ZK_WGRAD_F4", "0") == "1"
+
+
+def bf16_sign_needed() -> bool:
+    """Whether producers of a binary block's input (BN epilogues, the stem)
+    must also write the bf16 +-1 sign image."""
+    return not WGRAD_F4
 
 
 class _BnSum:
@@ -110,9 +124,11 @@ class _BinaryBlockFn(torch.autograd.Function):
         # epilogue (zk_bn_apply_sign): reuse its sign images and STE mask.
         cached = getattr(x, "_zk_sign", None)
         sx4 = None
+        need_sx = mfma and not (fp4 and WGRAD_F4)  # bf16 sign image (wgrad / bf16 fwd)
         if (mfma and cached is not None and cached[0] == clip
-                and tuple(cached[1].shape) == (B, H, W, Cin)
-                and (not fp4 or (len(cached) > 3 and cached[3] is not None))):
+                and tuple(cached[2].shape) == (B * H * W * Cin // 32,)
+                and (not need_sx or cached[1] is not None)
+                and (not (fp4 or WGRAD_F4) or (len(cached) > 3 and cached[3] is not None))):
             bits, sx, mask = None, cached[1], cached[2]
             sx4 = cached[3] if fp4 else None
         else:
@@ -120,7 +136,7 @@ class _BinaryBlockFn(torch.autograd.Function):
             mask = torch.empty(nwords, dtype=torch.int32, device=dev)
             # bf16 image: the weight-gradient operand (and the bf16 forward's)
             sx = (torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
-                  if mfma and (will_backward or not fp4) else None)
+                  if need_sx and (will_backward or not fp4) else None)
             sx4 = (torch.empty((B, H, W, Cin // 2), dtype=torch.uint8, device=dev)
                    if fp4 else None)
             check(L.zk_sign_pack(xn.data_ptr(), bits.data_ptr() if bits is not None else None,
@@ -164,7 +180,7 @@ class _BinaryBlockFn(torch.autograd.Function):
                                  stride, pt, pl, Ho, Wo, int(pad_ones), int(act_relu), st),
                   "zk_bconv_fwd")
         if not will_backward:
-            sx = None
+            sx = sx4 = None
 
         scale = torch.empty(Cout, dtype=torch.float32, device=dev)
         shift = torch.empty_like(scale)
@@ -190,13 +206,15 @@ class _BinaryBlockFn(torch.autograd.Function):
         out = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=dev)
         if next_sign is not None and Cout % 64 == 0:
             # also quantise the output for the next binary block (same clip)
-            sx_next = torch.empty_like(out)
+            sx_next = torch.empty_like(out) if bf16_sign_needed() else None
             mask_next = torch.empty(P * Cout // 32, dtype=torch.int32, device=dev)
             sx4_next = (torch.empty((B, Ho, Wo, Cout // 2), dtype=torch.uint8, device=dev)
                         if FP4 else None)
             check(L.zk_bn_apply_sign(y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
                                      res.data_ptr() if res is not None else None,
-                                     out.data_ptr(), sx_next.data_ptr(), mask_next.data_ptr(),
+                                     out.data_ptr(),
+                                     sx_next.data_ptr() if sx_next is not None else None,
+                                     mask_next.data_ptr(),
                                      sx4_next.data_ptr() if sx4_next is not None else None,
                                      clip, P, Cout, st), "zk_bn_apply_sign")
             next_sign[:] = [clip, sx_next, mask_next, sx4_next]
@@ -215,7 +233,7 @@ class _BinaryBlockFn(torch.autograd.Function):
         pred = side.get("pred")
         ctx.pred = (pred if (pred is not None and identity and mfma
                              and tuple(pred.y.shape) == (B, H, W, Cin)) else None)
-        ctx.save_for_backward(bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx)
+        ctx.save_for_backward(bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx, sx4)
         ctx.params = (weight, gamma, beta)
         ctx.geom = (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo)
         ctx.meta = meta
@@ -226,7 +244,7 @@ class _BinaryBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx = ctx.saved_tensors
+        bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx, sx4 = ctx.saved_tensors
         (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
         (_, act_relu, clip, pad_ones, identity, _, _, _) = ctx.meta
         dev = dout.device
@@ -279,23 +297,26 @@ class _BinaryBlockFn(torch.autograd.Function):
             # then overlaps this block's dgrad and the next block's backward
             w_direct = direct_grad(weight_p, channels_last=True)
             dweight = None
-            side = streams.active() and w_direct is not None and sx is not None
+            f4 = WGRAD_F4 and sx4 is not None
+            sxw = sx4 if f4 else sx  # weight-gradient sign operand
+            side = streams.active() and w_direct is not None and sxw is not None
             if side:
                 sstream = streams.side_stream(dev)
                 ready = torch.cuda.Event()
                 ready.record()  # dy written (compute stream)
                 sstream.wait_event(ready)
                 with torch.cuda.stream(sstream):
-                    _wgrad(L, dy, sx, w_ohwi, w_direct.permute(0, 2, 3, 1), ctx, sstream.cuda_stream)
+                    _wgrad(L, dy, sxw, w_ohwi, w_direct.permute(0, 2, 3, 1), ctx,
+                           sstream.cuda_stream, f4)
                     done = torch.cuda.Event()
                     done.record(sstream)
-                for t in (dy, sx, w_ohwi):
+                for t in (dy, sxw, w_ohwi):
                     t.record_stream(sstream)
             else:
                 dw = (w_direct.permute(0, 2, 3, 1) if w_direct is not None  # OHWI view
                       else torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev))
-                if sx is not None:
-                    _wgrad(L, dy, sx, w_ohwi, dw, ctx, st)
+                if sxw is not None:
+                    _wgrad(L, dy, sxw, w_ohwi, dw, ctx, st, f4)
                 else:
                     check(L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w_ohwi.data_ptr(),
                                            dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
@@ -325,9 +346,10 @@ class _BinaryBlockFn(torch.autograd.Function):
                                            stride, pt, pl, -1, st), "zk_igemm_dgrad")
                 dx = dx.permute(0, 3, 1, 2)
             if side:
-                # earlier blocks' side-stream wgrads: order the compute stream
-                # after them (they overlapped this block) and signal readiness
-                streams.flush()
+                # earlier blocks' side-stream wgrads: signal their readiness
+                # (the bucketer's comm stream waits for their events; the
+                # compute stream only at the end of the backward)
+                streams.flush(wait=False)
                 streams.defer_ready(done, weight_p)
             elif w_direct is not None:
                 grad_ready(weight_p)
@@ -337,20 +359,22 @@ class _BinaryBlockFn(torch.autograd.Function):
         return dx, dres_out, dweight, dgamma, dbeta, None, None
 
 
-def _wgrad(L, dy, sx, w_ohwi, dw, ctx, st) -> None:
+def _wgrad(L, dy, sx, w_ohwi, dw, ctx, st, f4: bool = False) -> None:
     """Binary-conv weight gradient (dyᵀ ⊛ sign(x), kernel STE mask) added
     into ``dw`` (OHWI fp32) on stream ``st``: split-K partial sums go to a
-    workspace slab (plain stores) and one reduce kernel adds them, masked."""
+    workspace slab (plain stores) and one reduce kernel adds them, masked.
+    ``f4``: ``sx`` is the e2m1 sign image (zk_igemm_wgrad_f4)."""
     (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
     (_, _, clip, pad_ones) = ctx.meta[:4]
-    ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Ho, Wo, Cout, kh, kw, stride, pt, pl,
-                                         0, -1)
+    name = "zk_igemm_wgrad_f4" if f4 else "zk_igemm_wgrad"
+    ws_bytes = getattr(L, name + "_ws_bytes")(B, Cin, H, W, Ho, Wo, Cout, kh, kw, stride, pt,
+                                              pl, 0, -1)
     ws = (torch.empty(max(ws_bytes, 0) // 4, dtype=torch.float32, device=dy.device)
           if ws_bytes > 0 else None)
-    check(L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w_ohwi.data_ptr(), dw.data_ptr(), B, H,
+    check(getattr(L, name)(dy.data_ptr(), sx.data_ptr(), w_ohwi.data_ptr(), dw.data_ptr(), B, H,
                            W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl, int(pad_ones), clip, 0,
                            -1, ws.data_ptr() if ws is not None else None, max(ws_bytes, 0), st),
-          "zk_igemm_wgrad")
+          name)
 
 
 def _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx):

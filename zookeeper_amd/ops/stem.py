@@ -200,14 +200,15 @@ class _StemFn(torch.autograd.Function):
             out = torch.empty_like(p)
             if holder is not None and Cout % 32 == 0:
                 # also quantise the output for the first binary block
-                from zookeeper_amd.ops.binary import FP4
+                from zookeeper_amd.ops.binary import FP4, bf16_sign_needed
 
-                sx = torch.empty_like(p)
+                sx = torch.empty_like(p) if bf16_sign_needed() else None
                 mask = torch.empty(P2 * Cout // 32, dtype=torch.int32, device=dev)
                 sx4 = (torch.empty((B, H2, W2, Cout // 2), dtype=torch.uint8, device=dev)
                        if FP4 else None)
                 check(L.zk_bn_apply_bf16_sign(p.data_ptr(), coef2.data_ptr(), out.data_ptr(),
-                                              sx.data_ptr(), mask.data_ptr(),
+                                              sx.data_ptr() if sx is not None else None,
+                                              mask.data_ptr(),
                                               sx4.data_ptr() if sx4 is not None else None,
                                               sign_clip, P2, Cout, 0, st),
                       "zk_bn_apply_bf16_sign")

@@ -48,6 +48,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
+from zookeeper_amd.ops import streams as side_streams
 from zookeeper_amd.parallel.flat import FlatParams
 
 
@@ -160,6 +161,9 @@ class GradBucketer:
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(view.device))
         self.comm_stream.wait_event(ready)
+        # weight gradients still running on the side stream (ops/streams.py)
+        for ev in side_streams.unwaited_events():
+            self.comm_stream.wait_event(ev)
         with torch.cuda.stream(self.comm_stream):
             if self.timing:
                 ev = self._events()
