@@ -140,6 +140,41 @@ def test_bottleneck_residual_handoff_matches_autograd_sum(monkeypatch):
         assert (a - b).abs().max().item() <= 1e-2 * (b.abs().max().item() + 1e-6)
 
 
+def test_binary_transition_handoff_matches_autograd_sum(monkeypatch):
+    """E18 stage transition: x's binary-conv gradient handed to the shortcut
+    avg-pool's backward (zk_avgpool2_bwd_add) equals autograd's separate sum."""
+    from zookeeper_amd.models.binary_resnet import BinaryResBlock
+    from zookeeper_amd.ops import norm_pool
+
+    torch.manual_seed(5)
+    blk = _prep(BinaryResBlock(64, 128, 2, backend="hip"))
+    x = _cl(torch.randn(4, 64, 16, 16, device="cuda").to(torch.bfloat16))
+    g = torch.randn(4, 128, 8, 8, device="cuda").to(torch.bfloat16)
+
+    def run():
+        xi = x.clone().requires_grad_(True)
+        for p in blk.parameters():
+            p.grad = None
+        blk(xi).backward(g)
+        return xi.grad.double(), [p.grad.double().clone() for p in blk.parameters()]
+
+    made = []
+    real = norm_pool.ResidualHandoff
+
+    def spy():
+        made.append(real())
+        return made[-1]
+
+    monkeypatch.setattr(norm_pool, "ResidualHandoff", spy)
+    gx, gp = run()
+    assert made and made[-1].dres is None  # created, filled and consumed
+    monkeypatch.setattr(norm_pool, "ResidualHandoff", lambda: None)
+    gx0, gp0 = run()
+    assert (gx - gx0).abs().max().item() <= 1e-2 * gx0.abs().max().item()
+    for a, b in zip(gp, gp0):
+        assert (a - b).abs().max().item() <= 1e-2 * (b.abs().max().item() + 1e-6)
+
+
 def _step(m, x, y):
     from zookeeper_amd.train.losses import softmax_cross_entropy
 

@@ -415,9 +415,12 @@ __global__ __launch_bounds__(256) void avgpool2_fwd_kernel(const uint16_t* __res
   }
 }
 
+// add (optional, [B][H][W][C]): x's other gradient (a residual block's main
+// path, ops.binary_block's hand-off) summed in the same pass.
 __global__ __launch_bounds__(256) void avgpool2_bwd_kernel(const uint16_t* __restrict__ dy,
                                                            uint16_t* __restrict__ dx, int B,
-                                                           int H, int W, int C, int Ho, int Wo) {
+                                                           int H, int W, int C, int Ho, int Wo,
+                                                           const uint16_t* __restrict__ add) {
   const int CG = C / 8;
   const long long total = (long long)B * H * W * CG;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -432,6 +435,12 @@ __global__ __launch_bounds__(256) void avgpool2_bwd_kernel(const uint16_t* __res
       load8_bf16(dy + (((long long)b * Ho + (hi >> 1)) * Wo + (wi >> 1)) * C + cg * 8, v);
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] *= 0.25f;
+    }
+    if (add) {
+      float a[8];
+      load8_bf16(add + pix * C + cg * 8, a);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += a[q];
     }
     store8_bf16(dx + pix * C + cg * 8, v);
   }
@@ -691,7 +700,20 @@ ZK_EXPORT int zk_avgpool2_bwd(const void* dy, void* dx, int B, int H, int W, int
   if (C % 8) return (int)hipErrorInvalidValue;
   const long long work = (long long)B * H * W * (C / 8);
   hipLaunchKernelGGL(avgpool2_bwd_kernel, dim3(flat_grid(work)), dim3(256), 0, st,
-                     (const uint16_t*)dy, (uint16_t*)dx, B, H, W, C, Ho, Wo);
+                     (const uint16_t*)dy, (uint16_t*)dx, B, H, W, C, Ho, Wo, nullptr);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// zk_avgpool2_bwd + add ([B][H][W][C] bf16, the input's other gradient):
+// dx = upsample(dy) / 4 + add, one rounding.
+ZK_EXPORT int zk_avgpool2_bwd_add(const void* dy, const void* add, void* dx, int B, int H, int W,
+                                  int C, int Ho, int Wo, hipStream_t st) {
+  if (C % 8 || !add) return (int)hipErrorInvalidValue;
+  const long long work = (long long)B * H * W * (C / 8);
+  hipLaunchKernelGGL(avgpool2_bwd_kernel, dim3(flat_grid(work)), dim3(256), 0, st,
+                     (const uint16_t*)dy, (uint16_t*)dx, B, H, W, C, Ho, Wo,
+                     (const uint16_t*)add);
   ZK_CHECK_LAUNCH();
   return 0;
 }

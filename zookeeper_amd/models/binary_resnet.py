@@ -37,6 +37,7 @@ import torch.nn.functional as F
 from zookeeper_amd.core import Field, factory
 from zookeeper_amd.models.base import ModelFactory
 from zookeeper_amd.nn.layers import (
+    _use_native,
     AvgPool2d,
     BatchNorm,
     ImageStem,
@@ -74,11 +75,25 @@ class BinaryResBlock(nn.Module):
             )
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        residual = self.downsample(x) if self.downsample is not None else x
         if self.backend == "hip" and x.is_cuda:
             from zookeeper_amd import ops
+            from zookeeper_amd.ops import norm_pool
 
-            return ops.binary_block(x, residual, self.conv, self.bn)
+            handoff = None
+            if self.downsample is not None:
+                pool, conv, bn = self.downsample
+                if (_use_native(x) and x.shape[1] % 8 == 0 and pool.pool_size == (2, 2)
+                        and pool.stride == (2, 2)):
+                    # x's two gradients (shortcut avg-pool + binary conv) are
+                    # summed in the avg-pool backward instead of an add pass
+                    handoff = norm_pool.ResidualHandoff()
+                    residual = bn(conv(norm_pool.avg_pool2(x, handoff=handoff)))
+                else:
+                    residual = self.downsample(x)
+            else:
+                residual = x
+            return ops.binary_block(x, residual, self.conv, self.bn, dx_handoff=handoff)
+        residual = self.downsample(x) if self.downsample is not None else x
         return self.bn(self.conv(x)) + residual
 
 

@@ -344,7 +344,13 @@ class _BinaryBlockFn(torch.autograd.Function):
                                            dres.data_ptr() if dres is not None else None,
                                            dx.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
                                            stride, pt, pl, -1, st), "zk_igemm_dgrad")
-                dx = dx.permute(0, 3, 1, 2)
+                handoff = ctx.meta[7].get("dx_handoff")
+                if handoff is not None:
+                    # x's other consumer (the shortcut's avg-pool) adds it in
+                    # its backward, which runs after this one
+                    handoff.dres, dx = dx, None
+                else:
+                    dx = dx.permute(0, 3, 1, 2)
             if side:
                 # earlier blocks' side-stream wgrads: signal their readiness
                 # (the bucketer's comm stream waits for their events; the
@@ -419,7 +425,8 @@ def _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx):
 
 def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
                  act: Optional[str] = None, clip_value: float = 1.0,
-                 pad_value: float = 0.0, quantize_output: bool = True) -> torch.Tensor:
+                 pad_value: float = 0.0, quantize_output: bool = True,
+                 dx_handoff=None) -> torch.Tensor:
     """Run ``bn(act(conv(x))) + residual`` with the fused HIP kernels.
 
     ``conv`` must be a binary ``QuantConv2d`` (ste_sign input and kernel,
@@ -432,6 +439,11 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
     (attached to the returned tensor as ``_zk_sign`` = (clip, sx, mask, sx4);
     a block with the same clip value reuses them instead of re-reading its
     input).
+
+    ``dx_handoff`` (an ``ops.norm_pool.ResidualHandoff``): x's gradient is left
+    there instead of returned, for x's other consumer whose backward runs
+    after this one and adds it (a stage transition's shortcut
+    ``avg_pool2(x, handoff=...)``), saving autograd's separate add pass.
     """
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)
@@ -450,7 +462,7 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
     will_backward = torch.is_grad_enabled() and (
         x.requires_grad or conv.weight.requires_grad or bn.training)
     holder: list = [] if quantize_output else None
-    side = {"pred": getattr(x, "_zk_bnsum", None)}
+    side = {"pred": getattr(x, "_zk_bnsum", None), "dx_handoff": dx_handoff}
     meta = (conv.stride[0], act == "relu", float(clip_value), pad_value == 1.0, identity,
             will_backward, holder, side)
     out = _BinaryBlockFn.apply(x, None if identity else residual, conv.weight, bn.weight,

@@ -206,7 +206,7 @@ def max_pool(x: torch.Tensor, k: int, s: int, padding: str = "valid") -> torch.T
 
 class _AvgPool2Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, handoff=None):
         B, C, H, W = x.shape
         Ho, Wo = H // 2, W // 2
         xn = _nhwc(x)
@@ -214,6 +214,7 @@ class _AvgPool2Fn(torch.autograd.Function):
         check(lib().zk_avgpool2_fwd(xn.data_ptr(), y.data_ptr(), B, H, W, C, Ho, Wo,
                                     stream_ptr(x.device)), "zk_avgpool2_fwd")
         ctx.geom = (B, H, W, C, Ho, Wo)
+        ctx.handoff = handoff
         return y.permute(0, 3, 1, 2)
 
     @staticmethod
@@ -221,10 +222,23 @@ class _AvgPool2Fn(torch.autograd.Function):
         B, H, W, C, Ho, Wo = ctx.geom
         g = _nhwc(dy.to(torch.bfloat16))
         dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
-        check(lib().zk_avgpool2_bwd(g.data_ptr(), dx.data_ptr(), B, H, W, C, Ho, Wo,
-                                    stream_ptr(dy.device)), "zk_avgpool2_bwd")
-        return dx.permute(0, 3, 1, 2)
+        add = ctx.handoff.take() if ctx.handoff is not None else None
+        if add is not None:
+            # x's main-path gradient, left by the block that ran first
+            if tuple(add.shape) != (B, H, W, C) or not add.is_contiguous():
+                raise RuntimeError("avg_pool2: hand-off gradient has the wrong layout")
+            check(lib().zk_avgpool2_bwd_add(g.data_ptr(), add.data_ptr(), dx.data_ptr(), B, H, W,
+                                            C, Ho, Wo, stream_ptr(dy.device)),
+                  "zk_avgpool2_bwd_add")
+        else:
+            check(lib().zk_avgpool2_bwd(g.data_ptr(), dx.data_ptr(), B, H, W, C, Ho, Wo,
+                                        stream_ptr(dy.device)), "zk_avgpool2_bwd")
+        return dx.permute(0, 3, 1, 2), None
 
 
-def avg_pool2(x: torch.Tensor) -> torch.Tensor:
-    return _AvgPool2Fn.apply(x)
+def avg_pool2(x: torch.Tensor, handoff: "ResidualHandoff" = None) -> torch.Tensor:
+    """2x2/2 average pool.  ``handoff``: x's other gradient (left there by a
+    consumer whose backward runs first, e.g. ``ops.binary_block`` of a stage
+    transition) is added in the backward pass instead of autograd's separate
+    add."""
+    return _AvgPool2Fn.apply(x, handoff)
