@@ -6,7 +6,9 @@ or a thin feature map, where the 64-channel-chunked implicit GEMMs of
 * BinaryNet's first layer: float input, ``ste_sign`` ±1 kernel, 3×3
   ``valid`` (examples/larq_experiment.py:62-69) — the kernel's sign is taken
   when packing, its STE mask (``|w| ≤ 1``) applied in the weight gradient;
-* QuickNet's stem conv (3×3/2 over the image) and its 16→64 1×1 conv.
+* QuickNet's stem conv (3×3/2 over the image) and its 16→64 1×1 conv at
+  small image sizes (``supported`` sends outputs above ``_MAX_PIXELS`` back to
+  the library convolution, which is faster there).
 
 forward   im2col of a 128-pixel tile built in LDS, ``v_mfma_f32_16x16x32_bf16``
           over the whole K (padded to 32 / 64), bf16 NHWC out;
@@ -45,7 +47,21 @@ def supported(x: torch.Tensor, weight: torch.Tensor, stride, padding: str, group
         return False
     # a data gradient is only available for 1x1 stride-1 convs with Cout <= 64
     needs_dx = x.requires_grad and torch.is_grad_enabled()
-    return not needs_dx or (kh == kw == 1 and s[0] == 1 and Cout <= 64 and Cin % 16 == 0)
+    if needs_dx and not (kh == kw == 1 and s[0] == 1 and Cout <= 64 and Cin % 16 == 0):
+        return False
+    # Large images stay on the library convolution: at ImageNet size the
+    # split-K weight gradient (im2col built element by element, transposed
+    # 2-byte LDS stores) and the forward run far off the HBM roofline --
+    # measured on MI355X, QuickNetLarge batch 512: its stem convs took
+    # 3.05 ms (wgrad) + 1.21 ms (fwd) per step on these kernels (19.7k img/s)
+    # against ~0.7 ms for every library kernel together in round 1 (22.7k).
+    # BinaryNet's CIFAR-shape first layer (~0.23 M output pixels) keeps them.
+    B, _, H, W = x.shape
+    _, _, Ho, Wo = _geometry(H, W, kh, kw, s[0], padding)
+    return B * Ho * Wo <= _MAX_PIXELS
+
+
+_MAX_PIXELS = 1 << 20
 
 
 def _pack(w2: torch.Tensor, KP: int) -> torch.Tensor:
