@@ -2077,6 +2077,11 @@ void wgrad_defaults(const IGeom& g, int& variant, int& target_blocks) {
     } else if (big && g.kh == 3 && g.kw == 3 && g.Cin == 256 && g.Cout % 256 == 0) {
       variant = 8;
       if (target_blocks <= 0) target_blocks = 512;
+    } else if (big && g.kh == 3 && g.kw == 3 && g.Cin == 512 && g.Cout % 256 == 0) {
+      // 7x7x512 at batch 512: 256x256 tiles, 384 blocks 198 us vs 128x128
+      // at 2048 blocks 217-221 us (tools/tune_bconv.py --tbs 128..768)
+      variant = 8;
+      if (target_blocks <= 0) target_blocks = 384;
     } else if (g.Cin == 64 && g.s == 2 && g.Cout % 128 == 0 && (9 * g.Cin) % 192 == 0) {
       variant = 2;
       if (target_blocks <= 0) target_blocks = 512;
