@@ -65,6 +65,21 @@ if __name__ == "__main__":
 
         time.sleep(60)  # would hang; the launcher must terminate us
         sys.exit(0)
+    if mode == "hang":
+        # rank 1 hangs without ever joining the collective; rank 0's
+        # all-reduce must time out (ZK_DIST_TIMEOUT_S) and exit non-zero so
+        # the launcher tears the job down instead of waiting forever
+        import time
+
+        from zookeeper_amd.parallel import dist as zdist
+
+        zdist.init("gloo")
+        if rank == 1:
+            time.sleep(600)
+            sys.exit(0)
+        t = torch.ones(4)
+        torch.distributed.all_reduce(t)  # raises after the timeout
+        sys.exit(0)
     if mode == "bnsync":
         # BN running statistics drift apart per rank; all_reduce_buffers
         # must leave every rank with the cross-rank mean

@@ -43,6 +43,25 @@ def test_launcher_propagates_failure(tmp_path):
     assert _launch("fail", tmp_path) == 3
 
 
+@pytest.mark.timeout(120)
+def test_hung_rank_is_detected_by_the_collective_timeout(tmp_path):
+    """A rank that never reaches a collective: the others' collective times
+    out (ZK_DIST_TIMEOUT_S -> init_process_group(timeout=...)), they exit
+    non-zero and the launcher terminates the hung rank — the job ends in
+    seconds with a failure code instead of hanging."""
+    import time
+
+    from zookeeper_amd.parallel.launch import spawn
+
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", ZK_DIST_TIMEOUT_S="5")
+    env.pop("RANK", None)
+    t0 = time.monotonic()
+    rc = spawn([sys.executable, os.path.join(HERE, "dp_worker.py"), "hang", str(tmp_path)], 2,
+               env=env)
+    assert rc != 0
+    assert time.monotonic() - t0 < 90
+
+
 def test_bucketer_layout():
     import torch.nn as nn
 

@@ -41,7 +41,13 @@ def env_world() -> int:
 
 
 def init(backend: str = "auto", timeout_s: float = 600.0) -> DistInfo:
-    """Initialise (once) and return the rank / device binding."""
+    """Initialise (once) and return the rank / device binding.
+
+    ``timeout_s`` (overridden by ``ZK_DIST_TIMEOUT_S``) bounds every
+    collective: a rank that dies or hangs makes the others' collectives raise
+    after it instead of blocking forever, and the launcher then tears the job
+    down (failure detection)."""
+    timeout_s = float(os.environ.get("ZK_DIST_TIMEOUT_S", timeout_s))
     global _INFO
     if _INFO.backend != "none" or (dist.is_available() and dist.is_initialized()):
         return _INFO
