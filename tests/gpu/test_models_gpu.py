@@ -140,6 +140,60 @@ def test_bottleneck_residual_handoff_matches_autograd_sum(monkeypatch):
         assert (a - b).abs().max().item() <= 1e-2 * (b.abs().max().item() + 1e-6)
 
 
+@pytest.mark.parametrize("cin,width,stride,hw", [(64, 64, 1, 14), (256, 128, 2, 14)])
+def test_downsample_bottleneck_handoff_matches_autograd_sum(monkeypatch, cin, width, stride, hw):
+    """Downsampling bottleneck: conv1's input gradient handed to the shortcut
+    conv's data-gradient epilogue (1x1 pointwise at stride 1, the strided
+    conv kernel at stride 2) equals autograd's separate sum."""
+    from zookeeper_amd.models.resnet import Bottleneck
+    from zookeeper_amd.ops import norm_pool
+
+    torch.manual_seed(6)
+    blk = _prep(Bottleneck(cin, width, stride))
+    with torch.no_grad():
+        blk.bn3.weight.fill_(0.5)
+    x = _cl(torch.randn(4, cin, hw, hw, device="cuda").to(torch.bfloat16))
+    ho = hw // stride
+    g = torch.randn(4, width * 4, ho, ho, device="cuda").to(torch.bfloat16)
+
+    def run():
+        xi = x.clone().requires_grad_(True)
+        for p in blk.parameters():
+            p.grad = None
+        blk(xi).backward(g)
+        return xi.grad.double(), [p.grad.double().clone() for p in blk.parameters()]
+
+    made = []
+    real = norm_pool.ResidualHandoff
+
+    def spy():
+        made.append(real())
+        return made[-1]
+
+    monkeypatch.setattr(norm_pool, "ResidualHandoff", spy)
+    gx, gp = run()
+    # created, filled by conv1, consumed (closed) by the shortcut conv
+    assert made and made[-1].closed and made[-1].dres is None
+    monkeypatch.setattr(norm_pool, "ResidualHandoff", lambda: None)
+    gx0, gp0 = run()
+    assert (gx - gx0).abs().max().item() <= 1e-2 * gx0.abs().max().item()
+    for a, b in zip(gp, gp0):
+        assert (a - b).abs().max().item() <= 1e-2 * (b.abs().max().item() + 1e-6)
+
+
+def test_handoff_order_guard():
+    """A producer that runs after its consumer gets False from give() (the
+    gradient then goes back to autograd instead of being dropped)."""
+    from zookeeper_amd.ops.norm_pool import ResidualHandoff
+
+    h = ResidualHandoff()
+    assert h.take() is None and h.closed
+    assert h.give(torch.zeros(1)) is False and h.dres is None
+    h2 = ResidualHandoff()
+    t = torch.ones(2)
+    assert h2.give(t) is True and h2.take() is t
+
+
 def test_binary_transition_handoff_matches_autograd_sum(monkeypatch):
     """E18 stage transition: x's binary-conv gradient handed to the shortcut
     avg-pool's backward (zk_avgpool2_bwd_add) equals autograd's separate sum."""

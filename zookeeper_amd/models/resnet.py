@@ -38,16 +38,35 @@ class Bottleneck(nn.Module):
             )
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        idt = self.down(x) if self.down is not None else x
-        handoff = None
-        if self.down is None and self.conv1.uses_pointwise(x):
-            from zookeeper_amd.ops import norm_pool
+        handoff = give = None
+        if self.down is not None:
+            dconv, dbn = self.down
+            if self.conv1.uses_pointwise(x) and (dconv.uses_pointwise(x)
+                                                 or dconv.uses_native_conv(x)):
+                from zookeeper_amd.ops import norm_pool
 
-            if norm_pool.supported(x):  # the tail's channels = x's (identity)
-                # x's two gradients (shortcut + main path) summed in conv1's
-                # data-gradient epilogue instead of a separate add pass
-                handoff = norm_pool.ResidualHandoff()
-        y = self.bn1(self.conv1(x, handoff=handoff) if handoff is not None else self.conv1(x))
+                # x's two gradients (conv1 + shortcut conv) summed in the
+                # shortcut conv's data-gradient epilogue: conv1's backward
+                # runs first and leaves its gradient there
+                give = norm_pool.ResidualHandoff()
+                idt = dbn(dconv(x, handoff=give))
+            else:
+                idt = self.down(x)
+        else:
+            idt = x
+            if self.conv1.uses_pointwise(x):
+                from zookeeper_amd.ops import norm_pool
+
+                if norm_pool.supported(x):  # the tail's channels = x's (identity)
+                    # x's two gradients (shortcut + main path) summed in conv1's
+                    # data-gradient epilogue instead of a separate add pass
+                    handoff = norm_pool.ResidualHandoff()
+        if handoff is not None:
+            y = self.bn1(self.conv1(x, handoff=handoff))
+        elif give is not None:
+            y = self.bn1(self.conv1(x, give=give))
+        else:
+            y = self.bn1(self.conv1(x))
         y = self.bn2(self.conv2(y))
         y = self.conv3(y)
         if _use_native(y):

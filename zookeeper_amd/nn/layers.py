@@ -163,12 +163,31 @@ class QuantConv2d(nn.Module):
 
         return pointwise.supported(x, self.weight, self.stride, self.groups, self.bias)
 
-    def forward(self, x: torch.Tensor, handoff=None) -> torch.Tensor:
-        if handoff is not None:
-            # the caller checked uses_pointwise(x) (see models/resnet.py)
-            from zookeeper_amd.ops import pointwise
+    def uses_native_conv(self, x: torch.Tensor) -> bool:
+        """True when ``forward(x)`` runs on the native float-conv path
+        (``ops/conv.py``, any stride), which can consume a gradient hand-off."""
+        if not (self.input_quantizer is None and self.kernel_quantizer is None
+                and _use_native(x)):
+            return False
+        from zookeeper_amd.ops import conv as conv_op
 
-            return pointwise.conv1x1(x, self.weight, handoff)
+        return conv_op.supported(x, self.weight, self.stride, self.padding, self.groups,
+                                 self.bias, self.pad_values)
+
+    def forward(self, x: torch.Tensor, handoff=None, give=None) -> torch.Tensor:
+        if handoff is not None or give is not None:
+            # gradient hand-off (norm_pool.ResidualHandoff); the caller checked
+            # uses_pointwise(x) / uses_native_conv(x) (see models/resnet.py)
+            if self.uses_pointwise(x):
+                from zookeeper_amd.ops import pointwise
+
+                return pointwise.conv1x1(x, self.weight, handoff, give)
+            if give is None and self.uses_native_conv(x):
+                from zookeeper_amd.ops import conv as conv_op
+
+                return conv_op.conv2d(x, self.weight, self.stride[0], self.padding,
+                                      handoff=handoff)
+            raise RuntimeError("gradient hand-off needs the native 1x1 / conv path")
         if self.groups > 1 and self._is_depthwise3x3() and _use_native(x):
             from zookeeper_amd.ops import depthwise
 

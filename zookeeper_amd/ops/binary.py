@@ -345,10 +345,10 @@ class _BinaryBlockFn(torch.autograd.Function):
                                            dx.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
                                            stride, pt, pl, -1, st), "zk_igemm_dgrad")
                 handoff = ctx.meta[7].get("dx_handoff")
-                if handoff is not None:
+                if handoff is not None and handoff.give(dx):
                     # x's other consumer (the shortcut's avg-pool) adds it in
                     # its backward, which runs after this one
-                    handoff.dres, dx = dx, None
+                    dx = None
                 else:
                     dx = dx.permute(0, 3, 1, 2)
             if side:

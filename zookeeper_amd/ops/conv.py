@@ -63,7 +63,7 @@ def _nhwc(t: torch.Tensor) -> torch.Tensor:
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride, padding):
+    def forward(ctx, x, weight, stride, padding, handoff=None):
         B, Cin, H, W = x.shape
         Cout, _, kh, kw = weight.shape
         pt, pl, Ho, Wo = geometry(H, W, kh, kw, stride, padding)
@@ -78,6 +78,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.save_for_backward(xn)
         ctx.weight = weight
         ctx.geom = (B, Cin, H, W, Cout, kh, kw, stride, pt, pl, Ho, Wo)
+        ctx.handoff = handoff
         return y.permute(0, 3, 1, 2)
 
     @staticmethod
@@ -91,12 +92,19 @@ class _ConvFn(torch.autograd.Function):
         L = lib()
         st = stream_ptr(dev)
         dx = dweight = None
+        # + x's other gradient, left by a consumer that ran first (ResidualHandoff)
+        dres = ctx.handoff.take() if ctx.handoff is not None else None
         if ctx.needs_input_grad[0]:
             wt = weight.detach().permute(2, 3, 1, 0).reshape(T, Cin, Cout).to(torch.bfloat16)
             wt = wt.contiguous()
             dxn = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
-            check(L.zk_igemm_dgrad(g.data_ptr(), wt.data_ptr(), None, None, dxn.data_ptr(), B, H,
-                                   W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl, -1, st),
+            if dres is not None and (tuple(dres.shape) != (B, H, W, Cin)
+                                     or not dres.is_contiguous()):
+                raise RuntimeError(f"hand-off gradient {tuple(dres.shape)} does not match the "
+                                   f"conv input {(B, H, W, Cin)}")
+            check(L.zk_igemm_dgrad(g.data_ptr(), wt.data_ptr(), None,
+                                   dres.data_ptr() if dres is not None else None, dxn.data_ptr(),
+                                   B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl, -1, st),
                   "zk_igemm_dgrad(conv)")
             dx = dxn.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
@@ -118,10 +126,13 @@ class _ConvFn(torch.autograd.Function):
                 grad_ready(weight)
             else:
                 dweight = dw.permute(0, 3, 1, 2)
-        return dx, dweight, None, None
+        return dx, dweight, None, None, None
 
 
-def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: str) -> torch.Tensor:
+def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: str,
+           handoff=None) -> torch.Tensor:
     """Float convolution with TF padding semantics (see ``supported``) as MFMA
-    implicit GEMMs.  Returns a channels_last bf16 tensor."""
-    return _ConvFn.apply(x, weight, int(stride), padding)
+    implicit GEMMs.  Returns a channels_last bf16 tensor.  ``handoff``: the
+    data gradient also adds x's other gradient left there
+    (``norm_pool.ResidualHandoff``)."""
+    return _ConvFn.apply(x, weight, int(stride), padding, handoff)

@@ -123,10 +123,9 @@ class _BatchNormFn(torch.autograd.Function):
                                           y.data_ptr() if y is not None else None,
                                           bcoef.data_ptr(), dx.data_ptr(), dres.data_ptr(), P, C,
                                           st), "zk_bn_bwd_dx_res_bf16")
-            if ctx.handoff is not None:
+            if ctx.handoff is not None and ctx.handoff.give(dres):
                 # the residual's consumer adds it in its data-gradient epilogue
                 # (see ResidualHandoff): no separate gradient-accumulation pass
-                ctx.handoff.dres = dres
                 dres = None
             else:
                 dres = _back(dres, ctx.dim)
@@ -150,15 +149,32 @@ class ResidualHandoff:
     here and returns none for it, and the first layer's data-gradient kernel
     adds it in its epilogue (``zk_igemm_dgrad``'s ``dres``).  Only valid when
     that first layer computes the full gradient of ``x`` — the caller pairs a
-    handoff with a native layer it knows consumes it."""
+    handoff with a native layer it knows consumes it.
 
-    __slots__ = ("dres",)
+    The same object serves any producer / consumer pair whose backward order
+    follows from the graph (a stage transition's binary conv → its shortcut
+    avg-pool, a downsampling bottleneck's conv1 → its shortcut conv).
+    ``take`` closes it: a producer that would run after its consumer
+    (``give`` returns False) returns its gradient to autograd instead, so an
+    unexpected order costs the fused add, never a gradient."""
+
+    __slots__ = ("dres", "closed")
 
     def __init__(self):
         self.dres = None
+        self.closed = False
+
+    def give(self, d) -> bool:
+        """Producer side: leave ``d`` for the consumer; False if it already ran."""
+        if self.closed:
+            return False
+        self.dres = d
+        return True
 
     def take(self):
+        """Consumer side: the producer's gradient (or None); closes the hand-off."""
         d, self.dres = self.dres, None
+        self.closed = True
         return d
 
 

@@ -54,7 +54,7 @@ def _rows(x: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, handoff=None):
+    def forward(ctx, x, weight, handoff=None, give=None):
         B, Cin, H, W = x.shape
         Cout = weight.shape[0]
         x2 = _rows(x)
@@ -66,7 +66,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                                    stream_ptr(x.device)), "zk_igemm_dgrad(1x1 fwd)")
         ctx.save_for_backward(x2, w2)
         ctx.weight = weight
-        ctx.handoff = handoff
+        ctx.handoff, ctx.give = handoff, give
         ctx.shape = (B, Cin, H, W, Cout)
         return y2.view(B, H, W, Cout).permute(0, 3, 1, 2)
 
@@ -92,7 +92,10 @@ class _Conv1x1Fn(torch.autograd.Function):
                                    dres.data_ptr() if dres is not None else None, dx2.data_ptr(),
                                    B, H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0, -1, st),
                   "zk_igemm_dgrad(1x1)")
-            dx = dx2.view(B, H, W, Cin).permute(0, 3, 1, 2)
+            if ctx.give is not None and ctx.give.give(dx2.view(B, H, W, Cin)):
+                dx = None  # x's other consumer adds it (a downsampling shortcut conv)
+            else:
+                dx = dx2.view(B, H, W, Cin).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             target = direct_grad(weight)
             dw = target.view(Cout, Cin) if target is not None else torch.zeros(
@@ -112,12 +115,13 @@ class _Conv1x1Fn(torch.autograd.Function):
                 grad_ready(weight)
             else:
                 dweight = dw.view(Cout, Cin, 1, 1)
-        return dx, dweight, None
+        return dx, dweight, None, None
 
 
-def conv1x1(x: torch.Tensor, weight: torch.Tensor, handoff=None) -> torch.Tensor:
+def conv1x1(x: torch.Tensor, weight: torch.Tensor, handoff=None, give=None) -> torch.Tensor:
     """``F.conv2d(x, weight)`` for a 1×1 stride-1 kernel (see ``supported``),
     as MFMA implicit GEMMs.  Returns a channels_last bf16 tensor.  With a
-    ``norm_pool.ResidualHandoff`` the data gradient also adds the gradient a
-    residual tail left there for the same input."""
-    return _Conv1x1Fn.apply(x, weight, handoff)
+    ``norm_pool.ResidualHandoff`` as ``handoff`` the data gradient also adds
+    the gradient another consumer of the same input left there; as ``give``
+    the data gradient is left there for that consumer instead of returned."""
+    return _Conv1x1Fn.apply(x, weight, handoff, give)
