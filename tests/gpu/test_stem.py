@@ -157,3 +157,36 @@ def test_recompute_fused_stem_matches_materialising(hw, B, monkeypatch):
         assert e1 < max(1.5 * e0, 2e-2), (n, e1, e0)
     for n in b0:
         torch.testing.assert_close(b1[n], b0[n], atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("nb", [1500, 50176])
+def test_two_pass_finalize_matches_one_pass(nb):
+    """zk_bn_finalize_partials_ws (coalesced fp64 first pass over the
+    per-tile partial rows, then the finalize over 256 rows) gives the
+    coefficients and running statistics of the one-pass kernel."""
+    from zookeeper_amd.ops._native import lib, stream_ptr
+
+    L, st = lib(), stream_ptr()
+    C = 64
+    torch.manual_seed(7)
+    part = torch.randn(nb, 2, C, device="cuda")
+    part[:, 1] = part[:, 1].abs() * 3 + 1.0  # sums of squares
+    P = float(nb * 128)
+    outs = []
+    for ws in (False, True):
+        coef = torch.empty(4, C, device="cuda")
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        if ws:
+            buf = torch.empty(L.zk_bn_finalize_ws_bytes(C) // 8, dtype=torch.float64,
+                              device="cuda")
+            assert L.zk_bn_finalize_partials_ws(part.data_ptr(), nb, C, P, None, None, 1e-5, 0.9,
+                                                rm.data_ptr(), rv.data_ptr(), coef.data_ptr(),
+                                                buf.data_ptr(), st) == 0
+        else:
+            assert L.zk_bn_finalize_partials(part.data_ptr(), nb, C, P, None, None, 1e-5, 0.9,
+                                             rm.data_ptr(), rv.data_ptr(), coef.data_ptr(),
+                                             st) == 0
+        torch.cuda.synchronize()
+        outs.append((coef, rm, rv))
+    for a, b in zip(outs[0], outs[1]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)

@@ -52,9 +52,14 @@ def main():
         x.data_ptr(), xp.data_ptr(), B, H, W, Cin, Hp, Wp, pt, pl, st), args.reps)
     L.zk_stem_pack_weight(w.data_ptr(), ws.data_ptr(), Cout, K, K, Cin, st)
     for v in range(4):
+        y1.fill_(0)
+        L.zk_stem_conv_fwd(xp.data_ptr(), ws.data_ptr(), y1.data_ptr(), part.data_ptr(), B, Cin,
+                           Cout, K, K, s, Ho, Wo, Hp, Wp, v, ctypes.byref(nb), st)
+        torch.cuda.synchronize()
         row[f"conv_fwd_v{v}_us"] = timeit(lambda: L.zk_stem_conv_fwd(
             xp.data_ptr(), ws.data_ptr(), y1.data_ptr(), part.data_ptr(), B, Cin, Cout, K, K, s,
             Ho, Wo, Hp, Wp, v, ctypes.byref(nb), st), args.reps)
+        print(f"conv_fwd v{v}: {row[f'conv_fwd_v{v}_us']:.1f} us", flush=True)
     coef = torch.empty(4, Cout, device="cuda")
     rm, rv = torch.zeros(Cout, device="cuda"), torch.ones(Cout, device="cuda")
     L.zk_stem_conv_fwd(xp.data_ptr(), ws.data_ptr(), y1.data_ptr(), part.data_ptr(), B, Cin, Cout,
@@ -62,6 +67,14 @@ def main():
     row["finalize_us"] = timeit(lambda: L.zk_bn_finalize_partials(
         part.data_ptr(), nb.value, Cout, float(B * Ho * Wo), None, None, 1e-5, 0.9,
         rm.data_ptr(), rv.data_ptr(), coef.data_ptr(), st), args.reps)
+    fws = torch.empty(L.zk_bn_finalize_ws_bytes(Cout) // 8, dtype=torch.float64, device="cuda")
+    coef2 = torch.empty_like(coef)
+    row["finalize_ws_us"] = timeit(lambda: L.zk_bn_finalize_partials_ws(
+        part.data_ptr(), nb.value, Cout, float(B * Ho * Wo), None, None, 1e-5, 0.9,
+        rm.data_ptr(), rv.data_ptr(), coef2.data_ptr(), fws.data_ptr(), st), args.reps)
+    row["finalize_ws_coef_maxrel"] = ((coef2 - coef).abs() / coef.abs().clamp_min(1e-12)).max().item()
+    print(f"finalize {row['finalize_us']:.1f} us, two-pass {row['finalize_ws_us']:.1f} us",
+          flush=True)
     H2, W2 = 56, 56
     p = torch.empty(B, H2, W2, Cout, dtype=torch.bfloat16, device="cuda")
     arg = torch.empty(B, H2, W2, Cout, dtype=torch.uint8, device="cuda")
@@ -72,7 +85,8 @@ def main():
         Cout, H2, W2, 3, 2, 0, 0, ctypes.byref(nb2), st), args.reps)
     dp = torch.randn(B, H2, W2, Cout, device="cuda").to(torch.bfloat16)
     row["pool_bwd_sums_us"] = timeit(lambda: L.zk_stem_pool_bwd_sums(
-        dp.data_ptr(), arg.data_ptr(), y1.data_ptr(), coef.data_ptr(), part2.data_ptr(), B, Ho,
+        dp.data_ptr(), arg.data_ptr(), y1.data_ptr(), p.data_ptr(), coef.data_ptr(),
+        part2.data_ptr(), B, Ho,
         Wo, Cout, H2, W2, 3, 2, 0, 0, ctypes.byref(nb2), st), args.reps)
     bcoef = torch.randn(3, Cout, device="cuda")
     dy1 = torch.empty_like(y1)

@@ -216,15 +216,16 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void stem_conv_fwd_kernel(
 // partial sums [nb][2][C] (fp32) -> BN coefficients [4][C] (scale, shift,
 // mean, rstd) + Keras-momentum running statistics (Bessel-corrected var).
 // ---------------------------------------------------------------------------
+template <typename T>
 __global__ __launch_bounds__(256) void bn_finalize_partials_kernel(
-    const float* __restrict__ part, int nb, int C, double P, const float* __restrict__ gamma,
+    const T* __restrict__ part, int nb, int C, double P, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float momentum, float* __restrict__ rmean,
     float* __restrict__ rvar, float* __restrict__ coef) {
   const int c = blockIdx.x;
   double s1 = 0, s2 = 0;
   for (int i = threadIdx.x; i < nb; i += blockDim.x) {
-    s1 += part[((long long)i * 2) * C + c];
-    s2 += part[((long long)i * 2 + 1) * C + c];
+    s1 += (double)part[((long long)i * 2) * C + c];
+    s2 += (double)part[((long long)i * 2 + 1) * C + c];
   }
   __shared__ double r1[256], r2[256];
   r1[threadIdx.x] = s1;
@@ -252,6 +253,27 @@ __global__ __launch_bounds__(256) void bn_finalize_partials_kernel(
       rmean[c] = momentum * rmean[c] + (1.f - momentum) * (float)mean;
       rvar[c] = momentum * rvar[c] + (1.f - momentum) * (float)unb;
     }
+  }
+}
+
+// First pass of the two-pass finalize: [nb][n] fp32 partial rows -> [G][n]
+// fp64 (block b sums a contiguous range of rows, each thread one column over
+// every (256/n)-th row: coalesced rows instead of one strided column per
+// block; fixed order, deterministic).  n | 256.
+__global__ __launch_bounds__(256) void partials_colsum_kernel(const float* __restrict__ part,
+                                                              int nb, int n, int rows_per_block,
+                                                              double* __restrict__ out) {
+  const int col = threadIdx.x % n, rg = threadIdx.x / n, RG = 256 / n;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(nb, r0 + rows_per_block);
+  double s = 0;
+  for (int r = r0 + rg; r < r1; r += RG) s += part[(long long)r * n + col];
+  __shared__ double red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (rg == 0) {
+    for (int k = 1; k < RG; ++k) s += red[k * n + col];
+    out[(long long)blockIdx.x * n + col] = s;
   }
 }
 
@@ -773,7 +795,10 @@ ZK_EXPORT int zk_stem_conv_fwd(const void* xp, const void* ws, void* y, void* pa
                        (float*)part, g, mt);                                                \
     break;                                                                                  \
   }
-  switch (variant < 0 ? 0 : variant) {
+  // default: 128-pixel tiles at ImageNet batch >= ~330 (tools/tune_stem.py,
+  // batch 512: 450 us vs 555 us for the 256-pixel tiles tuned at batch 256)
+  if (variant < 0) variant = M >= 4 * 1024 * 1024 ? 3 : 0;
+  switch (variant) {
     case 0: ZK_STEM_FWD(256, 4, 1, 3)
     case 1: ZK_STEM_FWD(128, 2, 2, 4)
     case 2: ZK_STEM_FWD(256, 2, 2, 4)
@@ -796,9 +821,34 @@ ZK_EXPORT int zk_bn_finalize_partials(const void* part, int nb, int C, double P,
                                       const void* gamma, const void* beta, float eps,
                                       float momentum, void* rmean, void* rvar, void* coef,
                                       hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_partials_kernel, dim3(C), dim3(256), 0, st, (const float*)part,
-                     nb, C, P, (const float*)gamma, (const float*)beta, eps, momentum,
-                     (float*)rmean, (float*)rvar, (float*)coef);
+  hipLaunchKernelGGL(bn_finalize_partials_kernel<float>, dim3(C), dim3(256), 0, st,
+                     (const float*)part, nb, C, P, (const float*)gamma, (const float*)beta, eps,
+                     momentum, (float*)rmean, (float*)rvar, (float*)coef);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// zk_bn_finalize_partials for many partial rows (the stem conv writes one
+// per 128- or 256-pixel tile: ~25-50k at batch 512): a coalesced first pass
+// into ws ([256][2C] fp64, zk_bn_finalize_ws_bytes) then the finalize over
+// 256 rows.  Falls back to the one-pass form when 2C does not divide 256.
+ZK_EXPORT long long zk_bn_finalize_ws_bytes(int C) { return 256LL * 2 * C * 8; }
+
+ZK_EXPORT int zk_bn_finalize_partials_ws(const void* part, int nb, int C, double P,
+                                         const void* gamma, const void* beta, float eps,
+                                         float momentum, void* rmean, void* rvar, void* coef,
+                                         void* ws, hipStream_t st) {
+  const int n = 2 * C;
+  if (!ws || n > 256 || 256 % n || nb < 1024)
+    return zk_bn_finalize_partials(part, nb, C, P, gamma, beta, eps, momentum, rmean, rvar, coef,
+                                   st);
+  constexpr int G = 256;
+  const int rpb = (nb + G - 1) / G;
+  hipLaunchKernelGGL(partials_colsum_kernel, dim3(G), dim3(256), 0, st, (const float*)part, nb,
+                     n, rpb, (double*)ws);
+  hipLaunchKernelGGL(bn_finalize_partials_kernel<double>, dim3(C), dim3(256), 0, st,
+                     (const double*)ws, G, C, P, (const float*)gamma, (const float*)beta, eps,
+                     momentum, (float*)rmean, (float*)rvar, (float*)coef);
   ZK_CHECK_LAUNCH();
   return 0;
 }

@@ -77,6 +77,9 @@ SIGNATURES = {
     "zk_stem_max_parts": (I32, [I32, I32, I32]),
     "zk_stem_max_pool_parts": (I32, []),
     "zk_bn_finalize_partials": (I32, [P, I32, I32, C.c_double, P, P, F32, F32, P, P, P, P]),
+    "zk_bn_finalize_partials_ws": (I32, [P, I32, I32, C.c_double, P, P, F32, F32, P, P, P, P,
+                                         P]),
+    "zk_bn_finalize_ws_bytes": (I64, [I32]),
     "zk_reduce_partials": (I32, [P, I32, I32, P, P]),
     "zk_stem_pool_fwd": (I32, [P, P, P, P, P] + [I32] * 10 + [IP, P]),
     "zk_stem_pool_bwd_sums": (I32, [P, P, P, P, P, P] + [I32] * 10 + [IP, P]),

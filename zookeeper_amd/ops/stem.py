@@ -135,12 +135,17 @@ class _StemFn(torch.autograd.Function):
 
         def finalize1(part, nb):
             coef1 = torch.empty((4, Cout), dtype=torch.float32, device=dev)
-            check(L.zk_bn_finalize_partials(part.data_ptr(), nb, Cout, float(P1),
-                                            g1.data_ptr() if g1 is not None else None,
-                                            b1.data_ptr() if b1 is not None else None, bn1.eps,
-                                            bn1.momentum, bn1.running_mean.data_ptr(),
-                                            bn1.running_var.data_ptr(), coef1.data_ptr(), st),
-                  "zk_bn_finalize_partials")
+            # one partial row per conv tile (~25-50k): coalesced two-pass reduction
+            fws = torch.empty(L.zk_bn_finalize_ws_bytes(Cout) // 8, dtype=torch.float64,
+                              device=dev)
+            check(L.zk_bn_finalize_partials_ws(part.data_ptr(), nb, Cout, float(P1),
+                                               g1.data_ptr() if g1 is not None else None,
+                                               b1.data_ptr() if b1 is not None else None,
+                                               bn1.eps, bn1.momentum,
+                                               bn1.running_mean.data_ptr(),
+                                               bn1.running_var.data_ptr(), coef1.data_ptr(),
+                                               fws.data_ptr(), st),
+                  "zk_bn_finalize_partials_ws")
             return coef1
 
         p = torch.empty((B, H2, W2, Cout), dtype=torch.bfloat16, device=dev)
