@@ -193,13 +193,16 @@ class _StemFn(torch.autograd.Function):
         if bn2 is not None:
             if bn2.training:
                 coef2 = torch.empty((4, Cout), dtype=torch.float32, device=dev)
-                check(L.zk_bn_finalize_partials(part2.data_ptr(), nb2.value, Cout, float(P2),
-                                                g2.data_ptr() if g2 is not None else None,
-                                                b2.data_ptr() if b2 is not None else None,
-                                                bn2.eps, bn2.momentum,
-                                                bn2.running_mean.data_ptr(),
-                                                bn2.running_var.data_ptr(), coef2.data_ptr(), st),
-                      "zk_bn_finalize_partials")
+                fws2 = torch.empty(L.zk_bn_finalize_ws_bytes(Cout) // 8, dtype=torch.float64,
+                                   device=dev)
+                check(L.zk_bn_finalize_partials_ws(part2.data_ptr(), nb2.value, Cout, float(P2),
+                                                   g2.data_ptr() if g2 is not None else None,
+                                                   b2.data_ptr() if b2 is not None else None,
+                                                   bn2.eps, bn2.momentum,
+                                                   bn2.running_mean.data_ptr(),
+                                                   bn2.running_var.data_ptr(), coef2.data_ptr(),
+                                                   fws2.data_ptr(), st),
+                      "zk_bn_finalize_partials_ws")
             else:
                 coef2 = _bn_eval_coef(bn2, Cout, dev)
             out = torch.empty_like(p)
