@@ -1,5 +1,5 @@
-"""Default (variant -1) tile choices of the binary-conv kernels at the bench's
-per-GPU batch (512), where the batch-aware rules in igemm.hip pick 256x256
+"""Default (variant -1) tile choices of the binary-conv kernels at the
+per-GPU batches 512 and 1024 (the bench default), where the batch-aware rules in igemm.hip pick 256x256
 tiles / larger split-K grids: data gradient, weight gradient and MX-FP4
 forward must agree with an explicitly chosen variant that the per-variant
 fp64 tests (test_bconv_bwd_kernels.py, test_fp4_forward.py) validate."""
@@ -9,7 +9,6 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-B = 512
 SHAPES = [  # H, W, Cin, Cout, stride (BinaryResNet-E18 / QuickNet 3x3 layers)
     (7, 7, 512, 512, 1),
     (14, 14, 256, 256, 1),
@@ -25,8 +24,9 @@ def _gpu():
         pytest.skip("needs a GPU")
 
 
+@pytest.mark.parametrize("B", [512, 1024])
 @pytest.mark.parametrize("H,W,cin,cout,s", SHAPES)
-def test_defaults_match_reference_variant(H, W, cin, cout, s):
+def test_defaults_match_reference_variant(H, W, cin, cout, s, B):
     from zookeeper_amd.nn.layers import same_padding
     from zookeeper_amd.ops._native import lib, stream_ptr
 

@@ -76,6 +76,23 @@ struct ConvArgs {
   int korder;
 };
 
+// ZK_TILE_HUGE=<bitmask> (A/B): which batch >= 1024 tile rules apply --
+// 1: 28x28x128 wgrad on conv3 64x64, 2: 256-input-channel wgrad 256x256 x 3
+// stages, 4: 64 -> 128 transition wgrad at 1024 blocks, 8: 7x7x512 wgrad on
+// 128x128, 16: 28x28x128 dgrad variant 27.  Default 16: each wgrad rule wins
+// alone (tools/tune_bconv.py --batch 1024) but costs 0.4-0.9 % of the E18
+// step, where those kernels overlap the data-gradient chain on the side
+// stream (bench A/B, 40 steps each: none 43.7k, 1 43.5k, 2 43.5k, 4 43.6k,
+// 8 43.3k, 16 43.8k img/s).
+bool huge_tiles_env(int bit = 31) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ZK_TILE_HUGE");
+    v = (e && *e) ? atoi(e) : 16;
+  }
+  return (v & bit) != 0;
+}
+
 int korder_env() {
   static int v = -1;
   if (v < 0) {
@@ -2012,7 +2029,7 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     else if (c3 && Cin == 512)
       variant = 24;
     else if (c3 && Cin == 128)
-      variant = 23;
+      variant = g.B >= 1024 && huge_tiles_env(16) ? 27 : 23;  // batch 1024: 323 vs 338 us
     else if (c3 && Cin == 64)
       variant = 27;
     else if (Cin % 128 == 0)
@@ -2066,25 +2083,38 @@ void wgrad_defaults(const IGeom& g, int& variant, int& target_blocks) {
     // the 128-channel layers (28x28x128: 262 -> 183 us), and 256x256 tiles
     // with 512 blocks for the 256-input-channel 3x3 layers (14x14x256:
     // 235 -> 168 us; 256 -> 512 stride 2: 130 -> 106 us).
+    // Batch >= 1024, opt-in (ZK_TILE_HUGE, see huge_tiles_env; standalone
+    // tools/tune_bconv.py --batch 1024): 28x28x128 on the 64x64 three-row
+    // conv3 tiles (406 -> 347 us), 256-input-channel layers on 256x256 x 3
+    // stages at 1024 blocks (417 -> 349 us), the 64 -> 128 transition at 1024
+    // blocks (329 -> 222 us), 7x7x512 on 128x128 at 2048 blocks (392 vs 400).
     const bool c3 = conv3_ok(g, 0);
-    const bool big = g.B >= 512;
+    const bool big = g.B >= 512, huge = g.B >= 1024;
     if (c3 && g.Cin == 64 && g.Cout % 64 == 0) {
+      variant = 20;
+      if (target_blocks <= 0) target_blocks = 512;
+    } else if (huge && huge_tiles_env(1) && c3 && g.Cin == 128 && g.Cout % 64 == 0) {
       variant = 20;
       if (target_blocks <= 0) target_blocks = 512;
     } else if (c3 && g.Cin == 128 && g.Cout % 128 == 0) {
       variant = 28;
       if (target_blocks <= 0) target_blocks = big ? 1024 : 512;
+    } else if (huge && huge_tiles_env(2) && g.kh == 3 && g.kw == 3 && g.Cin == 256 &&
+               g.Cout % 256 == 0) {
+      variant = 12;
+      if (target_blocks <= 0) target_blocks = 1024;
     } else if (big && g.kh == 3 && g.kw == 3 && g.Cin == 256 && g.Cout % 256 == 0) {
       variant = 8;
       if (target_blocks <= 0) target_blocks = 512;
-    } else if (big && g.kh == 3 && g.kw == 3 && g.Cin == 512 && g.Cout % 256 == 0) {
+    } else if (big && !(huge && huge_tiles_env(8)) && g.kh == 3 && g.kw == 3 && g.Cin == 512 &&
+               g.Cout % 256 == 0) {
       // 7x7x512 at batch 512: 256x256 tiles, 384 blocks 198 us vs 128x128
       // at 2048 blocks 217-221 us (tools/tune_bconv.py --tbs 128..768)
       variant = 8;
       if (target_blocks <= 0) target_blocks = 384;
     } else if (g.Cin == 64 && g.s == 2 && g.Cout % 128 == 0 && (9 * g.Cin) % 192 == 0) {
       variant = 2;
-      if (target_blocks <= 0) target_blocks = 512;
+      if (target_blocks <= 0) target_blocks = huge && huge_tiles_env(4) ? 1024 : 512;
     } else if (g.Cin == 64 || g.Cout % 128 != 0) {
       variant = 7;
       if (target_blocks <= 0) target_blocks = 2048;
