@@ -62,7 +62,7 @@ def parse(argv=None):
                     help="pool: device-resident synthetic batches; stream: host pipeline "
                          "(pinned ring + side-stream H2D) inside the timed region")
     ap.add_argument("--pool", type=int, default=4, help="device-resident synthetic batches")
-    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--bucket-mb", type=float, default=10.0)
     ap.add_argument("--graph", default="auto", choices=["0", "1", "auto"],
                     help="replay forward+backward as a HIP graph; auto: when the warmup "
                          "shows the step host-bound")

@@ -70,7 +70,7 @@ class TrainingExperiment(Experiment):
     # Keep this many batches resident on the device and cycle them (synthetic
     # benchmarking); 0 = stream from the host through the pinned ring.
     device_pool: int = Field(0)
-    bucket_mb: float = Field(25.0)
+    bucket_mb: float = Field(10.0)
     print_summary: bool = Field(True)
 
     def run_dir(self) -> Optional[str]:

@@ -37,7 +37,7 @@ def prepare_model(model: nn.Module, device: torch.device) -> nn.Module:
 
 class Trainer:
     def __init__(self, model: nn.Module, loss, optimizer: OptimizerSpec,
-                 info: Optional[zdist.DistInfo] = None, bucket_mb: float = 25.0,
+                 info: Optional[zdist.DistInfo] = None, bucket_mb: float = 10.0,
                  first_bucket_mb: float = 1.0, grad_dtype: Optional[torch.dtype] = None,
                  graph: Union[bool, str] = False, graph_warmup: int = 3,
                  comm_timing: bool = False, metric_fns: Optional[dict] = None):
