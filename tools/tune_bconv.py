@@ -20,7 +20,7 @@ from zookeeper_amd.ops._native import lib, stream_ptr  # noqa: E402
 
 DG_VARIANTS = 8
 WG_VARIANTS = 8
-IG_VARIANTS = list(range(18)) + list(range(20, 35))
+IG_VARIANTS = list(range(18)) + list(range(20, 35)) + list(range(40, 49))
 IGW_VARIANTS = list(range(13)) + list(range(20, 35))  # 20+: conv3 (3x3 s1)
 IGF_VARIANTS = list(range(15)) + list(range(20, 28))
 IGF4_VARIANTS = [-1] + list(range(10)) + list(range(20, 29))
