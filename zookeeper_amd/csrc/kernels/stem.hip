@@ -51,6 +51,48 @@ __global__ __launch_bounds__(256) void stem_pack_input_kernel(const uint16_t* __
   }
 }
 
+// Cin == 3 with an even left pad: two padded pixels per thread -- their 12
+// input bytes are three aligned dwords (w even), their 16 output bytes one
+// aligned uint4 -- instead of three 2-byte loads and one 8-byte store per
+// pixel (the load instruction count bound the one-pixel form).
+__global__ __launch_bounds__(256) void stem_pack_input3_kernel(const uint16_t* __restrict__ x,
+                                                               uint4* __restrict__ xp,
+                                                               StemGeom g) {
+  const int Wp2 = g.Wp / 2;
+  const long long total = (long long)g.B * g.Hp * Wp2;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int wq = (int)(i % Wp2);
+    const long long r = i / Wp2;
+    const int hp = (int)(r % g.Hp);
+    const int b = (int)(r / g.Hp);
+    const int h = hp - g.pt, w = 2 * wq - g.pl;  // w even
+    uint32_t o[4] = {0u, 0u, 0u, 0u};
+    if (h >= 0 && h < g.H) {
+      const uint16_t* row = x + ((long long)b * g.H + h) * g.W * 3;
+      if (w >= 0 && w + 1 < g.W) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(row + (long long)w * 3);
+        const uint32_t d0 = src[0], d1 = src[1], d2 = src[2];  // c0 c1 | c2 c0' | c1' c2'
+        o[0] = d0;
+        o[1] = d1 & 0xffffu;
+        o[2] = (d1 >> 16) | (d2 << 16);
+        o[3] = d2 >> 16;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int wk = w + k;
+          if (wk >= 0 && wk < g.W) {
+            const uint16_t* px = row + (long long)wk * 3;
+            o[2 * k] = px[0] | ((uint32_t)px[1] << 16);
+            o[2 * k + 1] = px[2];
+          }
+        }
+      }
+    }
+    xp[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // w fp32 [Cout][KH][KW][Cin] -> ws bf16 [KH][Cout][32]: j = kw*4 + c
 __global__ void stem_pack_weight_kernel(const float* __restrict__ w, uint16_t* __restrict__ ws,
                                         StemGeom g) {
@@ -758,6 +800,16 @@ ZK_EXPORT int zk_stem_pack_input(const void* x, void* xp, int B, int H, int W, i
   StemGeom g{B, H, W, Cin, 0, 0, 0, 0, pt, pl, 0, 0, Hp, Wp};
   if (Cin > 4) return (int)hipErrorInvalidValue;
   long long total = (long long)B * Hp * Wp;
+  if (Cin == 3 && W % 2 == 0 && Wp % 2 == 0 && pl % 2 == 0 &&
+      ((uintptr_t)x & 3) == 0 && ((uintptr_t)xp & 15) == 0) {
+    total /= 2;  // two padded pixels per thread
+    long long blocks = (total + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(stem_pack_input3_kernel, dim3((int)blocks), dim3(256), 0, st,
+                       (const uint16_t*)x, (uint4*)xp, g);
+    ZK_CHECK_LAUNCH();
+    return 0;
+  }
   long long blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(stem_pack_input_kernel, dim3((int)blocks), dim3(256), 0, st,
