@@ -68,6 +68,12 @@ def parse(argv=None):
                          "shows the step host-bound")
     ap.add_argument("--allow-shared-gpu", action="store_true",
                     help="(rehearsal) let several ranks share a GPU (ZK_DIST_BACKEND=gloo)")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="keep the bucketed all-reduce on with one GPU (1-rank RCCL group): "
+                         "the exact multi-GPU step, with its comm timings")
+    ap.add_argument("--rt", action="append", default=[], metavar="KEY=VALUE",
+                    help="Runtime component option (zookeeper_amd/train/runtime.py), e.g. "
+                         "--rt bconv_fp4=False --rt tile_huge=0; recorded in the JSON")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -87,9 +93,10 @@ def self_launch(args) -> int:
     from zookeeper_amd.parallel.launch import spawn
 
     if not args.allow_shared_gpu:
-        import torch  # device_count() does not initialise the GPU on this image
+        # env + sysfs only: the parent must never initialise the HIP runtime
+        from zookeeper_amd.parallel.devices import visible_gpu_count
 
-        have = torch.cuda.device_count()
+        have = visible_gpu_count()
         if have and have < args.gpus:
             print(f"error: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr)
             return 2
@@ -115,7 +122,20 @@ def main() -> int:
     from zookeeper_amd.parallel import dist as zdist
     from zookeeper_amd.train import Adam, OptimizerSpec, Trainer
 
-    info = zdist.init()
+    from zookeeper_amd.core.utils import parse_value_from_string
+    from zookeeper_amd.train.runtime import Runtime
+
+    runtime = Runtime()
+    rt_conf = {}
+    for kv in args.rt:
+        k, _, v = kv.partition("=")
+        rt_conf[k] = parse_value_from_string(v)
+    rt_conf.setdefault("graph", {"0": "off", "1": "on", "auto": "auto"}[args.graph])
+    if args.force_dp:
+        rt_conf["force_dp"] = True
+    configure(runtime, rt_conf)
+    runtime.apply()
+    info = zdist.init(single_group=runtime.force_dp)
     if info.world != args.gpus:
         print(f"error: --gpus {args.gpus} but the job has {info.world} rank(s)", file=sys.stderr)
         return 2
@@ -140,11 +160,12 @@ def main() -> int:
     model = cfg.model
     backend = base_getattr(cfg, "model").resolved_backend()
     torch.manual_seed(1234)
+    dp = info.world > 1 or runtime.force_dp
     trainer = Trainer(model, "sparse_categorical_crossentropy", base_getattr(cfg, "optimizer"),
-                      info, bucket_mb=args.bucket_mb,
-                      graph="auto" if args.graph == "auto" else args.graph == "1",
+                      info, bucket_mb=args.bucket_mb, graph=runtime.trainer_graph(),
                       graph_warmup=max(1, min(3, args.warmup - 1)),  # capture inside the warmup
-                      comm_timing=info.world > 1 and torch.cuda.is_available())
+                      comm_timing=dp and runtime.comm_timing and torch.cuda.is_available(),
+                      force_dp=runtime.force_dp)
     prep = cfg.preprocessing
     loader = None
     if args.data == "stream":
@@ -212,10 +233,17 @@ def main() -> int:
                  + ("device-resident pool" if args.data == "pool" else
                     "host source streamed: native gather into pinned slots + side-stream H2D")
                  + "; random-init weights)")
+    # the headline metric string only for the headline configuration on its
+    # real transport: one GPU per rank, RCCL between them
+    rehearsal = args.allow_shared_gpu or (info.world > 1 and info.backend != "nccl") \
+        or not torch.cuda.is_available()
+    headline = (args.model == "BinaryResNetE18" and S == 224 and args.num_classes == 1000)
+    metric = METRIC if headline else OTHER_METRIC.format(model=args.model)
+    if rehearsal:
+        metric = f"rehearsal ({info.backend if info.world > 1 else 'cpu'}, not a measurement): " \
+            + metric
     out = {
-        "metric": METRIC if (args.model == "BinaryResNetE18" and S == 224
-                             and args.num_classes == 1000)
-        else OTHER_METRIC.format(model=args.model),
+        "metric": metric,
         "value": round(value, 2),
         "unit": "images/sec",
         "n_gpus": info.world,
@@ -241,7 +269,9 @@ def main() -> int:
             "optimizer": "adam+weight_clip (fused)",
             "hip_graph": trainer.graph,
             "data_path": args.data,
-            "buckets": trainer.bucketer.num_buckets if info.world > 1 else 0,
+            "buckets": trainer.bucketer.num_buckets if trainer.bucketer.enabled else 0,
+            "dist_backend": info.backend,
+            "runtime": runtime.as_dict(),
             "final_loss": round(final_loss, 4),
         },
     }

@@ -6,8 +6,12 @@ broadcast -- runs multi-rank.
 
     python tests/dp_gpu_worker.py <same|split> <outdir>
 
-Environment: ``ZK_WGRAD_SIDE=0|1`` (side-stream weight gradients),
-``ZK_TEST_GRAPH=0|1`` (HIP-graph replay under DP).  The bucketer never
+Environment (test knobs of this worker only): ``ZK_TEST_SIDE=0|1``
+(side-stream weight gradients, ``runtime.wgrad_side_stream``),
+``ZK_TEST_GRAPH=0|1`` (HIP-graph replay under DP), ``ZK_TEST_FORCE_DP=1``
+(one rank, but a 1-rank process group of ``ZK_TEST_BACKEND`` -- ``nccl`` is
+RCCL -- with the bucketed all-reduce forced on: the exact multi-GPU path on
+the box's one GPU).  The bucketer never
 synchronises the host: ordering is carried by events alone
 (compute → comm stream at bucket-ready, comm → compute before the optimizer).
 
@@ -36,8 +40,16 @@ def run(mode: str, out: str) -> None:
     from zookeeper_amd.parallel import dist as zdist
     from zookeeper_amd.train import SGD, Trainer
 
+    from zookeeper_amd.ops.options import set_options
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    info = zdist.init("gloo") if world > 1 else zdist.init()
+    force = os.environ.get("ZK_TEST_FORCE_DP", "0") == "1"
+    backend = os.environ.get("ZK_TEST_BACKEND", "gloo")
+    set_options(wgrad_side_stream=os.environ.get("ZK_TEST_SIDE", "1") == "1")
+    if world > 1 or force:
+        info = zdist.init(backend, single_group=force)
+    else:
+        info = zdist.init()
     torch.manual_seed(1234)
     model = BinaryResNetE((64, 64, 3), 10, 18, backend="hip")
     if info.rank == 1:  # different init on rank 1: the broadcast must fix it
@@ -51,7 +63,7 @@ def run(mode: str, out: str) -> None:
     graph = os.environ.get("ZK_TEST_GRAPH", "0") == "1"
     tr = Trainer(model, "sparse_categorical_crossentropy", spec, info, bucket_mb=2.0,
                  first_bucket_mb=0.25, graph=graph, graph_warmup=1,
-                 comm_timing=world > 1)
+                 comm_timing=world > 1 or force, force_dp=force)
     init = tr.flat.data.detach().cpu().clone()  # after the initial broadcast
     g = torch.Generator().manual_seed(99)
     steps, per = int(os.environ.get("ZK_TEST_STEPS", "2")), 4
@@ -68,10 +80,11 @@ def run(mode: str, out: str) -> None:
     timings = tr.bucketer.pop_timings()
     torch.save({"params": tr.flat.data.cpu(), "init": init, "loss": float(loss),
                 "buckets": tr.bucketer.num_buckets, "graph": tr.graph,
-                "comm_steps": len(timings),
+                "comm_steps": len(timings), "timings": timings,
+                "backend": info.backend, "bucketer": tr.bucketer.enabled,
                 "slots": [(sl.name, sl.offset, sl.numel) for sl in tr.flat.slots],
                 "ranges": list(tr.bucketer.ranges)},
-               os.path.join(out, f"{mode}_w{world}_r{info.rank}.pt"))
+               os.path.join(out, f"{mode}_w{world}{'dp' if force else ''}_r{info.rank}.pt"))
     zdist.shutdown()
 
 

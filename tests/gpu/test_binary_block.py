@@ -7,6 +7,8 @@ import copy
 import pytest
 import torch
 
+from zookeeper_amd.ops.options import OPTS
+
 from zookeeper_amd.models.binary_resnet import BinaryResBlock
 from zookeeper_amd.models.quicknet import QuickNetBlock
 
@@ -192,7 +194,7 @@ def test_fused_bn_backward_sums_match_separate_reduce(monkeypatch, second_consum
     g = torch.randn(4, 64, 28, 28, device="cuda").to(torch.bfloat16)
     res = []
     for fuse in (True, False):
-        monkeypatch.setattr(binary, "FUSE_BNSUM", fuse)
+        monkeypatch.setattr(OPTS, "fuse_bnsum", fuse)
         bs = [copy.deepcopy(b) for b in blocks]
         xx = x.clone().requires_grad_(True)
         h = xx

@@ -11,6 +11,8 @@ import copy
 import pytest
 import torch
 
+from zookeeper_amd.ops.options import OPTS
+
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [-1] + list(range(10)) + list(range(20, 29))
@@ -158,7 +160,7 @@ def test_binary_block_fp4_matches_bf16_path(monkeypatch, cin, cout, stride):
     g = torch.randn(4, cout, ho, ho, device="cuda").to(torch.bfloat16)
     res = []
     for fp4 in (True, False):
-        monkeypatch.setattr(binary, "FP4", fp4)
+        monkeypatch.setattr(OPTS, "bconv_fp4", fp4)
         b = copy.deepcopy(blk)
         xx = x.clone().requires_grad_(True)
         out = b(xx)

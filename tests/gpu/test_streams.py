@@ -5,6 +5,8 @@ signalled (each direct-gradient parameter reported ready exactly once)."""
 import pytest
 import torch
 
+from zookeeper_amd.ops.options import OPTS
+
 pytestmark = pytest.mark.gpu
 
 
@@ -24,7 +26,7 @@ def _grads(side: bool, monkeypatch):
     from zookeeper_amd.train.losses import get_loss
     from zookeeper_amd.train.trainer import prepare_model
 
-    monkeypatch.setattr(streams, "ENABLED", side)
+    monkeypatch.setattr(OPTS, "wgrad_side_stream", side)
     torch.manual_seed(1234)
     dev = torch.device("cuda", 0)
     model = prepare_model(BinaryResNetE((64, 64, 3), 10, 18, backend="hip"), dev).train()

@@ -27,7 +27,7 @@ def _json_lines(out: str):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_bench_self_spawns_ranks(n):
     res = subprocess.run([sys.executable, BENCH, "--gpus", str(n), *ARGS], env=_env(),
                          capture_output=True, text=True, timeout=280, cwd=ROOT)
@@ -40,6 +40,9 @@ def test_bench_self_spawns_ranks(n):
     assert rec["config"]["global_batch"] == 2 * n
     assert rec["steps"] == 2 and rec["warmup"] == 1
     assert rec["value"] > 0 and rec["higher_is_better"] is True
+    # a gloo/CPU rehearsal never carries the bare headline metric string
+    assert rec["metric"].startswith("rehearsal")
+    assert rec["config"]["dist_backend"] == "gloo"
 
 
 @pytest.mark.timeout(120)
@@ -65,3 +68,17 @@ def test_bench_single_rank_json_contract():
     assert rec["n_gpus"] == 1 and rec["scaling"] == "weak"
     for key in ("model", "global_batch", "seq_len", "parallelism"):
         assert key in rec["config"]
+
+
+@pytest.mark.timeout(200)
+def test_bench_force_dp_single_rank_runs_the_bucketer():
+    """``--force-dp``: one rank, but the bucketed all-reduce path is on (a
+    1-rank process group; gloo here, RCCL on a GPU)."""
+    res = subprocess.run([sys.executable, BENCH, *ARGS, "--force-dp", "--rt", "korder=0"],
+                         env=_env(), capture_output=True, text=True, timeout=180, cwd=ROOT)
+    assert res.returncode == 0, res.stderr[-3000:]
+    (rec,) = _json_lines(res.stdout)
+    assert rec["n_gpus"] == 1
+    assert rec["config"]["buckets"] >= 1
+    assert rec["config"]["runtime"]["force_dp"] is True
+    assert rec["config"]["runtime"]["korder"] == 0

@@ -41,7 +41,7 @@ def rel(a, b, ref):
 def main():
     combos = [("2", "1", "0"), ("2", "1", "0"), ("2", "0", "0"), ("1", "1", "0")]
     for steps, side, hs in combos:
-        env = dict(ZK_TEST_STEPS=steps, ZK_WGRAD_SIDE=side, ZK_COMM_HOST_SYNC=hs)
+        env = dict(ZK_TEST_STEPS=steps, ZK_TEST_SIDE=side, ZK_COMM_HOST_SYNC=hs)
         with tempfile.TemporaryDirectory() as d1, tempfile.TemporaryDirectory() as d2:
             assert run(d1, 1, **env) == 0
             assert run(d2, 1, **env) == 0

@@ -26,8 +26,6 @@
 //     pixel rows) so every lane owns one pixel and 4 consecutive channels
 //     per register group: the epilogue moves 8 B per access;
 //   * XCD-aware tile order: consecutive M tiles of one N tile share an XCD.
-#include <stdlib.h>
-
 #include "mfma_common.h"
 
 namespace {
@@ -76,31 +74,26 @@ struct ConvArgs {
   int korder;
 };
 
-// ZK_TILE_HUGE=<bitmask> (A/B): which batch >= 1024 tile rules apply --
-// 1: 28x28x128 wgrad on conv3 64x64, 2: 256-input-channel wgrad 256x256 x 3
-// stages, 4: 64 -> 128 transition wgrad at 1024 blocks, 8: 7x7x512 wgrad on
-// 128x128, 16: 28x28x128 dgrad variant 27.  Default 16: each wgrad rule wins
-// alone (tools/tune_bconv.py --batch 1024) but costs 0.4-0.9 % of the E18
-// step, where those kernels overlap the data-gradient chain on the side
-// stream (bench A/B, 40 steps each: none 43.7k, 1 43.5k, 2 43.5k, 4 43.6k,
-// 8 43.3k, 16 43.8k img/s).
-bool huge_tiles_env(int bit = 31) {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ZK_TILE_HUGE");
-    v = (e && *e) ? atoi(e) : 16;
-  }
-  return (v & bit) != 0;
-}
+// Host-side kernel options, set from Python (ops/options.py -> zk_set_option;
+// the Runtime component owns the values, no environment variables):
+//   tile_huge (key 0, bitmask): which batch >= 1024 tile rules apply --
+//     1: 28x28x128 wgrad on conv3 64x64, 2: 256-input-channel wgrad 256x256 x 3
+//     stages, 4: 64 -> 128 transition wgrad at 1024 blocks, 8: 7x7x512 wgrad on
+//     128x128, 16: 28x28x128 dgrad variant 27.  Default 16: each wgrad rule wins
+//     alone (tools/tune_bconv.py --batch 1024) but costs 0.4-0.9 % of the E18
+//     step, where those kernels overlap the data-gradient chain on the side
+//     stream (bench A/B, 40 steps each: none 43.7k, 1 43.5k, 2 43.5k, 4 43.6k,
+//     8 43.3k, 16 43.8k img/s).
+//   korder (key 1): K-step order, see ConvArgs::korder.
+//   deterministic (key 2): split-K weight gradients through slabs reduced in
+//     a fixed order (no float atomics).
+int g_opt_tile_huge = 16;
+int g_opt_korder = 0;
+int g_opt_deterministic = 0;
 
-int korder_env() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ZK_KORDER");
-    v = (e && *e) ? atoi(e) : 0;
-  }
-  return v;
-}
+bool huge_tiles_env(int bit = 31) { return (g_opt_tile_huge & bit) != 0; }
+
+int korder_env() { return g_opt_korder; }
 
 // Reduce-scatter of 32 values over the 32 lanes of each wave half: after
 // the 5 butterfly steps lane r holds the half's total of value r (31
@@ -2083,7 +2076,7 @@ void wgrad_defaults(const IGeom& g, int& variant, int& target_blocks) {
     // the 128-channel layers (28x28x128: 262 -> 183 us), and 256x256 tiles
     // with 512 blocks for the 256-input-channel 3x3 layers (14x14x256:
     // 235 -> 168 us; 256 -> 512 stride 2: 130 -> 106 us).
-    // Batch >= 1024, opt-in (ZK_TILE_HUGE, see huge_tiles_env; standalone
+    // Batch >= 1024, opt-in (tile_huge option, see huge_tiles_env; standalone
     // tools/tune_bconv.py --batch 1024): 28x28x128 on the 64x64 three-row
     // conv3 tiles (406 -> 347 us), 256-input-channel layers on 256x256 x 3
     // stages at 1024 blocks (417 -> 349 us), the 64 -> 128 transition at 1024
@@ -2352,4 +2345,24 @@ ZK_EXPORT int zk_igemm_fwd_supported(int B, int H, int W, int Cin, int Cout, int
                             pt, pl, Ho, Wo, pad_ones, 0, variant, 1, nullptr) == 0;
   return zk_igemm_fwd(nullptr, nullptr, nullptr, nullptr, B, H, W, Cin, Cout, kh, kw, stride, pt,
                       pl, Ho, Wo, pad_ones, 0, variant, 1, nullptr) == 0;
+}
+
+// Host-side kernel options (see g_opt_* above; ops/options.py).  Returns 0,
+// or -1 for an unknown key.
+ZK_EXPORT int zk_set_option(int key, int value) {
+  switch (key) {
+    case 0: g_opt_tile_huge = value; return 0;
+    case 1: g_opt_korder = value; return 0;
+    case 2: g_opt_deterministic = value; return 0;
+    default: return -1;
+  }
+}
+
+ZK_EXPORT int zk_get_option(int key) {
+  switch (key) {
+    case 0: return g_opt_tile_huge;
+    case 1: return g_opt_korder;
+    case 2: return g_opt_deterministic;
+    default: return -1;
+  }
 }

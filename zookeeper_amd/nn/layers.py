@@ -21,7 +21,6 @@ i.e. physically OHWI — the layout the HIP implicit-GEMM kernels consume.
 from __future__ import annotations
 
 import math
-import os
 from typing import Optional, Tuple, Union
 
 import torch
@@ -37,9 +36,14 @@ def _pair(v: IntPair) -> Tuple[int, int]:
     return (v, v) if isinstance(v, int) else tuple(v)  # type: ignore[return-value]
 
 
-# 1x1 convs as MFMA / hipBLASLt GEMMs (ops/pointwise.py); ZK_PW_GEMM=0 keeps
+# 1x1 convs as MFMA GEMMs (ops/pointwise.py); ``runtime.pw_gemm=False`` keeps
 # them on the library convolution (A/B measurements)
-_PW_GEMM = os.environ.get("ZK_PW_GEMM", "1") != "0"
+
+
+def _pw_gemm() -> bool:
+    from zookeeper_amd.ops.options import OPTS
+
+    return OPTS.pw_gemm
 
 
 def _use_native(x: torch.Tensor) -> bool:
@@ -157,7 +161,7 @@ class QuantConv2d(nn.Module):
         """True when ``forward(x)`` runs on the native 1×1 GEMM path
         (``ops/pointwise.py``), which can take a residual-gradient hand-off."""
         if not (self.input_quantizer is None and self.kernel_quantizer is None
-                and self.kernel_size == (1, 1) and _PW_GEMM and _use_native(x)):
+                and self.kernel_size == (1, 1) and _pw_gemm() and _use_native(x)):
             return False
         from zookeeper_amd.ops import pointwise
 
@@ -194,7 +198,7 @@ class QuantConv2d(nn.Module):
             if depthwise.supported(x, self.weight):
                 return depthwise.depthwise_conv3x3(x, self.weight, self.stride[0], self.padding)
         if (self.input_quantizer is None and self.kernel_quantizer is None
-                and self.kernel_size == (1, 1) and _PW_GEMM and _use_native(x)):
+                and self.kernel_size == (1, 1) and _pw_gemm() and _use_native(x)):
             from zookeeper_amd.ops import pointwise
 
             if pointwise.supported(x, self.weight, self.stride, self.groups, self.bias):

@@ -35,6 +35,8 @@ SIGNATURES = {
     "zk_igemm_wgrad_f4": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),
     "zk_igemm_wgrad_f4_ws_bytes": (I64, [I32] * 14),
     "zk_igemm_dgrad_supported": (I32, [I32] * 13),
+    "zk_set_option": (I32, [I32, I32]),
+    "zk_get_option": (I32, [I32]),
     "zk_igemm_fwd_bf16": (I32, [P, P, P] + [I32] * 14 + [P]),
     "zk_igemm_fwd_bf16_supported": (I32, [I32] * 13),
     "zk_igemm_fwd_supported": (I32, [I32] * 15),

@@ -31,6 +31,12 @@ from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stre
                                         zeroed_scratch)
 
 
+# The forward kernels store the exact +-1 dot product as int16: a reduction
+# length K = kh*kw*Cin of 32768 could reach +32768 (all signs agreeing) and
+# wrap, so longer reductions take the library path.
+INT16_MAX_K = 32767
+
+
 def conv_supported(x: torch.Tensor, weight: torch.Tensor, stride, padding: str, groups: int,
                    bias: Optional[torch.Tensor] = None, pad_value: float = 0.0) -> bool:
     if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and weight.dim() == 4
@@ -42,12 +48,15 @@ def conv_supported(x: torch.Tensor, weight: torch.Tensor, stride, padding: str, 
     s = tuple(stride)
     return (s[0] == s[1] and s[0] <= 2 and kh <= 4 and kw <= 4 and x.shape[1] == Cin
             and Cin % 64 == 0 and Cout % 64 == 0
+            and kh * kw * Cin <= INT16_MAX_K
             and x.shape[0] * x.shape[2] * x.shape[3] < (1 << 24))
 
 
 def dense_supported(x: torch.Tensor, weight: torch.Tensor, bias=None) -> bool:
     return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and bias is None
-            and weight.shape[1] == x.shape[1] and x.shape[1] % 64 == 0)
+            and weight.device == x.device
+            and weight.shape[1] == x.shape[1] and x.shape[1] % 64 == 0
+            and x.shape[1] <= INT16_MAX_K)
 
 
 def _ones(owner, C: int, dev) -> tuple:

@@ -11,7 +11,7 @@ One autograd op per block (used by BinaryResNet-E and QuickNet on the
 3. ``zk_igemm_fwd_fp4`` MX-FP4 MFMA implicit GEMM (v_mfma_f32_32x32x64_f8f6f4,
    ±1 exact in e2m1, 4× the bf16 MFMA rate) on an LDS-DMA ring
    (igemm.hip) → exact int16 output (+ optional ReLU) and exact int64 BN
-   statistics (``ZK_BCONV_FP4=0``: the bf16 MFMA form ``zk_igemm_fwd``;
+   statistics (``runtime.bconv_fp4=False``: the bf16 MFMA form ``zk_igemm_fwd``;
    ``zk_bconv_fwd``, XNOR-popcount on bit tiles, for channel counts that do
    not tile by 64);
 4. ``zk_bn_finalize`` per-channel scale/shift, running statistics (Keras
@@ -30,45 +30,51 @@ output and per-channel vectors — no bf16 copy of the real-valued input.
 
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 
 from zookeeper_amd.nn.layers import same_padding
 from zookeeper_amd.ops import streams
+from zookeeper_amd.ops.options import OPTS
 from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
                                         zeroed_scratch)
 
 
-# Binary forward on MX-FP4 MFMA (4x the bf16 rate); ZK_BCONV_FP4=0 selects
-# the bf16 MFMA form (same exact integer outputs).
-FP4 = os.environ.get("ZK_BCONV_FP4", "1") != "0"
 # Copies of the forward BN statistics the conv blocks add into (block b into
 # copy b % STAT_STRIPES; zk_bn_finalize sums them): one [2][Cout] array took
 # thousands of serialised int64 atomics per cache line on the 56x56 layers.
 STAT_STRIPES = 32
-# ZK_FUSE_BNSUM=1: the BN-backward reduction (sum g, sum g*yhat) of a block
-# whose output only feeds the next block's identity shortcut + conv is done
-# in that block's dgrad epilogue, which writes exactly this gradient
-# (zk_igemm_dgrad_bnsum).  Off by default: measured on MI355X (E18, batch
-# 256) the extra epilogue work on the latency-bound dgrad tiles cost more
-# (33.4k -> 31.0k img/s) than the separate reduce kernels it removes.
-FUSE_BNSUM = os.environ.get("ZK_FUSE_BNSUM", "0") == "1"
-# ZK_WGRAD_F4=1: weight gradients read the e2m1 sign image the MX-FP4
-# forward already uses (zk_igemm_wgrad_f4: a quarter of the sx bytes, DMA'd
-# beside dy and expanded to bf16 +-1 in LDS), and no bf16 sign image is
-# written at all.  Off by default: measured on MI355X (E18, batch 512) the
-# in-LDS expansion costs more than the bytes it saves -- 128x128 tiles
-# 217 -> 352 us, 256x256 170 -> 183 us, conv3 64-channel 183 -> 203 us
-# (tools/tune_bconv.py), whole step 40.6k -> 40.1k img/s.
-WGRAD_F4 = FP4 and os.environ.get("ZK_WGRAD_F4", "0") == "1"
+# Variant switches (ops/options.py, set through the Runtime component):
+#   bconv_fp4  -- binary forward on MX-FP4 MFMA (4x the bf16 rate); off: the
+#                 bf16 MFMA form (same exact integer outputs);
+#   fuse_bnsum -- the BN-backward reduction (sum g, sum g*yhat) of a block
+#                 whose output only feeds the next block's identity shortcut
+#                 + conv is done in that block's dgrad epilogue, which writes
+#                 exactly this gradient (zk_igemm_dgrad_bnsum).  Off: measured
+#                 on MI355X (E18, batch 256) the extra epilogue work on the
+#                 latency-bound dgrad tiles cost more (33.4k -> 31.0k img/s)
+#                 than the separate reduce kernels it removes;
+#   wgrad_f4   -- weight gradients read the e2m1 sign image the MX-FP4
+#                 forward already uses (zk_igemm_wgrad_f4: a quarter of the
+#                 sx bytes, expanded to bf16 +-1 in LDS), and no bf16 sign
+#                 image is written.  Off: the in-LDS expansion costs more
+#                 than the bytes it saves -- 128x128 tiles 217 -> 352 us,
+#                 whole step 40.6k -> 40.1k img/s (batch 512).
+
+
+def _fp4() -> bool:
+    return OPTS.bconv_fp4
+
+
+def _wgrad_f4() -> bool:
+    return OPTS.bconv_fp4 and OPTS.wgrad_f4
 
 
 def bf16_sign_needed() -> bool:
     """Whether producers of a binary block's input (BN epilogues, the stem)
     must also write the bf16 +-1 sign image."""
-    return not WGRAD_F4
+    return not _wgrad_f4()
 
 
 class _BnSum:
@@ -118,7 +124,10 @@ class _BinaryBlockFn(torch.autograd.Function):
         # MFMA path (igemm.hip) for channel counts that tile by 64: the
         # forward and both gradients run as bf16 ±1 implicit GEMMs on the
         # sign image sx; otherwise the XNOR-popcount forward on packed bits.
-        mfma = Cout % 64 == 0 and Cin % 64 == 0 and stride <= 2 and kh <= 4 and kw <= 4
+        # (K = kh*kw*Cin <= 32767: the exact dot product is stored as int16)
+        mfma = (Cout % 64 == 0 and Cin % 64 == 0 and stride <= 2 and kh <= 4 and kw <= 4
+                and kh * kw * Cin <= 32767)
+        FP4, WGRAD_F4 = _fp4(), _wgrad_f4()
         fp4 = mfma and FP4
         # The previous block may already have quantised this input in its BN
         # epilogue (zk_bn_apply_sign): reuse its sign images and STE mask.
@@ -223,10 +232,10 @@ class _BinaryBlockFn(torch.autograd.Function):
                                 res.data_ptr() if res is not None else None, out.data_ptr(), P,
                                 Cout, st), "zk_bn_apply")
 
-        # BN-backward fusion hand-off (see FUSE_BNSUM): this block's reduction
+        # BN-backward fusion hand-off (OPTS.fuse_bnsum): this block's reduction
         # may be done by its successor; the predecessor's by this block.
         ctx.bnsum = None
-        if FUSE_BNSUM and will_backward and bn.training:
+        if OPTS.fuse_bnsum and will_backward and bn.training:
             sums_buf = zeroed_scratch(bn, "bwd_sums", (STAT_STRIPES, 2, Cout), torch.float32, dev)
             ctx.bnsum = _BnSum(y, mean, rstd, sums_buf)
             side["bnsum"] = ctx.bnsum
@@ -297,7 +306,7 @@ class _BinaryBlockFn(torch.autograd.Function):
             # then overlaps this block's dgrad and the next block's backward
             w_direct = direct_grad(weight_p, channels_last=True)
             dweight = None
-            f4 = WGRAD_F4 and sx4 is not None
+            f4 = _wgrad_f4() and sx4 is not None
             sxw = sx4 if f4 else sx  # weight-gradient sign operand
             side = streams.active() and w_direct is not None and sxw is not None
             if side:
@@ -451,6 +460,8 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
         raise ValueError("binary_block needs Cin % 32 == 0 and Cout % 8 == 0")
     if conv.stride[0] != conv.stride[1]:
         raise ValueError("binary_block needs a square stride")
+    if conv.weight.shape[1] * conv.weight.shape[2] * conv.weight.shape[3] > 32767:
+        raise ValueError("binary_block needs kh*kw*Cin <= 32767 (exact int16 conv output)")
     for name, t in (("conv.weight", conv.weight), ("bn.weight", bn.weight),
                     ("residual", residual)):
         if t is not None and t.device != x.device:

@@ -21,15 +21,14 @@ the MIOpen ``igemm_*_gtcx35`` kernels that round 1 still ran for them.
 
 from __future__ import annotations
 
-import os
 from typing import Optional, Tuple
 
 import torch
 
 from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
+from zookeeper_amd.ops.options import OPTS
 
 _INF = float("inf")
-ENABLED = os.environ.get("ZK_CONV_MFMA", "1") != "0"
 
 
 def geometry(H: int, W: int, kh: int, kw: int, stride: int, padding: str) -> Tuple[int, int, int, int]:
@@ -46,7 +45,7 @@ def geometry(H: int, W: int, kh: int, kw: int, stride: int, padding: str) -> Tup
 
 def supported(x: torch.Tensor, weight: torch.Tensor, stride, padding: str, groups: int,
               bias: Optional[torch.Tensor] = None, pad_value: float = 0.0) -> bool:
-    if not (ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+    if not (OPTS.conv_mfma and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
             and weight.device == x.device
             and weight.dim() == 4 and groups == 1 and bias is None and pad_value == 0.0):
         return False

@@ -22,20 +22,19 @@ through ``F.pad``).  The reference delegates these convs to Keras
 
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 
 from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
+from zookeeper_amd.ops.options import OPTS
 
 _INF = float("inf")
-ENABLED = os.environ.get("ZK_CONV3_MFMA", "1") != "0"
 
 
 def supported(x: torch.Tensor, weight: torch.Tensor, stride, padding: str, groups: int,
               bias: Optional[torch.Tensor] = None, pad_value: float = 0.0) -> bool:
-    return (ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+    return (OPTS.conv3_mfma and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
             and weight.device == x.device
             and weight.dim() == 4 and tuple(weight.shape[2:]) == (3, 3) and groups == 1
             and tuple(stride) == (1, 1) and padding == "same" and pad_value == 0.0

@@ -1,0 +1,96 @@
+"""Kernel-selection options of the native training path, in one place.
+
+Every switch that picks between kernel variants or execution schedules lives
+here as an attribute of :data:`OPTS`, read by the ops **at call time** (not at
+import time), so a run can change them before its first step.  They are set
+from typed config through the :class:`~zookeeper_amd.train.runtime.Runtime`
+component (``runtime.bconv_fp4=False`` on the CLI, sweepable with ``--grid``,
+written into ``config.json`` and the bench JSON) — no environment variables.
+
+The native library keeps its own copy of the options it consults on the host
+side of a launch (tile rules, K-step order, deterministic reductions); it is
+pushed through ``zk_set_option`` whenever :func:`set_options` runs.
+
+Defaults are the measured winners (README "Round-2 measurements that decided
+defaults").
+"""
+
+from __future__ import annotations
+
+import dataclasses
+from typing import Any, Dict
+
+
+@dataclasses.dataclass
+class KernelOptions:
+    # Binary forward on MX-FP4 MFMA (4x the bf16 rate); False selects the
+    # bf16 MFMA form (same exact integer outputs).
+    bconv_fp4: bool = True
+    # BN-backward sums of a block reduced in its successor's dgrad epilogue
+    # (measured slower: 40.7k -> 37.8k img/s at batch 512).
+    fuse_bnsum: bool = False
+    # Weight gradients on the e2m1 sign image (measured slower, 40.6k -> 40.1k).
+    wgrad_f4: bool = False
+    # Binary-conv weight gradients on a side HIP stream (44.9k vs 41.7k off).
+    wgrad_side_stream: bool = True
+    # HIP priority of that side stream (0 = default, negative = higher).
+    wgrad_priority: int = 0
+    # Recompute-fused ImageNet stem (False: the materialising kernels).
+    stem_fused: bool = True
+    # Float convolutions on the MFMA implicit-GEMM kernels (False: library).
+    conv_mfma: bool = True
+    conv3_mfma: bool = True
+    # 1x1 float convolutions as MFMA GEMMs.
+    pw_gemm: bool = True
+    # Batch >= 1024 tile-rule bitmask (igemm.hip, see tile_rule comments).
+    tile_huge: int = 16
+    # K-step order of the implicit GEMMs: 0 tap-major, 1 channel-chunk-major.
+    korder: int = 0
+    # Bit-reproducible gradients: split-K weight gradients reduced from slabs
+    # in a fixed order, BN / bias sums without float atomics.
+    deterministic: bool = False
+
+
+OPTS = KernelOptions()
+
+# keys the native library reads (zk_set_option); values are ints
+_NATIVE_KEYS = {"tile_huge": 0, "korder": 1, "deterministic": 2}
+
+
+def _push_native() -> None:
+    from zookeeper_amd.ops import _native
+
+    if not _native.available():
+        return
+    L = _native.lib()
+    fn = getattr(L, "zk_set_option", None)
+    if fn is None:
+        return
+    for name, key in _NATIVE_KEYS.items():
+        fn(key, int(getattr(OPTS, name)))
+
+
+def set_options(**kwargs: Any) -> KernelOptions:
+    """Update :data:`OPTS` (unknown names raise) and push the native ones."""
+    fields = {f.name: f for f in dataclasses.fields(KernelOptions)}
+    for k, v in kwargs.items():
+        if k not in fields:
+            raise TypeError(f"unknown kernel option {k!r}; known: {sorted(fields)}")
+        typ = fields[k].type
+        if typ in ("bool", bool):
+            v = bool(v)
+        elif typ in ("int", int):
+            v = int(v)
+        setattr(OPTS, k, v)
+    _push_native()
+    return OPTS
+
+
+def snapshot() -> Dict[str, Any]:
+    """The current options as a plain dict (run records, bench JSON)."""
+    return dataclasses.asdict(OPTS)
+
+
+def reset() -> None:
+    """Restore the defaults (tests)."""
+    set_options(**dataclasses.asdict(KernelOptions()))

@@ -27,11 +27,12 @@ from typing import Optional
 import torch
 
 from zookeeper_amd.nn.layers import same_padding
+from zookeeper_amd.ops.options import OPTS
 from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
                                         zeroed_scratch)
 
-# The recompute-fused kernels of stem_fused.hip are the default (ZK_STEM_FUSED=0
-# selects the materialising kernels of stem.hip): they never write the
+# The recompute-fused kernels of stem_fused.hip are the default
+# (``runtime.stem_fused=False`` selects the materialising kernels of stem.hip): they never write the
 # 112x112x64 conv output or its gradient, E18 at batch 1024 42.95k -> 44.6k
 # img/s.  Round 1 kept them opt-in for a run-to-run gradient difference seen
 # only with them; re-measured in round 2 (tools/grad_determinism.py, hw 64 /
@@ -41,7 +42,6 @@ from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stre
 # a near-total cancellation (|g| ~ 4e-3), changes by O(1) relative on some
 # repeats with either stem -- a property of the reductions, not of these
 # kernels (the stem alone is bit-reproducible, tools/one_stem.py --check).
-_FUSED = os.environ.get("ZK_STEM_FUSED", "1") == "1"
 
 
 def supported(x: torch.Tensor, conv, bn1, pool_k: int, pool_s: int) -> bool:
@@ -57,7 +57,7 @@ def supported(x: torch.Tensor, conv, bn1, pool_k: int, pool_s: int) -> bool:
 def _fused_ok(KH, Cout, Cin, KW, s, pk, ps, Ho, Wo, pt2, pl2, H2, W2) -> bool:
     """Geometry the recompute-fused kernels (stem_fused.hip) cover: 7-row
     kernels, 64 output channels, stride 2, 3x3/2 'same' max pool."""
-    return (_FUSED and KH == 7 and Cout == 64 and Cin <= 4 and KW <= 8 and s == 2 and pk == 3
+    return (OPTS.stem_fused and KH == 7 and Cout == 64 and Cin <= 4 and KW <= 8 and s == 2 and pk == 3
             and ps == 2 and pt2 in (0, 1) and pl2 in (0, 1) and H2 == (Ho + pt2 + 1) // 2
             and W2 == (Wo + pl2 + 1) // 2)
 
@@ -214,12 +214,12 @@ class _StemFn(torch.autograd.Function):
             out = torch.empty_like(p)
             if holder is not None and Cout % 32 == 0:
                 # also quantise the output for the first binary block
-                from zookeeper_amd.ops.binary import FP4, bf16_sign_needed
+                from zookeeper_amd.ops.binary import _fp4, bf16_sign_needed
 
                 sx = torch.empty_like(p) if bf16_sign_needed() else None
                 mask = torch.empty(P2 * Cout // 32, dtype=torch.int32, device=dev)
                 sx4 = (torch.empty((B, H2, W2, Cout // 2), dtype=torch.uint8, device=dev)
-                       if FP4 else None)
+                       if _fp4() else None)
                 check(L.zk_bn_apply_bf16_sign(p.data_ptr(), coef2.data_ptr(), out.data_ptr(),
                                               sx.data_ptr() if sx is not None else None,
                                               mask.data_ptr(),

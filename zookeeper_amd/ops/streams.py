@@ -25,24 +25,21 @@ Ordering is explicit with HIP events:
 
 Only active inside :func:`session` (the trainer opens one per step and
 flushes at its end), so direct callers of the ops keep single-stream
-semantics.  ``ZK_WGRAD_SIDE=0`` disables it.
+semantics.  ``runtime.wgrad_side_stream=False`` disables it.
 """
 
 from __future__ import annotations
 
 import contextlib
-import os
 from typing import Dict, List, Tuple
 
 import torch
 
 from zookeeper_amd.ops._native import grad_ready
-
-ENABLED = os.environ.get("ZK_WGRAD_SIDE", "1") != "0"
-_PRIORITY = int(os.environ.get("ZK_WGRAD_PRIORITY", "0"))
+from zookeeper_amd.ops.options import OPTS
 
 _active = False
-_streams: Dict[int, torch.cuda.Stream] = {}
+_streams: Dict[Tuple[int, int], torch.cuda.Stream] = {}
 _pending: List[Tuple[torch.cuda.Event, object]] = []
 # side-stream events whose gradients were signalled ready without the
 # compute stream waiting for them (flush(wait=False)); joined at session exit
@@ -55,12 +52,13 @@ def active() -> bool:
 
 def side_stream(device: torch.device) -> torch.cuda.Stream:
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    s = _streams.get(idx)
+    prio = OPTS.wgrad_priority
+    s = _streams.get((idx, prio))
     if s is None:
-        # ZK_WGRAD_PRIORITY: HIP stream priority of the side stream (0 = the
-        # default / lowest, negative = higher than the compute stream)
-        s = torch.cuda.Stream(device=idx, priority=_PRIORITY)
-        _streams[idx] = s
+        # runtime.wgrad_priority: HIP stream priority of the side stream (0 =
+        # the default / lowest, negative = higher than the compute stream)
+        s = torch.cuda.Stream(device=idx, priority=prio)
+        _streams[(idx, prio)] = s
     return s
 
 
@@ -101,7 +99,7 @@ def session(device: torch.device):
     """Enable the side stream for one training step's backward; everything
     deferred is flushed (compute stream ordered after it) on exit."""
     global _active
-    use = ENABLED and device.type == "cuda"
+    use = OPTS.wgrad_side_stream and device.type == "cuda"
     _pending.clear()
     _unwaited.clear()
     _active = use

@@ -62,7 +62,11 @@ from zookeeper_amd.parallel.flat import FlatParams
 class GradBucketer:
     def __init__(self, flat: FlatParams, world: int, bucket_mb: float = 10.0,
                  first_bucket_mb: float = 1.0, group=None, grad_dtype: Optional[torch.dtype] = None,
-                 timing: bool = False):
+                 timing: bool = False, force: bool = False):
+        """``force``: stay enabled with one rank (needs an initialised
+        process group, e.g. a 1-rank RCCL communicator from
+        ``zdist.init(single_group=True)``), so a single-GPU run exercises the
+        exact multi-GPU path: comm stream, events, RCCL kernels."""
         self.flat, self.world, self.group = flat, world, group
         self.grad_dtype = grad_dtype
         limit0 = int(first_bucket_mb * 2**20 / 4)
@@ -95,12 +99,16 @@ class GradBucketer:
         self._hooks = []
         self._seen = [False] * len(flat.slots)
         self._suspended = False
-        self.enabled = world > 1
+        self.enabled = world > 1 or bool(force)
+        if self.enabled and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("GradBucketer needs an initialised process group "
+                               "(zookeeper_amd.parallel.dist.init(single_group=True) for one rank)")
         self.cuda = flat.grad.is_cuda
         self.comm_stream = torch.cuda.Stream(flat.grad.device) if (self.enabled and self.cuda) else None
         self.timing = bool(timing) and self.comm_stream is not None
-        # diagnostics only: ZK_COMM_HOST_SYNC=1 synchronises the device before
-        # each collective and after the last (isolates stream-ordering bugs)
+        # debugging hook only: ZK_COMM_HOST_SYNC=1 synchronises the device
+        # before each collective and after the last (isolates stream-ordering
+        # bugs)
         hs = os.environ.get("ZK_COMM_HOST_SYNC", "0") if self.cuda else "0"
         self._sync_launch = hs in ("1", "launch")
         self._sync_finish = hs in ("1", "finish")

@@ -40,8 +40,12 @@ def env_world() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
-def init(backend: str = "auto", timeout_s: float = 600.0) -> DistInfo:
+def init(backend: str = "auto", timeout_s: float = 600.0, single_group: bool = False) -> DistInfo:
     """Initialise (once) and return the rank / device binding.
+
+    ``single_group``: also create a process group when the job has one rank
+    (``force_dp``: a 1-rank RCCL communicator, so the bucketed all-reduce
+    path runs on one GPU exactly as it does on eight).
 
     ``timeout_s`` (overridden by ``ZK_DIST_TIMEOUT_S``) bounds every
     collective: a rank that dies or hangs makes the others' collectives raise
@@ -64,15 +68,20 @@ def init(backend: str = "auto", timeout_s: float = 600.0) -> DistInfo:
         # ZK_DIST_BACKEND=gloo rehearses a multi-rank GPU run with several
         # ranks sharing one GPU (RCCL wants a distinct GPU per rank)
         backend = os.environ.get("ZK_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
-    if world > 1:
+    if world > 1 or single_group:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            from zookeeper_amd.parallel.launch import free_port
+
+            os.environ["MASTER_PORT"] = str(free_port())
         os.environ.setdefault("MASTER_PORT", "29500")
         kwargs = dict(backend=backend, rank=rank, world_size=world,
                       timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kwargs["device_id"] = device
         dist.init_process_group(**kwargs)
-    _INFO = DistInfo(rank, world, local, device, backend if world > 1 else "none")
+    grouped = world > 1 or single_group
+    _INFO = DistInfo(rank, world, local, device, backend if grouped else "none")
     return _INFO
 
 
@@ -95,6 +104,20 @@ def all_reduce_max(value: float) -> float:
                      device=_INFO.device if _INFO.backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def all_reduce_max_values(values, device=None):
+    """Element-wise MAX of a few floats over the ranks of the default group
+    (every rank gets the same list back).  Uses a device tensor for RCCL and
+    a host tensor otherwise; a no-op without a process group."""
+    values = [float(v) for v in values]
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return values
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.tensor(values, dtype=torch.float64,
+                     device=(device if device is not None else _INFO.device) if on_dev else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.tolist()]
 
 
 def all_reduce_mean_(t: torch.Tensor) -> torch.Tensor:

@@ -45,6 +45,7 @@ from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 from zookeeper_amd.core.utils import parse_value_from_string
+from zookeeper_amd.parallel.devices import visible_gpu_count, visible_gpu_ids
 
 
 def parse_grid(specs: Sequence[str]) -> List[Tuple[str, List[Any]]]:
@@ -74,25 +75,13 @@ def run_name(overrides: Dict[str, Any]) -> str:
 
 
 def count_gpus() -> int:
-    """Visible GPUs without initialising HIP in this process."""
-    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        val = os.environ.get(var)
-        if val:
-            return len([d for d in val.split(",") if d.strip() != ""])
-    try:
-        import torch
-
-        return torch.cuda.device_count()  # does not initialise the runtime
-    except Exception:
-        return 0
+    """Visible GPUs without initialising HIP in this process (environment and
+    the KFD sysfs topology only, ``parallel/devices.py``)."""
+    return visible_gpu_count()
 
 
 def visible_ids() -> List[str]:
-    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        val = os.environ.get(var)
-        if val:
-            return [d.strip() for d in val.split(",") if d.strip() != ""]
-    return [str(i) for i in range(count_gpus())]
+    return visible_gpu_ids()
 
 
 @dataclass

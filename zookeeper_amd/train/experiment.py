@@ -29,6 +29,7 @@ from zookeeper_amd.data.dataset import Dataset
 from zookeeper_amd.data.loader import DeviceLoader
 from zookeeper_amd.data.preprocessing import Preprocessing
 from zookeeper_amd.train.optimizers import OptimizerSpec
+from zookeeper_amd.train.runtime import Runtime
 
 
 class Experiment:
@@ -72,6 +73,9 @@ class TrainingExperiment(Experiment):
     device_pool: int = Field(0)
     bucket_mb: float = Field(10.0)
     print_summary: bool = Field(True)
+    # kernel variants and schedule (side stream, graph replay, deterministic
+    # reductions, ...): typed, recorded in config.json, sweepable
+    runtime: Runtime = ComponentField(Runtime)
 
     def run_dir(self) -> Optional[str]:
         if self.output_dir is None:
@@ -84,11 +88,13 @@ class TrainingExperiment(Experiment):
         from zookeeper_amd.parallel import dist as zdist
         from zookeeper_amd.parallel.ddp import all_reduce_buffers
         from zookeeper_amd.train import checkpoint as ckpt
-        from zookeeper_amd.train.metrics import MetricsLogger, resolve_metrics
+        from zookeeper_amd.train.metrics import MetricsLogger, comm_summary, resolve_metrics
         from zookeeper_amd.train.trainer import Trainer
 
         logit_metrics = {k: f for k, f in resolve_metrics(self.metrics).items() if f is not None}
-        info = zdist.init()
+        rt = self.runtime
+        rt.apply()
+        info = zdist.init(single_group=rt.force_dp)
         torch.manual_seed(self.seed)
         if info.is_main:
             print(self, flush=True)
@@ -101,8 +107,11 @@ class TrainingExperiment(Experiment):
         model = self.model
         if info.is_main and self.print_summary:
             print(summary(model), flush=True)
+        dp = info.world > 1 or rt.force_dp
         trainer = Trainer(model, self.loss, base_getattr(self, "optimizer"), info,
-                          bucket_mb=self.bucket_mb, metric_fns=logit_metrics)
+                          bucket_mb=self.bucket_mb, metric_fns=logit_metrics,
+                          graph=rt.trainer_graph(), force_dp=rt.force_dp,
+                          comm_timing=dp and rt.comm_timing and info.device.type == "cuda")
         trainer.optimizer.total_steps = total_steps
 
         run_dir = self.run_dir()
@@ -130,6 +139,7 @@ class TrainingExperiment(Experiment):
         it = iter(loader)
         step = start_step
         t_start = time.perf_counter()
+        t_other = 0.0  # validation, checkpoints, BN buffer sync: not training throughput
         last_rec = {}
         while step < total_steps:
             batch = next(it)
@@ -139,9 +149,11 @@ class TrainingExperiment(Experiment):
             step += 1
             epoch_end = step % steps_per_epoch == 0
             if step % self.log_every == 0 or epoch_end or step == total_steps:
-                last_rec = metrics.flush(step, {"epoch": step / steps_per_epoch,
-                                                "lr": trainer.optimizer.spec.lr_at(
-                                                    step - 1, total_steps)})
+                extra = {"epoch": step / steps_per_epoch,
+                         "lr": trainer.optimizer.spec.lr_at(step - 1, total_steps)}
+                extra.update(comm_summary(trainer.bucketer.pop_timings()))
+                last_rec = metrics.flush(step, extra)
+            t_o = time.perf_counter()
             save_now = run_dir is not None and (
                 (self.checkpoint_every and step % self.checkpoint_every == 0)
                 or step == total_steps)
@@ -159,11 +171,18 @@ class TrainingExperiment(Experiment):
                     print(f"validation step={step} " +
                           " ".join(f"{k}={v:.5g}" for k, v in val.items()), flush=True)
                     result["validation"] = val
+            dt_other = time.perf_counter() - t_o
+            t_other += dt_other
+            metrics.exclude(dt_other)
         loader.close()
         wall = time.perf_counter() - t_start
-        result.update(steps=step, train=last_rec, wall_s=wall,
+        train_s = max(wall - t_other, 1e-9)
+        result.update(steps=step, train=last_rec, wall_s=wall, train_s=train_s,
                       final_loss=last_rec.get("loss"),
-                      images_per_sec=(step - start_step) * global_batch / max(wall, 1e-9))
+                      # training steps only (validation / checkpoint time excluded)
+                      images_per_sec=(step - start_step) * global_batch / train_s,
+                      end_to_end_images_per_sec=(step - start_step) * global_batch / max(wall, 1e-9),
+                      runtime=rt.as_dict())
         # a sweep (zookeeper_amd/sweep.py) collects every run's result here
         out = os.environ.get("ZK_RESULT_JSON")
         if out and info.is_main:
@@ -195,7 +214,7 @@ class TrainingExperiment(Experiment):
             loss, hits = trainer.eval_step(x, y)
             tot_loss += loss.float()
             for k in keys:
-                tot_hits[k] += (trainer.last_metrics[k] if k in trainer.last_metrics
+                tot_hits[k] += (trainer.eval_metrics[k] if k in trainer.eval_metrics
                                 else hits).float()
         loader.close()
         vals = torch.stack([tot_loss] + [tot_hits[k] for k in keys]).double()

@@ -4,7 +4,8 @@ Per step the trainer only adds loss and hit counts into device scalars (no
 host synchronisation); a flush does one ``.item()`` round-trip, averages
 across data-parallel ranks, and appends a JSON line to ``metrics.jsonl`` on
 rank 0 (loss, the configured metrics, images/sec per GPU and for the whole
-job, step time).  The reference relied on Keras' progress bar and
+job, step time, and under data parallelism the per-step all-reduce time and
+the part of it exposed after backward).  The reference relied on Keras' progress bar and
 ``compile(metrics=...)`` (examples/larq_experiment.py:118,142).
 
 Configured metric names follow Keras: ``accuracy`` /
@@ -36,6 +37,22 @@ def topk_hits(k: int) -> Callable[[torch.Tensor, torch.Tensor], torch.Tensor]:
         return (top == labels.view(-1, 1)).any(dim=1).sum()
 
     return fn
+
+
+def comm_summary(timings: Sequence[Dict[str, float]]) -> Dict[str, float]:
+    """Median per-step communication of a logging window, from
+    ``GradBucketer.pop_timings()``: ``comm_ms`` (first collective start ->
+    last end), ``exposed_ms`` (how long communication ran past the end of
+    backward).  Empty without data parallelism / timing."""
+    if not timings:
+        return {}
+
+    def med(key):
+        xs = sorted(t[key] for t in timings)
+        return xs[len(xs) // 2]
+
+    return {"comm_ms": med("comm_ms"), "exposed_ms": med("exposed_ms"),
+            "exposed_ms_max": max(t["exposed_ms"] for t in timings)}
 
 
 def resolve_metrics(names: Optional[Sequence[str]]) -> Dict[str, Optional[Callable]]:
@@ -89,6 +106,11 @@ class MetricsLogger:
                 acc += extra[k].detach().float()
         self.examples += batch
         self.steps += 1
+
+    def exclude(self, seconds: float) -> None:
+        """Leave ``seconds`` (validation, checkpoints) out of the next flush's
+        throughput."""
+        self._t0 += seconds
 
     def flush(self, step: int, extra: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
         if self.steps == 0:

@@ -1,0 +1,78 @@
+"""``Runtime``: the execution / kernel-selection switches of a run as typed,
+configurable Fields.
+
+The reference's premise is that everything a run depends on is injected
+through ``Field``s and reproducible from the resolved config
+(zookeeper/core/component.py:461-695).  The native training path has a
+number of schedule and kernel-variant choices (side-stream weight gradients,
+MX-FP4 forward, fused stem, tile rules, HIP-graph replay, deterministic
+reductions, ...); they live here instead of in environment variables, so a
+run can set them on the CLI (``runtime.bconv_fp4=False``), sweep them
+(``--grid runtime.tile_huge=[0,16]``), and they are written into
+``config.json`` and the bench JSON.
+
+:meth:`Runtime.apply` pushes the kernel options into
+:data:`zookeeper_amd.ops.options.OPTS` (and the native library); the trainer
+reads the schedule options (``graph``, ``force_dp``, ``comm_timing``)
+directly.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+from typing import Any, Dict
+
+from zookeeper_amd.core.component import component
+from zookeeper_amd.core.field import Field
+from zookeeper_amd.ops import options as _options
+
+_KERNEL_FIELDS = tuple(f.name for f in dataclasses.fields(_options.KernelOptions))
+
+
+@component
+class Runtime:
+    # --- kernel variants (ops/options.py documents each and its measurement)
+    bconv_fp4: bool = Field(True)
+    fuse_bnsum: bool = Field(False)
+    wgrad_f4: bool = Field(False)
+    wgrad_side_stream: bool = Field(True)
+    wgrad_priority: int = Field(0)
+    stem_fused: bool = Field(True)
+    conv_mfma: bool = Field(True)
+    conv3_mfma: bool = Field(True)
+    pw_gemm: bool = Field(True)
+    tile_huge: int = Field(16)
+    korder: int = Field(0)
+    # Bit-reproducible gradients (fixed-order reductions, no float atomics on
+    # the gradient path); slower.
+    deterministic: bool = Field(False)
+
+    # --- schedule
+    # HIP-graph replay of forward + backward: "off", "on", or "auto" (replay
+    # only if the warmup shows the step host-bound; decided on every rank
+    # together under data parallelism).
+    graph: str = Field("off")
+    # Keep the bucketed all-reduce on even with one rank (a 1-rank RCCL
+    # group): exercises the data-parallel path on a single GPU.
+    force_dp: bool = Field(False)
+    # Time every bucket's collective (comm_ms / exposed_ms in metrics.jsonl).
+    comm_timing: bool = Field(True)
+
+    def __post_configure__(self) -> None:
+        if self.graph not in ("off", "on", "auto"):
+            raise ValueError(f"runtime.graph must be 'off', 'on' or 'auto', got {self.graph!r}")
+
+    def kernel_options(self) -> Dict[str, Any]:
+        return {k: getattr(self, k) for k in _KERNEL_FIELDS}
+
+    def apply(self) -> _options.KernelOptions:
+        """Make these kernel options current (``ops.options.OPTS``)."""
+        return _options.set_options(**self.kernel_options())
+
+    def trainer_graph(self):
+        return {"off": False, "on": True, "auto": "auto"}[self.graph]
+
+    def as_dict(self) -> Dict[str, Any]:
+        d = self.kernel_options()
+        d.update(graph=self.graph, force_dp=self.force_dp, comm_timing=self.comm_timing)
+        return d

@@ -40,7 +40,8 @@ class Trainer:
                  info: Optional[zdist.DistInfo] = None, bucket_mb: float = 10.0,
                  first_bucket_mb: float = 1.0, grad_dtype: Optional[torch.dtype] = None,
                  graph: Union[bool, str] = False, graph_warmup: int = 3,
-                 comm_timing: bool = False, metric_fns: Optional[dict] = None):
+                 comm_timing: bool = False, metric_fns: Optional[dict] = None,
+                 force_dp: bool = False):
         self.info = info or zdist.info()
         if info is None and self.info.world == 1 and self.info.device.type == "cpu" \
                 and torch.cuda.is_available():
@@ -56,14 +57,17 @@ class Trainer:
         # exposed as ``last_metrics`` (graph mode: static graph outputs)
         self.metric_fns = dict(metric_fns or {})
         self.last_metrics: dict = {}
+        self.eval_metrics: dict = {}  # eval_step's (kept apart: graph replays reuse last_metrics)
         self.flat = FlatParams(self.model, self.device)
         if self.info.world > 1:
             # One broadcast of the flat parameter buffer + the BN buffers.
             zdist.broadcast_(self.flat.data)
             for b in self.model.buffers():
                 zdist.broadcast_(b)
+        # force_dp: the bucketed all-reduce stays on with one rank (a 1-rank
+        # RCCL group), so one GPU runs the exact data-parallel code path
         self.bucketer = GradBucketer(self.flat, self.info.world, bucket_mb, first_bucket_mb,
-                                     grad_dtype=grad_dtype, timing=comm_timing)
+                                     grad_dtype=grad_dtype, timing=comm_timing, force=force_dp)
         self.optimizer = optimizer.create(self.flat, grad_scale=1.0 / self.info.world)
         # HIP-graph replay of zero-grad + forward + loss + backward: one graph
         # launch instead of ~300 kernel launches and the Python / autograd
@@ -124,6 +128,12 @@ class Trainer:
                 ev[1].record()
                 ev[1].synchronize()
                 t_gpu = ev[0].elapsed_time(ev[1]) / 1e3
+                if self.bucketer.enabled:
+                    # every rank must take the same path: replayed graphs issue
+                    # the bucket collectives after the replay in index order,
+                    # eager steps during backward in readiness order -- mixed,
+                    # the ranks' collectives would not match
+                    t_host, t_gpu = zdist.all_reduce_max_values([t_host, t_gpu], self.device)
                 self.graph_probe = (t_host, t_gpu)
                 self.graph = t_host > 0.85 * t_gpu  # host-bound: replay
             return out
@@ -147,7 +157,7 @@ class Trainer:
         try:
             logits = self.model(x)
             if self.metric_fns:
-                self.last_metrics = {k: f(logits, y) for k, f in self.metric_fns.items()}
+                self.eval_metrics = {k: f(logits, y) for k, f in self.metric_fns.items()}
             return self.loss_fn(logits, y)
         finally:
             self.model.train(was)
