@@ -11,8 +11,8 @@
 #   prof[:model[:batch]]               rocprofv3 --kernel-trace --stats of bench.py
 #   pmc[:model]      three rocprofv3 PMC passes over 2 training steps (SQ MFMA/LDS,
 #                    FETCH_SIZE, WRITE_SIZE; one counter group per run)
-#   pmcconv:op:shape PMC passes over one conv kernel (tools/one_conv.py), e.g.
-#                    pmcconv:dgrad:56,56,64,64,1
+#   pmcconv:op:shape[:batch] PMC passes over one conv kernel (tools/one_conv.py), e.g.
+#                    pmcconv:dgrad:56,56,64,64,1:1024
 #   benchargs:<a,b>  bench.py with arbitrary comma-separated arguments
 #   profargs:<a,b>   rocprofv3 --kernel-trace --stats of bench.py with those arguments
 #   tune[:args]      tools/tune_bconv.py with the given (comma-separated) args; '+'
@@ -95,13 +95,15 @@ for spec in "$@"; do
     pmcconv)
       R="$(pwd)"
       nm="${a1}_${a2//,/_}"
-      gpu_step 120 "$OUT/pmcconv_${nm}_time.log" python tools/one_conv.py --op "$a1" --shape "$a2" --reps 50 || exit $?
+      bt="${a3:-256}"
+      nm="${nm}_b${bt}"
+      gpu_step 120 "$OUT/pmcconv_${nm}_time.log" python tools/one_conv.py --op "$a1" --shape "$a2" --batch "$bt" --reps 50 || exit $?
       for pass in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT" \
                   "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"; do
         tag=$(echo "$pass" | cut -d' ' -f1)
         (cd /tmp && gpu_step 90 "$R/$OUT/pmcconv_${nm}_${tag}.log" timeout -s KILL 80 rocprofv3 --pmc $pass \
           -d "$R/$OUT/pmcconv_${nm}_${tag}" -o run --output-format csv -- python3 "$R/tools/one_conv.py" \
-          --op "$a1" --shape "$a2" --reps 5) || exit $?
+          --op "$a1" --shape "$a2" --batch "$bt" --reps 5) || exit $?
       done
       ;;
     pmcpy)

@@ -48,7 +48,12 @@ def _grads(side: bool, monkeypatch):
 def test_side_stream_wgrad_matches_single_stream(monkeypatch):
     g_side, ready_side, flat = _grads(True, monkeypatch)
     g_one, ready_one, _ = _grads(False, monkeypatch)
-    assert ((g_side - g_one).norm() / g_one.norm()).item() < 1e-5
+    # fp32-atomic ordering noise in the split-K / BN-backward sums (~1e-7),
+    # amplified through the binary blocks (README "Known issues"): measured
+    # 1e-6 .. 8e-5 over the whole gradient; a missing or doubled weight
+    # gradient is O(1).  The deterministic mode is bit-exact
+    # (tests/gpu/test_determinism.py).
+    assert ((g_side - g_one).norm() / g_one.norm()).item() < 1e-3
     # every binary conv weight reported ready once, in both modes
     convs = [s.name for s in flat.slots if s.name.endswith("conv.weight")]
     for name in convs:

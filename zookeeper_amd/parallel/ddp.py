@@ -188,7 +188,20 @@ class GradBucketer:
                 self._works.append((self._stager.submit(b, lo, hi, view, self.comm_stream),
                                     view, b))
             else:
-                self._works.append((self._issue(view), view, b))
+                work, tmp = self._issue(view)
+                # RCCL: order the comm stream after this collective right away
+                # (a stream wait, the host does not block), so the bucket's
+                # end event marks the collective's own completion instead of
+                # the end of backward (finish() would otherwise record every
+                # end event behind the last bucket's launch)
+                work.wait()
+                if tmp is not None:
+                    view.copy_(tmp, non_blocking=True)
+                if self.timing:
+                    ev = self._events()
+                    ev["end"][b] = ev["mk"]()
+                    ev["end"][b].record(self.comm_stream)
+                self._works.append(((_DoneWork(), None), view, b))
         self._launched[b] = True
 
     def _issue(self, view: torch.Tensor):
@@ -225,7 +238,7 @@ class GradBucketer:
                     work.wait()  # comm stream waits on the collective's stream
                     if tmp is not None:
                         view.copy_(tmp, non_blocking=True)
-                    if self.timing:
+                    if self.timing and b not in self._events()["end"]:
                         ev = self._events()
                         ev["end"][b] = ev["mk"]()
                         ev["end"][b].record(self.comm_stream)
@@ -268,6 +281,13 @@ class GradBucketer:
         for s in self.flat.slots:
             if hasattr(s.param, "_zk_grad_ready"):
                 del s.param._zk_grad_ready
+
+
+class _DoneWork:
+    """A collective the comm stream is already ordered after."""
+
+    def wait(self):
+        return True
 
 
 class _StagedWork:

@@ -140,7 +140,13 @@ class Trainer:
         if self._graph is None:
             self._static_in = (x.clone(), y.clone())  # clone keeps x's channels_last strides
             self._graph = torch.cuda.CUDAGraph()
-            with self.bucketer.suspended(), torch.cuda.graph(self._graph):
+            # thread_local capture: other threads keep their HIP calls -- the
+            # RCCL process group's watchdog queries its work events while we
+            # capture, which a global-mode capture turns into
+            # hipErrorStreamCaptureUnsupported (found on the 1-rank RCCL test)
+            torch.cuda.synchronize(self.device)
+            with self.bucketer.suspended(), torch.cuda.graph(self._graph,
+                                                             capture_error_mode="thread_local"):
                 self._static_out = self._forward_backward(*self._static_in)
         else:
             self._static_in[0].copy_(x)
