@@ -127,3 +127,99 @@ def test_model_forward_bit_identical_and_gradient_noise_bounded():
     # the BN backward sums use striped fp32 atomics: ordering noise, amplified
     # through near-cancelling sums (see tests/gpu/test_graph.py), stays small
     assert ((g1 - g0).norm() / g0.norm()).item() < 2e-2
+
+
+@pytest.fixture
+def deterministic():
+    from zookeeper_amd.ops import options
+
+    options.set_options(deterministic=True)
+    try:
+        yield
+    finally:
+        options.reset()
+
+
+def _e18_grads(steps_x, model_seed=1234):
+    from zookeeper_amd.models.binary_resnet import BinaryResNetE
+    from zookeeper_amd.parallel.flat import FlatParams
+    from zookeeper_amd.train.losses import get_loss
+    from zookeeper_amd.train.trainer import prepare_model
+
+    torch.manual_seed(model_seed)
+    dev = torch.device("cuda", 0)
+    model = prepare_model(BinaryResNetE((64, 64, 3), 10, 18, backend="hip"), dev).train()
+    flat = FlatParams(model, dev)
+    loss_fn = get_loss("sparse_categorical_crossentropy")
+    x, y = steps_x
+    flat.zero_grad()
+    from zookeeper_amd.ops import streams
+
+    loss, _ = loss_fn(model(x), y)
+    with streams.session(dev):  # side-stream weight gradients on, as in training
+        loss.backward()
+    torch.cuda.synchronize()
+    return loss.detach().clone(), flat.grad.clone(), [b.clone() for b in model.buffers()]
+
+
+def _batch(seed=9, n=8):
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, 3, 64, 64, generator=g).to(dev, torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (n,), generator=g).to(dev)
+    return x, y
+
+
+def test_deterministic_mode_gradients_bit_identical(deterministic):
+    """Runtime(deterministic=True): no float atomics on the gradient path
+    (BN-backward sums per block + fixed-order sum, float BN statistics per
+    block, per-row losses summed in order, slab split-K weight gradients):
+    two forward + backward passes give bit-identical loss, gradients and BN
+    running statistics."""
+    batch = _batch()
+    l0, g0, b0 = _e18_grads(batch)
+    l1, g1, b1 = _e18_grads(batch)
+    assert torch.equal(l0, l1)
+    diff = (g0 != g1).nonzero()
+    assert diff.numel() == 0, f"{diff.shape[0]} gradient elements differ, first at {diff[:5]}"
+    for a, b in zip(b0, b1):
+        assert torch.equal(a, b)
+
+
+def test_deterministic_resume_matches_uninterrupted_run(tmp_path, deterministic):
+    """Save at step k, resume in a fresh model/trainer, run to 2k: bit-equal
+    to the uninterrupted 2k-step run (deterministic mode)."""
+    from zookeeper_amd.core import configure
+    from zookeeper_amd.models.binary_resnet import BinaryResNetE
+    from zookeeper_amd.train import Adam, Trainer
+    from zookeeper_amd.train import checkpoint as ckpt
+
+    k = 2
+    batches = [_batch(seed=100 + i) for i in range(2 * k)]
+
+    def make():
+        torch.manual_seed(1234)
+        spec = Adam()
+        configure(spec, {"learning_rate": 1e-3})
+        model = BinaryResNetE((64, 64, 3), 10, 18, backend="hip")
+        return Trainer(model, "sparse_categorical_crossentropy", spec)
+
+    full = make()
+    for x, y in batches:
+        full.train_step(x, y)
+    torch.cuda.synchronize()
+    ref = full.flat.data.detach().clone()
+
+    first = make()
+    for x, y in batches[:k]:
+        first.train_step(x, y)
+    torch.cuda.synchronize()
+    path = ckpt.save(str(tmp_path), k, first.model, first.optimizer)
+    resumed = make()
+    ckpt.load(path, resumed.model, resumed.optimizer)
+    for x, y in batches[k:]:
+        resumed.train_step(x, y)
+    torch.cuda.synchronize()
+    got = resumed.flat.data.detach()
+    assert torch.equal(got, ref), (got - ref).abs().max().item()

@@ -48,7 +48,9 @@ def main():
     ap.add_argument("--ops", default="fwd4,dgrad,wgrad")
     ap.add_argument("--dvariant", type=int, default=-1)
     ap.add_argument("--wvariant", type=int, default=-1)
-    ap.add_argument("--shapes", default="all", help="all or H,W,Cin,Cout,s;...")
+    ap.add_argument("--shapes", default="all", help="all or H+W+Cin+Cout+s/... ('+' or ',')")
+    ap.add_argument("--dvariants", default=None, help="dgrad variants to compare (+-separated)")
+    ap.add_argument("--wvariants", default=None, help="wgrad variants to compare (+-separated)")
     args = ap.parse_args()
     from zookeeper_amd.models.binary_resnet import stage_shapes
     from zookeeper_amd.nn.layers import same_padding
@@ -59,7 +61,8 @@ def main():
     if args.shapes == "all":
         shapes = sorted(set(stage_shapes((224, 224, 3))), key=lambda s: (-s[0], s[2], s[4]))
     else:
-        shapes = [tuple(int(v) for v in s.split(",")) for s in args.shapes.split(";")]
+        shapes = [tuple(int(v) for v in s.replace("+", ",").split(","))
+                  for s in args.shapes.split("/")]
     rows = []
     tot = {"fwd4": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     counts = {}
@@ -114,17 +117,34 @@ def main():
                 "dgrad": (S_out + 2 * S_in + S_in / 16, BF16_PEAK),  # dy, dres, dx, mask
                 "wgrad": (S_out + S_in, BF16_PEAK)}          # dy, sx
         fns = {"fwd4": fwd4, "dgrad": dgrad, "wgrad": wgrad}
+        runs = []
         for op in args.ops.split(","):
-            us = timeit(fns[op], args.reps)
+            vs = {"dgrad": args.dvariants, "wgrad": args.wvariants}.get(op)
+            for v in ([int(x) for x in vs.split("+")] if vs else [None]):
+                runs.append((op, v))
+        for op, v in runs:
+            if v is not None:
+                if op == "dgrad":
+                    args.dvariant = v
+                else:
+                    args.wvariant = v
+                    nb = L.zk_igemm_wgrad_ws_bytes(B, cin, H, W, Ho, Ho, cout, 3, 3, s, pt, pt, 0, v)
+                    ws = torch.empty(max(nb, 4) // 4, device="cuda")
+            try:
+                us = timeit(fns[op], args.reps)
+            except AssertionError:
+                print(f"{op} v{v}: unsupported for this shape", flush=True)
+                continue
             nbytes, peak = need[op]
             t_c, t_m = flops / peak * 1e6, nbytes / HBM * 1e6
-            rec = {"op": op, "shape": [H, W, cin, cout, s], "us": round(us, 1),
+            rec = {"op": op, "variant": v, "shape": [H, W, cin, cout, s], "us": round(us, 1),
                    "pflops": round(flops / us / 1e9, 3), "gbps": round(nbytes / us / 1e3, 1),
                    "floor_compute_us": round(t_c, 1), "floor_hbm_us": round(t_m, 1),
                    "x_floor": round(us / max(t_c, t_m), 2), "layers": counts.get((H, W, cin, cout, s), 0)}
             rows.append(rec)
-            tot[op] += us * rec["layers"]
-            print(f"{op:6s} {H:3d}x{W:<3d} {cin:4d}->{cout:<4d} s{s}  {us:8.1f} us  "
+            if v is None:
+                tot[op] += us * rec["layers"]
+            print(f"{op:6s}{'' if v is None else ' v' + str(v):5s} {H:3d}x{W:<3d} {cin:4d}->{cout:<4d} s{s}  {us:8.1f} us  "
                   f"{rec['pflops']:6.3f} PF/s  {rec['gbps']:7.1f} GB/s  floor c {t_c:6.1f} "
                   f"m {t_m:6.1f}  x{rec['x_floor']:.2f}  (x{rec['layers']} layers)", flush=True)
         del x, dy, dx, dres, sx, sx4, ws, y

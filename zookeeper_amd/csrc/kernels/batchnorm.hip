@@ -185,6 +185,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   }
   __syncthreads();
   float* out = sums + (long long)(blockIdx.x % stripes) * 2 * C;  // striped copies
+  // one copy per block (stripes >= blocks, the deterministic mode): plain
+  // stores, summed in a fixed order by bn_bwd_coef
+  const bool own = stripes >= (int)gridDim.x;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const int gcg = c / 8, k = c % 8;
     float a = 0.f, b = 0.f;
@@ -192,8 +195,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       a += red[0][rr * CG + gcg][k];
       b += red[1][rr * CG + gcg][k];
     }
-    atomicAdd(out + c, a);
-    atomicAdd(out + C + c, b);
+    if (own) {
+      out[c] = a;
+      out[C + c] = b;
+    } else {
+      atomicAdd(out + c, a);
+      atomicAdd(out + C + c, b);
+    }
   }
 }
 
@@ -387,11 +395,14 @@ ZK_EXPORT int zk_bn_apply_sign(const void* y, const void* scale, const void* shi
 }
 
 // sums: [stripes][2][C] fp32 copies (block b adds into copy b % stripes).
+ZK_EXPORT int zk_bn_bwd_reduce_blocks() { return 512; }
+
 ZK_EXPORT int zk_bn_bwd_reduce(const void* g, const void* y, const void* mean, const void* rstd,
                                void* sums, long long P, int C, int stripes, hipStream_t stream) {
   if (stripes < 1) stripes = 1;
   // 512 blocks x 4 rows in flight per thread: enough bytes in flight for
-  // HBM, few enough per-block atomics into the 2*C sums
+  // HBM, few enough per-block atomics into the 2*C sums.  stripes >= 512:
+  // every block owns a copy (no atomics: bit-reproducible).
   const int blocks = 512;
 #define ZK_RED_CASE(cg)                                                                   \
   case cg:                                                                                \

@@ -762,6 +762,36 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
+  // dgrad epilogue operands (STE mask words, residual gradient) are loaded
+  // BEFORE the main loop: their HBM latency overlaps the prologue DMAs and
+  // the K-steps instead of following the last MFMA (the short-K 64 / 128-
+  // channel layers spent a third of each block waiting for them).
+  constexpr int PTM = FWD ? 1 : TM, PTN = FWD ? 1 : TN;
+  uint32_t pmw[PTM][PTN];
+  uint2 pdv[PTM][PTN][4];
+  if constexpr (!FWD) {
+    if (!args.psums) {
+      const uint32_t* mask = args.mask;
+      const uint16_t* dres = args.dres;
+      const int CW = g.Cin >> 5;
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const long long m = m0 + wm * WTM + a * 32 + r32;
+        const bool live = m < M;
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int nb = n0 + wn * WTN + b * 32;
+          pmw[a][b] = !mask ? 0xFFFFFFFFu : live ? mask[m * CW + (nb >> 5)] : 0u;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            pdv[a][b][q] = (dres && live)
+                               ? *reinterpret_cast<const uint2*>(dres + m * g.Cin + nb + 8 * q + 4 * h)
+                               : make_uint2(0u, 0u);
+        }
+      }
+    }
+  }
+
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < NK) issue(p);
@@ -884,29 +914,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
       }
     } else {
       uint16_t* dx = reinterpret_cast<uint16_t*>(args.out);
-      const uint32_t* mask = args.mask;
-      const uint16_t* dres = args.dres;
-      const int CW = g.Cin >> 5;
-      // every mask word / residual-gradient load of the tile first, then the
-      // stores: the loads overlap instead of each waiting behind the
-      // previous (possibly aliasing) store
-      uint32_t mw[TM][TN];
-      uint2 dv[TM][TN][4];
-#pragma unroll
-      for (int a = 0; a < TM; ++a) {
-        const long long m = m0 + wm * WTM + a * 32 + r32;
-        const bool live = m < M;
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          const int nb = n0 + wn * WTN + b * 32;
-          mw[a][b] = !mask ? 0xFFFFFFFFu : live ? mask[m * CW + (nb >> 5)] : 0u;
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            dv[a][b][q] = (dres && live)
-                              ? *reinterpret_cast<const uint2*>(dres + m * g.Cin + nb + 8 * q + 4 * h)
-                              : make_uint2(0u, 0u);
-        }
-      }
+      // mask words / residual gradient: prefetched before the main loop
+      const auto& mw = pmw;
+      const auto& dv = pdv;
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
         const long long m = m0 + wm * WTM + a * 32 + r32;
@@ -1219,6 +1229,13 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
     case 32: ZK_IGD3(256, 64, 4, 1, 4, 64)
     case 33: ZK_IGD3(128, 128, 2, 2, 4, 32)
     case 34: ZK_IGD3(256, 128, 4, 2, 3, 32)
+    // smaller LDS footprints: more resident blocks per CU (latency hiding on
+    // the short-K, memory-bound 64 / 128-channel layers)
+    case 35: ZK_IGD3(256, 64, 4, 1, 2, 32)   // 32 KB: 5 WG/CU
+    case 36: ZK_IGD3(128, 64, 2, 1, 2, 32)   // 24 KB
+    case 37: ZK_IGD3(128, 64, 2, 1, 2, 64)   // 48 KB
+    case 38: ZK_IGD3(128, 64, 2, 1, 3, 32)   // 36 KB
+    case 39: ZK_IGD3(256, 64, 4, 1, 3, 32)   // 48 KB
 #undef ZK_IGD3
     default: return (int)hipErrorInvalidValue;
   }

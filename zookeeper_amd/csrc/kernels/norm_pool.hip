@@ -32,7 +32,10 @@ __device__ __forceinline__ void store8_bf16(uint16_t* p, const float (&v)[8]) {
                  zk::pack_bf16x2(v[4], v[5]), zk::pack_bf16x2(v[6], v[7]));
 }
 
-template <int CG>
+// PARTS: per-block partial sums [block][2][C] with plain stores (summed in a
+// fixed order by bn_finalize_f64_kernel: run-to-run deterministic) instead of
+// fp64 atomics into one [2][C] row.
+template <int CG, bool PARTS = false>
 __global__ __launch_bounds__(256) void bn_stats_bf16_kernel(const uint16_t* __restrict__ x,
                                                             double* __restrict__ sums,
                                                             long long P) {
@@ -74,22 +77,36 @@ __global__ __launch_bounds__(256) void bn_stats_bf16_kernel(const uint16_t* __re
       a += red[0][rr * CG + c / 8][c % 8];
       b += red[1][rr * CG + c / 8][c % 8];
     }
-    atomicAdd(sums + c, a);
-    atomicAdd(sums + C + c, b);
+    if (PARTS) {
+      sums[(2LL * blockIdx.x) * C + c] = a;
+      sums[(2LL * blockIdx.x + 1) * C + c] = b;
+    } else {
+      atomicAdd(sums + c, a);
+      atomicAdd(sums + C + c, b);
+    }
   }
 }
 
+// sums: [nparts][2][C] (nparts = 1: the atomically accumulated row, re-zeroed
+// here for the next use; > 1: per-block partials summed in block order).
 __global__ void bn_finalize_f64_kernel(double* __restrict__ sums, int C, double P,
                                        const float* __restrict__ gamma,
                                        const float* __restrict__ beta, float eps, float momentum,
                                        float* __restrict__ rmean, float* __restrict__ rvar,
-                                       float* __restrict__ coef) {
+                                       float* __restrict__ coef, int nparts) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const double mean = sums[c] / P;
-  double var = sums[C + c] / P - mean * mean;
-  sums[c] = 0.0;  // re-zeroed for the next use (persistent per-layer buffer)
-  sums[C + c] = 0.0;
+  double s1 = 0.0, s2 = 0.0;
+  for (int j = 0; j < nparts; ++j) {
+    s1 += sums[(2LL * j) * C + c];
+    s2 += sums[(2LL * j + 1) * C + c];
+  }
+  const double mean = s1 / P;
+  double var = s2 / P - mean * mean;
+  if (nparts == 1) {
+    sums[c] = 0.0;  // re-zeroed for the next use (persistent per-layer buffer)
+    sums[C + c] = 0.0;
+  }
   if (var < 0) var = 0;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
   const float g = gamma ? gamma[c] : 1.f;
@@ -503,7 +520,55 @@ ZK_EXPORT int zk_bn_finalize_f64(const void* sums, int C, double P, const void* 
                                  void* rvar, void* coef, hipStream_t st) {
   hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
                      (double*)sums, C, P, (const float*)gamma, (const float*)beta, eps,
-                     momentum, (float*)rmean, (float*)rvar, (float*)coef);
+                     momentum, (float*)rmean, (float*)rvar, (float*)coef, 1);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// Deterministic forms (the Runtime's deterministic mode): per-block partials
+// [zk_bn_bwd_parts_max()][2][C] fp64 with plain stores, summed in block order
+// by zk_bn_finalize_f64_parts.
+ZK_EXPORT int zk_bn_stats_bf16_parts(const void* x, void* parts, long long P, int C,
+                                     int* nparts, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const int grid = red_grid(P, C);
+  if (nparts) *nparts = grid;
+#define CASE(cg)                                                                           \
+  case cg:                                                                                 \
+    hipLaunchKernelGGL((bn_stats_bf16_kernel<cg, true>), dim3(grid), dim3(256), 0, st,     \
+                       (const uint16_t*)x, (double*)parts, P);                             \
+    break;
+  ZK_CG_CASES(C, CASE)
+#undef CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_bn_finalize_f64_parts(const void* parts, int nparts, int C, double P,
+                                       const void* gamma, const void* beta, float eps,
+                                       float momentum, void* rmean, void* rvar, void* coef,
+                                       hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
+                     (double*)parts, C, P, (const float*)gamma, (const float*)beta, eps,
+                     momentum, (float*)rmean, (float*)rvar, (float*)coef, nparts < 1 ? 1 : nparts);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+ZK_EXPORT int zk_bn_bwd_reduce_relu_bf16_parts(const void* g, const void* x, const void* coef,
+                                               void* parts, long long P, int C, int* nparts,
+                                               hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const int grid = red_grid(P, C);
+  if (nparts) *nparts = grid;
+#define CASE(cg)                                                                         \
+  case cg:                                                                               \
+    hipLaunchKernelGGL((bn_bwd_reduce_bf16_kernel<cg, true, true>), dim3(grid), dim3(256), \
+                       0, st, (const uint16_t*)g, (const uint16_t*)x, nullptr,           \
+                       (const float*)coef, (float*)parts, P);                            \
+    break;
+  ZK_CG_CASES(C, CASE)
+#undef CASE
   ZK_CHECK_LAUNCH();
   return 0;
 }

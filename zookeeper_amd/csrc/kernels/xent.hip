@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const float* __restrict__
                                                        float* __restrict__ lse_out,
                                                        float* __restrict__ loss_sum,
                                                        int* __restrict__ correct, int B, int C,
-                                                       float eps) {
+                                                       float eps, float* __restrict__ row_loss) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
@@ -54,9 +54,29 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const float* __restrict__
     lse_out[row] = lse;
     const float nll = lse - xr[y];
     const float smooth = lse - sum / (float)C;
-    atomicAdd(loss_sum, (1.f - eps) * nll + eps * smooth);
+    const float lr = (1.f - eps) * nll + eps * smooth;
+    if (row_loss)
+      row_loss[row] = lr;  // deterministic mode: summed in row order by xent_sum_kernel
+    else
+      atomicAdd(loss_sum, lr);
     if (cand == (int)y) atomicAdd(correct, 1);
   }
+}
+
+// loss_sum = sum of row_loss in a fixed order (one block: per-thread strided
+// partial sums, then a fixed tree): bit-reproducible, unlike the atomics.
+__global__ __launch_bounds__(256) void xent_sum_kernel(const float* __restrict__ row_loss,
+                                                       float* __restrict__ loss_sum, int B) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < B; i += 256) s += row_loss[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss_sum[0] += red[0];
 }
 
 __global__ __launch_bounds__(256) void xent_bwd_kernel(const float* __restrict__ x,
@@ -83,10 +103,15 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(const float* __restrict__
 }  // namespace
 
 // loss_sum (fp32) and correct (int32) are accumulated (zeroed by the caller).
+// row_loss (optional, [B] fp32): per-row losses summed in a fixed order
+// instead of fp32 atomics (the deterministic mode).
 ZK_EXPORT int zk_xent_fwd(const float* x, const void* labels, float* lse, float* loss_sum,
-                          int* correct, int B, int C, float eps, hipStream_t st) {
+                          int* correct, int B, int C, float eps, float* row_loss,
+                          hipStream_t st) {
   hipLaunchKernelGGL(xent_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st, x,
-                     (const long long*)labels, lse, loss_sum, correct, B, C, eps);
+                     (const long long*)labels, lse, loss_sum, correct, B, C, eps, row_loss);
+  if (row_loss)
+    hipLaunchKernelGGL(xent_sum_kernel, dim3(1), dim3(256), 0, st, row_loss, loss_sum, B);
   ZK_CHECK_LAUNCH();
   return 0;
 }

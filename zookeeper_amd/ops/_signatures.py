@@ -36,6 +36,10 @@ SIGNATURES = {
     "zk_igemm_wgrad_f4_ws_bytes": (I64, [I32] * 14),
     "zk_igemm_dgrad_supported": (I32, [I32] * 13),
     "zk_set_option": (I32, [I32, I32]),
+    "zk_bn_bwd_reduce_blocks": (I32, []),
+    "zk_bn_stats_bf16_parts": (I32, [P, P, I64, I32, IP, P]),
+    "zk_bn_finalize_f64_parts": (I32, [P, I32, I32, C.c_double, P, P, F32, F32, P, P, P, P]),
+    "zk_bn_bwd_reduce_relu_bf16_parts": (I32, [P, P, P, P, I64, I32, IP, P]),
     "zk_get_option": (I32, [I32]),
     "zk_igemm_fwd_bf16": (I32, [P, P, P] + [I32] * 14 + [P]),
     "zk_igemm_fwd_bf16_supported": (I32, [I32] * 13),
@@ -70,7 +74,7 @@ SIGNATURES = {
     "zk_dw_dgrad": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_dw_wgrad": (I32, [P, P, P] + [I32] * 10 + [P]),
     # softmax cross-entropy
-    "zk_xent_fwd": (I32, [P, P, P, P, P, I32, I32, F32, P]),
+    "zk_xent_fwd": (I32, [P, P, P, P, P, I32, I32, F32, P, P]),
     "zk_xent_bwd": (I32, [P, P, P, P, P, I32, I32, F32, P]),
     # fused ImageNet stem
     "zk_stem_pack_input": (I32, [P, P] + [I32] * 8 + [P]),

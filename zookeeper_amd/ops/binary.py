@@ -63,6 +63,14 @@ STAT_STRIPES = 32
 #                 whole step 40.6k -> 40.1k img/s (batch 512).
 
 
+def bwd_stripes() -> int:
+    """Copies of the BN-backward sums: STAT_STRIPES striped atomic copies, or
+    one per reduce block in the deterministic mode."""
+    if OPTS.deterministic:
+        return int(lib().zk_bn_bwd_reduce_blocks())
+    return STAT_STRIPES
+
+
 def _fp4() -> bool:
     return OPTS.bconv_fp4
 
@@ -235,7 +243,7 @@ class _BinaryBlockFn(torch.autograd.Function):
         # BN-backward fusion hand-off (OPTS.fuse_bnsum): this block's reduction
         # may be done by its successor; the predecessor's by this block.
         ctx.bnsum = None
-        if OPTS.fuse_bnsum and will_backward and bn.training:
+        if OPTS.fuse_bnsum and not OPTS.deterministic and will_backward and bn.training:
             sums_buf = zeroed_scratch(bn, "bwd_sums", (STAT_STRIPES, 2, Cout), torch.float32, dev)
             ctx.bnsum = _BnSum(y, mean, rstd, sums_buf)
             side["bnsum"] = ctx.bnsum
@@ -263,14 +271,17 @@ class _BinaryBlockFn(torch.autograd.Function):
 
         g = _nhwc(dout.to(torch.bfloat16))
         weight_p, gamma_p, beta_p = ctx.params
-        sums = zeroed_scratch(ctx.bn, "bwd_sums", (STAT_STRIPES, 2, Cout), torch.float32, dev)
+        # deterministic mode: one copy of the sums per reduce block (plain
+        # stores, fixed-order sum in zk_bn_bwd_coef) instead of striped atomics
+        stripes = bwd_stripes()
+        sums = zeroed_scratch(ctx.bn, "bwd_sums", (stripes, 2, Cout), torch.float32, dev)
         bs = ctx.bnsum
         fused = bs is not None and bs.dx is not None
         if not (fused and bs.reduced(dout)):
             if fused:
                 sums.zero_()  # the successor reduced a gradient that was accumulated later
             check(L.zk_bn_bwd_reduce(g.data_ptr(), y.data_ptr(), mean.data_ptr(),
-                                     rstd.data_ptr(), sums.data_ptr(), P, Cout, STAT_STRIPES, st),
+                                     rstd.data_ptr(), sums.data_ptr(), P, Cout, stripes, st),
                   "zk_bn_bwd_reduce")
         # else: the successor's dgrad epilogue reduced exactly this gradient
         # BN coefficients + gamma/beta gradients in one launch; gradients go
@@ -284,7 +295,7 @@ class _BinaryBlockFn(torch.autograd.Function):
         coef = torch.empty((3, Cout), dtype=torch.float32, device=dev)
         check(L.zk_bn_bwd_coef(sums.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                                gamma.data_ptr() if gamma is not None else None, float(P), Cout,
-                               STAT_STRIPES, coef.data_ptr(),
+                               stripes, coef.data_ptr(),
                                dgamma.data_ptr() if dgamma is not None else None,
                                dbeta.data_ptr() if dbeta is not None else None, st),
               "zk_bn_bwd_coef")

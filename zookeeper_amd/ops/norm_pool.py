@@ -7,9 +7,12 @@ the layout every model in the zoo uses.
 
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from zookeeper_amd.nn.layers import same_padding
+from zookeeper_amd.ops.options import OPTS
 from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
                                         zeroed_scratch)
 
@@ -41,7 +44,19 @@ class _BatchNormFn(torch.autograd.Function):
         st = stream_ptr(dev)
         L = lib()
         coef = torch.empty((4, C), dtype=torch.float32, device=dev)
-        if bn.training:
+        if bn.training and OPTS.deterministic:
+            # per-block partials, summed in block order (no fp64 atomics)
+            parts = torch.empty((L.zk_bn_bwd_parts_max(), 2, C), dtype=torch.float64, device=dev)
+            n = ctypes.c_int(0)
+            check(L.zk_bn_stats_bf16_parts(xn.data_ptr(), parts.data_ptr(), P, C, ctypes.byref(n),
+                                           st), "zk_bn_stats_bf16_parts")
+            check(L.zk_bn_finalize_f64_parts(parts.data_ptr(), n.value, C, float(P),
+                                             gamma.data_ptr() if gamma is not None else None,
+                                             beta.data_ptr() if beta is not None else None,
+                                             bn.eps, bn.momentum, bn.running_mean.data_ptr(),
+                                             bn.running_var.data_ptr(), coef.data_ptr(), st),
+                  "zk_bn_finalize_f64_parts")
+        elif bn.training:
             sums = zeroed_scratch(bn, "stats_f64", (2, C), torch.float64, dev)
             check(L.zk_bn_stats_bf16(xn.data_ptr(), sums.data_ptr(), P, C, st), "zk_bn_stats_bf16")
             check(L.zk_bn_finalize_f64(sums.data_ptr(), C, float(P),
@@ -86,16 +101,35 @@ class _BatchNormFn(torch.autograd.Function):
         st = stream_ptr(dev)
         L = lib()
         g = _nhwc(dy.to(torch.bfloat16))
-        sums = zeroed_scratch(ctx.bn, "bwd_sums", (2, C), torch.float32, dev)
-        if ctx.relu_rc:
-            check(L.zk_bn_bwd_reduce_relu_bf16(g.data_ptr(), xn.data_ptr(), coef.data_ptr(),
-                                               sums.data_ptr(), P, C, st),
-                  "zk_bn_bwd_reduce_relu_bf16")
+        stripes = 1
+        if OPTS.deterministic:
+            # per-block partials (plain stores), summed in block order by
+            # zk_bn_bwd_coef (stripes = parts): bit-reproducible
+            sums = torch.empty((L.zk_bn_bwd_parts_max(), 2, C), dtype=torch.float32, device=dev)
+            n = ctypes.c_int(0)
+            if ctx.relu_rc:
+                check(L.zk_bn_bwd_reduce_relu_bf16_parts(g.data_ptr(), xn.data_ptr(),
+                                                         coef.data_ptr(), sums.data_ptr(), P, C,
+                                                         ctypes.byref(n), st),
+                      "zk_bn_bwd_reduce_relu_bf16_parts")
+            else:
+                check(L.zk_bn_bwd_reduce_bf16_parts(g.data_ptr(), xn.data_ptr(),
+                                                    y.data_ptr() if y is not None else None,
+                                                    coef.data_ptr(), sums.data_ptr(), P, C,
+                                                    ctypes.byref(n), st),
+                      "zk_bn_bwd_reduce_bf16_parts")
+            stripes = n.value
         else:
-            check(L.zk_bn_bwd_reduce_bf16(g.data_ptr(), xn.data_ptr(),
-                                          y.data_ptr() if y is not None else None,
-                                          coef.data_ptr(), sums.data_ptr(), P, C, st),
-                  "zk_bn_bwd_reduce_bf16")
+            sums = zeroed_scratch(ctx.bn, "bwd_sums", (2, C), torch.float32, dev)
+            if ctx.relu_rc:
+                check(L.zk_bn_bwd_reduce_relu_bf16(g.data_ptr(), xn.data_ptr(), coef.data_ptr(),
+                                                   sums.data_ptr(), P, C, st),
+                      "zk_bn_bwd_reduce_relu_bf16")
+            else:
+                check(L.zk_bn_bwd_reduce_bf16(g.data_ptr(), xn.data_ptr(),
+                                              y.data_ptr() if y is not None else None,
+                                              coef.data_ptr(), sums.data_ptr(), P, C, st),
+                      "zk_bn_bwd_reduce_bf16")
         gamma_p, beta_p = ctx.params
         dg_direct = direct_grad(gamma_p) if ctx.has_gamma else None
         db_direct = direct_grad(beta_p) if ctx.has_beta else None
@@ -105,7 +139,8 @@ class _BatchNormFn(torch.autograd.Function):
             torch.zeros(C, device=dev) if ctx.has_beta else None)
         bcoef = torch.empty((3, C), dtype=torch.float32, device=dev)
         check(L.zk_bn_bwd_coef(sums.data_ptr(), coef[2].data_ptr(), coef[3].data_ptr(),
-                               gamma.data_ptr() if gamma is not None else None, float(P), C, 1,
+                               gamma.data_ptr() if gamma is not None else None, float(P), C,
+                               stripes,
                                bcoef.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
                                dbeta.data_ptr() if dbeta is not None else None, st),
               "zk_bn_bwd_coef")

@@ -5,6 +5,7 @@ from __future__ import annotations
 import torch
 
 from zookeeper_amd.ops._native import check, lib, stream_ptr
+from zookeeper_amd.ops.options import OPTS
 
 
 class _SoftmaxXentFn(torch.autograd.Function):
@@ -17,8 +18,12 @@ class _SoftmaxXentFn(torch.autograd.Function):
         lse = torch.empty(B, dtype=torch.float32, device=dev)
         acc = torch.zeros(2, dtype=torch.float32, device=dev)  # [loss_sum, correct (int bits)]
         correct = acc[1:].view(torch.int32)
+        # deterministic mode: per-row losses summed in a fixed order
+        row_loss = torch.empty(B, dtype=torch.float32, device=dev) if OPTS.deterministic else None
         check(lib().zk_xent_fwd(x.data_ptr(), y.data_ptr(), lse.data_ptr(), acc.data_ptr(),
-                                correct.data_ptr(), B, C, float(eps), stream_ptr(dev)),
+                                correct.data_ptr(), B, C, float(eps),
+                                row_loss.data_ptr() if row_loss is not None else None,
+                                stream_ptr(dev)),
               "zk_xent_fwd")
         ctx.save_for_backward(x, y, lse)
         ctx.eps, ctx.in_dtype = float(eps), logits.dtype
