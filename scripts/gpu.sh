@@ -52,10 +52,10 @@ for spec in "$@"; do
   case "$kind" in
     tests)
       if [ -n "${a1:-}" ]; then
-        gpu_step 600 "$OUT/pytest_$n.log" python -u -m pytest tests -m gpu -x -q \
+        ZK_CURVE_DIR="$OUT/curves" gpu_step 600 "$OUT/pytest_$n.log" python -u -m pytest tests -m gpu -x -q \
           --timeout 120 --timeout-method thread -k "$a1" || exit $?
       else
-        gpu_step 900 "$OUT/pytest_$n.log" python -u -m pytest tests -m gpu -x -q \
+        ZK_CURVE_DIR="$OUT/curves" gpu_step 900 "$OUT/pytest_$n.log" python -u -m pytest tests -m gpu -x -q \
           --timeout 120 --timeout-method thread || exit $?
       fi
       ;;

@@ -8,7 +8,8 @@ the same Adam settings (the reference trains BinaryNet with Keras Adam,
 examples/larq_experiment.py:118-122).  After ~150 steps the native run's
 held-out accuracy must be well above chance and within a stated tolerance of
 the fp32 run's; the loss curves are written to $ZK_CURVE_DIR when set
-(profiles/r2_convergence_*.json hold the recorded ones).
+(profiles/r3/convergence_*.json hold the recorded ones; the GPU suite is run
+with ZK_CURVE_DIR=gpurun_out/curves by scripts/gpu.sh).
 """
 
 import copy
@@ -93,13 +94,20 @@ def _models(name):
         ref = BinaryResNetE((64, 64, 3), 10, 18, backend="torch")
         ref.load_state_dict(hip.state_dict())
         return hip, ref, 64
+    if name == "QuickNet":
+        from zookeeper_amd.models.quicknet import QuickNetModule
+
+        hip = QuickNetModule((64, 64, 3), 10, (2, 2, 2, 2), (32, 64, 128, 256), backend="hip")
+        ref = QuickNetModule((64, 64, 3), 10, (2, 2, 2, 2), (32, 64, 128, 256), backend="torch")
+        ref.load_state_dict(hip.state_dict())
+        return hip, ref, 64
     hip = BinaryNetModule((32, 32, 3), 10, filters=64, dense_units=256)
     ref = copy.deepcopy(hip)
     return hip, ref, 32
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("name", ["BinaryResNetE18", "BinaryNet"])
+@pytest.mark.parametrize("name", ["BinaryResNetE18", "BinaryNet", "QuickNet"])
 def test_native_training_matches_fp32(name):
     hip, ref, hw = _models(name)
     tpl = _templates(10, hw)

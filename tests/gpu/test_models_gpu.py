@@ -308,3 +308,48 @@ def test_binary_models_step_loss_matches_fp32_oracle(name):
     assert abs(loss - loss_r) < 0.15 * abs(loss_r) + 0.1, (loss, loss_r)
     for n, p in m.named_parameters():
         assert torch.isfinite(p.grad).all() and p.grad.abs().sum() > 0, n
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("name", ["QuickNetLarge", "BinaryResNetE18"])
+def test_binary_models_grad_direction_vs_fp32_oracle(name):
+    """Model-level gradient direction of the binary networks: per-parameter
+    cosine similarity of the native bf16 step's gradients with the fp32
+    oracle's (torch backend, fp32, same weights and inputs), judged against
+    what bf16 itself costs -- the same model on the library bf16 path
+    (torch backend, bf16 input) vs the same oracle.  A binary network
+    amplifies rounding into sign flips, so the bound is relative: the native
+    path must be at least as close to fp32 as library bf16 is (mean cosine
+    within 0.03, worst parameter within 0.1), and the mean must be clearly
+    aligned (> 0.7).  The inputs are bf16-exact and at least 1e-2 from zero,
+    so the first layer sees the same signs on every path."""
+    from zookeeper_amd.models.binary_resnet import BinaryResNetE
+    from zookeeper_amd.models.quicknet import QuickNetModule
+
+    torch.manual_seed(3)
+
+    def make(backend):
+        if name == "QuickNetLarge":
+            return QuickNetModule((64, 64, 3), 10, (2, 2, 2, 2), (64, 128, 256, 512),
+                                  backend=backend)
+        return BinaryResNetE((64, 64, 3), 10, 18, backend=backend)
+
+    m = make("hip")
+    ref, lib16 = make("torch"), make("torch")
+    ref.load_state_dict(m.state_dict())
+    lib16.load_state_dict(m.state_dict())
+    m, ref, lib16 = _prep(m), _prep(ref), _prep(lib16)
+    x = _cl(torch.randn(32, 3, 64, 64, device="cuda").to(torch.bfloat16))
+    y = torch.randint(0, 10, (32,), device="cuda")
+    _step(m, x, y)
+    _step(ref, x.float(), y)
+    out16 = lib16(x)
+    F.cross_entropy(out16.float(), y).backward()
+    cn, cl = _cosines(m, ref), _cosines(lib16, ref)
+    mean_n, mean_l = sum(cn.values()) / len(cn), sum(cl.values()) / len(cl)
+    worst = sorted(cn.items(), key=lambda t: t[1])[:4]
+    print(f"{name}: mean cos native {mean_n:.4f} library-bf16 {mean_l:.4f}; "
+          f"worst native {worst}; worst library {min(cl.values()):.4f}")
+    assert mean_n > 0.7, (mean_n, worst)
+    assert mean_n >= mean_l - 0.03, (mean_n, mean_l)
+    assert min(cn.values()) >= min(cl.values()) - 0.1, (worst, min(cl.values()))

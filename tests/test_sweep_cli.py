@@ -188,3 +188,42 @@ def test_sweep_records_throughput_and_loss(tmp_path):
         assert s["exit_code"] == 0 and s["steps"] == 2
         assert s["images_per_sec"] > 0
         assert s["final_loss"] == s["final_loss"] and s["final_loss"] > 0  # finite
+
+
+@pytest.mark.timeout(600)
+def test_config5_grid_dp2_runs_on_disjoint_device_pairs(tmp_path):
+    """BASELINE config 5, rehearsed on the CPU: an lr x wd grid of four
+    TrainingExperiment runs across 8 (faked) GPUs, each run data-parallel on
+    its own pair (--gpus-per-run 2 -> every run relaunched as 2 ranks over
+    gloo).  All four runs start before any finishes, each writes
+    result.json, and sweep.json carries per-run images/sec and final loss."""
+    sweep_dir = tmp_path / "sweep"
+    cmd = [sys.executable, os.path.join(ROOT, "examples", "train_imagenet.py"), "TrainImageNet",
+           "--grid", "learning_rate=[1e-3,2e-3]", "--grid", "optimizer.weight_decay=[0.0,5e-5]",
+           "--gpus-per-run", "2",
+           "model=BinaryNet", "model.filters=16", "model.dense_units=64",
+           "input_shape=(32,32,3)", "dataset.image_shape=(32,32,3)", "dataset.num_classes=10",
+           "dataset.num_train_examples=64", "dataset.num_validation_examples=0",
+           "batch_size=4", "steps_per_epoch=3", "epochs=1", "log_every=1", "print_summary=False"]
+    env = _env(ZK_SWEEP_DIR=str(sweep_dir), HIP_VISIBLE_DEVICES="0,1,2,3,4,5,6,7",
+               ZK_DIST_TIMEOUT_S="240")
+    res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=560)
+    assert res.returncode == 0, res.stdout[-4000:] + res.stderr[-4000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("[sweep]")]
+    starts = [ln for ln in lines if ln.startswith("[sweep] start")]
+    assert len(starts) == 4
+    assert all(ln.startswith("[sweep] start") for ln in lines[:4]), lines  # concurrent
+    pairs = sorted(ln.split("devices ")[1] for ln in starts)
+    assert pairs == ["['0', '1']", "['2', '3']", "['4', '5']", "['6', '7']"], pairs
+    summary = json.load(open(sweep_dir / "sweep.json"))
+    assert len(summary) == 4
+    for rec in summary:
+        assert rec["exit_code"] == 0, rec
+        assert len(rec["devices"]) == 2
+        assert rec["images_per_sec"] > 0 and rec["final_loss"] == rec["final_loss"]
+        assert os.path.exists(sweep_dir / rec["name"] / "result.json")
+        log = open(sweep_dir / rec["name"] / "stdout.log").read()
+        assert "world" in log or rec["steps"] == 3
+    grid = sorted((r["overrides"]["learning_rate"], r["overrides"]["optimizer.weight_decay"])
+                  for r in summary)
+    assert grid == [("0.001", "0.0"), ("0.001", "5e-05"), ("0.002", "0.0"), ("0.002", "5e-05")]

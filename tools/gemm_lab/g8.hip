@@ -198,6 +198,44 @@ __global__ __launch_bounds__(NTH, 1) void g8_kernel(const uint16_t* __restrict__
       __builtin_amdgcn_sched_barrier(0);
     }
 
+  } else if constexpr (V == 3) {
+    // V3: ping-pong.  Waves 0-3 (rows 0-127) and 4-7 (rows 128-255) form two
+    // groups, one wave of each per SIMD; group 1 runs one s_barrier behind
+    // group 0, so while one group's wave issues its 16 MFMAs the other
+    // group's wave on the same SIMD reads its fragments and issues its DMA
+    // (cdna_hip_programming.md, the 256^2 template's staggered groups).
+    // Phase (t, p): k-half kh = p>>1, row half mh = p&1; reads its own
+    // fragments, issues piece p of K-tile t+1, s_barrier, lgkmcnt(0), MFMAs,
+    // s_barrier.  A piece is retired by a counted vmcnt at the START of the
+    // phase BEFORE the one that reads it (one barrier more than unstaggered).
+    const int grp = __builtin_amdgcn_readfirstlane(wave >> 2);  // scalar branch around s_barrier
+    uint4 af[4], bfv[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) issue(0, p);
+    wait_vmcnt<4>();
+    barrier();
+    if (grp == 1) barrier();  // stagger
+    for (int t = 0; t < NT; ++t) {
+      const bool more = t + 1 < NT;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int kh = p >> 1, mh = p & 1;
+        if (p == 1) {
+          if (more) wait_vmcnt<2>(); else wait_vmcnt<0>();
+        }
+        if (p == 3 && more) wait_vmcnt<2>();
+        readA(af, t, kh, mh);
+        if (mh == 0) readB(bfv, t, kh);
+        if (more) issue(t + 1, p);
+        barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(af, bfv, mh);
+        __builtin_amdgcn_sched_barrier(0);
+        barrier();
+      }
+    }
+    if (grp == 0) barrier();  // same barrier count in both groups
   } else {
     // V2: a ring of 4 half-tile slot pairs (A, B pieces of 32 k each): half-
     // tile h computes in phases 2h (rows 0-63) and 2h+1 (rows 64-127); A_j is
@@ -335,10 +373,13 @@ int main(int argc, char** argv) {
                             LDS_BYTES));
   const int m_tiles = M / BM, tiles = m_tiles * (N / BN);
   int rc_all = 0;
-  for (int v = 1; v <= 2; ++v) {
+  CHECK(hipFuncSetAttribute((const void*)g8_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            LDS_BYTES));
+  for (int v = 1; v <= 3; ++v) {
   auto run = [&]() {
     if (v == 1) g8_kernel<1><<<tiles, NTH, LDS_BYTES>>>(A, B, C, M, N, K, m_tiles);
-    else g8_kernel<2><<<tiles, NTH, LDS_BYTES>>>(A, B, C, M, N, K, m_tiles);
+    else if (v == 2) g8_kernel<2><<<tiles, NTH, LDS_BYTES>>>(A, B, C, M, N, K, m_tiles);
+    else g8_kernel<3><<<tiles, NTH, LDS_BYTES>>>(A, B, C, M, N, K, m_tiles);
   };
   CHECK(hipMemset(C, 0, (size_t)M * N * 4));
   run();

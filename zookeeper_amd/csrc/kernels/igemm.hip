@@ -1229,13 +1229,6 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
     case 32: ZK_IGD3(256, 64, 4, 1, 4, 64)
     case 33: ZK_IGD3(128, 128, 2, 2, 4, 32)
     case 34: ZK_IGD3(256, 128, 4, 2, 3, 32)
-    // smaller LDS footprints: more resident blocks per CU (latency hiding on
-    // the short-K, memory-bound 64 / 128-channel layers)
-    case 35: ZK_IGD3(256, 64, 4, 1, 2, 32)   // 32 KB: 5 WG/CU
-    case 36: ZK_IGD3(128, 64, 2, 1, 2, 32)   // 24 KB
-    case 37: ZK_IGD3(128, 64, 2, 1, 2, 64)   // 48 KB
-    case 38: ZK_IGD3(128, 64, 2, 1, 3, 32)   // 36 KB
-    case 39: ZK_IGD3(256, 64, 4, 1, 3, 32)   // 48 KB
 #undef ZK_IGD3
     default: return (int)hipErrorInvalidValue;
   }
@@ -2008,9 +2001,22 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
 
 }  // namespace
 
+// dgrad8.hip: the persistent phase-pipelined stride-1 data gradient (variants 60-62)
+int zk_dgrad8_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
+                   int B, int H, int W, int Cin, int Ho, int Wo, int Cout, int kh, int kw,
+                   int stride, int pt, int pl, int variant, bool dry, hipStream_t st);
+
 namespace {
 int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
                      const IGeom& g, const BnSum& bs, int variant, hipStream_t stream) {
+  if (variant >= 60 && variant <= 65) {
+    if (bs.sums) return (int)hipErrorInvalidValue;  // fused BN sums: register-epilogue kernels
+    const int rc = zk_dgrad8_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Ho, g.Wo,
+                                  g.Cout, g.kh, g.kw, g.s, g.pt, g.pl, variant, g_dry_run, stream);
+    if (rc) return rc;
+    if (!g_dry_run) ZK_CHECK_LAUNCH();
+    return 0;
+  }
   if (variant < 0) {
     // Tuned on MI355X (tools/tune_bconv.py --only igemm, E18 shapes, batch
     // 256): 128x128 at 2 WG/CU for Cin >= 128 (8-wave 256x128 for the

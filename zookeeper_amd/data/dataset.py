@@ -349,6 +349,8 @@ class HFDataset(SplitDataset):
     download: bool = Field(False)
     image_key: str = Field("image")
     label_key: str = Field("label")
+    # threads decoding a batch's images (encoded bytes decoded on a pool)
+    decode_threads: int = Field(8)
 
     def _load_hf(self, split: Optional[str] = None):
         """The whole dataset (``split=None``) or one split.  ``download=False``
@@ -417,27 +419,102 @@ class HFDataset(SplitDataset):
         return len(self._load_hf(name))
 
     def load_base_split(self, name: str, decoders) -> Source:
-        return _HFSource(self._load_hf(name), self.image_key, self.label_key, decoders)
+        return _HFSource(self._load_hf(name), self.image_key, self.label_key, decoders,
+                         threads=self.decode_threads)
+
+
+# ---------------------------------------------------------------------------
+# Parallel image decode.  The reference decodes inside tf.data's C++ runtime
+# (map(preprocessing) on TF's thread pool, examples/larq_experiment.py:126-139);
+# here a batch's images are decoded by a pool of Python threads -- PIL's
+# decoders and resizers release the GIL, so the threads run concurrently --
+# straight into the batch array (no per-image list + np.stack copy).  The
+# loader's producer thread calls get_batch one batch ahead of the step
+# (data/loader.py), so decode overlaps the GPU work.
+# ---------------------------------------------------------------------------
+_POOLS: Dict[int, Any] = {}
+
+
+def decode_pool(threads: int):
+    """A process-wide thread pool of ``threads`` workers (created once)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    pool = _POOLS.get(threads)
+    if pool is None:
+        pool = ThreadPoolExecutor(max_workers=threads, thread_name_prefix="zk-decode")
+        _POOLS[threads] = pool
+    return pool
+
+
+def decode_into(out: np.ndarray, items: Sequence[Any], fn, threads: int) -> np.ndarray:
+    """``out[k] = fn(items[k])`` for every k, on ``threads`` threads (in
+    contiguous chunks, one per thread)."""
+    n = len(items)
+    if threads <= 1 or n <= 1:
+        for k in range(n):
+            out[k] = fn(items[k])
+        return out
+
+    def work(lo, hi):
+        for k in range(lo, hi):
+            out[k] = fn(items[k])
+
+    step = -(-n // threads)
+    futs = [decode_pool(threads).submit(work, lo, min(n, lo + step)) for lo in range(0, n, step)]
+    for f in futs:
+        f.result()  # re-raises a decode error
+    return out
 
 
 class _HFSource(Source):
-    def __init__(self, ds, image_key: str, label_key: str, decoders=None):
+    def __init__(self, ds, image_key: str, label_key: str, decoders=None, threads: int = 8):
         self.ds, self.image_key, self.label_key = ds, image_key, label_key
         self.decoders = decoders or {}
+        self.threads = threads
+        # read encoded images (bytes) and decode them on the pool instead of
+        # letting datasets decode every row in this thread
+        self._encoded = False
+        if threads > 1 and image_key not in self.decoders:
+            try:
+                import datasets as hf
+
+                feat = ds.features.get(image_key) if hasattr(ds, "features") else None
+                if isinstance(feat, hf.Image) and feat.decode:
+                    self.ds = ds.cast_column(image_key, hf.Image(decode=False))
+                    self._encoded = True
+            except Exception:  # older datasets / non-image column: decode row by row
+                pass
 
     def __len__(self) -> int:
         return len(self.ds)
 
     def get_batch(self, indices: np.ndarray) -> Batch:
         rows = self.ds[np.asarray(indices).tolist()]
-        decode = self.decoders.get(self.image_key, _to_uint8_hwc)
-        images = np.stack([decode(im) for im in rows[self.image_key]])
-        return {"image": images, "label": np.asarray(rows[self.label_key], dtype=np.int64)}
+        items = rows[self.image_key]
+        decode = (_decode_encoded if self._encoded
+                  else self.decoders.get(self.image_key, _to_uint8_hwc))
+        first = decode(items[0])
+        out = np.empty((len(items),) + first.shape, dtype=np.uint8)
+        out[0] = first
+        decode_into(out[1:], items[1:], decode, self.threads)
+        return {"image": out, "label": np.asarray(rows[self.label_key], dtype=np.int64)}
 
 
 def _to_uint8_hwc(im: Any) -> np.ndarray:
     a = np.asarray(im, dtype=np.uint8)
     return a[..., None] if a.ndim == 2 else a
+
+
+def _decode_encoded(item: Any) -> np.ndarray:
+    """A datasets ``Image(decode=False)`` cell ({"bytes", "path"}) -> uint8 HWC."""
+    import io
+
+    from PIL import Image
+
+    data = item.get("bytes") if isinstance(item, dict) else None
+    src = io.BytesIO(data) if data is not None else item["path"]
+    with Image.open(src) as im:
+        return _to_uint8_hwc(im.convert("RGB") if im.mode not in ("L", "RGB") else im)
 
 
 class ImageFolderDataset(SplitDataset):
@@ -448,6 +525,8 @@ class ImageFolderDataset(SplitDataset):
     image_size: Tuple[int, int] = Field((224, 224))
     train_split: str = Field("train")
     validation_split: Optional[str] = Field("val")
+    # threads decoding a batch (PIL releases the GIL while decoding/resizing)
+    decode_threads: int = Field(8)
 
     def _classes(self) -> List[str]:
         d = os.path.join(self.root, self.train_split.split("[")[0].split("+")[0])
@@ -465,25 +544,36 @@ class ImageFolderDataset(SplitDataset):
             for f in sorted(os.listdir(os.path.join(base, c))):
                 files.append(os.path.join(base, c, f))
                 labels.append(classes[c])
-        return _FileSource(files, np.asarray(labels, dtype=np.int64), tuple(self.image_size))
+        return _FileSource(files, np.asarray(labels, dtype=np.int64), tuple(self.image_size),
+                           threads=self.decode_threads)
 
 
 class _FileSource(Source):
-    def __init__(self, files: List[str], labels: np.ndarray, size: Tuple[int, int]):
-        self.files, self.labels, self.size = files, labels, size
+    def __init__(self, files: List[str], labels: np.ndarray, size: Tuple[int, int],
+                 threads: int = 8):
+        self.files, self.labels, self.size, self.threads = files, labels, size, threads
 
     def __len__(self) -> int:
         return len(self.files)
 
-    def get_batch(self, indices: np.ndarray) -> Batch:
+    def _decode(self, path: str) -> np.ndarray:
         from PIL import Image
 
-        out = []
-        for i in np.asarray(indices):
-            with Image.open(self.files[i]) as im:
-                im = im.convert("RGB").resize((self.size[1], self.size[0]))
-                out.append(np.asarray(im, dtype=np.uint8))
-        return {"image": np.stack(out), "label": self.labels[np.asarray(indices)]}
+        with Image.open(path) as im:
+            # JPEG: let libjpeg decode at the smallest DCT scale (1/2, 1/4,
+            # 1/8) still >= the target size -- most of a large photo's
+            # decode cost -- before the resize (measured on this host's CPU,
+            # 500x375 -> 224x224: ~2-3x with 8 threads, where full-size
+            # decodes did not scale with threads at all)
+            im.draft("RGB", (self.size[1], self.size[0]))
+            im = im.convert("RGB").resize((self.size[1], self.size[0]))
+            return np.asarray(im, dtype=np.uint8)
+
+    def get_batch(self, indices: np.ndarray) -> Batch:
+        idx = np.asarray(indices)
+        out = np.empty((len(idx), self.size[0], self.size[1], 3), dtype=np.uint8)
+        decode_into(out, [self.files[i] for i in idx], self._decode, self.threads)
+        return {"image": out, "label": self.labels[idx]}
 
     @property
     def image_shape(self):
