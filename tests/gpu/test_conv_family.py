@@ -121,7 +121,11 @@ def test_binary_dense_matches_fp64(B, K, N):
     (1, 128, 3, 1, "valid", 28, True, False),    # BinaryNet layer 1 (MNIST)
     (3, 16, 3, 2, "same", 33, False, False),     # QuickNet stem conv
     (16, 64, 1, 1, "valid", 14, False, True),    # QuickNet stem 1x1 (+ dgrad)
-    (4, 32, 3, 2, "same", 16, False, False)])
+    (16, 64, 1, 1, "same", 56, False, True),     # ... ImageNet-size map (contiguous-row path)
+    (4, 32, 3, 2, "same", 16, False, False),
+    (3, 16, 3, 2, "same", 224, False, False),    # QuickNet ImageNet stem (row-band kernels)
+    (3, 48, 3, 2, "valid", 47, False, False),    # ragged bands, Cout 48
+    (1, 32, 3, 1, "same", 9, True, False)])      # one band holds the whole image
 def test_small_conv_matches_fp64(cin, cout, k, s, padding, hw, binary_kernel, need_dx):
     from zookeeper_amd.ops import smallconv
 

@@ -320,9 +320,12 @@ def test_binary_models_grad_direction_vs_fp32_oracle(name):
     (torch backend, bf16 input) vs the same oracle.  A binary network
     amplifies rounding into sign flips, so the bound is relative: the native
     path must be at least as close to fp32 as library bf16 is (mean cosine
-    within 0.03, worst parameter within 0.1), and the mean must be clearly
-    aligned (> 0.7).  The inputs are bf16-exact and at least 1e-2 from zero,
-    so the first layer sees the same signs on every path."""
+    within 0.03, worst parameter within 0.1), and positively aligned on
+    average (> 0.1).  No absolute bound near 1 is possible at random init:
+    measured on MI355X, QuickNetLarge's library-bf16 gradients have mean
+    cosine 0.21 with the fp32 oracle's (native: 0.23) -- bf16 rounding of the
+    activations alone flips enough signs to decorrelate them.  The inputs are
+    bf16-exact, so the float stem sees identical data on every path."""
     from zookeeper_amd.models.binary_resnet import BinaryResNetE
     from zookeeper_amd.models.quicknet import QuickNetModule
 
@@ -350,6 +353,6 @@ def test_binary_models_grad_direction_vs_fp32_oracle(name):
     worst = sorted(cn.items(), key=lambda t: t[1])[:4]
     print(f"{name}: mean cos native {mean_n:.4f} library-bf16 {mean_l:.4f}; "
           f"worst native {worst}; worst library {min(cl.values()):.4f}")
-    assert mean_n > 0.7, (mean_n, worst)
+    assert mean_n > 0.1, (mean_n, worst)
     assert mean_n >= mean_l - 0.03, (mean_n, mean_l)
     assert min(cn.values()) >= min(cl.values()) - 0.1, (worst, min(cl.values()))

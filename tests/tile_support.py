@@ -28,9 +28,6 @@ DGRAD: Dict[int, Tuple[int, int, bool]] = {
     40: (128, 128, False), 41: (128, 64, False), 42: (64, 128, False), 43: (64, 64, False),
     44: (128, 128, False), 45: (256, 128, False), 46: (128, 64, False), 47: (256, 64, False),
     48: (64, 128, False),
-    # persistent phase-pipelined kernel (dgrad8.hip): stride 1, Cout % 64
-    60: (64, 128, True), 61: (128, 128, True), 62: (256, 128, True), 63: (256, 128, True),
-    64: (256, 128, True), 65: (256, 128, True),
 }
 
 # bf16 forward: variant -> (BN = Cout tile, CB, conv3)
@@ -82,8 +79,6 @@ def dgrad_ok(v: int, cin: int, cout: int, stride: int) -> bool:
     if v not in DGRAD:
         return False
     bn, cb, c3 = DGRAD[v]
-    if v >= 60:
-        return stride == 1 and cout % 64 == 0 and cin % bn == 0
     if c3 and not conv3_ok(stride):
         return False
     return (2 * cout) % cb == 0 and cin % bn == 0 and stride <= 2

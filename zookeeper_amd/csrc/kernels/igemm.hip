@@ -1999,24 +1999,8 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
 #undef ZK_IGW3
 }
 
-}  // namespace
-
-// dgrad8.hip: the persistent phase-pipelined stride-1 data gradient (variants 60-62)
-int zk_dgrad8_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
-                   int B, int H, int W, int Cin, int Ho, int Wo, int Cout, int kh, int kw,
-                   int stride, int pt, int pl, int variant, bool dry, hipStream_t st);
-
-namespace {
 int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
                      const IGeom& g, const BnSum& bs, int variant, hipStream_t stream) {
-  if (variant >= 60 && variant <= 65) {
-    if (bs.sums) return (int)hipErrorInvalidValue;  // fused BN sums: register-epilogue kernels
-    const int rc = zk_dgrad8_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Ho, g.Wo,
-                                  g.Cout, g.kh, g.kw, g.s, g.pt, g.pl, variant, g_dry_run, stream);
-    if (rc) return rc;
-    if (!g_dry_run) ZK_CHECK_LAUNCH();
-    return 0;
-  }
   if (variant < 0) {
     // Tuned on MI355X (tools/tune_bconv.py --only igemm, E18 shapes, batch
     // 256): 128x128 at 2 WG/CU for Cin >= 128 (8-wave 256x128 for the

@@ -28,7 +28,7 @@ import torch.nn.functional as F
 from zookeeper_amd.core import Field, factory
 from zookeeper_amd.models.base import ModelFactory
 from zookeeper_amd.nn.layers import (BatchNorm, GlobalAvgPool, QuantConv2d, _use_native,
-                                     glorot_normal_, pad_same_nhwc)
+                                     glorot_normal_, pad_same_nhwc, pooled_dense)
 from zookeeper_amd.nn.quantizers import ste_sign
 
 
@@ -131,8 +131,7 @@ class QuickNetModule(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = self.body(self.stem(x))
-        x = self.pool(F.relu(x)).float()
-        return F.linear(x, self.fc.weight, self.fc.bias)
+        return pooled_dense(x, self.pool, self.fc, relu=True)
 
 
 class _QuickNetBase(ModelFactory):

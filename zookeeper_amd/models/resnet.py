@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from zookeeper_amd.core import Field, factory
 from zookeeper_amd.models.base import ModelFactory
 from zookeeper_amd.nn.layers import (BatchNorm, GlobalAvgPool, ImageStem, MaxPool2d, QuantConv2d,
-                                     _use_native, glorot_normal_)
+                                     _use_native, glorot_normal_, pooled_dense)
 
 
 class Bottleneck(nn.Module):
@@ -104,8 +104,7 @@ class ResNetModule(nn.Module):
         self.input_shape, self.num_classes = tuple(input_shape), num_classes
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.pool(self.body(self.stem(x))).float()
-        return F.linear(x, self.fc.weight, self.fc.bias)
+        return pooled_dense(self.body(self.stem(x)), self.pool, self.fc, relu=False)
 
 
 @factory

@@ -409,8 +409,32 @@ class AvgPool2d(nn.Module):
 
 
 class GlobalAvgPool(nn.Module):
+    """Keras ``GlobalAveragePooling2D``; channels-last bf16 maps on the GPU run
+    the native pool kernel (``ops/head.py``), fp32 accumulation."""
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if _use_native(x):
+            from zookeeper_amd.ops.head import gap_supported, global_avg_pool
+
+            if gap_supported(x):
+                return global_avg_pool(x)
         return x.mean(dim=(2, 3))
+
+
+def pooled_dense(x: torch.Tensor, pool: nn.Module, fc: nn.Linear, relu: bool) -> torch.Tensor:
+    """fp32 logits of the ImageNet models' head: ``fc(pool(relu?(x)).float())``.
+
+    Native path (bf16 channels-last on the GPU): one fused ReLU + average-pool
+    kernel and fp32 MFMA GEMMs for the dense layer, forward and backward
+    (``ops/head.py``) -- no library kernel.  Else the PyTorch ops."""
+    if _use_native(x):
+        from zookeeper_amd.ops.head import classifier_head, head_supported
+
+        if head_supported(x, fc.weight):
+            return classifier_head(x, fc.weight, fc.bias, relu)
+    if relu:
+        x = F.relu(x)
+    return F.linear(pool(x).float(), fc.weight, fc.bias)
 
 
 class Flatten(nn.Module):

@@ -50,6 +50,10 @@ SIGNATURES = {
     # small-K convolutions (smallconv.hip)
     "zk_smallk_conv_fwd": (I32, [P, P, P] + [I32] * 12 + [P]),
     "zk_smallk_conv_wgrad": (I32, [P, P, P, P] + [I32] * 12 + [F32, I32, P]),
+    "zk_band_conv_ok": (I32, [I32] * 10),
+    "zk_band_conv_fwd": (I32, [P, P, P] + [I32] * 12 + [P]),
+    "zk_band_conv_wgrad_parts": (I32, [I32] * 4),
+    "zk_band_conv_wgrad": (I32, [P] * 5 + [I32] * 12 + [F32, I32, P]),
     # batch norm
     "zk_bn_finalize": (I32, [P, I32, I32, C.c_double, P, P, F32, F32, P, P, P, P, P, P, P]),
     "zk_bn_apply": (I32, [P, P, P, P, P, I64, I32, P]),
@@ -76,6 +80,11 @@ SIGNATURES = {
     # softmax cross-entropy
     "zk_xent_fwd": (I32, [P, P, P, P, P, I32, I32, F32, P, P]),
     "zk_xent_bwd": (I32, [P, P, P, P, P, I32, I32, F32, P]),
+    # classifier head: (ReLU) + global average pool + fp32 dense layer
+    "zk_head_fwd": (I32, [P, P, P, P, P] + [I32] * 5 + [P]),
+    "zk_head_bwd": (I32, [P] * 8 + [I32] * 5 + [P]),
+    "zk_gap_fwd": (I32, [P, P] + [I32] * 5 + [P]),
+    "zk_gap_bwd": (I32, [P, P, P] + [I32] * 4 + [P]),
     # fused ImageNet stem
     "zk_stem_pack_input": (I32, [P, P] + [I32] * 8 + [P]),
     "zk_stem_pack_weight": (I32, [P, P] + [I32] * 4 + [P]),

@@ -10,10 +10,15 @@ or a thin feature map, where the 64-channel-chunked implicit GEMMs of
   small image sizes (``supported`` sends outputs above ``_MAX_PIXELS`` back to
   the library convolution, which is faster there).
 
+3x3 convs over 1 or 3 channels (the image) take the row-band kernels at any
+size: a block stages whole input rows in LDS and gathers im2col operands from
+there (``zk_band_conv_*``); other shapes the generic 128-pixel-tile kernels.
+
 forward   im2col of a 128-pixel tile built in LDS, ``v_mfma_f32_16x16x32_bf16``
           over the whole K (padded to 32 / 64), bf16 NHWC out;
 backward  weight gradient: split-K over pixels, fp32 atomics straight into the
-          flat gradient buffer; data gradient (only the 1×1 stride-1 case
+          flat gradient buffer (row-band path: per-block partials summed in a
+          fixed order); data gradient (only the 1×1 stride-1 case
           needs one) = the same forward kernel on dY with Wᵀ (K = Cout ≤ 64).
 """
 
@@ -58,7 +63,17 @@ def supported(x: torch.Tensor, weight: torch.Tensor, stride, padding: str, group
     # BinaryNet's CIFAR-shape first layer (~0.23 M output pixels) keeps them.
     B, _, H, W = x.shape
     _, _, Ho, Wo = _geometry(H, W, kh, kw, s[0], padding)
-    return B * Ho * Wo <= _MAX_PIXELS
+    # ... except the image-reading 3x3 convs, which the row-band kernels take
+    # at any size (QuickNet's 224x224 stem conv included), and 1x1 stride-1
+    # convs, whose im2col rows are contiguous channel vectors (16-B copies)
+    if kh == kw == 1 and s[0] == 1 and Cin % 8 == 0:
+        return True
+    return B * Ho * Wo <= _MAX_PIXELS or _band(B, H, W, Cin, Ho, Wo, Cout, kh, kw, s[0])
+
+
+def _band(B, H, W, Cin, Ho, Wo, Cout, kh, kw, s) -> bool:
+    """The row-band kernels take this geometry (3x3 over 1 or 3 channels)."""
+    return bool(lib().zk_band_conv_ok(B, H, W, Cin, Ho, Wo, Cout, kh, kw, s))
 
 
 _MAX_PIXELS = 1 << 20
@@ -85,9 +100,12 @@ class _SmallConvFn(torch.autograd.Function):
         wp = _pack(w2, KP)
         xn = x.permute(0, 2, 3, 1).contiguous()
         y = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x.device)
-        check(lib().zk_smallk_conv_fwd(xn.data_ptr(), wp.data_ptr(), y.data_ptr(), B, H, W, Cin,
-                                       Ho, Wo, Cout, kh, kw, stride, pt, pl,
-                                       stream_ptr(x.device)), "zk_smallk_conv_fwd")
+        band = _band(B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride)
+        fwd = lib().zk_band_conv_fwd if band else lib().zk_smallk_conv_fwd
+        check(fwd(xn.data_ptr(), wp.data_ptr(), y.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
+                  stride, pt, pl, stream_ptr(x.device)),
+              "zk_band_conv_fwd" if band else "zk_smallk_conv_fwd")
+        ctx.band = band
         ctx.save_for_backward(xn)
         ctx.weight, ctx.kclip = weight, kclip
         ctx.geom = (B, Cin, H, W, Cout, kh, kw, stride, pt, pl, Ho, Wo)
@@ -120,10 +138,19 @@ class _SmallConvFn(torch.autograd.Function):
             wf = weight.detach().permute(0, 2, 3, 1)
             if wf.dtype != torch.float32 or not wf.is_contiguous():
                 wf = wf.float().contiguous()
-            check(L.zk_smallk_conv_wgrad(g.data_ptr(), xn.data_ptr(), wf.data_ptr(), dw.data_ptr(),
-                                         B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl,
-                                         _INF if kclip is None else float(kclip), 0, st),
-                  "zk_smallk_conv_wgrad")
+            clip = _INF if kclip is None else float(kclip)
+            if ctx.band:
+                # per-block partials + fixed-order reduction (deterministic)
+                n = L.zk_band_conv_wgrad_parts(B, Ho, Wo, 0)
+                part = torch.empty((n, Cout, 32), dtype=torch.float32, device=dev)
+                check(L.zk_band_conv_wgrad(g.data_ptr(), xn.data_ptr(), wf.data_ptr(),
+                                           dw.data_ptr(), part.data_ptr(), B, H, W, Cin, Ho, Wo,
+                                           Cout, kh, kw, s, pt, pl, clip, 0, st),
+                      "zk_band_conv_wgrad")
+            else:
+                check(L.zk_smallk_conv_wgrad(g.data_ptr(), xn.data_ptr(), wf.data_ptr(),
+                                             dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, s,
+                                             pt, pl, clip, 0, st), "zk_smallk_conv_wgrad")
             if target is not None:
                 grad_ready(weight)
             else:
