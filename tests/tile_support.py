@@ -24,6 +24,8 @@ DGRAD: Dict[int, Tuple[int, int, bool]] = {
     24: (128, 64, True), 25: (256, 64, True), 26: (128, 64, True), 27: (64, 64, True),
     28: (64, 32, True), 29: (64, 32, True), 30: (64, 32, True), 31: (64, 64, True),
     32: (64, 64, True), 33: (128, 32, True), 34: (128, 32, True),
+    35: (64, 64, True), 36: (64, 64, True), 37: (128, 64, True), 38: (64, 32, True),
+    39: (64, 64, True),
     # LDS-staged (coalesced) epilogue variants
     40: (128, 128, False), 41: (128, 64, False), 42: (64, 128, False), 43: (64, 64, False),
     44: (128, 128, False), 45: (256, 128, False), 46: (128, 64, False), 47: (256, 64, False),

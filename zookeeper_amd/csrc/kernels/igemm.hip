@@ -1229,6 +1229,13 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
     case 32: ZK_IGD3(256, 64, 4, 1, 4, 64)
     case 33: ZK_IGD3(128, 128, 2, 2, 4, 32)
     case 34: ZK_IGD3(256, 128, 4, 2, 3, 32)
+    // 128-pixel wave tiles (TM = 4): 6 fragment reads per 8 MFMAs instead of
+    // 4 per 4 -- the 64x64 wave tile sits exactly at the LDS read rate
+    case 35: ZK_IGD3(512, 64, 4, 1, 3, 64)
+    case 36: ZK_IGD3(512, 64, 4, 1, 2, 64)
+    case 37: ZK_IGD3(512, 128, 4, 2, 2, 64)
+    case 38: ZK_IGD3(512, 64, 4, 1, 4, 32)
+    case 39: ZK_IGD3(384, 64, 4, 1, 3, 64)
 #undef ZK_IGD3
     default: return (int)hipErrorInvalidValue;
   }

@@ -151,35 +151,54 @@ __global__ __launch_bounds__(256) void smallk_wgrad_kernel(const uint16_t* __res
 #pragma unroll
   for (int i = 0; i < MAXT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (long long c0 = kbeg; c0 < kend; c0 += SK_BM) {
-    __syncthreads();  // the previous stage's fragment reads are done
-    for (int e = tid; e < SK_BM * cv; e += 256) {
+  // Software-pipelined staging: stage s+1's dY (and, 1x1, x) vectors are
+  // loaded into registers while stage s's MFMAs run; the transposed 2-B LDS
+  // stores happen after the barrier that retires stage s's fragment reads.
+  constexpr int DV = NC ? NC : 8;  // 16-B dY vectors per thread per stage (Cout/16)
+  constexpr int XV = KP / 8 * SK_BM / 256;  // 16-B x vectors per thread (1x1 path)
+  uint4 rd[DV], rx[XV > 0 ? XV : 1];
+  auto load_stage = [&](long long c0) {
+#pragma unroll
+    for (int u = 0; u < DV; ++u) {
+      const int e = tid + 256 * u;
       const int r = e / cv, j = e % cv;
       const long long p = c0 + r;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (p < kend) v = *reinterpret_cast<const uint4*>(dy + p * g.Cout + j * 8);
-      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        sD[(j * 8 + 2 * i) * PS + r] = (uint16_t)(vv[i] & 0xffff);
-        sD[(j * 8 + 2 * i + 1) * PS + r] = (uint16_t)(vv[i] >> 16);
-      }
+      rd[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (e < SK_BM * cv && p < kend) rd[u] = *reinterpret_cast<const uint4*>(dy + p * g.Cout + j * 8);
     }
     if (PW) {
-      // 1x1: a pixel's im2col row is its Cin channels (16-B loads, 2-B
-      // transposed LDS stores as for dY)
-      const int xv = KP / 8;
-      for (int e = tid; e < SK_BM * xv; e += 256) {
+      constexpr int xv = KP / 8;
+#pragma unroll
+      for (int u = 0; u < XV; ++u) {
+        const int e = tid + 256 * u;
         const int r = e / xv, j = e % xv;
         const long long p = c0 + r;
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (p < kend && j * 8 < g.Cin) v = *reinterpret_cast<const uint4*>(x + p * g.Cin + j * 8);
-        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+        rx[u] = make_uint4(0u, 0u, 0u, 0u);
+        if (p < kend && j * 8 < g.Cin) rx[u] = *reinterpret_cast<const uint4*>(x + p * g.Cin + j * 8);
+      }
+    }
+  };
+  auto scatter = [&](uint16_t* S, const uint4& v, int r, int j) {
+    const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          sC[(j * 8 + 2 * i) * PS + r] = (uint16_t)(vv[i] & 0xffff);
-          sC[(j * 8 + 2 * i + 1) * PS + r] = (uint16_t)(vv[i] >> 16);
-        }
+    for (int i = 0; i < 4; ++i) {
+      S[(j * 8 + 2 * i) * PS + r] = (uint16_t)(vv[i] & 0xffff);
+      S[(j * 8 + 2 * i + 1) * PS + r] = (uint16_t)(vv[i] >> 16);
+    }
+  };
+  load_stage(kbeg);
+  for (long long c0 = kbeg; c0 < kend; c0 += SK_BM) {
+    __syncthreads();  // the previous stage's fragment reads are done
+#pragma unroll
+    for (int u = 0; u < DV; ++u) {
+      const int e = tid + 256 * u;
+      if (e < SK_BM * cv) scatter(sD, rd[u], e / cv, e % cv);
+    }
+    if (PW) {
+#pragma unroll
+      for (int u = 0; u < XV; ++u) {
+        const int e = tid + 256 * u;
+        scatter(sC, rx[u], e / (KP / 8), e % (KP / 8));
       }
     } else {
       for (int e = tid; e < SK_BM * KP; e += 256) {
@@ -194,6 +213,7 @@ __global__ __launch_bounds__(256) void smallk_wgrad_kernel(const uint16_t* __res
         sC[k * PS + r] = v;
       }
     }
+    if (c0 + SK_BM < kend) load_stage(c0 + SK_BM);
     __syncthreads();
 #pragma unroll
     for (int ks = 0; ks < SK_BM / 32; ++ks) {
@@ -458,37 +478,45 @@ __global__ __launch_bounds__(256) void band_wgrad_kernel(const uint16_t* __restr
   for (int i = tid; i < g.Cout * 32; i += 256) out[i] = red[i];
 }
 
-// dw[co][k] (OHWI, fp32) += sum of the per-block partials, masked by |w| <= clip.
-// A block owns 64 outputs; its 4 waves sum the partials p = wave (mod 4) in
-// index order and combine in wave order (deterministic).
-__global__ __launch_bounds__(256) void band_wgrad_reduce(const float* __restrict__ part, int nparts,
-                                                         int Cout, int K,
-                                                         const float* __restrict__ w,
-                                                         float* __restrict__ dw, float clip) {
+// dw[co][k] (OHWI, fp32) += sum of the per-block partials, masked by |w| <= clip,
+// in two fixed-order passes wide enough to keep many loads in flight (one
+// pass of ~1000 dependent partial loads per thread ran ~70 us):
+//   pass 1: block (o-chunk of 64, slice of 32 parts) -> part2[slice][o]
+//   pass 2: thread o sums the slices in order and applies the mask.
+constexpr int BR_SLICE = 32;
+
+__global__ __launch_bounds__(256) void band_wgrad_reduce1(const float* __restrict__ part,
+                                                          int nparts, int n,
+                                                          float* __restrict__ part2) {
   __shared__ float red[4][64];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int o = blockIdx.x * 64 + lane;  // index into [Cout][32]
-  const int n = Cout * 32;
-  // 8 independent partial sums per thread keep 8 loads in flight (fixed order)
-  float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (o < n)
-    for (int p0 = wave; p0 < nparts; p0 += 32) {
+  const int o = blockIdx.x * 64 + lane, p0 = blockIdx.y * BR_SLICE;
+  float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int p = p0 + 4 * u;
-        if (p < nparts) s8[u] += part[(long long)p * n + o];
-      }
-    }
-  const float s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
-  red[wave][lane] = s;
+  for (int u = 0; u < 8; ++u) {
+    const int p = p0 + wave + 4 * u;
+    v[u] = (o < n && p < nparts) ? part[(long long)p * n + o] : 0.f;
+  }
+  red[wave][lane] = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
   __syncthreads();
-  if (wave == 0 && o < n) {
-    const float t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-    const int co = o >> 5, k = o & 31;
-    if (k < K) {
-      const int i = co * K + k;
-      if (fabsf(w[i]) <= clip) dw[i] += t;
-    }
+  if (wave == 0 && o < n)
+    part2[(long long)blockIdx.y * n + o] =
+        ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+__global__ __launch_bounds__(256) void band_wgrad_reduce2(const float* __restrict__ part2,
+                                                          int nslices, int Cout, int K,
+                                                          const float* __restrict__ w,
+                                                          float* __restrict__ dw, float clip) {
+  const int o = blockIdx.x * 256 + threadIdx.x;  // index into [Cout][32]
+  const int n = Cout * 32;
+  if (o >= n) return;
+  float t = 0.f;
+  for (int sl = 0; sl < nslices; ++sl) t += part2[(long long)sl * n + o];
+  const int co = o >> 5, k = o & 31;
+  if (k < K) {
+    const int i = co * K + k;
+    if (fabsf(w[i]) <= clip) dw[i] += t;
   }
 }
 
@@ -623,13 +651,14 @@ ZK_EXPORT int zk_band_conv_fwd(const void* x, const void* wp, void* y, int B, in
   return 0;
 }
 
-// Per-wave partial count the wgrad below needs scratch for (fp32 [n][Cout][32]).
+// Partial-row count the wgrad below needs scratch for (fp32 [n][Cout][32]).
 ZK_EXPORT int zk_band_conv_wgrad_parts(int B, int Ho, int Wo, int target_blocks) {
   const int R = max(1, min(Ho, 256 / max(1, Wo)));
   const int total = B * ((Ho + R - 1) / R);
   if (target_blocks <= 0) target_blocks = 1024;
   const int bpb = (total + target_blocks - 1) / target_blocks;
-  return (total + bpb - 1) / bpb;
+  const int blocks = (total + bpb - 1) / bpb;
+  return blocks + (blocks + 31) / 32;  // per-block partials + the reduction's slice sums
 }
 
 // dw fp32 OHWI += dY^T (*) x masked by |w| <= clip; part: scratch of
@@ -661,8 +690,13 @@ ZK_EXPORT int zk_band_conv_wgrad(const void* dy, const void* x, const void* w, v
 #undef ZK_BW_NC
 #undef ZK_BW
   ZK_CHECK_LAUNCH();
-  hipLaunchKernelGGL(band_wgrad_reduce, dim3((Cout * 32 + 63) / 64), dim3(256), 0, st,
-                     (const float*)part, blocks, Cout, g.K, (const float*)w, (float*)dw, clip);
+  const int n = Cout * 32, nslices = (blocks + BR_SLICE - 1) / BR_SLICE;
+  float* part2 = (float*)part + (long long)blocks * n;  // the tail of the scratch
+  hipLaunchKernelGGL(band_wgrad_reduce1, dim3((n + 63) / 64, nslices), dim3(256), 0, st,
+                     (const float*)part, blocks, n, part2);
+  ZK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(band_wgrad_reduce2, dim3((n + 255) / 256), dim3(256), 0, st,
+                     (const float*)part2, nslices, Cout, g.K, (const float*)w, (float*)dw, clip);
   ZK_CHECK_LAUNCH();
   return 0;
 }
