@@ -26,6 +26,8 @@ DGRAD: Dict[int, Tuple[int, int, bool]] = {
     32: (64, 64, True), 33: (128, 32, True), 34: (128, 32, True),
     35: (64, 64, True), 36: (64, 64, True), 37: (128, 64, True), 38: (64, 32, True),
     39: (64, 64, True),
+    # row-window kernel (conv3rw.hip): 64 -> 64 only, stride 1
+    50: (64, 64, True),
     # LDS-staged (coalesced) epilogue variants
     40: (128, 128, False), 41: (128, 64, False), 42: (64, 128, False), 43: (64, 64, False),
     44: (128, 128, False), 45: (256, 128, False), 46: (128, 64, False), 47: (256, 64, False),
@@ -81,6 +83,8 @@ def dgrad_ok(v: int, cin: int, cout: int, stride: int) -> bool:
     if v not in DGRAD:
         return False
     bn, cb, c3 = DGRAD[v]
+    if v == 50:
+        return stride == 1 and cin == 64 and cout == 64
     if c3 and not conv3_ok(stride):
         return False
     return (2 * cout) % cb == 0 and cin % bn == 0 and stride <= 2

@@ -2006,8 +2006,26 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
 #undef ZK_IGW3
 }
 
+}  // namespace
+
+// conv3rw.hip: row-window dgrad of the 64 -> 64 stride-1 3x3 conv (variant 50)
+int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres,
+                          void* dx, int B, int H, int W, int Cin, int Cout, bool dry,
+                          hipStream_t st);
+
+namespace {
 int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
                      const IGeom& g, const BnSum& bs, int variant, hipStream_t stream) {
+  if (variant == 50) {
+    if (bs.sums || g.s != 1 || g.kh != 3 || g.kw != 3 || g.pt != 1 || g.pl != 1 ||
+        g.Ho != g.H || g.Wo != g.W)
+      return (int)hipErrorInvalidValue;
+    const int rc = zk_conv3rw_dgrad_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Cout,
+                                         g_dry_run, stream);
+    if (rc) return rc;
+    if (!g_dry_run) ZK_CHECK_LAUNCH();
+    return 0;
+  }
   if (variant < 0) {
     // Tuned on MI355X (tools/tune_bconv.py --only igemm, E18 shapes, batch
     // 256): 128x128 at 2 WG/CU for Cin >= 128 (8-wave 256x128 for the
