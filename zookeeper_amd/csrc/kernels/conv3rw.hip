@@ -50,6 +50,9 @@ constexpr int RW_WBYTES = 9 * 64 * 128;          // resident weights
 constexpr int RW_ZERO = RW_WBYTES;               // 256 B of zeros
 constexpr int RW_RING_OFF = RW_WBYTES + 1024;    // ring base, 1 KB aligned
 
+// STE mask word of "every channel live" (the mask-less call)
+__device__ uint32_t g_rw_ones[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+
 struct RWArgs {
   const uint16_t* dy;    // [B][H][W][64]
   const uint16_t* wt;    // S^T [9][64 ci][64 co]
@@ -58,6 +61,13 @@ struct RWArgs {
   uint16_t* dx;          // [B][H][W][64]
   int B, H, W, ngroups, ipb, slot;
 };
+
+// vmcnt(0) through the builtin (expcnt / lgkmcnt left at their maxima), so
+// the compiler's own wait tracking knows every earlier load and store has
+// retired: after the asm-volatile form it still assumed the previous item's
+// epilogue loads outstanding and drained vmcnt again at the next item's
+// start -- right after issuing the row DMA, which it then waited for.
+__device__ __forceinline__ void rw_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 __device__ __forceinline__ f32x4 mfma16(const uint4& a, const uint4& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
@@ -122,9 +132,9 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
     for (int kc = 0; kc < 2; ++kc) aoff[j][kc] = ci * 128 + (((kc * 4 + kq) ^ rw_swz_w(ci)) * 16);
   }
 
-  // The previous item's packed dx chunks: stored one block per tap during
-  // the next item's MFMAs, so the dx write stream overlaps compute instead of
-  // bursting from every wave at once between two items.
+  // The previous item's packed dx chunks, stored one block per tap during
+  // the next item's MFMAs (measured equal to storing them at once, 427-433 us
+  // either way at batch 1024; kept: it spreads the write stream).
   uint4 pend[RW_MB];
   long long poff[RW_MB];
 #pragma unroll
@@ -142,7 +152,7 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
         const int hr = h0 - 1 + r;
         if (hr >= 0 && hr < a.H) rw_load_row(a, smem, b, hr, lane);
       }
-      wait_vmcnt<0>();  // these rows (and, first time, the weights) are in LDS
+      rw_drain();  // these rows (and, first time, the weights) are in LDS
       __builtin_amdgcn_s_barrier();
     }
     // the next group's 4 new rows, one per wave (same image only)
@@ -167,14 +177,20 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
     uint32_t mw[RW_MB];
     uint4 dr[RW_MB];
     long long pgo[RW_MB];
+    // Unconditional loads from a valid address (pixel 0 for lanes without a
+    // pixel, a constant page without mask / dres) and no use before the
+    // epilogue: a predicated load, or one whose value is shifted right away,
+    // made the compiler drain vmcnt here -- which also waited for the row DMA
+    // just issued.
+    const uint32_t* mbase = a.mask ? a.mask : g_rw_ones;
+    const uint16_t* dbase = a.dres ? a.dres : reinterpret_cast<const uint16_t*>(g_zero_page);
 #pragma unroll
     for (int i = 0; i < RW_MB; ++i) {
       const bool ok = pr[i] >= 0;
-      pgo[i] = ok ? ((long long)b * a.H + h0 + pr[i]) * a.W + pw[i] : -1;
-      mw[i] = (ok && a.mask) ? a.mask[pgo[i] * 2 + nh] >> (kq * 8) : 0xFFu;
-      dr[i] = (ok && a.dres)
-                  ? *reinterpret_cast<const uint4*>(a.dres + pgo[i] * 64 + nh * 32 + kq * 8)
-                  : make_uint4(0u, 0u, 0u, 0u);
+      const long long pc = ok ? ((long long)b * a.H + h0 + pr[i]) * a.W + pw[i] : 0;
+      pgo[i] = ok ? pc : -1;
+      mw[i] = mbase[a.mask ? pc * 2 + nh : 0];
+      dr[i] = *reinterpret_cast<const uint4*>(dbase + (a.dres ? pc * 64 + nh * 32 + kq * 8 : 0));
     }
     f32x4 acc[RW_MB][2];
 #pragma unroll
@@ -200,8 +216,7 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int kh = t / 3, kw = t % 3;
-      if (t < RW_MB && poff[t] >= 0)
-        *reinterpret_cast<uint4*>(a.dx + poff[t]) = pend[t];
+      if (t < RW_MB && poff[t] >= 0) *reinterpret_cast<uint4*>(a.dx + poff[t]) = pend[t];
       int boff[RW_MB], bsw[RW_MB];  // pixel row base and its chunk swizzle key (zero chunk: key 0)
 #pragma unroll
       for (int i = 0; i < RW_MB; ++i) {
@@ -238,7 +253,7 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
     // the next item's rows (and this item's epilogue operands) have landed:
     // wait now, while only the previous epilogue's stores -- long since
     // issued -- are ahead of them
-    wait_vmcnt<0>();
+    rw_drain();
     // epilogue: lane = pixel, rows 4*kq .. +3 of each 16-ci block
 #pragma unroll
     for (int i = 0; i < RW_MB; ++i) {
@@ -250,8 +265,9 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
       }
       // this lane's 8 consecutive channels nh*32 + kq*8 + (0..7): block j holds 4j..4j+3
       float v[8];
+      const uint32_t bits = mw[i] >> (kq * 8);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = ((mw[i] >> e) & 1u) ? acc[i][e >> 2][e & 3] : 0.f;
+      for (int e = 0; e < 8; ++e) v[e] = ((bits >> e) & 1u) ? acc[i][e >> 2][e & 3] : 0.f;
       const uint32_t d4[4] = {dr[i].x, dr[i].y, dr[i].z, dr[i].w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += zk::bf16_to_f32((uint16_t)(d4[e >> 1] >> (16 * (e & 1))));
@@ -263,10 +279,11 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
 #pragma unroll
   for (int i = 0; i < RW_MB; ++i)
     if (poff[i] >= 0) *reinterpret_cast<uint4*>(a.dx + poff[i]) = pend[i];
-  wait_vmcnt<0>();  // no DMA outstanding at exit
+  rw_drain();  // no DMA outstanding at exit
 }
 
 int g_num_cus = 0;
+int g_lds_attr = 0;
 
 }  // namespace
 
@@ -282,20 +299,24 @@ int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, cons
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   if (dry) return 0;
   if (g_num_cus == 0) {
-    int dev = 0;
+    int dev = 0, n = 0;
     (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (g_num_cus <= 0) g_num_cus = 256;
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    g_num_cus = n > 0 ? n : 256;
+  }
+  if (lds > g_lds_attr) {
+    // as much dynamic LDS as this geometry needs
     const hipError_t e = hipFuncSetAttribute((const void*)conv3rw_dgrad_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             160 * 1024);
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return (int)e;
+    g_lds_attr = lds;
   }
   RWArgs a{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
            (const uint16_t*)dres, (uint16_t*)dx, B, H, W, (H + RW_TR - 1) / RW_TR, 0, slot};
   const int nitems = B * a.ngroups;
   a.ipb = (nitems + g_num_cus - 1) / g_num_cus;
   const int grid = (nitems + a.ipb - 1) / a.ipb;
+  (void)hipGetLastError();  // a stale error of an unrelated earlier call is not ours
   hipLaunchKernelGGL(conv3rw_dgrad_kernel, dim3(grid), dim3(RW_NW * 64), lds, st, a);
   return (int)hipGetLastError();
 }

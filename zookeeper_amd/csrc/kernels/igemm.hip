@@ -87,9 +87,12 @@ struct ConvArgs {
 //   korder (key 1): K-step order, see ConvArgs::korder.
 //   deterministic (key 2): split-K weight gradients through slabs reduced in
 //     a fixed order (no float atomics).
+//   dgrad_rw (key 3): the row-window kernel (conv3rw.hip, variant 50) for the
+//     64 -> 64 stride-1 3x3 data gradient by default.
 int g_opt_tile_huge = 16;
 int g_opt_korder = 0;
 int g_opt_deterministic = 0;
+int g_opt_dgrad_rw = 1;
 
 bool huge_tiles_env(int bit = 31) { return (g_opt_tile_huge & bit) != 0; }
 
@@ -2016,16 +2019,6 @@ int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, cons
 namespace {
 int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
                      const IGeom& g, const BnSum& bs, int variant, hipStream_t stream) {
-  if (variant == 50) {
-    if (bs.sums || g.s != 1 || g.kh != 3 || g.kw != 3 || g.pt != 1 || g.pl != 1 ||
-        g.Ho != g.H || g.Wo != g.W)
-      return (int)hipErrorInvalidValue;
-    const int rc = zk_conv3rw_dgrad_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Cout,
-                                         g_dry_run, stream);
-    if (rc) return rc;
-    if (!g_dry_run) ZK_CHECK_LAUNCH();
-    return 0;
-  }
   if (variant < 0) {
     // Tuned on MI355X (tools/tune_bconv.py --only igemm, E18 shapes, batch
     // 256): 128x128 at 2 WG/CU for Cin >= 128 (8-wave 256x128 for the
@@ -2056,11 +2049,20 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     else if (c3 && Cin == 128)
       variant = g.B >= 1024 && huge_tiles_env(16) ? 27 : 23;  // batch 1024: 323 vs 338 us
     else if (c3 && Cin == 64)
-      variant = 27;
+      // row-window kernel for 64 -> 64 (stage 1 of E18 / QuickNet, batch
+      // 1024: 430 vs 513-574 us for variant 27; profiles/r3/f_conv3rw.md)
+      variant = (g_opt_dgrad_rw && g.Cout == 64 && g.W <= 64 && !bs.sums) ? 50 : 27;
     else if (Cin % 128 == 0)
       variant = 0;
     else
       variant = 7;
+  }
+  if (variant == 50) {  // conv3rw.hip (explicit, or the default above)
+    if (bs.sums || g.s != 1 || g.kh != 3 || g.kw != 3 || g.pt != 1 || g.pl != 1 ||
+        g.Ho != g.H || g.Wo != g.W)
+      return (int)hipErrorInvalidValue;
+    return zk_conv3rw_dgrad_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Cout,
+                                 g_dry_run, stream);
   }
   const int rc = igemm_dgrad_variant(variant, dy, wt, mask, dres, dx, g, bs, stream);
   if (rc) return rc;
@@ -2386,6 +2388,7 @@ ZK_EXPORT int zk_set_option(int key, int value) {
     case 0: g_opt_tile_huge = value; return 0;
     case 1: g_opt_korder = value; return 0;
     case 2: g_opt_deterministic = value; return 0;
+    case 3: g_opt_dgrad_rw = value; return 0;
     default: return -1;
   }
 }
@@ -2395,6 +2398,7 @@ ZK_EXPORT int zk_get_option(int key) {
     case 0: return g_opt_tile_huge;
     case 1: return g_opt_korder;
     case 2: return g_opt_deterministic;
+    case 3: return g_opt_dgrad_rw;
     default: return -1;
   }
 }

@@ -49,12 +49,15 @@ class KernelOptions:
     # Bit-reproducible gradients: split-K weight gradients reduced from slabs
     # in a fixed order, BN / bias sums without float atomics.
     deterministic: bool = False
+    # Row-window data gradient for the 64 -> 64 stride-1 3x3 binary conv
+    # (conv3rw.hip: resident weights, LDS ring of dY rows).
+    dgrad_rw: bool = True
 
 
 OPTS = KernelOptions()
 
 # keys the native library reads (zk_set_option); values are ints
-_NATIVE_KEYS = {"tile_huge": 0, "korder": 1, "deterministic": 2}
+_NATIVE_KEYS = {"tile_huge": 0, "korder": 1, "deterministic": 2, "dgrad_rw": 3}
 
 
 def _push_native() -> None:

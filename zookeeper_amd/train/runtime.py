@@ -43,6 +43,7 @@ class Runtime:
     pw_gemm: bool = Field(True)
     tile_huge: int = Field(16)
     korder: int = Field(0)
+    dgrad_rw: bool = Field(True)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
     deterministic: bool = Field(False)
