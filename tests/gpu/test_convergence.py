@@ -8,7 +8,7 @@ the same Adam settings (the reference trains BinaryNet with Keras Adam,
 examples/larq_experiment.py:118-122).  After ~150 steps the native run's
 held-out accuracy must be well above chance and within a stated tolerance of
 the fp32 run's; the loss curves are written to $ZK_CURVE_DIR when set
-(profiles/r3/convergence_*.json hold the recorded ones; the GPU suite is run
+(profiles/r3/convergence_{BinaryNet,BinaryResNetE18,QuickNet}.json hold the recorded ones, with the row-window dgrad and fused BN sums on; the GPU suite is run
 with ZK_CURVE_DIR=gpurun_out/curves by scripts/gpu.sh).
 """
 

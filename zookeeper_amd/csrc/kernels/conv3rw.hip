@@ -60,6 +60,14 @@ struct RWArgs {
   const uint16_t* dres;  // residual gradient [B][H][W][64] (optional)
   uint16_t* dx;          // [B][H][W][64]
   int B, H, W, ngroups, ipb, slot;
+  // optional: the predecessor block's BN-backward reduction over the stored
+  // dx (its output gradient): psums[stripe][0][c] += sum dx,
+  // [1][c] += sum dx * (ypred - mean[c]) * rstd[c]  (ypred int16 [B][H][W][64])
+  const int16_t* ypred;
+  const float* pmean;
+  const float* prstd;
+  float* psums;
+  int stripes;
 };
 
 // vmcnt(0) through the builtin (expcnt / lgkmcnt left at their maxima), so
@@ -132,6 +140,16 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
     for (int kc = 0; kc < 2; ++kc) aoff[j][kc] = ci * 128 + (((kc * 4 + kq) ^ rw_swz_w(ci)) * 16);
   }
 
+  // fused BN-backward sums of this lane's 8 channels, over all its pixels
+  const bool bnsum = a.psums != nullptr;
+  float s1[8], s2[8], mu[8], rs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s1[e] = s2[e] = 0.f;
+    mu[e] = bnsum ? a.pmean[nh * 32 + kq * 8 + e] : 0.f;
+    rs[e] = bnsum ? a.prstd[nh * 32 + kq * 8 + e] : 0.f;
+  }
+
   // The previous item's packed dx chunks, stored one block per tap during
   // the next item's MFMAs (measured equal to storing them at once, 427-433 us
   // either way at batch 1024; kept: it spreads the write stream).
@@ -175,7 +193,7 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
     // epilogue operands (STE mask byte, 16 B of residual gradient) requested
     // now and consumed after the MFMAs, which hide their latency
     uint32_t mw[RW_MB];
-    uint4 dr[RW_MB];
+    uint4 dr[RW_MB], yp[RW_MB];
     long long pgo[RW_MB];
     // Unconditional loads from a valid address (pixel 0 for lanes without a
     // pixel, a constant page without mask / dres) and no use before the
@@ -191,6 +209,9 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
       pgo[i] = ok ? pc : -1;
       mw[i] = mbase[a.mask ? pc * 2 + nh : 0];
       dr[i] = *reinterpret_cast<const uint4*>(dbase + (a.dres ? pc * 64 + nh * 32 + kq * 8 : 0));
+      yp[i] = *reinterpret_cast<const uint4*>(
+          bnsum ? reinterpret_cast<const uint16_t*>(a.ypred) + pc * 64 + nh * 32 + kq * 8
+                : reinterpret_cast<const uint16_t*>(g_zero_page));
     }
     f32x4 acc[RW_MB][2];
 #pragma unroll
@@ -273,12 +294,42 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
       for (int e = 0; e < 8; ++e) v[e] += zk::bf16_to_f32((uint16_t)(d4[e >> 1] >> (16 * (e & 1))));
       pend[i] = make_uint4(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
                            zk::pack_bf16x2(v[4], v[5]), zk::pack_bf16x2(v[6], v[7]));
+      if (bnsum) {
+        // sums of the values as stored (bf16), as the separate reduce would see them
+        const uint32_t pw4[4] = {pend[i].x, pend[i].y, pend[i].z, pend[i].w};
+        const uint32_t y4[4] = {yp[i].x, yp[i].y, yp[i].z, yp[i].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gv = zk::bf16_to_f32((uint16_t)(pw4[e >> 1] >> (16 * (e & 1))));
+          const float yv = (float)(int16_t)(uint16_t)(y4[e >> 1] >> (16 * (e & 1)));
+          s1[e] += gv;
+          s2[e] += gv * (yv - mu[e]) * rs[e];
+        }
+      }
       poff[i] = pgo[i] * 64 + nh * 32 + kq * 8;
     }
   }
 #pragma unroll
   for (int i = 0; i < RW_MB; ++i)
     if (poff[i] >= 0) *reinterpret_cast<uint4*>(a.dx + poff[i]) = pend[i];
+  if (bnsum) {
+    // the 16 lanes of a kq group hold the same 8 channels (other pixels)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        s1[e] += __shfl_xor(s1[e], off, 64);
+        s2[e] += __shfl_xor(s2[e], off, 64);
+      }
+    if (r16 == 0) {
+      float* ps = a.psums + (long long)(blockIdx.x % a.stripes) * 2 * 64;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        atomicAdd(ps + nh * 32 + kq * 8 + e, s1[e]);
+        atomicAdd(ps + 64 + nh * 32 + kq * 8 + e, s2[e]);
+      }
+    }
+  }
   rw_drain();  // no DMA outstanding at exit
 }
 
@@ -288,11 +339,15 @@ int g_lds_attr = 0;
 }  // namespace
 
 // Entry used by igemm.hip's dgrad dispatch (variant 50).  Stride-1 'same'
-// 3x3, Cin = Cout = 64, 1 <= W <= 64.  dry: validate only.
+// 3x3, Cin = Cout = 64, 1 <= W <= 64; psums (optional): the predecessor's
+// fused BN-backward sums (per-lane registers over the whole persistent range,
+// one atomic per channel and lane group at the end).  dry: validate only.
 int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres,
-                          void* dx, int B, int H, int W, int Cin, int Cout, bool dry,
-                          hipStream_t st) {
+                          void* dx, int B, int H, int W, int Cin, int Cout, const void* ypred,
+                          const void* pmean, const void* prstd, void* psums, int stripes,
+                          bool dry, hipStream_t st) {
   if (Cin != 64 || Cout != 64 || W < 1 || W > 64 || H < 1 || B < 1) return (int)hipErrorInvalidValue;
+  if (psums && (!ypred || !pmean || !prstd)) return (int)hipErrorInvalidValue;
   if ((long long)B * H * W * 64 >= (1LL << 40)) return (int)hipErrorInvalidValue;
   const int slot = ((W + 7) / 8) * 1024;
   const int lds = RW_RING_OFF + RW_RING * slot;
@@ -312,7 +367,9 @@ int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, cons
     g_lds_attr = lds;
   }
   RWArgs a{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
-           (const uint16_t*)dres, (uint16_t*)dx, B, H, W, (H + RW_TR - 1) / RW_TR, 0, slot};
+           (const uint16_t*)dres, (uint16_t*)dx, B, H, W, (H + RW_TR - 1) / RW_TR, 0, slot,
+           (const int16_t*)ypred, (const float*)pmean, (const float*)prstd, (float*)psums,
+           stripes < 1 ? 1 : stripes};
   const int nitems = B * a.ngroups;
   a.ipb = (nitems + g_num_cus - 1) / g_num_cus;
   const int grid = (nitems + a.ipb - 1) / a.ipb;

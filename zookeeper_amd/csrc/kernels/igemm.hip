@@ -2013,8 +2013,9 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
 
 // conv3rw.hip: row-window dgrad of the 64 -> 64 stride-1 3x3 conv (variant 50)
 int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres,
-                          void* dx, int B, int H, int W, int Cin, int Cout, bool dry,
-                          hipStream_t st);
+                          void* dx, int B, int H, int W, int Cin, int Cout, const void* ypred,
+                          const void* pmean, const void* prstd, void* psums, int stripes,
+                          bool dry, hipStream_t st);
 
 namespace {
 int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
@@ -2051,18 +2052,18 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     else if (c3 && Cin == 64)
       // row-window kernel for 64 -> 64 (stage 1 of E18 / QuickNet, batch
       // 1024: 430 vs 513-574 us for variant 27; profiles/r3/f_conv3rw.md)
-      variant = (g_opt_dgrad_rw && g.Cout == 64 && g.W <= 64 && !bs.sums) ? 50 : 27;
+      variant = (g_opt_dgrad_rw && g.Cout == 64 && g.W <= 64) ? 50 : 27;
     else if (Cin % 128 == 0)
       variant = 0;
     else
       variant = 7;
   }
   if (variant == 50) {  // conv3rw.hip (explicit, or the default above)
-    if (bs.sums || g.s != 1 || g.kh != 3 || g.kw != 3 || g.pt != 1 || g.pl != 1 ||
-        g.Ho != g.H || g.Wo != g.W)
+    if (g.s != 1 || g.kh != 3 || g.kw != 3 || g.pt != 1 || g.pl != 1 || g.Ho != g.H ||
+        g.Wo != g.W)
       return (int)hipErrorInvalidValue;
-    return zk_conv3rw_dgrad_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Cout,
-                                 g_dry_run, stream);
+    return zk_conv3rw_dgrad_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Cout, bs.ypred,
+                                 bs.mean, bs.rstd, bs.sums, bs.stripes, g_dry_run, stream);
   }
   const int rc = igemm_dgrad_variant(variant, dy, wt, mask, dres, dx, g, bs, stream);
   if (rc) return rc;

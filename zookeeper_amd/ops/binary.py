@@ -243,12 +243,20 @@ class _BinaryBlockFn(torch.autograd.Function):
         # BN-backward fusion hand-off (OPTS.fuse_bnsum): this block's reduction
         # may be done by its successor; the predecessor's by this block.
         ctx.bnsum = None
-        if OPTS.fuse_bnsum and not OPTS.deterministic and will_backward and bn.training:
+        # Always offered when a successor could take the row-window dgrad
+        # (64 channels, W <= 64: its persistent blocks add the sums once per
+        # block, nothing like the per-tile atomics that made fuse_bnsum lose).
+        rw_out = OPTS.dgrad_rw and Cout == 64 and Wo <= 64
+        if ((OPTS.fuse_bnsum or rw_out) and not OPTS.deterministic and will_backward
+                and bn.training):
             sums_buf = zeroed_scratch(bn, "bwd_sums", (STAT_STRIPES, 2, Cout), torch.float32, dev)
             ctx.bnsum = _BnSum(y, mean, rstd, sums_buf)
             side["bnsum"] = ctx.bnsum
         pred = side.get("pred")
+        rw_in = (OPTS.dgrad_rw and Cin == 64 and Cout == 64 and stride == 1 and kh == kw == 3
+                 and W <= 64 and pt == pl == 1)
         ctx.pred = (pred if (pred is not None and identity and mfma
+                             and (OPTS.fuse_bnsum or rw_in)
                              and tuple(pred.y.shape) == (B, H, W, Cin)) else None)
         ctx.save_for_backward(bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx, sx4)
         ctx.params = (weight, gamma, beta)
