@@ -46,6 +46,11 @@ def run(mode: str, out: str) -> None:
     force = os.environ.get("ZK_TEST_FORCE_DP", "0") == "1"
     backend = os.environ.get("ZK_TEST_BACKEND", "gloo")
     set_options(wgrad_side_stream=os.environ.get("ZK_TEST_SIDE", "1") == "1")
+    # ZK_TEST_RT="key=value,...": further kernel options (diagnostics)
+    for kv in filter(None, os.environ.get("ZK_TEST_RT", "").split(",")):
+        k, v = kv.split("=")
+        set_options(**{k: (v.lower() in ("1", "true")) if v.lower() in ("0", "1", "true", "false")
+                       else int(v)})
     if world > 1 or force:
         info = zdist.init(backend, single_group=force)
     else:

@@ -83,6 +83,9 @@ def test_rejected_sets_are_the_expected_ones():
         assert (c3 and s != 1) or cin % bn != 0
     for v, cin, cout, s in ts.rejected(ts.wgrad_ok, ts.WGRAD, shapes):
         bm, bn, c3 = ts.WGRAD[v]
+        if v == 51:  # the row-window kernel: Cin = Cout in {64, ..., 512} only
+            assert s != 1 or cin != cout
+            continue
         assert (c3 and s != 1) or cout % bm != 0 or (cin if c3 else 9 * cin) % bn != 0
     # every variant is exercised by at least one generated shape
     assert {p[0] for p in ts.pairs(ts.dgrad_ok, ts.DGRAD, shapes)} == set(ts.DGRAD)

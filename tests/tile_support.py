@@ -55,6 +55,8 @@ WGRAD: Dict[int, Tuple[int, int, bool]] = {
     24: (64, 128, True), 25: (64, 64, True), 26: (128, 128, True), 27: (64, 64, True),
     28: (128, 64, True), 29: (64, 64, True), 30: (64, 64, True), 32: (128, 64, True),
     33: (64, 64, True), 34: (128, 64, True),
+    # row-window kernel (conv3rw.hip): Cin = Cout in {64, 128, 256, 512}, stride 1
+    51: (64, 64, True),
 }
 
 # wgrad on the e2m1 sign image (zk_igemm_wgrad_f4): variant -> same tuple;
@@ -104,6 +106,8 @@ def wgrad_ok(v: int, cin: int, cout: int, stride: int) -> bool:
     if v not in table:
         return False
     bm, bn, c3 = table[v]
+    if v == 51:
+        return stride == 1 and cin == cout and cin in (64, 128, 256, 512)
     if v >= 100 and cin % 32:
         return False
     if c3:

@@ -28,6 +28,12 @@
 //   * XCD-aware tile order: consecutive M tiles of one N tile share an XCD.
 #include "mfma_common.h"
 
+// conv3rw.hip: row-window wgrad of the 64 -> 64 stride-1 3x3 conv (variant 51)
+int zk_conv3rw_wgrad_impl(const void* dy, const void* sx, const void* w, void* dw, int B, int H,
+                          int W, int Cin, int Cout, int pad_ones, float clip, void* slab,
+                          long long slab_bytes, long long* need, int* splits, bool dry,
+                          hipStream_t st);
+
 namespace {
 
 // Support queries (zk_igemm_*_supported): every launcher validates the
@@ -89,10 +95,13 @@ struct ConvArgs {
 //     a fixed order (no float atomics).
 //   dgrad_rw (key 3): the row-window kernel (conv3rw.hip, variant 50) for the
 //     64 -> 64 stride-1 3x3 data gradient by default.
+//   wgrad_rw (key 4): the row-window kernel (conv3rw.hip, variant 51) for the
+//     64 -> 64 stride-1 3x3 weight gradient by default.
 int g_opt_tile_huge = 16;
 int g_opt_korder = 0;
 int g_opt_deterministic = 0;
 int g_opt_dgrad_rw = 1;
+int g_opt_wgrad_rw = 0;
 
 bool huge_tiles_env(int bit = 31) { return (g_opt_tile_huge & bit) != 0; }
 
@@ -1953,6 +1962,19 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
   return launch_igemm_wgrad<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, ws, wsb, need, st)
 #define ZK_IGW3(...) \
   return launch_igemm_wgrad3<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, ws, wsb, need, st)
+  if (v == 51) {  // conv3rw.hip row-window kernel + the fixed-order slab reduce
+    if (g.s != 1 || g.kh != 3 || g.kw != 3 || g.pt != 1 || g.pl != 1 || g.Ho != g.H ||
+        g.Wo != g.W)
+      return (int)hipErrorInvalidValue;
+    int splits = 0;
+    const int rc = zk_conv3rw_wgrad_impl(dy, sx, w, dw, g.B, g.H, g.W, g.Cin, g.Cout, po, clip,
+                                         ws, wsb, need, &splits, need != nullptr || g_dry_run, st);
+    if (rc || need || g_dry_run || splits == 0) return rc;
+    const long long n4 = (long long)g.Cout * 9 * g.Cin / 4;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st,
+                       (const float4*)ws, splits, n4, (const float4*)w, clip, (float4*)dw);
+    return 0;
+  }
   switch (v) {
     // conv3 family <BM, BN, WM, WN, BK, NS, TH, OCC>
     case 20: ZK_IGW3(64, 64, 2, 2, 32, 4, 3, 1);
@@ -2118,7 +2140,9 @@ void wgrad_defaults(const IGeom& g, int& variant, int& target_blocks) {
     // blocks (329 -> 222 us), 7x7x512 on 128x128 at 2048 blocks (392 vs 400).
     const bool c3 = conv3_ok(g, 0);
     const bool big = g.B >= 512, huge = g.B >= 1024;
-    if (c3 && g.Cin == 64 && g.Cout % 64 == 0) {
+    if (g_opt_wgrad_rw && c3 && g.Cin == 64 && g.Cout == 64 && g.W <= 64) {
+      variant = 51;  // row-window kernel (conv3rw.hip)
+    } else if (c3 && g.Cin == 64 && g.Cout % 64 == 0) {
       variant = 20;
       if (target_blocks <= 0) target_blocks = 512;
     } else if (huge && huge_tiles_env(1) && c3 && g.Cin == 128 && g.Cout % 64 == 0) {
@@ -2190,7 +2214,7 @@ int wgrad_f4_of(int v) {
     case 8: case 12: return 108;
     case 9: return 109;
     case 10: return 110;
-    case 20: case 29: return 120;
+    case 20: case 29: case 51: return 120;
     case 21: case 33: return 121;
     case 22: case 28: case 34: return 122;
     case 25: return 125;
@@ -2390,6 +2414,7 @@ ZK_EXPORT int zk_set_option(int key, int value) {
     case 1: g_opt_korder = value; return 0;
     case 2: g_opt_deterministic = value; return 0;
     case 3: g_opt_dgrad_rw = value; return 0;
+    case 4: g_opt_wgrad_rw = value; return 0;
     default: return -1;
   }
 }
@@ -2400,6 +2425,7 @@ ZK_EXPORT int zk_get_option(int key) {
     case 1: return g_opt_korder;
     case 2: return g_opt_deterministic;
     case 3: return g_opt_dgrad_rw;
+    case 4: return g_opt_wgrad_rw;
     default: return -1;
   }
 }

@@ -52,12 +52,15 @@ class KernelOptions:
     # Row-window data gradient for the 64 -> 64 stride-1 3x3 binary conv
     # (conv3rw.hip: resident weights, LDS ring of dY rows).
     dgrad_rw: bool = True
+    # Row-window weight gradient for the same layer (conv3rw.hip: the whole
+    # 64 x 576 dW in registers per persistent block, LDS ring of sign rows).
+    wgrad_rw: bool = False
 
 
 OPTS = KernelOptions()
 
 # keys the native library reads (zk_set_option); values are ints
-_NATIVE_KEYS = {"tile_huge": 0, "korder": 1, "deterministic": 2, "dgrad_rw": 3}
+_NATIVE_KEYS = {"tile_huge": 0, "korder": 1, "deterministic": 2, "dgrad_rw": 3, "wgrad_rw": 4}
 
 
 def _push_native() -> None:

@@ -44,6 +44,7 @@ class Runtime:
     tile_huge: int = Field(16)
     korder: int = Field(0)
     dgrad_rw: bool = Field(True)
+    wgrad_rw: bool = Field(False)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
     deterministic: bool = Field(False)
