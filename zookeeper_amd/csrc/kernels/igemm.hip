@@ -78,6 +78,10 @@ struct ConvArgs {
   // tap), 1 = channel-chunk-major (all taps of a chunk): the shifted
   // activation rows of the taps are re-read while still in L2.
   int korder;
+  // float forward through the LDS epilogue (a 1x1 conv as this GEMM, optional):
+  // the next BatchNorm's statistics of the stored bf16 outputs,
+  // fstats[stripe][0][c] += sum y, [1][c] += sum y^2 (fp64, stripe = block % stripes)
+  double* fstats;
 };
 
 // Host-side kernel options, set from Python (ops/options.py -> zk_set_option;
@@ -228,6 +232,12 @@ __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeo
   }
   uint16_t* dx = reinterpret_cast<uint16_t*>(args.out);
   const uint16_t* dres = args.dres;
+  // args.fstats: this thread's 8 channels are fixed (NT is a multiple of BN/8)
+  static_assert(NT % (BN / 8) == 0, "LDS epilogue: fixed channel chunk per thread");
+  const bool fst = args.fstats != nullptr;
+  float fs1[8], fs2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) fs1[k] = fs2[k] = 0.f;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     __syncthreads();  // the ring (p = 0) / the previous half's tile is free
@@ -273,9 +283,41 @@ __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeo
           v[2 * k + 1] += zk::bf16_to_f32((uint16_t)(dd[k] >> 16));
         }
       }
-      *reinterpret_cast<uint4*>(dx + off) =
-          make_uint4(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
-                     zk::pack_bf16x2(v[4], v[5]), zk::pack_bf16x2(v[6], v[7]));
+      const uint4 o = make_uint4(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
+                                 zk::pack_bf16x2(v[4], v[5]), zk::pack_bf16x2(v[6], v[7]));
+      *reinterpret_cast<uint4*>(dx + off) = o;
+      if (fst) {
+        const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float r = zk::bf16_to_f32((uint16_t)(ow[k >> 1] >> (16 * (k & 1))));  // as stored
+          fs1[k] += r;
+          fs2[k] += r * r;
+        }
+      }
+    }
+  }
+  if (fst) {
+    // threads tid = r * JC + j hold chunk j: sum their rows through LDS
+    // (16 floats per thread), then one fp64 atomic per channel and statistic
+    constexpr int JC = BN / 8, RPT = NT / JC;
+    static_assert(NT * 16 * 4 <= BM * BN * 2, "LDS epilogue: statistics exchange");
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();  // every thread is past its staged-tile reads
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[tid * 16 + k] = fs1[k];
+      red[tid * 16 + 8 + k] = fs2[k];
+    }
+    __syncthreads();
+    const int stripe = args.stripes > 1 ? (int)(blockIdx.x % args.stripes) : 0;
+    double* so = args.fstats + (long long)stripe * 2 * g.Cin;
+    for (int c = tid; c < 2 * BN; c += NT) {
+      const int which = c / BN, nl = c % BN, j = nl >> 3, k = nl & 7;
+      float t = 0.f;
+#pragma unroll 4
+      for (int r = 0; r < RPT; ++r) t += red[(r * JC + j) * 16 + which * 8 + k];
+      atomicAdd(so + which * g.Cin + n0 + nl, (double)t);
     }
   }
 }
@@ -998,12 +1040,14 @@ struct BnSum {
   const void* rstd;
   void* sums;
   int stripes;
+  void* fstats;  // LE variants only: ConvArgs::fstats (float forward statistics)
 };
 
 template <int BM, int BN, int WM, int WN, int NS, int CB = 128, bool LE = false>
 int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const void* dres,
                        void* dx, const IGeom& g, const BnSum& bs, hipStream_t stream) {
   if (LE && bs.sums) return (int)hipErrorInvalidValue;  // fused BN sums: register epilogue
+  if (!LE && bs.fstats) return (int)hipErrorInvalidValue;  // forward statistics: LDS epilogue
   if ((g.Cout * 2) % CB || g.Cin % BN || g.s > 2 || g.kh > 4 || g.kw > 4)
     return (int)hipErrorInvalidValue;
   if (g_dry_run) return 0;
@@ -1026,6 +1070,7 @@ int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const v
                 (const int16_t*)bs.ypred, (const float*)bs.mean, (const float*)bs.rstd,
                 (float*)bs.sums};
   args.korder = korder_env();
+  args.fstats = (double*)bs.fstats;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, g.s * g.s), dim3(WM * WN * 64), LDS, stream,
                      args, g, m_tiles);
   return 0;
@@ -1187,6 +1232,7 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
                         const void* dres, void* dx, const IGeom& g, const BnSum& bs,
                         hipStream_t st) {
 #define ZK_IGD(...) return launch_igemm_dgrad<__VA_ARGS__>(dy, wt, mask, dres, dx, g, bs, st)
+  if (bs.fstats && (v < 40 || v > 48)) return (int)hipErrorInvalidValue;  // LE variants only
   switch (v) {
     case 0: ZK_IGD(128, 128, 2, 2, 2);        // 64 KB: 2 WG/CU
     case 1: ZK_IGD(128, 128, 2, 2, 4, 64);    // 64 KB, 3 K-steps of 32 in flight
@@ -2081,6 +2127,7 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
       variant = 7;
   }
   if (variant == 50) {  // conv3rw.hip (explicit, or the default above)
+    if (bs.fstats) return (int)hipErrorInvalidValue;
     if (g.s != 1 || g.kh != 3 || g.kw != 3 || g.pt != 1 || g.pl != 1 || g.Ho != g.H ||
         g.Wo != g.W)
       return (int)hipErrorInvalidValue;
@@ -2119,6 +2166,25 @@ ZK_EXPORT int zk_igemm_dgrad_bnsum(const void* dy, const void* wt, const void* m
   return igemm_dgrad_impl(dy, wt, mask, dres, dx, g,
                           BnSum{ypred, mean, rstd, sums, stripes < 1 ? 1 : stripes}, variant,
                           stream);
+}
+
+// Float 1x1 forward as this GEMM (roles renamed as in ops/pointwise.py:
+// x = "dy" [P][K], W = "wt" [N][K], y = "dx" [P][N] bf16) with the next
+// BatchNorm's statistics of the stored outputs: fstats [stripes][2][N] fp64
+// += (sum y, sum y^2) (zeroed by the caller; zk_bn_finalize_f64_parts sums the
+// stripes).  Only the LDS-epilogue variants carry the statistics: any other
+// (default or explicit) choice returns hipErrorInvalidValue and the caller
+// keeps the separate statistics pass.
+ZK_EXPORT int zk_igemm_dgrad_fstats(const void* dy, const void* wt, void* dx, void* fstats,
+                                    int stripes, int B, int H, int W, int Cin, int Ho, int Wo,
+                                    int Cout, int kh, int kw, int stride, int pt, int pl,
+                                    int variant, hipStream_t stream) {
+  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+  if (!fstats || Cin % 8) return (int)hipErrorInvalidValue;
+  return igemm_dgrad_impl(dy, wt, nullptr, nullptr, dx, g,
+                          BnSum{nullptr, nullptr, nullptr, nullptr, stripes < 1 ? 1 : stripes,
+                                fstats},
+                          variant, stream);
 }
 
 namespace {

@@ -93,7 +93,8 @@ __global__ void bn_finalize_f64_kernel(double* __restrict__ sums, int C, double 
                                        const float* __restrict__ gamma,
                                        const float* __restrict__ beta, float eps, float momentum,
                                        float* __restrict__ rmean, float* __restrict__ rvar,
-                                       float* __restrict__ coef, int nparts) {
+                                       float* __restrict__ coef, int nparts,
+                                       int rezero) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double s1 = 0.0, s2 = 0.0;
@@ -103,9 +104,12 @@ __global__ void bn_finalize_f64_kernel(double* __restrict__ sums, int C, double 
   }
   const double mean = s1 / P;
   double var = s2 / P - mean * mean;
-  if (nparts == 1) {
-    sums[c] = 0.0;  // re-zeroed for the next use (persistent per-layer buffer)
-    sums[C + c] = 0.0;
+  if (nparts == 1 || rezero) {
+    // re-zeroed for the next use (persistent per-layer buffer)
+    for (int j = 0; j < nparts; ++j) {
+      sums[(2LL * j) * C + c] = 0.0;
+      sums[(2LL * j + 1) * C + c] = 0.0;
+    }
   }
   if (var < 0) var = 0;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
@@ -520,7 +524,7 @@ ZK_EXPORT int zk_bn_finalize_f64(const void* sums, int C, double P, const void* 
                                  void* rvar, void* coef, hipStream_t st) {
   hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
                      (double*)sums, C, P, (const float*)gamma, (const float*)beta, eps,
-                     momentum, (float*)rmean, (float*)rvar, (float*)coef, 1);
+                     momentum, (float*)rmean, (float*)rvar, (float*)coef, 1, 0);
   ZK_CHECK_LAUNCH();
   return 0;
 }
@@ -550,7 +554,22 @@ ZK_EXPORT int zk_bn_finalize_f64_parts(const void* parts, int nparts, int C, dou
                                        hipStream_t st) {
   hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
                      (double*)parts, C, P, (const float*)gamma, (const float*)beta, eps,
-                     momentum, (float*)rmean, (float*)rvar, (float*)coef, nparts < 1 ? 1 : nparts);
+                     momentum, (float*)rmean, (float*)rvar, (float*)coef, nparts < 1 ? 1 : nparts, 0);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// zk_bn_finalize_f64_parts over striped accumulators that are re-zeroed after
+// reading (the persistent [stripes][2][C] buffer the float forward GEMM's
+// epilogue adds its statistics into: zk_igemm_dgrad_fstats).
+ZK_EXPORT int zk_bn_finalize_f64_stripes(void* parts, int nparts, int C, double P,
+                                         const void* gamma, const void* beta, float eps,
+                                         float momentum, void* rmean, void* rvar, void* coef,
+                                         hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
+                     (double*)parts, C, P, (const float*)gamma, (const float*)beta, eps,
+                     momentum, (float*)rmean, (float*)rvar, (float*)coef, nparts < 1 ? 1 : nparts,
+                     1);
   ZK_CHECK_LAUNCH();
   return 0;
 }

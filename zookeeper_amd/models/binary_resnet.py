@@ -88,7 +88,8 @@ class BinaryResBlock(nn.Module):
                     # x's two gradients (shortcut avg-pool + binary conv) are
                     # summed in the avg-pool backward instead of an add pass
                     handoff = norm_pool.ResidualHandoff()
-                    residual = bn(conv(norm_pool.avg_pool2(x, handoff=handoff)))
+                    # (BN statistics from the 1x1 GEMM's epilogue: stats_for)
+                    residual = bn(conv(norm_pool.avg_pool2(x, handoff=handoff), stats_for=bn))
                 else:
                     residual = self.downsample(x)
             else:

@@ -97,7 +97,8 @@ class Transition(nn.Module):
             x = F.relu(max_pool(x, 2, 1, "valid"))  # relu∘max == max∘relu
         else:
             x = F.max_pool2d(F.relu(x), 2, 1)
-        return self.bn(self.conv(self.blur(x)))
+        # (BN statistics from the 1x1 GEMM's epilogue where it runs one: stats_for)
+        return self.bn(self.conv(self.blur(x), stats_for=self.bn))
 
 
 class QuickNetModule(nn.Module):

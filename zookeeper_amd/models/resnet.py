@@ -49,7 +49,7 @@ class Bottleneck(nn.Module):
                 # shortcut conv's data-gradient epilogue: conv1's backward
                 # runs first and leaves its gradient there
                 give = norm_pool.ResidualHandoff()
-                idt = dbn(dconv(x, handoff=give))
+                idt = dbn(dconv(x, handoff=give, stats_for=dbn))
             else:
                 idt = self.down(x)
         else:
@@ -61,14 +61,16 @@ class Bottleneck(nn.Module):
                     # x's two gradients (shortcut + main path) summed in conv1's
                     # data-gradient epilogue instead of a separate add pass
                     handoff = norm_pool.ResidualHandoff()
+        # stats_for: a 1x1 conv's GEMM epilogue also sums the next BN's batch
+        # statistics (no separate statistics pass over its output)
         if handoff is not None:
-            y = self.bn1(self.conv1(x, handoff=handoff))
+            y = self.bn1(self.conv1(x, handoff=handoff, stats_for=self.bn1))
         elif give is not None:
-            y = self.bn1(self.conv1(x, give=give))
+            y = self.bn1(self.conv1(x, give=give, stats_for=self.bn1))
         else:
-            y = self.bn1(self.conv1(x))
-        y = self.bn2(self.conv2(y))
-        y = self.conv3(y)
+            y = self.bn1(self.conv1(x, stats_for=self.bn1))
+        y = self.bn2(self.conv2(y, stats_for=self.bn2))
+        y = self.conv3(y, stats_for=self.bn3)
         if _use_native(y):
             from zookeeper_amd.ops import norm_pool
 

@@ -178,14 +178,17 @@ class QuantConv2d(nn.Module):
         return conv_op.supported(x, self.weight, self.stride, self.padding, self.groups,
                                  self.bias, self.pad_values)
 
-    def forward(self, x: torch.Tensor, handoff=None, give=None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, handoff=None, give=None, stats_for=None) -> torch.Tensor:
+        """``stats_for``: the BatchNorm that normalises the output next (its
+        statistics then come from the 1x1 GEMM's epilogue, ops/pointwise.py);
+        ignored by the other paths."""
         if handoff is not None or give is not None:
             # gradient hand-off (norm_pool.ResidualHandoff); the caller checked
             # uses_pointwise(x) / uses_native_conv(x) (see models/resnet.py)
             if self.uses_pointwise(x):
                 from zookeeper_amd.ops import pointwise
 
-                return pointwise.conv1x1(x, self.weight, handoff, give)
+                return pointwise.conv1x1(x, self.weight, handoff, give, stats_for)
             if give is None and self.uses_native_conv(x):
                 from zookeeper_amd.ops import conv as conv_op
 
@@ -202,14 +205,14 @@ class QuantConv2d(nn.Module):
             from zookeeper_amd.ops import pointwise
 
             if pointwise.supported(x, self.weight, self.stride, self.groups, self.bias):
-                return pointwise.conv1x1(x, self.weight)
+                return pointwise.conv1x1(x, self.weight, stats_for=stats_for)
         if (self.input_quantizer is None and self.kernel_quantizer is None
                 and self.kernel_size == (3, 3) and _use_native(x)):
             from zookeeper_amd.ops import conv3x3
 
             if conv3x3.supported(x, self.weight, self.stride, self.padding, self.groups,
                                  self.bias, self.pad_values):
-                return conv3x3.conv3x3(x, self.weight)
+                return conv3x3.conv3x3(x, self.weight, stats_for=stats_for)
         if self._binary() and _use_native(x):
             from zookeeper_amd.ops import bconv
 

@@ -28,6 +28,7 @@ SIGNATURES = {
     "zk_bconv_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
     "zk_igemm_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
     "zk_igemm_dgrad_bnsum": (I32, [P] * 9 + [I32] * 14 + [P]),
+    "zk_igemm_dgrad_fstats": (I32, [P] * 4 + [I32] * 14 + [P]),
     "zk_igemm_fwd": (I32, [P, P, P, P] + [I32] * 16 + [P]),
     "zk_igemm_fwd_fp4": (I32, [P, P, P, P] + [I32] * 16 + [P]),
     "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),
@@ -39,6 +40,7 @@ SIGNATURES = {
     "zk_bn_bwd_reduce_blocks": (I32, []),
     "zk_bn_stats_bf16_parts": (I32, [P, P, I64, I32, IP, P]),
     "zk_bn_finalize_f64_parts": (I32, [P, I32, I32, C.c_double, P, P, F32, F32, P, P, P, P]),
+    "zk_bn_finalize_f64_stripes": (I32, [P, I32, I32, C.c_double, P, P, F32, F32, P, P, P, P]),
     "zk_bn_bwd_reduce_relu_bf16_parts": (I32, [P, P, P, P, I64, I32, IP, P]),
     "zk_get_option": (I32, [I32]),
     "zk_igemm_fwd_bf16": (I32, [P, P, P] + [I32] * 14 + [P]),

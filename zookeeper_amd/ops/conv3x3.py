@@ -26,6 +26,7 @@ from typing import Optional
 
 import torch
 
+from zookeeper_amd.ops import pointwise
 from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
 from zookeeper_amd.ops.options import OPTS
 
@@ -50,7 +51,7 @@ def _nhwc(t: torch.Tensor) -> torch.Tensor:
 
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, stats_for=None):
         B, Cin, H, W = x.shape
         Cout = weight.shape[0]
         xn = _nhwc(x)
@@ -61,9 +62,12 @@ class _Conv3x3Fn(torch.autograd.Function):
         y = torch.empty((B, H, W, Cout), dtype=torch.bfloat16, device=x.device)
         # dgrad geometry with roles renamed: "Cin" = Cout (N), "Cout" = Cin (K),
         # mirrored pads kh - 1 - 1 = 1
-        check(lib().zk_igemm_dgrad(xn.data_ptr(), wf.data_ptr(), None, None, y.data_ptr(), B, H,
-                                   W, Cout, H, W, Cin, 3, 3, 1, 1, 1, -1, stream_ptr(x.device)),
-              "zk_igemm_dgrad(3x3 fwd)")
+        st = stream_ptr(x.device)
+        if not pointwise.forward_with_stats(stats_for, xn, wf, y, Cout,
+                                            (B, H, W, Cout, H, W, Cin, 3, 3, 1, 1, 1), st):
+            check(lib().zk_igemm_dgrad(xn.data_ptr(), wf.data_ptr(), None, None, y.data_ptr(), B,
+                                       H, W, Cout, H, W, Cin, 3, 3, 1, 1, 1, -1, st),
+                  "zk_igemm_dgrad(3x3 fwd)")
         ctx.save_for_backward(xn)
         ctx.weight = weight
         ctx.shape = (B, Cin, H, W, Cout)
@@ -106,10 +110,11 @@ class _Conv3x3Fn(torch.autograd.Function):
                 grad_ready(weight)
             else:
                 dweight = dw.permute(0, 3, 1, 2)
-        return dx, dweight
+        return dx, dweight, None
 
 
-def conv3x3(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+def conv3x3(x: torch.Tensor, weight: torch.Tensor, stats_for=None) -> torch.Tensor:
     """``same``-padded 3×3 stride-1 float convolution (see ``supported``) as
-    MFMA implicit GEMMs.  Returns a channels_last bf16 tensor."""
-    return _Conv3x3Fn.apply(x, weight)
+    MFMA implicit GEMMs.  Returns a channels_last bf16 tensor.  ``stats_for``:
+    see ``pointwise.forward_with_stats`` (tiles with the LDS epilogue only)."""
+    return _Conv3x3Fn.apply(x, weight, stats_for)

@@ -44,7 +44,21 @@ class _BatchNormFn(torch.autograd.Function):
         st = stream_ptr(dev)
         L = lib()
         coef = torch.empty((4, C), dtype=torch.float32, device=dev)
-        if bn.training and OPTS.deterministic:
+        pend = bn.__dict__.pop("_zk_pending_fstats", None)
+        if pend is not None and not (bn.training and pend[1] == xn.data_ptr()):
+            pend[0].zero_()  # produced for another tensor: unused, keep the buffer zero
+            pend = None
+        if pend is not None:
+            # statistics the producing GEMM's epilogue added up
+            # (pointwise.conv1x1(stats_for=bn)); the finalize re-zeroes them
+            parts, _, nparts = pend
+            check(L.zk_bn_finalize_f64_stripes(parts.data_ptr(), nparts, C, float(P),
+                                               gamma.data_ptr() if gamma is not None else None,
+                                               beta.data_ptr() if beta is not None else None,
+                                               bn.eps, bn.momentum, bn.running_mean.data_ptr(),
+                                               bn.running_var.data_ptr(), coef.data_ptr(), st),
+                  "zk_bn_finalize_f64_stripes")
+        elif bn.training and OPTS.deterministic:
             # per-block partials, summed in block order (no fp64 atomics)
             parts = torch.empty((L.zk_bn_bwd_parts_max(), 2, C), dtype=torch.float64, device=dev)
             n = ctypes.c_int(0)

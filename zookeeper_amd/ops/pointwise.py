@@ -28,9 +28,16 @@ from typing import Optional
 
 import torch
 
-from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
+from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
+                                        zeroed_scratch)
+from zookeeper_amd.ops.options import OPTS
 
 _INF = float("inf")
+# Striped fp64 copies of the forward BN statistics the GEMM epilogue adds
+# into (block b into copy b % FSTAT_STRIPES; zk_bn_finalize_f64_stripes sums
+# and re-zeroes them).
+FSTAT_STRIPES = 32
+_HIP_INVALID_VALUE = 1  # hipErrorInvalidValue: no LDS-epilogue tile for this shape
 
 
 def supported(x: torch.Tensor, weight: torch.Tensor, stride, groups: int,
@@ -41,6 +48,26 @@ def supported(x: torch.Tensor, weight: torch.Tensor, stride, groups: int,
             and tuple(stride) == (1, 1) and x.shape[1] == weight.shape[1]
             and bias is None and x.shape[1] % 64 == 0 and weight.shape[0] % 64 == 0
             and x.shape[0] * x.shape[2] * x.shape[3] < (1 << 24))
+
+
+def forward_with_stats(stats_for, x, wt, y, n: int, geom, st) -> bool:
+    """The float forward GEMM ``y = x * wt`` (``zk_igemm_dgrad`` geometry
+    ``geom`` = B, H, W, N, Ho, Wo, K, kh, kw, stride, pt, pl) with the batch
+    statistics of the BatchNorm ``stats_for`` summed in its LDS epilogue
+    (``zk_igemm_dgrad_fstats``); ``_BatchNormFn`` picks them up by y's
+    address instead of running a statistics pass.  Only in training outside
+    the deterministic mode (fp64 atomics).  False: nothing was launched
+    (no BN, or no LDS-epilogue tile for this shape) -- run the plain GEMM."""
+    if stats_for is None or not stats_for.training or OPTS.deterministic:
+        return False
+    parts = zeroed_scratch(stats_for, "fstats", (FSTAT_STRIPES, 2, n), torch.float64, y.device)
+    rc = lib().zk_igemm_dgrad_fstats(x.data_ptr(), wt.data_ptr(), y.data_ptr(), parts.data_ptr(),
+                                     FSTAT_STRIPES, *geom, -1, st)
+    if rc == _HIP_INVALID_VALUE:
+        return False
+    check(rc, "zk_igemm_dgrad_fstats")
+    stats_for.__dict__["_zk_pending_fstats"] = (parts, y.data_ptr(), FSTAT_STRIPES)
+    return True
 
 
 def _rows(x: torch.Tensor) -> torch.Tensor:
@@ -54,16 +81,20 @@ def _rows(x: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, handoff=None, give=None):
+    def forward(ctx, x, weight, handoff=None, give=None, stats_for=None):
         B, Cin, H, W = x.shape
         Cout = weight.shape[0]
         x2 = _rows(x)
         w2 = weight.detach().reshape(Cout, Cin).to(torch.bfloat16)
         y2 = torch.empty((x2.shape[0], Cout), dtype=torch.bfloat16, device=x.device)
+        L = lib()
+        st = stream_ptr(x.device)
         # dgrad kernel, roles renamed: N = Cout ("Cin"), K = Cin ("Cout")
-        check(lib().zk_igemm_dgrad(x2.data_ptr(), w2.data_ptr(), None, None, y2.data_ptr(),
-                                   B, H, W, Cout, H, W, Cin, 1, 1, 1, 0, 0, -1,
-                                   stream_ptr(x.device)), "zk_igemm_dgrad(1x1 fwd)")
+        if not forward_with_stats(stats_for, x2, w2, y2, Cout, (B, H, W, Cout, H, W, Cin,
+                                                                 1, 1, 1, 0, 0), st):
+            check(L.zk_igemm_dgrad(x2.data_ptr(), w2.data_ptr(), None, None, y2.data_ptr(),
+                                   B, H, W, Cout, H, W, Cin, 1, 1, 1, 0, 0, -1, st),
+                  "zk_igemm_dgrad(1x1 fwd)")
         ctx.save_for_backward(x2, w2)
         ctx.weight = weight
         ctx.handoff, ctx.give = handoff, give
@@ -115,13 +146,18 @@ class _Conv1x1Fn(torch.autograd.Function):
                 grad_ready(weight)
             else:
                 dweight = dw.view(Cout, Cin, 1, 1)
-        return dx, dweight, None, None
+        return dx, dweight, None, None, None
 
 
-def conv1x1(x: torch.Tensor, weight: torch.Tensor, handoff=None, give=None) -> torch.Tensor:
+def conv1x1(x: torch.Tensor, weight: torch.Tensor, handoff=None, give=None,
+            stats_for=None) -> torch.Tensor:
     """``F.conv2d(x, weight)`` for a 1×1 stride-1 kernel (see ``supported``),
     as MFMA implicit GEMMs.  Returns a channels_last bf16 tensor.  With a
     ``norm_pool.ResidualHandoff`` as ``handoff`` the data gradient also adds
     the gradient another consumer of the same input left there; as ``give``
-    the data gradient is left there for that consumer instead of returned."""
-    return _Conv1x1Fn.apply(x, weight, handoff, give)
+    the data gradient is left there for that consumer instead of returned.
+    ``stats_for``: the BatchNorm module that normalises the output next; in
+    training (outside the deterministic mode) its batch statistics come from
+    this GEMM's epilogue (``zk_igemm_dgrad_fstats``) instead of a separate
+    pass over y."""
+    return _Conv1x1Fn.apply(x, weight, handoff, give, stats_for)
