@@ -35,6 +35,10 @@ class KernelOptions:
     wgrad_side_stream: bool = True
     # HIP priority of that side stream (0 = default, negative = higher).
     wgrad_priority: int = 0
+    # HIP priority of the stream the training step runs on (0: the current
+    # stream; negative: a higher-priority stream, so the data-gradient chain's
+    # small kernels are dispatched ahead of queued side-stream work).
+    compute_priority: int = 0
     # Recompute-fused ImageNet stem (False: the materialising kernels).
     stem_fused: bool = True
     # Float convolutions on the MFMA implicit-GEMM kernels (False: library).
@@ -55,6 +59,9 @@ class KernelOptions:
     # Row-window weight gradient for the same layer (conv3rw.hip: the whole
     # 64 x 576 dW in registers per persistent block, LDS ring of sign rows).
     wgrad_rw: bool = False
+    # Float conv GEMMs with the LDS epilogue also sum the next BatchNorm's
+    # batch statistics (pointwise.forward_with_stats; no statistics pass).
+    bn_stats_epilogue: bool = True
 
 
 OPTS = KernelOptions()

@@ -58,7 +58,8 @@ def forward_with_stats(stats_for, x, wt, y, n: int, geom, st) -> bool:
     address instead of running a statistics pass.  Only in training outside
     the deterministic mode (fp64 atomics).  False: nothing was launched
     (no BN, or no LDS-epilogue tile for this shape) -- run the plain GEMM."""
-    if stats_for is None or not stats_for.training or OPTS.deterministic:
+    if (stats_for is None or not stats_for.training or OPTS.deterministic
+            or not OPTS.bn_stats_epilogue):
         return False
     parts = zeroed_scratch(stats_for, "fstats", (FSTAT_STRIPES, 2, n), torch.float64, y.device)
     rc = lib().zk_igemm_dgrad_fstats(x.data_ptr(), wt.data_ptr(), y.data_ptr(), parts.data_ptr(),

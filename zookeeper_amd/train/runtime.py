@@ -37,6 +37,7 @@ class Runtime:
     wgrad_f4: bool = Field(False)
     wgrad_side_stream: bool = Field(True)
     wgrad_priority: int = Field(0)
+    compute_priority: int = Field(0)
     stem_fused: bool = Field(True)
     conv_mfma: bool = Field(True)
     conv3_mfma: bool = Field(True)
@@ -45,6 +46,7 @@ class Runtime:
     korder: int = Field(0)
     dgrad_rw: bool = Field(True)
     wgrad_rw: bool = Field(False)
+    bn_stats_epilogue: bool = Field(True)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
     deterministic: bool = Field(False)

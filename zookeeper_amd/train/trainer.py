@@ -18,6 +18,7 @@ import torch
 import torch.nn as nn
 
 from zookeeper_amd.ops import streams
+from zookeeper_amd.ops.options import OPTS
 from zookeeper_amd.parallel import dist as zdist
 from zookeeper_amd.parallel.ddp import GradBucketer
 from zookeeper_amd.parallel.flat import FlatParams
@@ -93,6 +94,7 @@ class Trainer:
         self._graph = None
         self._static_in = None
         self._static_out = None
+        self._compute_streams: dict = {}  # runtime.compute_priority -> stream
 
     def _forward_backward(self, x: torch.Tensor, y: torch.Tensor):
         self.flat.zero_grad()
@@ -109,7 +111,23 @@ class Trainer:
     def train_step(self, x: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """One training step.  In graph mode the returned tensors are the
         graph's static outputs: overwritten by the next step (consume or
-        clone them before)."""
+        clone them before).  ``runtime.compute_priority`` < 0: the step runs
+        on a higher-priority HIP stream, ordered after / before the caller's
+        stream by stream waits."""
+        prio = OPTS.compute_priority
+        if prio == 0 or self.device.type != "cuda":
+            return self._train_step(x, y)
+        cs = self._compute_streams.get(prio)
+        if cs is None:
+            cs = self._compute_streams[prio] = torch.cuda.Stream(self.device, priority=prio)
+        outer = torch.cuda.current_stream(self.device)
+        cs.wait_stream(outer)
+        with torch.cuda.stream(cs):
+            out = self._train_step(x, y)
+        outer.wait_stream(cs)
+        return out
+
+    def _train_step(self, x: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         if not self.graph or self._eager_steps < self.graph_warmup:
             probe = self._graph_auto and self._eager_steps == self.graph_warmup - 1
             if probe:
