@@ -28,11 +28,13 @@ on both sides; the reported time is the MAX over ranks.  Per-step GPU times
 (events between consecutive steps) give the median / p10 / p90.  Rank 0
 prints one JSON line.
 
-Weak scaling: the per-GPU batch (``--batch``, default 1024) is fixed, the
-global batch is ``batch × N``.  1024 images per GPU use a small part of the
-288 GB of HBM; smaller batches leave the 14x14 / 7x7 stages latency-bound
-(1 GPU, E18: 41.3k img/s at 512, 43.1k at 768, 44.0k at 1024), and the
-fixed-size gradient all-reduce is a smaller share of a longer step.
+Weak scaling: the per-GPU batch (``--batch``, default 1536) is fixed, the
+global batch is ``batch × N``.  1536 images per GPU use a part of the 288 GB
+of HBM; smaller batches leave the 14x14 / 7x7 stages latency-bound (1 GPU,
+E18, round 2: 41.3k img/s at 512, 43.1k at 768, 44.0k at 1024; round 3:
+46.7k at 1024, 47.9k at 1536, 2048 no faster and with multi-second
+allocator stalls), and the fixed-size gradient all-reduce is a smaller share
+of a longer step.
 """
 
 import argparse
@@ -53,7 +55,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=1024, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=1536, help="per-GPU batch")
     ap.add_argument("--model", default="BinaryResNetE18")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--num-classes", type=int, default=1000)

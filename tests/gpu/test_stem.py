@@ -143,7 +143,7 @@ def test_recompute_fused_stem_matches_materialising(hw, B, monkeypatch):
     ref = {n: p.grad for n, p in oracle.named_parameters()}
     runs = {}
     for fused in (False, True):
-        monkeypatch.setattr(stem_mod, "_FUSED", fused)
+        monkeypatch.setattr(stem_mod.OPTS, "stem_fused", fused)  # runtime.stem_fused
         m = copy.deepcopy(base)
         y = m(x)
         y.backward(g)

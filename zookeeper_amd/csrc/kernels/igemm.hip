@@ -106,6 +106,17 @@ int g_opt_korder = 0;
 int g_opt_deterministic = 0;
 int g_opt_dgrad_rw = 1;
 int g_opt_wgrad_rw = 0;
+// wgrad_slab_mb (key 5): cap on the split-K slab bytes of one weight gradient
+// (splits <= cap / |dW|); 0 = no cap (splits from the block target alone).
+int g_opt_wgrad_slab_mb = 0;
+
+// splits limited by the slab cap (plan_wgrad / plan_wgrad3)
+inline long long cap_splits(long long splits, long long dw_bytes) {
+  if (g_opt_wgrad_slab_mb <= 0 || dw_bytes <= 0) return splits;
+  long long cap = ((long long)g_opt_wgrad_slab_mb << 20) / dw_bytes;
+  if (cap < 1) cap = 1;
+  return splits < cap ? splits : cap;
+}
 
 bool huge_tiles_env(int bit = 31) { return (g_opt_tile_huge & bit) != 0; }
 
@@ -1629,6 +1640,7 @@ bool plan_wgrad(const IGeom& g, int target_blocks, WgradPlan& p) {
   long long splits = (target_blocks + tiles - 1) / tiles;
   const long long max_splits = (P + 4 * BK - 1) / (4 * BK);  // >= 4 K-steps per split
   if (splits > max_splits) splits = max_splits;
+  splits = cap_splits(splits, (long long)g.Cout * NTOT * 4);
   if (splits < 1) splits = 1;
   long long kps = (P + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;
@@ -1954,6 +1966,7 @@ bool plan_wgrad3(const IGeom& g, int target_blocks, WgradPlan& p) {
   long long splits = (target_blocks + tiles - 1) / tiles;
   const long long max_splits = (E + 4 * BK - 1) / (4 * BK);
   if (splits > max_splits) splits = max_splits;
+  splits = cap_splits(splits, (long long)g.Cout * g.kh * g.kw * g.Cin * 4);
   if (splits < 1) splits = 1;
   long long kps = (E + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;
@@ -2481,6 +2494,7 @@ ZK_EXPORT int zk_set_option(int key, int value) {
     case 2: g_opt_deterministic = value; return 0;
     case 3: g_opt_dgrad_rw = value; return 0;
     case 4: g_opt_wgrad_rw = value; return 0;
+    case 5: g_opt_wgrad_slab_mb = value; return 0;
     default: return -1;
   }
 }
@@ -2492,6 +2506,7 @@ ZK_EXPORT int zk_get_option(int key) {
     case 2: return g_opt_deterministic;
     case 3: return g_opt_dgrad_rw;
     case 4: return g_opt_wgrad_rw;
+    case 5: return g_opt_wgrad_slab_mb;
     default: return -1;
   }
 }

@@ -37,7 +37,9 @@ class KernelOptions:
     wgrad_priority: int = 0
     # HIP priority of the stream the training step runs on (0: the current
     # stream; negative: a higher-priority stream, so the data-gradient chain's
-    # small kernels are dispatched ahead of queued side-stream work).
+    # small kernels are dispatched ahead of queued side-stream work).  E18:
+    # batch 1024, 60 steps 46.97k vs 46.68k img/s; batch 1536, 200 steps
+    # 47.89k vs 48.00k: no gain, default off.
     compute_priority: int = 0
     # Recompute-fused ImageNet stem (False: the materialising kernels).
     stem_fused: bool = True
@@ -62,12 +64,16 @@ class KernelOptions:
     # Float conv GEMMs with the LDS epilogue also sum the next BatchNorm's
     # batch statistics (pointwise.forward_with_stats; no statistics pass).
     bn_stats_epilogue: bool = True
+    # Cap (MB) on one weight gradient's split-K slabs (fewer splits for the
+    # deep 3x3 layers, whose slabs reach ~130 MB); 0 = no cap.
+    wgrad_slab_mb: int = 0
 
 
 OPTS = KernelOptions()
 
 # keys the native library reads (zk_set_option); values are ints
-_NATIVE_KEYS = {"tile_huge": 0, "korder": 1, "deterministic": 2, "dgrad_rw": 3, "wgrad_rw": 4}
+_NATIVE_KEYS = {"tile_huge": 0, "korder": 1, "deterministic": 2, "dgrad_rw": 3, "wgrad_rw": 4,
+                "wgrad_slab_mb": 5}
 
 
 def _push_native() -> None:
