@@ -199,13 +199,17 @@ def main() -> int:
     zdist.barrier()
     sync()
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if cuda else []
+    mem0 = torch.cuda.memory_stats(info.device) if cuda else {}
+    host_t = []  # host time per step (enqueue, including any blocking call)
     t0 = time.perf_counter()
     if marks:
         marks[0].record()
     for i in range(args.steps):
+        th = time.perf_counter()
         loss, _ = step(args.warmup + i)
         if marks:
             marks[i + 1].record()
+        host_t.append(time.perf_counter() - th)
         if info.is_main and (i + 1) % 50 == 0:
             print(f"[bench] step {i + 1}/{args.steps}", file=sys.stderr, flush=True)
     t_enq = time.perf_counter() - t0  # host time to enqueue (no sync yet)
@@ -215,6 +219,17 @@ def main() -> int:
     elapsed = zdist.all_reduce_max(elapsed)
     final_loss = float(loss.item())
     step_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)] if marks else []
+    mem1 = torch.cuda.memory_stats(info.device) if cuda else {}
+    # allocator activity inside the timed region (device mallocs / frees /
+    # OOM retries would stall the host: reported so an outlier step has a cause)
+    alloc_delta = {k: mem1.get(k, 0) - mem0.get(k, 0)
+                   for k in ("num_device_alloc", "num_device_free", "num_alloc_retries")}
+    if info.is_main and step_ms:
+        worst = max(range(len(step_ms)), key=lambda i: step_ms[i])
+        hw = max(range(len(host_t)), key=lambda i: host_t[i])
+        print(f"[bench] slowest step {worst}: GPU {step_ms[worst]:.2f} ms; slowest host step "
+              f"{hw}: {1e3 * host_t[hw]:.2f} ms; allocator in timed region {alloc_delta}",
+              file=sys.stderr, flush=True)
     comm = trainer.bucketer.pop_timings()
     if loader is not None:
         loader.close()
@@ -255,6 +270,7 @@ def main() -> int:
         "ms_per_step_median": r3(_percentile(step_ms, 0.5)),
         "ms_per_step_p10": r3(_percentile(step_ms, 0.1)),
         "ms_per_step_p90": r3(_percentile(step_ms, 0.9)),
+        "ms_per_step_max": r3(max(step_ms)) if step_ms else None,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -338,8 +338,7 @@ class _BinaryBlockFn(torch.autograd.Function):
                            sstream.cuda_stream, f4)
                     done = torch.cuda.Event()
                     done.record(sstream)
-                for t in (dy, sxw, w_ohwi):
-                    t.record_stream(sstream)
+                streams.keep(dy, sxw, w_ohwi)  # released once the compute stream joins
             else:
                 dw = (w_direct.permute(0, 2, 3, 1) if w_direct is not None  # OHWI view
                       else torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev))
