@@ -108,7 +108,8 @@ int g_opt_dgrad_rw = 1;
 int g_opt_wgrad_rw = 0;
 // wgrad_slab_mb (key 5): cap on the split-K slab bytes of one weight gradient
 // (splits <= cap / |dW|); 0 = no cap (splits from the block target alone).
-int g_opt_wgrad_slab_mb = 0;
+// Default 32 MB (ops/options.py has the measurements).
+int g_opt_wgrad_slab_mb = 32;
 
 // splits limited by the slab cap (plan_wgrad / plan_wgrad3)
 inline long long cap_splits(long long splits, long long dw_bytes) {

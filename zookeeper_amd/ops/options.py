@@ -65,8 +65,11 @@ class KernelOptions:
     # batch statistics (pointwise.forward_with_stats; no statistics pass).
     bn_stats_epilogue: bool = True
     # Cap (MB) on one weight gradient's split-K slabs (fewer splits for the
-    # deep 3x3 layers, whose slabs reach ~130 MB); 0 = no cap.
-    wgrad_slab_mb: int = 0
+    # deep 3x3 layers, whose slabs reached ~130 MB of writes + reads; the
+    # side stream then also holds fewer CUs); 0 = no cap.  E18, 100 steps:
+    # batch 1024 46.6k -> 47.6k, batch 1536 47.7k -> 48.4k img/s (16 MB:
+    # 38k, too few splits for the 512-channel layers; 48/64 MB: 48.5k).
+    wgrad_slab_mb: int = 32
 
 
 OPTS = KernelOptions()

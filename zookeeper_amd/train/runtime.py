@@ -47,7 +47,7 @@ class Runtime:
     dgrad_rw: bool = Field(True)
     wgrad_rw: bool = Field(False)
     bn_stats_epilogue: bool = Field(True)
-    wgrad_slab_mb: int = Field(0)
+    wgrad_slab_mb: int = Field(32)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
     deterministic: bool = Field(False)
