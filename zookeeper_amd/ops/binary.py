@@ -285,15 +285,8 @@ class _BinaryBlockFn(torch.autograd.Function):
         sums = zeroed_scratch(ctx.bn, "bwd_sums", (stripes, 2, Cout), torch.float32, dev)
         bs = ctx.bnsum
         fused = bs is not None and bs.dx is not None
-        if not (fused and bs.reduced(dout)):
-            if fused:
-                sums.zero_()  # the successor reduced a gradient that was accumulated later
-            check(L.zk_bn_bwd_reduce(g.data_ptr(), y.data_ptr(), mean.data_ptr(),
-                                     rstd.data_ptr(), sums.data_ptr(), P, Cout, stripes, st),
-                  "zk_bn_bwd_reduce")
-        # else: the successor's dgrad epilogue reduced exactly this gradient
-        # BN coefficients + gamma/beta gradients in one launch; gradients go
-        # straight into the flat gradient buffer when the trainer manages it.
+        # BN coefficients + gamma/beta gradients; gradients go straight into
+        # the flat gradient buffer when the trainer manages it.
         dg_direct = direct_grad(gamma_p) if ctx.has_gamma else None
         db_direct = direct_grad(beta_p) if ctx.has_beta else None
         dgamma = dg_direct if dg_direct is not None else (
@@ -301,12 +294,33 @@ class _BinaryBlockFn(torch.autograd.Function):
         dbeta = db_direct if db_direct is not None else (
             torch.zeros(Cout, device=dev) if ctx.has_beta else None)
         coef = torch.empty((3, Cout), dtype=torch.float32, device=dev)
-        check(L.zk_bn_bwd_coef(sums.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                               gamma.data_ptr() if gamma is not None else None, float(P), Cout,
-                               stripes, coef.data_ptr(),
-                               dgamma.data_ptr() if dgamma is not None else None,
-                               dbeta.data_ptr() if dbeta is not None else None, st),
-              "zk_bn_bwd_coef")
+        coef_done = False
+        if not (fused and bs.reduced(dout)):
+            if fused:
+                sums.zero_()  # the successor reduced a gradient that was accumulated later
+            if OPTS.bn_coef_tail and not OPTS.deterministic:
+                # reduce + coefficients in one launch (the last block finishes)
+                counter = zeroed_scratch(ctx.bn, "bwd_counter", (1,), torch.int32, dev)
+                check(L.zk_bn_bwd_reduce_coef(
+                    g.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                    sums.data_ptr(), P, Cout, stripes, counter.data_ptr(),
+                    gamma.data_ptr() if gamma is not None else None, coef.data_ptr(),
+                    dgamma.data_ptr() if dgamma is not None else None,
+                    dbeta.data_ptr() if dbeta is not None else None, st),
+                    "zk_bn_bwd_reduce_coef")
+                coef_done = True
+            else:
+                check(L.zk_bn_bwd_reduce(g.data_ptr(), y.data_ptr(), mean.data_ptr(),
+                                         rstd.data_ptr(), sums.data_ptr(), P, Cout, stripes, st),
+                      "zk_bn_bwd_reduce")
+        # else: the successor's dgrad epilogue reduced exactly this gradient
+        if not coef_done:
+            check(L.zk_bn_bwd_coef(sums.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                   gamma.data_ptr() if gamma is not None else None, float(P),
+                                   Cout, stripes, coef.data_ptr(),
+                                   dgamma.data_ptr() if dgamma is not None else None,
+                                   dbeta.data_ptr() if dbeta is not None else None, st),
+                  "zk_bn_bwd_coef")
         if dg_direct is not None:
             grad_ready(gamma_p)
             dgamma = None

@@ -70,6 +70,10 @@ class KernelOptions:
     # batch 1024 46.6k -> 47.6k, batch 1536 47.7k -> 48.4k img/s (16 MB:
     # 38k, too few splits for the 512-channel layers; 48/64 MB: 48.5k).
     wgrad_slab_mb: int = 32
+    # The binary BN-backward reduce's last-arriving block also computes the
+    # coefficients and gamma/beta gradients (zk_bn_bwd_reduce_coef): no
+    # separate coef launch in the data-gradient chain.
+    bn_coef_tail: bool = True
 
 
 OPTS = KernelOptions()
