@@ -72,8 +72,12 @@ class KernelOptions:
     wgrad_slab_mb: int = 32
     # The binary BN-backward reduce's last-arriving block also computes the
     # coefficients and gamma/beta gradients (zk_bn_bwd_reduce_coef): no
-    # separate coef launch in the data-gradient chain.
-    bn_coef_tail: bool = True
+    # separate coef launch in the data-gradient chain.  Measured slower (E18
+    # batch 1536, interleaved 100-step windows on one box: off 47.60k /
+    # 47.65k, on 47.30k / 47.10k img/s): the agent-scope release in every
+    # block and the last block's serial stripe reads cost more than the coef
+    # launch's wait for a CU slot.  Off.
+    bn_coef_tail: bool = False
 
 
 OPTS = KernelOptions()

@@ -48,7 +48,7 @@ class Runtime:
     wgrad_rw: bool = Field(False)
     bn_stats_epilogue: bool = Field(True)
     wgrad_slab_mb: int = Field(32)
-    bn_coef_tail: bool = Field(True)
+    bn_coef_tail: bool = Field(False)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
     deterministic: bool = Field(False)
