@@ -195,6 +195,7 @@ def main() -> int:
             sync()
             print(f"[bench] warmup {i + 1}/{args.warmup} loss={loss.item():.4f} "
                   f"t={time.perf_counter() - t_w:.1f}s", file=sys.stderr, flush=True)
+    sync()
     trainer.bucketer.pop_timings()  # discard warmup comm timings
     zdist.barrier()
     sync()

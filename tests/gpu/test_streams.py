@@ -50,11 +50,25 @@ def test_side_stream_wgrad_matches_single_stream(monkeypatch):
     g_one, ready_one, _ = _grads(False, monkeypatch)
     # fp32-atomic ordering noise in the split-K / BN-backward sums (~1e-7),
     # amplified through the binary blocks (README "Known issues"): measured
-    # 1e-6 .. 8e-5 over the whole gradient; a missing or doubled weight
-    # gradient is O(1).  The deterministic mode is bit-exact
-    # (tests/gpu/test_determinism.py).
-    assert ((g_side - g_one).norm() / g_one.norm()).item() < 1e-3
+    # 1e-6 .. 3.4e-3 over the whole gradient; a missing or doubled weight
+    # gradient is O(1).  The deterministic mode is bit-exact (next test).
+    assert ((g_side - g_one).norm() / g_one.norm()).item() < 3e-2
     # every binary conv weight reported ready once, in both modes
     convs = [s.name for s in flat.slots if s.name.endswith("conv.weight")]
     for name in convs:
         assert ready_side.count(name) == 1 and ready_one.count(name) == 1, name
+
+
+def test_side_stream_wgrad_bit_exact_in_deterministic_mode(monkeypatch):
+    """With fixed-order reductions the side stream changes only where the
+    weight gradients run, not what they compute: bit-identical gradients."""
+    from zookeeper_amd.ops import options
+
+    old = options.OPTS.deterministic
+    try:
+        options.set_options(deterministic=True)
+        g_side, _, _ = _grads(True, monkeypatch)
+        g_one, _, _ = _grads(False, monkeypatch)
+    finally:
+        options.set_options(deterministic=old)
+    assert torch.equal(g_side, g_one), ((g_side - g_one).norm() / g_one.norm()).item()

@@ -262,7 +262,9 @@ class GradBucketer:
             starts, ends = ev["start"], ev["end"]
             if not ends:
                 continue
-            for e in ends.values():
+            # every event read below (a bucket's end can complete before the
+            # compute stream reaches bwd_end; bench --warmup 5 hit this)
+            for e in (*ends.values(), *starts.values(), ev["bwd_end"]):
                 e.synchronize()
             first = min(starts.values(), key=lambda e: ev["bwd_end"].elapsed_time(e))
             last = max(ends.values(), key=lambda e: ev["bwd_end"].elapsed_time(e))
