@@ -69,6 +69,8 @@ class KernelOptions:
     # side stream then also holds fewer CUs); 0 = no cap.  E18, 100 steps:
     # batch 1024 46.6k -> 47.6k, batch 1536 47.7k -> 48.4k img/s (16 MB:
     # 38k, too few splits for the 512-channel layers; 48/64 MB: 48.5k).
+    # Same-box sweep at batch 1536: 28 MB 47.52k, 32 MB 47.79k / 47.71k,
+    # 36 MB 47.17k, 40 MB 47.46k img/s.
     wgrad_slab_mb: int = 32
     # The binary BN-backward reduce's last-arriving block also computes the
     # coefficients and gamma/beta gradients (zk_bn_bwd_reduce_coef): no
