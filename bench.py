@@ -16,11 +16,12 @@ error, never a silent 1-GPU run.
 
 A timed step is the complete training step: uint8→bf16 normalisation/flip
 of the batch, forward, softmax-CE, backward with bucketed all-reduce on a
-comm stream, fused Adam + weight_clip.  ``--data pool`` (default) cycles a
-few device-resident synthetic batches; ``--data stream`` feeds the synthetic
-source through the host input pipeline (native row gather into pinned
-slots, side-stream H2D, event hand-off), so the host→device path is inside
-the timed region.  When the warmup shows the step host-bound (small
+comm stream, fused Adam + weight_clip.  ``--data stream`` (default) feeds
+the synthetic source through the host input pipeline (native row gather into
+pinned slots, side-stream H2D, event hand-off), so the host→device path of
+the reference's ``tf.data`` pipeline (examples/larq_experiment.py:126-139) is
+inside the timed region; ``--data pool`` cycles a few device-resident
+synthetic batches instead.  When the warmup shows the step host-bound (small
 ``--batch``), zero-grad + forward + loss + backward are replayed as one HIP
 graph (``--graph auto``; under DP the all-reduce runs after the replay).
 ``--steps`` steps are timed between a barrier + ``torch.cuda.synchronize()``
@@ -60,7 +61,7 @@ def parse(argv=None):
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--num-classes", type=int, default=1000)
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
-    ap.add_argument("--data", default="pool", choices=["pool", "stream"],
+    ap.add_argument("--data", default="stream", choices=["pool", "stream"],
                     help="pool: device-resident synthetic batches; stream: host pipeline "
                          "(pinned ring + side-stream H2D) inside the timed region")
     ap.add_argument("--pool", type=int, default=4, help="device-resident synthetic batches")
@@ -78,6 +79,16 @@ def parse(argv=None):
                          "--rt bconv_fp4=False --rt tile_huge=0; recorded in the JSON")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
+
+
+def _native_digest(backend):
+    """Source digest embedded in the loaded native library (which kernels ran)."""
+    if backend != "hip":
+        return None
+    from zookeeper_amd.ops import _native
+
+    d = _native.build_digest()
+    return d[:16] if d else None
 
 
 def _percentile(xs, q):
@@ -137,7 +148,7 @@ def main() -> int:
         rt_conf["force_dp"] = True
     configure(runtime, rt_conf)
     runtime.apply()
-    info = zdist.init(single_group=runtime.force_dp)
+    info = zdist.init(single_group=runtime.force_dp, comm=runtime.comm_config())
     if info.world != args.gpus:
         print(f"error: --gpus {args.gpus} but the job has {info.world} rank(s)", file=sys.stderr)
         return 2
@@ -285,11 +296,19 @@ def main() -> int:
             "image_shape": [S, S, 3],
             "parallelism": f"dp{info.world}",
             "backend": backend,
+            "native_digest": _native_digest(backend),
             "optimizer": "adam+weight_clip (fused)",
             "hip_graph": trainer.graph,
             "data_path": args.data,
             "buckets": trainer.bucketer.num_buckets if trainer.bucketer.enabled else 0,
             "dist_backend": info.backend,
+            "comm": {"cpu_affinity_cpus": len(info.cpus) if info.cpus else None,
+                     "rccl_env": info.rccl_env,
+                     "rccl_high_priority": bool(runtime.comm_high_priority and dp),
+                     "bucket_mb": args.bucket_mb,
+                     "bucket_sizes_mb": [round((hi - lo) * 4 / 2**20, 2)
+                                         for lo, hi in trainer.bucketer.ranges],
+                     "bucket_order_checks": trainer.bucketer.order_checks},
             "runtime": runtime.as_dict(),
             "final_loss": round(final_loss, 4),
         },

@@ -51,10 +51,13 @@ def run(mode: str, out: str) -> None:
         k, v = kv.split("=")
         set_options(**{k: (v.lower() in ("1", "true")) if v.lower() in ("0", "1", "true", "false")
                        else int(v)})
+    # ZK_TEST_CHECK_ORDER=1: every step compares the launched bucket order
+    # across ranks (runtime.check_bucket_order)
+    comm = zdist.CommConfig(check_bucket_order=os.environ.get("ZK_TEST_CHECK_ORDER", "0") == "1")
     if world > 1 or force:
-        info = zdist.init(backend, single_group=force)
+        info = zdist.init(backend, single_group=force, comm=comm)
     else:
-        info = zdist.init()
+        info = zdist.init(comm=comm)
     torch.manual_seed(1234)
     model = BinaryResNetE((64, 64, 3), 10, 18, backend="hip")
     if info.rank == 1:  # different init on rank 1: the broadcast must fix it
@@ -88,7 +91,9 @@ def run(mode: str, out: str) -> None:
                 "comm_steps": len(timings), "timings": timings,
                 "backend": info.backend, "bucketer": tr.bucketer.enabled,
                 "slots": [(sl.name, sl.offset, sl.numel) for sl in tr.flat.slots],
-                "ranges": list(tr.bucketer.ranges)},
+                "ranges": list(tr.bucketer.ranges),
+                "order_checks": tr.bucketer.order_checks,
+                "last_order": list(tr.bucketer.last_order)},
                os.path.join(out, f"{mode}_w{world}{'dp' if force else ''}_r{info.rank}.pt"))
     zdist.shutdown()
 

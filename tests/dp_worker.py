@@ -30,12 +30,13 @@ def data(global_batch=8, steps=3):
     return xs, ys
 
 
-def train(rank, world, bucket_mb):
+def train(rank, world, bucket_mb, check_order=False):
     from zookeeper_amd.core import configure
     from zookeeper_amd.parallel import dist as zdist
     from zookeeper_amd.train import Adam, Trainer
 
-    info = zdist.init("gloo") if world > 1 else zdist.DistInfo()
+    comm = zdist.CommConfig(check_bucket_order=check_order)
+    info = zdist.init("gloo", comm=comm) if world > 1 else zdist.DistInfo()
     spec = Adam()
     configure(spec, {"learning_rate": 0.01})
     model = make_model()
@@ -97,6 +98,21 @@ if __name__ == "__main__":
         all_reduce_buffers(bn)
         torch.save({"before": before, "after": bn.state_dict()},
                    os.path.join(out, f"bn{rank}.pt"))
+        zdist.shutdown()
+        sys.exit(0)
+    if mode == "order":
+        # the bucket-order check must flag ranks that launch differently
+        from zookeeper_amd.parallel import dist as zdist
+
+        tr = train(rank, world, bucket_mb=0.001, check_order=True)
+        ok_checks = tr.bucketer.order_checks
+        try:
+            tr.bucketer._compare_order([0, 1] if rank == 0 else [1, 0])
+            flagged = False
+        except RuntimeError:
+            flagged = True
+        torch.save({"checks": ok_checks, "order": tr.bucketer.last_order, "flagged": flagged},
+                   os.path.join(out, f"order{rank}.pt"))
         zdist.shutdown()
         sys.exit(0)
     tr = train(rank, world, bucket_mb=0.001)

@@ -177,68 +177,6 @@ def test_igemm_wgrad_matches_reference(variant, cin, cout, stride, hw, pad_ones,
     assert err <= 1e-4 * ref.abs().max().item() + 1e-3, err
 
 
-@pytest.mark.parametrize("slab", [False, True])
-@pytest.mark.parametrize("variant,cin,cout,stride,hw,pad_ones",
-                         ts.pairs(ts.wgrad_ok, ts.WGRAD_F4, WGRAD_SHAPES) +
-                         [(-1, *s) for s in WGRAD_SHAPES])
-def test_igemm_wgrad_f4_matches_reference(variant, cin, cout, stride, hw, pad_ones, slab):
-    """Weight gradient on the e2m1 sign image (zk_igemm_wgrad_f4: nibble rows
-    loaded to registers and expanded to bf16 +-1 in the LDS fill, zero / +1
-    padding), every tile variant and the tuned default, vs the fp64 ±1 conv
-    weight gradient; and bit-identical to the bf16-image kernel of the same
-    tile where one exists (same products, same order)."""
-    from zookeeper_amd.nn.layers import pad_same_nhwc, same_padding
-    from zookeeper_amd.nn.quantizers import sign_pm1
-    from zookeeper_amd.ops._native import lib, stream_ptr
-
-    torch.manual_seed(3)
-    L, st = lib(), stream_ptr()
-    B = 3
-    x = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
-    w = torch.empty(cout, 3, 3, cin, device="cuda").uniform_(-1.2, 1.2)
-    pt, pb = same_padding(hw, 3, stride)
-    ho = (hw + pt + pb - 3) // stride + 1
-    dy = torch.randn(B, ho, ho, cout, device="cuda").to(torch.bfloat16)
-    nwords = x.numel() // 32
-    bits = torch.empty(nwords, dtype=torch.int32, device="cuda")
-    sx4 = torch.empty(B, hw, hw, cin // 2, dtype=torch.uint8, device="cuda")
-    assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), None, None, sx4.data_ptr(), nwords, 1.0,
-                          st) == 0
-    dw = torch.full((cout, 3, 3, cin), 0.25, device="cuda")
-    ws = None
-    if slab:
-        nbytes = L.zk_igemm_wgrad_f4_ws_bytes(B, cin, hw, hw, ho, ho, cout, 3, 3, stride, pt, pt,
-                                              256, variant)
-        assert nbytes > 0, f"variant {variant} rejected a supported shape"
-        ws = torch.empty(nbytes // 4, device="cuda")
-    rc = L.zk_igemm_wgrad_f4(dy.data_ptr(), sx4.data_ptr(), w.data_ptr(), dw.data_ptr(), B, hw,
-                             hw, cin, ho, ho, cout, 3, 3, stride, pt, pt, pad_ones, 1.0, 256,
-                             variant, ws.data_ptr() if ws is not None else None,
-                             ws.numel() * 4 if ws is not None else 0, st)
-    assert rc == 0, f"variant {variant} rejected a supported shape"
-    torch.cuda.synchronize()
-    xs = sign_pm1(x.double()).permute(0, 3, 1, 2)
-    wsgn = sign_pm1(w.double()).permute(0, 3, 1, 2).requires_grad_(True)
-    xp = pad_same_nhwc(xs, (3, 3), (stride, stride), 1.0 if pad_ones else 0.0)
-    F.conv2d(xp, wsgn, stride=stride).backward(dy.double().permute(0, 3, 1, 2))
-    ref = wsgn.grad.permute(0, 2, 3, 1) * (w.double().abs() <= 1.0) + 0.25
-    err = (dw.double() - ref).abs().max().item()
-    assert err <= 1e-4 * ref.abs().max().item() + 1e-3, err
-    if slab and variant - 100 in ts.WGRAD and ts.wgrad_ok(variant - 100, cin, cout, stride):
-        sx = torch.empty_like(x)
-        assert L.zk_sign_pack(x.data_ptr(), bits.data_ptr(), None, sx.data_ptr(), None, nwords,
-                              1.0, st) == 0
-        nb = L.zk_igemm_wgrad_ws_bytes(B, cin, hw, hw, ho, ho, cout, 3, 3, stride, pt, pt, 256,
-                                       variant - 100)
-        if nb == ws.numel() * 4:  # same split plan
-            dw2 = torch.full_like(dw, 0.25)
-            assert L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w.data_ptr(), dw2.data_ptr(), B,
-                                    hw, hw, cin, ho, ho, cout, 3, 3, stride, pt, pt, pad_ones, 1.0,
-                                    256, variant - 100, ws.data_ptr(), nb, st) == 0
-            torch.cuda.synchronize()
-            assert torch.equal(dw, dw2)
-
-
 @pytest.mark.parametrize("variant,cin,cout,stride,hw,pad_ones,relu",
                          ts.pairs(ts.fwd_ok, ts.FWD, FWD_SHAPES))
 def test_igemm_fwd_matches_reference(variant, cin, cout, stride, hw, pad_ones, relu):

@@ -171,16 +171,14 @@ def test_chained_blocks_reuse_fused_quantisation():
         assert ((a - b).norm() / b.norm()).item() < 1e-3
 
 
-@pytest.mark.parametrize("path", ["generic", "row_window"])
 @pytest.mark.parametrize("second_consumer", [False, True])
-def test_fused_bn_backward_sums_match_separate_reduce(monkeypatch, second_consumer, path):
+def test_fused_bn_backward_sums_match_separate_reduce(monkeypatch, second_consumer):
     """A block whose output feeds only the next block (identity shortcut)
     gets its BN-backward sums from that block's dgrad epilogue
-    (zk_igemm_dgrad_bnsum): the generic implicit GEMM with fuse_bnsum, or the
-    row-window kernel (conv3rw.hip, 64 -> 64 stride 1), which always fuses.
-    Gradients must match the separate reduce (both off); with a second
-    consumer of the output (gradient accumulated after the dgrad) the block
-    must detect it and fall back."""
+    (zk_igemm_dgrad_bnsum): the row-window kernel (conv3rw.hip, 64 -> 64
+    stride 1), which always fuses.  Gradients must match the separate reduce
+    (dgrad_rw off); with a second consumer of the output (gradient
+    accumulated after the dgrad) the block must detect it and fall back."""
     _setup()
     from zookeeper_amd import ops
     from zookeeper_amd.ops import binary
@@ -197,8 +195,7 @@ def test_fused_bn_backward_sums_match_separate_reduce(monkeypatch, second_consum
     g = torch.randn(4, 64, 28, 28, device="cuda").to(torch.bfloat16)
     res = []
     for fuse in (True, False):
-        monkeypatch.setattr(OPTS, "fuse_bnsum", fuse and path == "generic")
-        monkeypatch.setattr(OPTS, "dgrad_rw", fuse and path == "row_window")
+        monkeypatch.setattr(OPTS, "dgrad_rw", fuse)
         bs = [copy.deepcopy(b) for b in blocks]
         xx = x.clone().requires_grad_(True)
         h = xx

@@ -24,10 +24,11 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 WORKER = os.path.join(os.path.dirname(HERE), "dp_gpu_worker.py")
 
 
-def _run(mode, out, nproc, side="1", graph="0", force="0", backend="gloo", rt=""):
+def _run(mode, out, nproc, side="1", graph="0", force="0", backend="gloo", rt="",
+         check_order="0"):
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4", ZK_TEST_SIDE=side,
                ZK_TEST_GRAPH=graph, ZK_TEST_FORCE_DP=force, ZK_TEST_BACKEND=backend,
-               ZK_TEST_RT=rt)
+               ZK_TEST_RT=rt, ZK_TEST_CHECK_ORDER=check_order)
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     if nproc == 1:
@@ -44,15 +45,31 @@ def _gpu():
         pytest.skip("needs a GPU")
 
 
+# Default mode (fp32 split-K atomics in the conv weight gradients; every
+# BN-backward sum fixed-order): stated run-to-run tolerance of the parameters
+# after the worker's SGD steps, relative L2.
+DEFAULT_MODE_REL = 1e-4
+
+
+def _close(a, b, exact):
+    if exact:
+        torch.testing.assert_close(a, b, atol=0, rtol=0)
+    else:
+        rel = ((a - b).norm() / b.norm()).item()
+        assert rel < DEFAULT_MODE_REL, rel
+
+
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["deterministic", "default"])
 @pytest.mark.parametrize("side,graph", [("1", "0"), ("0", "0"), ("1", "1")],
                          ids=["side-stream", "single-stream", "graph"])
-def test_two_ranks_match_single_process_on_same_data(tmp_path, side, graph):
+def test_two_ranks_match_single_process_on_same_data(tmp_path, side, graph, mode):
     """Deterministic mode: two ranks on the same batches average identical
     gradients (g + g = 2g, times 1/2, is exact in fp32), so the result must
-    equal the single-process run bit for bit (see the forced-DP test below
-    for why the non-deterministic path can only be compared after one step)."""
-    rt = "deterministic=1"
+    equal the single-process run bit for bit.  Default mode: equal up to the
+    weight gradients' atomic-ordering noise (DEFAULT_MODE_REL)."""
+    exact = mode == "deterministic"
+    rt = "deterministic=1" if exact else ""
     assert _run("same", tmp_path, 1, side, graph, rt=rt) == 0
     assert _run("same", tmp_path, 2, side, graph, rt=rt) == 0
     ref = torch.load(tmp_path / "same_w1_r0.pt", weights_only=True)
@@ -61,32 +78,40 @@ def test_two_ranks_match_single_process_on_same_data(tmp_path, side, graph):
     assert r0["buckets"] > 1
     assert r0["graph"] == (graph == "1") and ref["graph"] == (graph == "1")
     assert r0["comm_steps"] == 2  # every step's collectives were timed
-    torch.testing.assert_close(r0["params"], r1["params"], atol=0, rtol=0)
+    _close(r0["params"], r1["params"], exact)
     torch.testing.assert_close(r0["init"], ref["init"], atol=0, rtol=0)
     assert (ref["params"] - ref["init"]).norm().item() > 0
-    torch.testing.assert_close(r0["params"], ref["params"], atol=0, rtol=0)
+    _close(r0["params"], ref["params"], exact)
 
 
 @pytest.mark.timeout(300)
 def test_two_ranks_disjoint_data_stay_identical(tmp_path):
-    assert _run("split", tmp_path, 2) == 0
+    """Also the bucket-order debug check (runtime.check_bucket_order) with
+    side-stream weight gradients on: both ranks launch the same bucket
+    sequence every step, and the cross-rank comparison ran every step."""
+    assert _run("split", tmp_path, 2, side="1", check_order="1") == 0
     r0 = torch.load(tmp_path / "split_w2_r0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "split_w2_r1.pt", weights_only=True)
     torch.testing.assert_close(r0["params"], r1["params"], atol=0, rtol=0)
     assert r0["loss"] == r0["loss"] and r1["loss"] == r1["loss"]  # finite
+    assert r0["order_checks"] == r1["order_checks"] == 2
+    assert r0["last_order"] == r1["last_order"]
+    assert sorted(r0["last_order"]) == list(range(r0["buckets"]))
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["deterministic", "default"])
 @pytest.mark.parametrize("side,graph", [("1", "0"), ("0", "0"), ("1", "1")],
                          ids=["side-stream", "single-stream", "graph"])
-def test_rccl_single_rank_forced_dp_matches_plain_run(tmp_path, side, graph):
+def test_rccl_single_rank_forced_dp_matches_plain_run(tmp_path, side, graph, mode):
     """Deterministic mode (``runtime.deterministic``: no float atomics on the
     gradient path): the forced 1-rank RCCL run must equal the plain run BIT
-    FOR BIT.  (Outside it, fp32-atomics noise in the near-cancelling stem
-    BN-1 gradient -- ~1e-3 relative after one step -- is amplified by the
-    binary activations of step 2 into O(1) differences between ANY two runs,
-    DP or not: tools/dp_single_diag.py, profiles/r3/g_dp_forced_diag.md.)"""
-    rt = "deterministic=1"
+    FOR BIT.  Default mode: within DEFAULT_MODE_REL (round 3's default mode
+    used fp32 atomics in the BN-backward sums, whose noise the binary blocks
+    amplified into O(1) differences between any two runs after two steps:
+    profiles/r3/g_dp_forced_diag.md; those sums are fixed-order now)."""
+    exact = mode == "deterministic"
+    rt = "deterministic=1" if exact else ""
     assert _run("same", tmp_path, 1, side, graph, rt=rt) == 0
     assert _run("same", tmp_path, 1, side, graph, force="1", backend="nccl", rt=rt) == 0
     ref = torch.load(tmp_path / "same_w1_r0.pt", weights_only=True)
@@ -101,4 +126,4 @@ def test_rccl_single_rank_forced_dp_matches_plain_run(tmp_path, side, graph):
     torch.testing.assert_close(dp["init"], ref["init"], atol=0, rtol=0)
     assert (ref["params"] - ref["init"]).norm().item() > 0
     # a 1-rank all-reduce is the identity and nothing else differs
-    torch.testing.assert_close(dp["params"], ref["params"], atol=0, rtol=0)
+    _close(dp["params"], ref["params"], exact)

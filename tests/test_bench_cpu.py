@@ -74,11 +74,11 @@ def test_bench_single_rank_json_contract():
 def test_bench_force_dp_single_rank_runs_the_bucketer():
     """``--force-dp``: one rank, but the bucketed all-reduce path is on (a
     1-rank process group; gloo here, RCCL on a GPU)."""
-    res = subprocess.run([sys.executable, BENCH, *ARGS, "--force-dp", "--rt", "korder=0"],
+    res = subprocess.run([sys.executable, BENCH, *ARGS, "--force-dp", "--rt", "tile_huge=0"],
                          env=_env(), capture_output=True, text=True, timeout=180, cwd=ROOT)
     assert res.returncode == 0, res.stderr[-3000:]
     (rec,) = _json_lines(res.stdout)
     assert rec["n_gpus"] == 1
     assert rec["config"]["buckets"] >= 1
     assert rec["config"]["runtime"]["force_dp"] is True
-    assert rec["config"]["runtime"]["korder"] == 0
+    assert rec["config"]["runtime"]["tile_huge"] == 0

@@ -90,3 +90,33 @@ def test_download_false_refuses_to_fetch(tmp_path, capsys):
         ds.train()
     err = capsys.readouterr().err
     assert "WARNING: Field 'download' of component TinyHF is False." in err
+
+
+def test_mixed_gray_and_rgb_images_decode_to_one_channel_layout(tmp_path):
+    """Encoded images decoded on the pool (``Image`` feature): a dataset that
+    starts with an RGB image decodes every image -- grayscale ones too -- to
+    H x W x 3, whatever the order of the batch (the batch buffer
+    used to take its shape from whichever image came first)."""
+    from PIL import Image
+
+    rng = np.random.default_rng(1)
+    imgs = []
+    for k in range(6):
+        a = rng.integers(0, 255, (6, 5, 3), dtype=np.uint8)
+        im = Image.fromarray(a, "RGB")
+        imgs.append(im if k % 2 == 0 else im.convert("L"))
+    feats = datasets.Features({"image": datasets.Image(),
+                               "label": datasets.ClassLabel(num_classes=2)})
+    d = datasets.Dataset.from_dict({"image": imgs, "label": [k % 2 for k in range(6)]},
+                                   features=feats)
+    datasets.DatasetDict({"train": d}).save_to_disk(str(tmp_path / "mixed"))
+    ds = TinyHF()
+    configure(ds, {"name": "mixed", "data_dir": str(tmp_path), "train_split": "train",
+                   "validation_split": None, "decode_threads": 4})
+    src, _ = ds.train()
+    for order in ([0, 1, 2, 3], [1, 0, 3, 2], [5, 3, 1]):
+        b = src.get_batch(np.array(order))
+        assert b["image"].shape == (len(order), 6, 5, 3)
+        for j, k in enumerate(order):
+            ref = np.asarray(imgs[k].convert("RGB"))
+            assert np.array_equal(b["image"][j], ref)

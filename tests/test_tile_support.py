@@ -57,17 +57,6 @@ def test_wgrad_rule_matches_native(lib):
         assert native == ts.wgrad_ok(v, cin, cout, s), (v, cin, cout, s, hw)
 
 
-def test_wgrad_f4_rule_matches_native(lib):
-    for (cin, cout, s, hw), v in itertools.product(SHAPES, list(ts.WGRAD_F4) + [103, 31]):
-        pt, ho = _geom(cin, cout, s, hw)
-        native = lib.zk_igemm_wgrad_f4_ws_bytes(3, cin, hw, hw, ho, ho, cout, 3, 3, s, pt, pt,
-                                                256, v) >= 0
-        assert native == ts.wgrad_ok(v, cin, cout, s), (v, cin, cout, s, hw)
-        # the bf16-image entry point never runs an e2m1 variant
-        assert lib.zk_igemm_wgrad_ws_bytes(3, cin, hw, hw, ho, ho, cout, 3, 3, s, pt, pt, 256,
-                                           v) == -1
-
-
 def test_rejected_sets_are_the_expected_ones():
     """The combinations the GPU tests no longer generate, stated by rule:
     conv3 tiles (variant >= 20) need stride 1; a tile must divide the GEMM N

@@ -22,10 +22,8 @@ DGRAD: Dict[int, Tuple[int, int, bool]] = {
     15: (256, 64, False), 16: (128, 64, False), 17: (256, 64, False),
     20: (64, 128, True), 21: (64, 64, True), 22: (64, 128, True), 23: (128, 64, True),
     24: (128, 64, True), 25: (256, 64, True), 26: (128, 64, True), 27: (64, 64, True),
-    28: (64, 32, True), 29: (64, 32, True), 30: (64, 32, True), 31: (64, 64, True),
+    28: (64, 32, True), 29: (64, 32, True), 30: (64, 32, True),
     32: (64, 64, True), 33: (128, 32, True), 34: (128, 32, True),
-    35: (64, 64, True), 36: (64, 64, True), 37: (128, 64, True), 38: (64, 32, True),
-    39: (64, 64, True),
     # row-window kernel (conv3rw.hip): 64 -> 64 only, stride 1
     50: (64, 64, True),
     # LDS-staged (coalesced) epilogue variants
@@ -55,19 +53,6 @@ WGRAD: Dict[int, Tuple[int, int, bool]] = {
     24: (64, 128, True), 25: (64, 64, True), 26: (128, 128, True), 27: (64, 64, True),
     28: (128, 64, True), 29: (64, 64, True), 30: (64, 64, True), 32: (128, 64, True),
     33: (64, 64, True), 34: (128, 64, True),
-    # row-window kernel (conv3rw.hip): Cin = Cout in {64, 128, 256, 512}, stride 1
-    51: (64, 64, True),
-}
-
-# wgrad on the e2m1 sign image (zk_igemm_wgrad_f4): variant -> same tuple;
-# the tile of variant v - 100 (or its >= 3-stage form).
-WGRAD_F4: Dict[int, Tuple[int, int, bool]] = {
-    101: (128, 128, False), 102: (128, 192, False), 104: (128, 128, False), 107: (64, 64, False),
-    108: (256, 256, False), 109: (256, 256, False), 110: (256, 128, False), 111: (128, 128, False),
-    114: (128, 128, False), 118: (256, 256, False),
-    120: (64, 64, True), 121: (64, 64, True), 122: (128, 64, True), 123: (128, 64, True),
-    125: (64, 64, True),
-    126: (128, 128, True), 127: (64, 64, True), 128: (128, 64, True), 132: (128, 64, True),
 }
 
 
@@ -102,14 +87,9 @@ def fwd_ok(v: int, cin: int, cout: int, stride: int) -> bool:
 
 
 def wgrad_ok(v: int, cin: int, cout: int, stride: int) -> bool:
-    table = WGRAD_F4 if v >= 100 else WGRAD
-    if v not in table:
+    if v not in WGRAD:
         return False
-    bm, bn, c3 = table[v]
-    if v == 51:
-        return stride == 1 and cin == cout and cin in (64, 128, 256, 512)
-    if v >= 100 and cin % 32:
-        return False
+    bm, bn, c3 = WGRAD[v]
     if c3:
         return conv3_ok(stride) and cout % bm == 0 and cin % bn == 0
     return cout % bm == 0 and (9 * cin) % bn == 0 and cin % 8 == 0

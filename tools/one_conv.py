@@ -91,7 +91,7 @@ def run_one(args, shape: str) -> None:
     us = (time.perf_counter() - t0) / args.reps * 1e6
     flops = 2.0 * B * Ho * Ho * cout * 9 * cin
     print(f"{args.op} {shape} b{B} v{args.variant}: {us:.1f} us/call "
-          f"({flops / us / 1e9:.3f} PF/s) korder={__import__('zookeeper_amd.ops.options', fromlist=['OPTS']).OPTS.korder}",
+          f"({flops / us / 1e9:.3f} PF/s)",
           flush=True)
 
 

@@ -180,18 +180,12 @@ def main():
                     torch.cuda.synchronize()
                     ref_dw = dw.clone()
         igw = [int(v) for v in args.igw.split(",")] if args.igw else IGW_VARIANTS
-        if "igw" in fam and any(v >= 100 for v in igw):
-            # e2m1 sign image for the F4B variants (zk_igemm_wgrad_f4)
-            sx4w = torch.empty(B, H, W, cin // 2, dtype=torch.uint8, device="cuda")
-            L.zk_sign_pack(x.data_ptr(), None, None, None, sx4w.data_ptr(), nwords, 1.0, st)
         for v in (igw if "igw" in fam else ()):
-            f4 = v >= 100
-            fn = L.zk_igemm_wgrad_f4 if f4 else L.zk_igemm_wgrad
-            sxp = sx4w.data_ptr() if f4 else sx.data_ptr()
+            fn = L.zk_igemm_wgrad
+            sxp = sx.data_ptr()
             for tb in [int(t) for t in args.tbs.split(",")]:
                 dw.zero_()
-                nb = (L.zk_igemm_wgrad_f4_ws_bytes if f4 else L.zk_igemm_wgrad_ws_bytes)(
-                    B, cin, H, W, Ho, Ho, cout, 3, 3, s, pt, pt, tb, v)
+                nb = L.zk_igemm_wgrad_ws_bytes(B, cin, H, W, Ho, Ho, cout, 3, 3, s, pt, pt, tb, v)
                 wsb = torch.empty(max(nb, 4) // 4, device="cuda") if args.slab else None
                 wsp = wsb.data_ptr() if wsb is not None else None
                 wsn = wsb.numel() * 4 if wsb is not None else 0

@@ -96,7 +96,7 @@ def main():
     dw = torch.zeros(Cout, K, K, Cin, device="cuda")
     for tb in (256, 512, 1024, 2048):
         row[f"wgrad_tb{tb}_us"] = timeit(lambda: L.zk_stem_wgrad(
-            dy1.data_ptr(), xp.data_ptr(), dw.data_ptr(), B, Cin, Cout, K, K, s, Ho, Wo, Hp, Wp,
+            dy1.data_ptr(), xp.data_ptr(), dw.data_ptr(), None, B, Cin, Cout, K, K, s, Ho, Wo, Hp, Wp,
             tb, st), args.reps)
     # library reference: conv fwd + wgrad on the same shapes
     xn = x.permute(0, 3, 1, 2)

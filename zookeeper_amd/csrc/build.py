@@ -6,8 +6,14 @@
   (device + host code, wave64 CDNA4 only);
 * ``runtime/*.cpp`` are host-only C++17 (compiled by hipcc too, so one
   toolchain links everything);
-* objects are cached under ``build/zkamd/`` and rebuilt when the source or
-  any header is newer; compilation runs in parallel;
+* objects are cached under ``build/zkamd/`` and rebuilt when the CONTENT of
+  the source, any header or the compile command changes (a sha256 key next
+  to each object; modification times are not trusted -- a copied tree keeps
+  stale mtimes); compilation runs in parallel;
+* the library embeds ``source_digest()`` -- a sha256 over every kernel /
+  runtime source and header -- as ``const char* zk_build_digest()``; the
+  loader (``ops/_native.py``) refuses a library whose digest differs from
+  the tree it sits in;
 * the library links against ``libamdhip64.so.7`` — loaded after ``import
   torch`` it binds to torch's already-loaded HIP runtime (same SONAME).
 
@@ -20,12 +26,13 @@ from __future__ import annotations
 
 import argparse
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
-from typing import List
+from typing import List, Optional
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
@@ -57,39 +64,90 @@ def _obj_path(src: str) -> str:
     return os.path.join(OBJ_DIR, rel + ".o")
 
 
-def _stale(target: str, deps: List[str]) -> bool:
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
+def _hash_files(paths: List[str], h: Optional["hashlib._Hash"] = None) -> "hashlib._Hash":
+    h = h or hashlib.sha256()
+    for p in sorted(paths, key=lambda q: os.path.relpath(q, HERE)):
+        h.update(os.path.relpath(p, HERE).replace(os.sep, "/").encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h
 
 
-def compile_one(src: str, extra: List[str]) -> str:
-    obj = _obj_path(src)
-    if not _stale(obj, [src] + headers()):
-        return obj
-    os.makedirs(OBJ_DIR, exist_ok=True)
+def source_digest() -> Optional[str]:
+    """sha256 over the kernel / runtime sources and headers (None: no sources,
+    e.g. an installed package without ``csrc``)."""
+    files = sources() + headers()
+    if not files:
+        return None
+    return _hash_files(files).hexdigest()
+
+
+def _key_ok(path: str, key: str) -> bool:
+    try:
+        with open(path + ".key") as f:
+            return f.read() == key and os.path.exists(path)
+    except OSError:
+        return False
+
+
+def _write_key(path: str, key: str) -> None:
+    with open(path + ".key", "w") as f:
+        f.write(key)
+
+
+def _compile_cmd(src: str, obj: str, extra: List[str]) -> List[str]:
     cmd = [hipcc(), "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
            "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
     if src.endswith(".hip"):
         cmd += [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
     else:
         cmd += ["-x", "c++"]
-    cmd += extra + ["-c", src, "-o", obj]
+    return cmd + extra + ["-c", src, "-o", obj]
+
+
+def compile_one(src: str, extra: List[str], hdr_digest: str = "") -> str:
+    obj = _obj_path(src)
+    cmd = _compile_cmd(src, obj, extra)
+    key = _hash_files([src], hashlib.sha256(("\0".join(cmd[1:]) + hdr_digest).encode())).hexdigest()
+    if _key_ok(obj, key):
+        return obj
+    os.makedirs(OBJ_DIR, exist_ok=True)
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+    _write_key(obj, key)
     return obj
+
+
+def _digest_object(digest: str) -> str:
+    """A host object exporting ``zk_build_digest`` (the only generated source)."""
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    src = os.path.join(OBJ_DIR, "build_digest.cpp")
+    text = ('extern "C" __attribute__((visibility("default"))) const char* zk_build_digest() '
+            f'{{ return "{digest}"; }}\n')
+    old = None
+    if os.path.exists(src):
+        with open(src) as f:
+            old = f.read()
+    if old != text:
+        with open(src, "w") as f:
+            f.write(text)
+    return compile_one(src, [])
 
 
 def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
     srcs = sources()
     if force:
         shutil.rmtree(OBJ_DIR, ignore_errors=True)
+    digest = source_digest()
+    hdr = _hash_files(headers()).hexdigest()
     jobs = jobs or min(8, os.cpu_count() or 4)
     with ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: compile_one(s, []), srcs))
-    if _stale(OUT, objs) or force:
+        objs = list(ex.map(lambda s: compile_one(s, [], hdr), srcs))
+    objs.append(_digest_object(digest))
+    link_key = _hash_files(objs).hexdigest()
+    if force or not _key_ok(OUT, link_key):
         tmp = OUT + ".tmp"
         cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp, *objs,
                "-lpthread"]
@@ -97,8 +155,10 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
         if res.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
         os.replace(tmp, OUT)
+        _write_key(OUT, link_key)
     if verbose:
-        print(f"[zkamd] built {OUT} from {len(srcs)} sources", file=sys.stderr)
+        print(f"[zkamd] built {OUT} from {len(srcs)} sources (digest {digest[:16]})",
+              file=sys.stderr)
     return OUT
 
 

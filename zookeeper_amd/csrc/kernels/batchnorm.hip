@@ -127,32 +127,6 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const int16_t* __restrict
   }
 }
 
-// Optional in-launch finish of the BN-backward reduction (zk_bn_bwd_reduce_coef):
-// the last block to arrive computes bn_bwd_coef's outputs, so the small coef
-// kernel -- which on a busy chip waits for a free CU slot behind the
-// side-stream weight gradients (~45 us per call in the E18 step) -- drops out
-// of the data-gradient chain.
-struct CoefTail {
-  unsigned int* counter;  // zero on entry; the last block resets it (nullptr: no tail)
-  const float* gamma;
-  double P;
-  float* coef;    // [3][C]
-  float* dgamma;  // += sum g*yhat (optional)
-  float* dbeta;   // += sum g (optional)
-};
-
-// bn_bwd_coef_kernel's arithmetic for one channel from its summed statistics
-__device__ __forceinline__ void bn_coef_one(int c, int C, float sg, float sgy, float mean_c,
-                                            float rs, const CoefTail& t) {
-  const float k1 = (t.gamma ? t.gamma[c] : 1.f) * rs;
-  const float k3 = k1 * rs * (float)(sgy / t.P);
-  t.coef[c] = k1;
-  t.coef[C + c] = k3 * mean_c - k1 * (float)(sg / t.P);
-  t.coef[2 * C + c] = k3;
-  if (t.dgamma) t.dgamma[c] += sgy;
-  if (t.dbeta) t.dbeta[c] += sg;
-}
-
 // sums[0][c] += sum g ; sums[1][c] += sum g*yhat  (g bf16, y int16)
 template <int CG>  // channel groups of 8 per row = C / 8
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g,
@@ -160,8 +134,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
                                                             float* __restrict__ sums,
-                                                            long long P, int stripes,
-                                                            CoefTail tail) {
+                                                            long long P, int stripes) {
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;  // rows per block iteration
   const int cg = threadIdx.x % CG;
@@ -230,38 +203,6 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       atomicAdd(out + C + c, b);
     }
   }
-  if (tail.counter == nullptr || own) return;
-  // last-arriving block (cdna_hip_programming.md, in-launch split-K recipe):
-  // atomics done -> agent release -> ticket; the last ticket acquires, sums
-  // the stripes, writes the coefficients and re-zeroes stripes and counter
-  __shared__ int is_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned int t =
-        __hip_atomic_fetch_add(tail.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = t == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!is_last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float sg = 0.f, sgy = 0.f;
-    for (int j = 0; j < stripes; ++j) {
-      sg += sums[(2LL * j) * C + c];
-      sgy += sums[(2LL * j + 1) * C + c];
-      sums[(2LL * j) * C + c] = 0.f;
-      sums[(2LL * j + 1) * C + c] = 0.f;
-    }
-    bn_coef_one(c, C, sg, sgy, mean[c], rstd[c], tail);
-  }
-  if (threadIdx.x == 0) *tail.counter = 0u;
 }
 
 // dy = k1[c]*g + k0[c] - k3[c]*y   [times 1{y>0} if relu], with the folded
@@ -458,8 +399,7 @@ ZK_EXPORT int zk_bn_bwd_reduce_blocks() { return 512; }
 
 namespace {
 int bn_bwd_reduce_launch(const void* g, const void* y, const void* mean, const void* rstd,
-                         void* sums, long long P, int C, int stripes, const CoefTail& tail,
-                         hipStream_t stream) {
+                         void* sums, long long P, int C, int stripes, hipStream_t stream) {
   if (stripes < 1) stripes = 1;
   // 512 blocks x 4 rows in flight per thread: enough bytes in flight for
   // HBM, few enough per-block atomics into the 2*C sums.  stripes >= 512:
@@ -469,7 +409,7 @@ int bn_bwd_reduce_launch(const void* g, const void* y, const void* mean, const v
   case cg:                                                                                \
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<cg>, dim3(blocks), dim3(256), 0, stream,      \
                        (const uint16_t*)g, (const int16_t*)y, (const float*)mean,         \
-                       (const float*)rstd, (float*)sums, P, stripes, tail);               \
+                       (const float*)rstd, (float*)sums, P, stripes);                     \
     break;
   switch (C / 8) {
     ZK_RED_CASE(4)
@@ -488,23 +428,7 @@ int bn_bwd_reduce_launch(const void* g, const void* y, const void* mean, const v
 
 ZK_EXPORT int zk_bn_bwd_reduce(const void* g, const void* y, const void* mean, const void* rstd,
                                void* sums, long long P, int C, int stripes, hipStream_t stream) {
-  return bn_bwd_reduce_launch(g, y, mean, rstd, sums, P, C, stripes,
-                              CoefTail{nullptr, nullptr, 1.0, nullptr, nullptr, nullptr}, stream);
-}
-
-// zk_bn_bwd_reduce + zk_bn_bwd_coef in one launch (striped atomics only:
-// stripes < zk_bn_bwd_reduce_blocks()).  counter: one zeroed uint32 per layer
-// (persistent; the last block resets it).  Same outputs as the pair, up to
-// the summation order of the stripes.
-ZK_EXPORT int zk_bn_bwd_reduce_coef(const void* g, const void* y, const void* mean,
-                                    const void* rstd, void* sums, long long P, int C, int stripes,
-                                    void* counter, const void* gamma, void* coef, void* dgamma,
-                                    void* dbeta, hipStream_t stream) {
-  if (!counter || !coef || stripes >= zk_bn_bwd_reduce_blocks()) return (int)hipErrorInvalidValue;
-  return bn_bwd_reduce_launch(g, y, mean, rstd, sums, P, C, stripes,
-                              CoefTail{(unsigned int*)counter, (const float*)gamma, (double)P,
-                                       (float*)coef, (float*)dgamma, (float*)dbeta},
-                              stream);
+  return bn_bwd_reduce_launch(g, y, mean, rstd, sums, P, C, stripes, stream);
 }
 
 ZK_EXPORT int zk_bn_bwd_dx(const void* g, const void* y, const void* coef, void* dy, long long P,

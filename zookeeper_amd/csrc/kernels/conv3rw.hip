@@ -321,7 +321,32 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
         s1[e] += __shfl_xor(s1[e], off, 64);
         s2[e] += __shfl_xor(s2[e], off, 64);
       }
-    if (r16 == 0) {
+    if (a.stripes >= (int)gridDim.x) {
+      // one copy per block (plain stores; zk_bn_bwd_coef sums the copies in
+      // a fixed order): the 4 waves sharing a channel half combine through
+      // LDS in wave order -- run-to-run bit-reproducible
+      __syncthreads();  // every wave is past its last ring / weight read
+      float* red = reinterpret_cast<float*>(smem);  // [wave][2][32]
+      if (r16 == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[(wave * 2 + 0) * 32 + kq * 8 + e] = s1[e];
+          red[(wave * 2 + 1) * 32 + kq * 8 + e] = s2[e];
+        }
+      }
+      __syncthreads();
+      if (wave == 0) {
+        float* ps = a.psums + (long long)blockIdx.x * 2 * 64;
+#pragma unroll
+        for (int v = lane; v < 128; v += 64) {
+          const int which = v >> 6, c = v & 63, half = c >> 5, cc = c & 31;
+          float t = 0.f;
+#pragma unroll
+          for (int m = 0; m < RW_NW / 2; ++m) t += red[((2 * m + half) * 2 + which) * 32 + cc];
+          ps[which * 64 + c] = t;
+        }
+      }
+    } else if (r16 == 0) {
       float* ps = a.psums + (long long)(blockIdx.x % a.stripes) * 2 * 64;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -333,394 +358,10 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
   rw_drain();  // no DMA outstanding at exit
 }
 
-// ===========================================================================
-// Row-window weight gradient (variant 51 of the wgrad dispatch), same layer:
-//
-//   dW[co][kh][kw][ci] = sum_{b,h,w} dY[b][h][w][co] * S[b][h+kh-1][w+kw-1][ci]
-//
-// The conv3 implicit-GEMM wgrad (igemm.hip, variant 20) stages per K-step 32
-// dY rows plus three 34-row sign-image segments (one per kernel row): every
-// sign row is fetched three times per layer, ~1.64 GB of LDS fill for 822 MB
-// of operands, at the ~30 B/clk/CU gather rate its 576-cycle K-step needs.
-// Here:
-//   * a persistent block (one per CU, 4 waves) accumulates one 64 co x 64 ci
-//     channel tile of dW for all 9 taps -- the whole dW at C = 64 -- in
-//     registers (wave w: co block w & 1, ci block w >> 1, 9 32x32 fp32 tiles)
-//     over a contiguous range of work items (image b, group of 4 output
-//     rows), and writes its part of one fp32 slab at the end (reduced by
-//     igemm.hip's wgrad_reduce_kernel in a fixed order) or adds it with fp32
-//     atomics; C = 128 / 256 / 512 run (C/64)^2 tiles x 256/(C/64)^2 splits;
-//   * sign rows live in a 10-slot LDS ring in halo-extended layout (position
-//     p = column + 1, 72 positions: pad value at 0 and W + 1, zeros past
-//     it), dY rows of the item in a double buffer (64 positions, zeros past
-//     W); each row is fetched once per block: ~12.7 B/clk/CU per item;
-//   * K-chunk = 16 consecutive output pixels of one row: A = dY^T (32 co x 16
-//     px) and, per tap, B = the sign row h + kh - 1 at positions w0 + kw ..
-//     +15 (32 ci x 16 px), both read transposed (ds_read_b64_tr_b16) from
-//     the pixel-major rows; rows outside the image read a uniform pad block;
-//   * the next item's new sign rows + its dY rows (68-77 x 1 KB DMA pieces,
-//     also across an image boundary: ring slot = global row % 10) are issued
-//     inside the first half of the MFMA loop, a few pieces per K-chunk.
-// W <= 64 (up to four chunks per row; the last one zero-padded past W).
-// ===========================================================================
-constexpr int WW_TR = 3;                               // output rows per item
-constexpr int WW_NW = 8;                               // waves per block (2 per SIMD)
-constexpr int WW_RING = 8;                             // sign-row slots (window 5 + next 3)
-constexpr int WW_SSLOT = 72 * 128;                     // 72 slot rows x 64 ch (9 KB)
-constexpr int WW_DSLOT = 64 * 128;                     // 64 positions x 64 ch
-constexpr int WW_PAD_OFF = WW_RING * WW_SSLOT;         // all-pad slot (rows outside the image)
-constexpr int WW_DY_OFF = WW_PAD_OFF + WW_SSLOT;       // 82944
-constexpr int WW_RING_END = WW_DY_OFF + 2 * WW_TR * WW_DSLOT;  // 132096
-constexpr int WW_XCHG = 4 * 64 * 144 * 4;              // epilogue: one wave half's sums
-constexpr int WW_LDS = WW_RING_END > WW_XCHG ? WW_RING_END : WW_XCHG;  // 147456
-constexpr int WW_GRID = 256;                           // fixed: slab size is shape-only
-static_assert(WW_LDS <= 160 * 1024, "LDS");
-
-struct WWArgs {
-  const uint16_t* dy;  // [B][H][W][64]
-  const uint16_t* sx;  // sign(x) bf16 +-1 [B][H][W][64]
-  const float* w;      // weights [64][9][64] (STE mask |w| <= clip, atomic mode)
-  float* dw;           // [64][9][64] accumulated
-  float* slab;         // [splits][C][9 C] (optional)
-  int B, H, W, ngroups, ipb, pad_ones;
-  int C, nct;          // channels (Cin = Cout), 64-channel tiles per side (C / 64)
-  float clip;
-};
-
-__device__ __forceinline__ int ww_swz(int pos) { return ((pos >> 1) & 1) << 2; }  // tr_swz<128>
-
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-
-// 32x32x16 operand (8 consecutive positions of one channel) from a 128-B-row
-// [position][channel] image at `base`, with this lane's two precomputed
-// ds_read_b64_tr_b16 offsets (ww_tr_offsets).
-__device__ __forceinline__ uint4 ww_tr(const unsigned char* base, int o0, int o1) {
-  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_s16x4*)(uintptr_t)(const __attribute__((address_space(3))) void*)(base + o0));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_s16x4*)(uintptr_t)(const __attribute__((address_space(3))) void*)(base + o1));
-  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(uint4, v);
-}
-
-// tr_frag_swz<128>'s two offsets for positions k0 .. k0+15, channels c0 .. +31.
-// For k0 = 16 m + kw they are (16 m * 128) + the offsets of k0 = kw: the swizzle
-// key depends on position bit 1 only, so a lane's offsets per kw are constant.
-__device__ __forceinline__ void ww_tr_offsets(int k0, int c0, int lane, int& o0, int& o1) {
-  const int gq = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int row = k0 + 8 * (gq >> 1) + q;
-  const int colb = (c0 + 16 * (gq & 1) + 4 * p) * 2;
-  const int slot = colb >> 4, inner = colb & 15;
-  o0 = row * 128 + ((slot ^ ww_swz(row)) << 4) + inner;
-  o1 = (row + 4) * 128 + ((slot ^ ww_swz(row + 4)) << 4) + inner;
-}
-
-__global__ __launch_bounds__(WW_NW * 64) void conv3rw_wgrad_kernel(WWArgs a) {
-  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // waves w and w + 4 share one SIMD and one output tile: half 0 takes the
-  // even K-chunks of an item, half 1 the odd ones (each hides the other's
-  // LDS reads / DMA issue behind its MFMAs); summed through LDS at the end
-  const int hw = wave >> 2, wq = wave & 3;
-  const int nitems = a.B * a.ngroups;
-  // block = (pixel split, 64 x 64 channel tile); the tiles of one split are
-  // consecutive ids (same rows, other channel slices)
-  const int ntiles = a.nct * a.nct;
-  const int split = blockIdx.x / ntiles, tile = blockIdx.x - split * ntiles;
-  const int co0 = (tile % a.nct) * 64, ci0 = (tile / a.nct) * 64;
-  const int i0 = split * a.ipb;
-  const int i1 = min(nitems, i0 + a.ipb);
-  const int cb = wq & 1, nb = wq >> 1;
-  const int C2 = a.C * 2;
-  const long long rowb = (long long)a.W * C2;  // bytes per image row
-  const int K = (a.W + 7) >> 3;                // 1-KB DMA pieces per row
-  const int kpart = (a.W & 7) ? K - 1 : -1;    // the partial last piece
-
-  // Sign-row slot: row R holds image column R - 8 (R = 7: left pad, W + 8:
-  // right pad, both pre-filled; the DMA writes rows 8 .. 8K+7).  Fragment
-  // rows for output column w, tap kw: R = w + kw + 7.  dY slot: row = column.
-  // Lane-constant parts: fragment offsets (A: k0 = 0; B: k0 = kw + 7; the
-  // swizzle key is position bit 1, so chunk c adds a uniform c * 2 KB), and
-  // the DMA lane map (row 8k + pos8, chunk (lane & 7) ^ key(pos8)).
-  // (the second read of each fragment is 4 rows on: +512 B, same swizzle key)
-  int ao0, ao1, bo0[3], bo1;
-  ww_tr_offsets(0, cb * 32, lane, ao0, ao1);
-#pragma unroll
-  for (int kw = 0; kw < 3; ++kw) ww_tr_offsets(kw + 7, nb * 32, lane, bo0[kw], bo1);
-  const int pos8 = lane >> 3, chunk = (lane & 7) ^ ww_swz(pos8);
-  const int laneoff = pos8 * C2 + chunk * 16;
-  const unsigned char* dyb = reinterpret_cast<const unsigned char*>(a.dy) + co0 * 2;
-  const unsigned char* sxb = reinterpret_cast<const unsigned char*>(a.sx) + ci0 * 2;
-  const unsigned char* padsrc = reinterpret_cast<const unsigned char*>(
-      a.pad_ones ? (const void*)g_ones_page_bf16 : (const void*)g_zero_page) + chunk * 16;
-  const unsigned char* zsrc = reinterpret_cast<const unsigned char*>(g_zero_page) + chunk * 16;
-
-  // DMA piece k (0 .. K-1: columns 8k .. 8k+7) of a sign row into ring slot
-  // `slot`, of a dY row into dY buffer row `drow`.  Only the partial last
-  // piece needs per-lane selects.
-  auto sx_piece = [&](const unsigned char* row, int slot, int k) {
-    const unsigned char* src = row + k * 8 * C2 + laneoff;
-    if (k == kpart) {
-      const int col = k * 8 + pos8;
-      src = col < a.W ? src : col == a.W ? padsrc : zsrc;
-    }
-    glds16(src, smem + slot * WW_SSLOT + (k + 1) * 1024);
-  };
-  auto dy_piece = [&](const unsigned char* row, int drow, int k) {
-    const unsigned char* src = row + k * 8 * C2 + laneoff;
-    if (k == kpart && k * 8 + pos8 >= a.W) src = zsrc;
-    glds16(src, smem + WW_DY_OFF + drow * WW_DSLOT + k * 1024);
-  };
-  // A row set: nsx image sign rows from sxrow (ring slots from slot0,
-  // wrapping), then dY rows from dyrow into buffer rows from drow0.  Wave w
-  // issues pieces w, w + 4, ... (K per row, sign rows first) through a
-  // running (row, k) cursor: no divisions, no 64-bit multiplies per piece.
-  struct RowSet {
-    const unsigned char* sxrow;
-    const unsigned char* dyrow;
-    int nsx, slot0, drow0;
-  };
-  struct Cursor {
-    int row, k;
-    bool dy;
-  };
-  // carry k into rows (K may be < 4 for narrow images)
-  auto normalise = [&](const RowSet& rs, Cursor& cu) {
-    while (cu.k >= K) {
-      cu.k -= K;
-      if (++cu.row == rs.nsx && !cu.dy) {
-        cu.dy = true;
-        cu.row = 0;
-      }
-    }
-  };
-  auto cursor0 = [&](const RowSet& rs) {
-    Cursor cu{0, wave, rs.nsx == 0};
-    normalise(rs, cu);
-    return cu;
-  };
-  auto issue_next = [&](const RowSet& rs, Cursor& cu) {
-    if (!cu.dy) {
-      int sl = rs.slot0 + cu.row;
-      sl -= sl >= WW_RING ? WW_RING : 0;
-      sx_piece(rs.sxrow + (long long)cu.row * rowb, sl, cu.k);
-    } else {
-      dy_piece(rs.dyrow + (long long)cu.row * rowb, rs.drow0 + cu.row, cu.k);
-    }
-    cu.k += WW_NW;
-    normalise(rs, cu);
-  };
-  auto rowptr = [&](const unsigned char* base, int b, int hr) {
-    return base + ((long long)b * a.H + hr) * rowb;
-  };
-
-  f32x16 acc[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-
-  if (i0 < nitems) {  // block-uniform
-    {  // pre-fill: sign slots zero with pad rows 7 and W + 8, the pad slot all
-       // pad, dY buffers zero (the DMA only ever writes the image columns)
-      const uint32_t pv = a.pad_ones ? 0x3F803F80u : 0u;
-      for (int i = tid; i < WW_RING_END / 16; i += WW_NW * 64) {
-        const int byte = i * 16, row = (byte % WW_SSLOT) >> 7;
-        uint32_t v = 0u;
-        if (byte >= WW_PAD_OFF && byte < WW_DY_OFF) v = pv;
-        else if (byte < WW_PAD_OFF && (row == 7 || row == a.W + 8)) v = pv;
-        reinterpret_cast<uint4*>(smem)[i] = make_uint4(v, v, v, v);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // before the first barrier
-    }
-    const int nch = (a.W + 15) >> 4;
-    for (int it = i0; it < i1; ++it) {
-      const int b = it / a.ngroups, g = it - b * a.ngroups, h0 = g * WW_TR;
-      const int rv = min(WW_TR, a.H - h0);
-      const int dbuf = (it - i0) & 1;
-      const long long gb = (long long)b * a.H;
-      // every wave drained its own DMAs (this item's rows) at the end of the
-      // previous item: the barrier publishes them, and no wave still reads the
-      // slots the prefetch below overwrites (the previous item's)
-      __builtin_amdgcn_s_barrier();
-      if (it == i0) {
-        const int s0 = max(h0 - 1, 0), s1 = min(h0 + rv, a.H - 1);  // image rows s0 .. s1
-        const RowSet rs{rowptr(sxb, b, s0), rowptr(dyb, b, h0), s1 - s0 + 1,
-                        (int)((gb + s0) % WW_RING), dbuf * WW_TR};
-        const int np = (rs.nsx + rv) * K;
-        Cursor cu = cursor0(rs);
-        for (int q = wave; q < np; q += WW_NW) issue_next(rs, cu);
-        rw_drain();
-        __builtin_amdgcn_s_barrier();
-      }
-      // the next item's rows: its image rows not already in the ring (slot =
-      // global row b*H + hr mod 8: a same-image window adds 3, a new image's
-      // first window 4, beside at most 5 / 4 rows of this one) and its dY rows
-      RowSet nx{sxb, dyb, 0, 0, (dbuf ^ 1) * WW_TR};
-      int np = 0;
-      if (it + 1 < i1) {
-        const int bn = (it + 1) / a.ngroups;
-        const int hn = (it + 1 - bn * a.ngroups) * WW_TR;
-        const int rvn = min(WW_TR, a.H - hn);
-        int sxn = max(hn - 1, 0);
-        if (bn == b) sxn = max(sxn, h0 + rv + 1);
-        nx.nsx = max(0, min(hn + rvn, a.H - 1) - sxn + 1);
-        nx.sxrow = rowptr(sxb, bn, sxn);
-        nx.dyrow = rowptr(dyb, bn, hn);
-        nx.slot0 = (int)(((long long)bn * a.H + sxn) % WW_RING);
-        np = (nx.nsx + rvn) * K;
-      }
-      Cursor cu = cursor0(nx);
-      const int nmine = np > wave ? (np - wave + WW_NW - 1) / WW_NW : 0;  // pieces of this wave
-      const int nsteps = rv * nch;
-      const int mysteps = (nsteps - hw + 1) >> 1;  // steps hw, hw + 2, ...
-      // DMA pieces in the first half of this wave's steps (pps per step): they
-      // land while the rest computes, before the drain at the item's end
-      const int half = max(1, mysteps >> 1), pps = (nmine + half - 1) / half;
-      int issued = 0;
-      // ring slot of this window's first row (h0 - 1; + 8 keeps it >= 0)
-      const int slm1 = (int)((gb + h0 - 1 + WW_RING) % WW_RING);
-
-      // this wave's step cursor (rr, cc); the per-lane addresses of its row
-      // (A: dY row; B: the three sign rows x three taps)
-      int rr = 0, cc = hw;
-      if (cc >= nch) {
-        cc -= nch;
-        ++rr;
-      }
-      int aaddr, baddr[9];
-      auto row_addrs = [&]() {
-        aaddr = WW_DY_OFF + (dbuf * WW_TR + rr) * WW_DSLOT + ao0;
-#pragma unroll
-        for (int kh = 0; kh < 3; ++kh) {
-          const int hr = h0 + rr + kh - 1;
-          int sl = slm1 + rr + kh;
-          sl -= sl >= WW_RING ? WW_RING : 0;
-          const int base = (hr >= 0 && hr < a.H) ? sl * WW_SSLOT : WW_PAD_OFF;
-#pragma unroll
-          for (int kw = 0; kw < 3; ++kw) baddr[kh * 3 + kw] = base + bo0[kw];
-        }
-      };
-      constexpr int ad = 512;  // ww_tr_offsets: o1 = o0 + 4 rows
-      row_addrs();
-      for (int s = 0; s < mysteps; ++s) {
-        for (int j = 0; j < pps && issued < nmine; ++j, ++issued) issue_next(nx, cu);
-        const unsigned char* cp = smem + cc * 16 * 128;
-        uint4 fa, fb[9];
-        fa = ww_tr(cp + aaddr, 0, ad);
-#pragma unroll
-        for (int t = 0; t < 9; ++t) fb[t] = ww_tr(cp + baddr[t], 0, ad);
-#pragma unroll
-        for (int t = 0; t < 9; ++t) acc[t] = mfma_bf16(fa, fb[t], acc[t]);
-        // next step of this wave: two chunks on
-        cc += 2;
-        if (cc >= nch) {
-          cc -= nch;
-          ++rr;
-          if (cc >= nch) {  // nch == 1
-            cc -= nch;
-            ++rr;
-          }
-          if (s + 1 < mysteps) row_addrs();
-        }
-      }
-      for (; issued < nmine; ++issued) issue_next(nx, cu);
-      rw_drain();
-    }
-  }
-
-  // epilogue: half 1 hands its sums to half 0 through LDS (wave wq's 144 x
-  // 64 floats, lane-contiguous float4s), half 0 adds and stores.
-  // D[co][ci] of tap t; lane: ci = nb*32 + (lane & 31),
-  // co = cb*32 + (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
-  __syncthreads();  // every wave is past its last LDS read / DMA (drained)
-  float4* xg = reinterpret_cast<float4*>(smem) + wq * 36 * 64 + lane;
-  if (hw == 1) {
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        xg[(t * 4 + q) * 64] = make_float4(acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2],
-                                           acc[t][4 * q + 3]);
-  }
-  __syncthreads();
-  if (hw == 1) return;
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 v = xg[(t * 4 + q) * 64];
-      acc[t][4 * q] += v.x;
-      acc[t][4 * q + 1] += v.y;
-      acc[t][4 * q + 2] += v.z;
-      acc[t][4 * q + 3] += v.w;
-    }
-  const int ci = nb * 32 + (lane & 31);
-  const int NT = 9 * a.C;
-  float* sl = a.slab ? a.slab + (long long)split * a.C * NT : nullptr;
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = cb * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      const long long idx = (long long)(co0 + co) * NT + t * a.C + ci0 + ci;
-      if (sl)
-        sl[idx] = acc[t][r];
-      else if (i0 < nitems && fabsf(a.w[idx]) <= a.clip)
-        atomicAdd(a.dw + idx, acc[t][r]);
-    }
-}
-
 int g_num_cus = 0;
 int g_lds_attr = 0;
-bool g_ww_attr = false;
 
 }  // namespace
-
-// Entry used by igemm.hip's wgrad dispatch (variant 51).  Stride-1 'same'
-// 3x3, Cin = Cout = C in {64, 128, 256, 512}, 1 <= W <= 64.  The grid is
-// fixed by the shape (256 blocks: (C/64)^2 channel tiles x pixel splits), so
-// the slab size is too.  slab (optional): [splits][C][9 C] fp32 partial sums
-// (the caller reduces them); otherwise fp32 atomics with the STE mask.
-// need (non-null): slab bytes only.  *splits: slab count (0: atomics).
-int zk_conv3rw_wgrad_impl(const void* dy, const void* sx, const void* w, void* dw, int B, int H,
-                          int W, int Cin, int Cout, int pad_ones, float clip, void* slab,
-                          long long slab_bytes, long long* need, int* splits, bool dry,
-                          hipStream_t st) {
-  if (Cin != Cout || (Cin != 64 && Cin != 128 && Cin != 256 && Cin != 512) || W < 1 || W > 63 ||
-      H < 1 || B < 1)
-    return (int)hipErrorInvalidValue;
-  if ((long long)B * H * W * Cin >= (1LL << 40)) return (int)hipErrorInvalidValue;
-  const int nct = Cin / 64, ntiles = nct * nct;
-  const int ngroups = (H + WW_TR - 1) / WW_TR;
-  const int nitems = B * ngroups;
-  const int nsplit0 = WW_GRID / ntiles;
-  const int ipb = (nitems + nsplit0 - 1) / nsplit0;
-  const int nsplit = (nitems + ipb - 1) / ipb;
-  const long long sb = (long long)nsplit * Cin * 9 * Cin * 4;
-  if (need) {
-    *need = sb;
-    return 0;
-  }
-  if (slab && slab_bytes < sb) slab = nullptr;
-  if (splits) *splits = slab ? nsplit : 0;
-  if (dry) return 0;
-  if (!g_ww_attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv3rw_wgrad_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, WW_LDS);
-    if (e != hipSuccess) return (int)e;
-    g_ww_attr = true;
-  }
-  WWArgs a{(const uint16_t*)dy, (const uint16_t*)sx, (const float*)w, (float*)dw, (float*)slab,
-           B, H, W, ngroups, ipb, pad_ones, Cin, nct, clip};
-  const int grid = nsplit * ntiles;
-  (void)hipGetLastError();
-  hipLaunchKernelGGL(conv3rw_wgrad_kernel, dim3((unsigned)grid), dim3(WW_NW * 64), WW_LDS, st, a);
-  return (int)hipGetLastError();
-}
 
 // Entry used by igemm.hip's dgrad dispatch (variant 50).  Stride-1 'same'
 // 3x3, Cin = Cout = 64, 1 <= W <= 64; psums (optional): the predecessor's

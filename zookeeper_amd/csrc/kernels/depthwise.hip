@@ -136,7 +136,8 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const uint16_t* __restric
 template <int K>
 __global__ __launch_bounds__(256) void dw_wgrad_kernel(const uint16_t* __restrict__ dy,
                                                        const uint16_t* __restrict__ x,
-                                                       float* __restrict__ dw, int B, int H,
+                                                       float* __restrict__ dw,
+                                                       float* __restrict__ slab, int B, int H,
                                                        int W, int C, int Ho, int Wo, int s,
                                                        int pt, int pl) {
   constexpr int KK = K * K;
@@ -181,7 +182,10 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const uint16_t* __restric
       const int g = c / 8, k = c % 8;
       float sum = 0.f;
       for (int r = 0; r < R; ++r) sum += red[r * CG + g][k];
-      atomicAdd(dw + (long long)c * KK + t, sum);
+      if (slab)  // deterministic mode: per-block partials, fixed-order reduce
+        slab[(long long)blockIdx.x * C * KK + (long long)c * KK + t] = sum;
+      else
+        atomicAdd(dw + (long long)c * KK + t, sum);
     }
     __syncthreads();
   }
@@ -209,17 +213,27 @@ ZK_EXPORT int zk_dw_dgrad(const void* dy, const float* w, void* dx, int B, int H
   return 0;
 }
 
-ZK_EXPORT int zk_dw_wgrad(const void* dy, const void* x, float* dw, int B, int H, int W, int C,
-                          int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st) {
+// Blocks of zk_dw_wgrad (the slab of the deterministic mode is [blocks][C*9]).
+ZK_EXPORT int zk_dw_wgrad_blocks(int B, int Ho, int Wo, int C) {
   const int CG = C / 8;
-  if (C % 8 || k != 3 || CG > 256 || 256 % CG) return (int)hipErrorInvalidValue;
+  if (C % 8 || CG > 256 || 256 % CG) return -1;
   const int R = 256 / CG;
   const long long P = (long long)B * Ho * Wo;
   long long blocks = (P + R - 1) / R;
-  if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(dw_wgrad_kernel<3>, dim3((int)blocks), dim3(256), 0, st,
-                     (const uint16_t*)dy, (const uint16_t*)x, dw, B, H, W, C, Ho, Wo, s, pt,
-                     pl);
+  return (int)(blocks > 1024 ? 1024 : blocks);
+}
+
+// dw [C][9] += per-channel 3x3 weight gradient; fp32 atomics, or with slab
+// (deterministic mode) per-block partials summed by zk_wgrad_slab_reduce.
+ZK_EXPORT int zk_dw_wgrad(const void* dy, const void* x, float* dw, void* slab, int B, int H,
+                          int W, int C, int Ho, int Wo, int k, int s, int pt, int pl,
+                          hipStream_t st) {
+  const int CG = C / 8;
+  if (C % 8 || k != 3 || CG > 256 || 256 % CG) return (int)hipErrorInvalidValue;
+  const int blocks = zk_dw_wgrad_blocks(B, Ho, Wo, C);
+  hipLaunchKernelGGL(dw_wgrad_kernel<3>, dim3(blocks), dim3(256), 0, st,
+                     (const uint16_t*)dy, (const uint16_t*)x, dw, (float*)slab, B, H, W, C, Ho,
+                     Wo, s, pt, pl);
   ZK_CHECK_LAUNCH();
   return 0;
 }

@@ -28,12 +28,6 @@
 //   * XCD-aware tile order: consecutive M tiles of one N tile share an XCD.
 #include "mfma_common.h"
 
-// conv3rw.hip: row-window wgrad of the 64 -> 64 stride-1 3x3 conv (variant 51)
-int zk_conv3rw_wgrad_impl(const void* dy, const void* sx, const void* w, void* dw, int B, int H,
-                          int W, int Cin, int Cout, int pad_ones, float clip, void* slab,
-                          long long slab_bytes, long long* need, int* splits, bool dry,
-                          hipStream_t st);
-
 namespace {
 
 // Support queries (zk_igemm_*_supported): every launcher validates the
@@ -74,10 +68,6 @@ struct ConvArgs {
   const float* pmean;
   const float* prstd;
   float* psums;
-  // K-step order: 0 = tap-major (all channel chunks of a tap, then the next
-  // tap), 1 = channel-chunk-major (all taps of a chunk): the shifted
-  // activation rows of the taps are re-read while still in L2.
-  int korder;
   // float forward through the LDS epilogue (a 1x1 conv as this GEMM, optional):
   // the next BatchNorm's statistics of the stored bf16 outputs,
   // fstats[stripe][0][c] += sum y, [1][c] += sum y^2 (fp64, stripe = block % stripes)
@@ -94,18 +84,13 @@ struct ConvArgs {
 //     step, where those kernels overlap the data-gradient chain on the side
 //     stream (bench A/B, 40 steps each: none 43.7k, 1 43.5k, 2 43.5k, 4 43.6k,
 //     8 43.3k, 16 43.8k img/s).
-//   korder (key 1): K-step order, see ConvArgs::korder.
 //   deterministic (key 2): split-K weight gradients through slabs reduced in
 //     a fixed order (no float atomics).
 //   dgrad_rw (key 3): the row-window kernel (conv3rw.hip, variant 50) for the
 //     64 -> 64 stride-1 3x3 data gradient by default.
-//   wgrad_rw (key 4): the row-window kernel (conv3rw.hip, variant 51) for the
-//     64 -> 64 stride-1 3x3 weight gradient by default.
 int g_opt_tile_huge = 16;
-int g_opt_korder = 0;
 int g_opt_deterministic = 0;
 int g_opt_dgrad_rw = 1;
-int g_opt_wgrad_rw = 0;
 // wgrad_slab_mb (key 5): cap on the split-K slab bytes of one weight gradient
 // (splits <= cap / |dW|); 0 = no cap (splits from the block target alone).
 // Default 32 MB (ops/options.py has the measurements).
@@ -120,8 +105,6 @@ inline long long cap_splits(long long splits, long long dw_bytes) {
 }
 
 bool huge_tiles_env(int bit = 31) { return (g_opt_tile_huge & bit) != 0; }
-
-int korder_env() { return g_opt_korder; }
 
 // Reduce-scatter of 32 values over the 32 lanes of each wave half: after
 // the 5 butterfly steps lane r holds the half's total of value r (31
@@ -466,9 +449,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
   };
   // Issue the glds of K-step ks into ring slot ks % NS.
   int cur_tap = -1;
-  const int korder = args.korder;
   auto issue = [&](int ks) {
-    const int ti = korder ? ks % T : ks / kchunks, kc = korder ? ks / T : ks % kchunks;
+    const int ti = ks / kchunks, kc = ks % kchunks;
     if (ti != cur_tap) {
       set_tap(ti);
       cur_tap = ti;
@@ -788,9 +770,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
     }
   }
 
-  const int korder = args.korder;
   auto issue = [&](int ks) {
-    const int th = korder ? ks % 3 : ks / kchunks, kc = korder ? ks / 3 : ks % kchunks;
+    const int th = ks / kchunks, kc = ks % kchunks;
     const int dh = FWD ? th - 1 : 1 - th;
     unsigned char* st = smem + (ks % NS) * STAGE;
     const long long base = m0 + (long long)dh * W - 1;  // LDS row 0
@@ -870,7 +851,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
     __builtin_amdgcn_s_barrier();
     if (ks + NS - 1 < NK) issue(ks + NS - 1);
     const unsigned char* st = smem + (ks % NS) * STAGE;
-    const int th = korder ? ks % 3 : ks / kchunks;
+    const int th = ks / kchunks;
     uint32_t okh[TM];
 #pragma unroll
     for (int a = 0; a < TM; ++a) okh[a] = (vh[a] >> th) & 1u;
@@ -1030,7 +1011,6 @@ int launch_conv3(const ConvArgs& args, const IGeom& g, hipStream_t stream) {
   static_assert(LDS <= 160 * 1024, "LDS");
   auto kern = igemm_conv3_kernel<FWD, BM, BN, WM, WN, NS, CB, F4>;
   ConvArgs ka = args;
-  ka.korder = korder_env();
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -1081,7 +1061,6 @@ int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const v
                 (const uint16_t*)dres, dx, nullptr, 0, 0, bs.stripes,
                 (const int16_t*)bs.ypred, (const float*)bs.mean, (const float*)bs.rstd,
                 (float*)bs.sums};
-  args.korder = korder_env();
   args.fstats = (double*)bs.fstats;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, g.s * g.s), dim3(WM * WN * 64), LDS, stream,
                      args, g, m_tiles);
@@ -1109,7 +1088,6 @@ int launch_igemm_fwd(const void* sx, const void* wf, void* y, void* stats, const
   const long long blocks = (long long)m_tiles * (g.Cout / BN);
   ConvArgs args{(const uint16_t*)sx, (const uint16_t*)wf, nullptr, nullptr, y,
                 (unsigned long long*)stats, pad_ones, relu, stripes};
-  args.korder = korder_env();
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, 1), dim3(WM * WN * 64), LDS, stream, args, g,
                      m_tiles);
   return 0;
@@ -1138,7 +1116,6 @@ int launch_igemm_fwd_bf16(const void* x, const void* wf, void* y, const IGeom& g
   const long long blocks = (long long)m_tiles * (g.Cout / BN);
   ConvArgs args{(const uint16_t*)x, (const uint16_t*)wf, nullptr, nullptr, y, nullptr, 0, relu,
                 1};
-  args.korder = korder_env();
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, 1), dim3(WM * WN * 64), LDS, stream, args, g,
                      m_tiles);
   return 0;
@@ -1295,40 +1272,15 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
     case 28: ZK_IGD3(256, 64, 4, 1, 4, 32)
     case 29: ZK_IGD3(256, 64, 4, 1, 3, 32)
     case 30: ZK_IGD3(128, 64, 2, 2, 4, 32)
-    case 31: ZK_IGD3(512, 64, 8, 1, 2, 64)
     case 32: ZK_IGD3(256, 64, 4, 1, 4, 64)
     case 33: ZK_IGD3(128, 128, 2, 2, 4, 32)
     case 34: ZK_IGD3(256, 128, 4, 2, 3, 32)
-    // 128-pixel wave tiles (TM = 4): 6 fragment reads per 8 MFMAs instead of
-    // 4 per 4 -- the 64x64 wave tile sits exactly at the LDS read rate
-    case 35: ZK_IGD3(512, 64, 4, 1, 3, 64)
-    case 36: ZK_IGD3(512, 64, 4, 1, 2, 64)
-    case 37: ZK_IGD3(512, 128, 4, 2, 2, 64)
-    case 38: ZK_IGD3(512, 64, 4, 1, 4, 32)
-    case 39: ZK_IGD3(384, 64, 4, 1, 3, 64)
 #undef ZK_IGD3
     default: return (int)hipErrorInvalidValue;
   }
 #undef ZK_IGD
 }
 
-
-// e2m1 sign nibbles -> bf16 (the weight gradients' sx operand read from the
-// 4-bit image the MX-FP4 forward already uses: a quarter of the bytes of the
-// bf16 image, which then need not be written at all).  w holds 8 channels
-// (channel 2j in the low nibble of byte j); a nibble is 0x2 = +1, 0xA = -1
-// or 0x0 = 0 (the zero page), bit 3 the sign, bit 1 the magnitude.  Result:
-// the 16-B bf16 chunk of those channels.
-__device__ __forceinline__ uint4 e2m1x8_to_bf16(uint32_t w) {
-  uint32_t o[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t b = w >> (8 * k);
-    o[k] = ((b & 0x8u) << 12) | (((b >> 1) & 1u) * 0x3F80u) | ((b & 0x80u) << 24) |
-           (((b >> 5) & 1u) * 0x3F800000u);
-  }
-  return make_uint4(o[0], o[1], o[2], o[3]);
-}
 
 // ===========================================================================
 // wgrad:  dW[co][n = (t, ci)] = sum_p dY[p][co] * sx[pixel(p, t)][ci]
@@ -1337,13 +1289,7 @@ __device__ __forceinline__ uint4 e2m1x8_to_bf16(uint32_t w) {
 //   sx = sign(x) as bf16 +-1 [B][H][W][Cin] (written by zk_sign_pack);
 //   padded taps read the zero page (pad_values 0) or the +1 page.
 // ===========================================================================
-//
-// F4B: sx is the e2m1 sign image [B][H][W][Cin/2] (MX-FP4 forward operand):
-// its rows ride the same LDS-DMA ring as dy (a quarter of the bytes), and
-// each K-step expands the NEXT stage's nibbles into one of two bf16 B images
-// (swizzled exactly as the DMA path fills it) after issuing its own MFMAs;
-// the nibble DMA therefore lands one stage earlier than dy (NS >= 3).
-template <int BM, int BN, int WM, int WN, int BK, int NS, bool F4B = false>
+template <int BM, int BN, int WM, int WN, int BK, int NS>
 __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ sx,
     const float* __restrict__ w, float* __restrict__ dw, float* __restrict__ slab, IGeom g,
@@ -1352,19 +1298,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
   constexpr int RA = BM * 2, RBB = BN * 2;      // bytes per pixel row of A / B
   constexpr int SA = BK * RA, SB = BK * RBB;    // bytes per stage
   static_assert(SA % (1024 * NWAVES) == 0 && SB % (1024 * NWAVES) == 0, "stage / waves");
-  static_assert(!F4B || NS >= 3, "F4B: nibbles of stage ks + 1 must land before stage ks's MFMAs");
-  constexpr int A_INS = SA / 1024 / NWAVES, B_INS = F4B ? 0 : SB / 1024 / NWAVES;
-  constexpr int B_ARR = B_INS > 0 ? B_INS : 1;
-  // F4B: nibble rows of RN bytes; N_INS glds per wave per stage (tail lanes
-  // read the zero page); expansion items = one 16-B nibble chunk each
-  constexpr int RN = BN / 2, SN = BK * RN;
-  constexpr int N_INS = F4B ? (SN + 1024 * NWAVES - 1) / (1024 * NWAVES) : 0;
-  constexpr int N_ARR = N_INS > 0 ? N_INS : 1;
-  constexpr int BPR = BN / 32, BITEMS = BK * BPR;
-  constexpr int B_IT = (BITEMS + NWAVES * 64 - 1) / (NWAVES * 64);
-  constexpr int LPS = A_INS + B_INS + N_INS;
-  constexpr int STAGE = SA + (F4B ? N_INS * NWAVES * 1024 : SB);
-  constexpr int BI_OFF = NS * STAGE;  // F4B: two expanded bf16 images of SB bytes
+  constexpr int A_INS = SA / 1024 / NWAVES, B_INS = SB / 1024 / NWAVES;
+  constexpr int LPS = A_INS + B_INS;
+  constexpr int STAGE = SA + SB;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
 
@@ -1392,8 +1328,6 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
   const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
   const unsigned char* pp = pad_ones ? reinterpret_cast<const unsigned char*>(g_ones_page_bf16)
                                      : zp;
-  const unsigned char* ppn = pad_ones ? reinterpret_cast<const unsigned char*>(g_ones_page_fp4)
-                                      : zp;
   const float invWo = 1.0f / (float)g.Wo, invHo = 1.0f / (float)g.Ho;
 
   // Per-lane fixed parts of the loader: (row within stage, byte within row)
@@ -1405,7 +1339,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
     const int slot = (off % RA) >> 4;
     a_byte[j] = m0 * 2 + ((slot ^ tr_swz<RA>(a_row[j])) << 4);
   }
-  int b_row[B_ARR], b_th[B_ARR], b_tw[B_ARR], b_cib[B_ARR];
+  int b_row[B_INS], b_th[B_INS], b_tw[B_INS], b_cib[B_INS];
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) {
     const int off = ((j * NWAVES + wave) * 64 + lane) * 16;
@@ -1417,38 +1351,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
     b_tw[j] = t % g.kw - g.pl;
     b_cib[j] = (n % g.Cin) * 2;
   }
-  int n_row[N_ARR], n_th[N_ARR], n_tw[N_ARR], n_cib[N_ARR];  // F4B; n_row < 0: tail lane
-#pragma unroll
-  for (int j = 0; j < N_INS; ++j) {
-    const int off = ((j * NWAVES + wave) * 64 + lane) * 16;
-    n_row[j] = off < SN ? off / RN : -1;
-    const int n = n0 + ((off % RN) >> 4) * 32;  // first column of the 32-channel chunk
-    const int t = n / g.Cin;
-    n_th[j] = t / g.kw - g.pt;
-    n_tw[j] = t % g.kw - g.pl;
-    n_cib[j] = (n % g.Cin) / 2;
-  }
-
   auto issue = [&](int ks) {
     unsigned char* st = smem + (ks % NS) * STAGE;
     const int k0 = kbeg + ks * BK;
-#pragma unroll
-    for (int j = 0; j < N_INS; ++j) {
-      const int p = k0 + n_row[j];
-      const unsigned char* src = zp;
-      if (n_row[j] >= 0 && p < kend) {
-        const int q1 = fdiv(p, g.Wo, invWo);
-        const int wo = p - q1 * g.Wo;
-        const int b = fdiv(q1, g.Ho, invHo);
-        const int ho = q1 - b * g.Ho;
-        const int hi = ho * g.s + n_th[j], wi = wo * g.s + n_tw[j];
-        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
-          src = sxb + (((long long)b * g.H + hi) * g.W + wi) * (g.Cin / 2) + n_cib[j];
-        else
-          src = ppn;
-      }
-      ZK_GLDS16(src, st + SA + (j * NWAVES + wave) * 1024);
-    }
 #pragma unroll
     for (int j = 0; j < A_INS; ++j) {
       const int p = k0 + a_row[j];
@@ -1475,26 +1380,6 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
     }
   };
 
-  // F4B: nibbles of stage ks (ring slot) -> bf16 image ks & 1
-  auto expand = [&](int ks) {
-    const unsigned char* nb = smem + (ks % NS) * STAGE + SA;
-    unsigned char* bi = smem + BI_OFF + (ks & 1) * SB;
-#pragma unroll
-    for (int j = 0; j < B_IT; ++j) {
-      const int it = j * NWAVES * 64 + tid;
-      if (it < BITEMS) {
-        const int r = it / BPR, hf = it % BPR;
-        const uint4 v = *reinterpret_cast<const uint4*>(nb + it * 16);
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-        unsigned char* rowp = bi + r * RBB;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          *reinterpret_cast<uint4*>(rowp + (((hf * 4 + c) ^ tr_swz<RBB>(r)) << 4)) =
-              e2m1x8_to_bf16(wv[c]);
-      }
-    }
-  };
-
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
@@ -1506,33 +1391,16 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < NK) issue(p);
-  if (F4B && NK > 0) {
-    // stage 0's nibbles -> image 0 (stages 1 .. NS-2 may stay in flight)
-    if (NK - 1 >= NS - 2)
+  for (int ks = 0; ks < NK; ++ks) {
+    if (ks + NS - 2 < NK)
       wait_vmcnt<LPS * (NS - 2)>();
     else
       wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    expand(0);
-  }
-  for (int ks = 0; ks < NK; ++ks) {
-    if constexpr (F4B) {
-      // dy of stage ks and the nibbles of stage ks + 1 (expanded below)
-      if (ks + 1 < NK && ks + NS - 2 <= NK - 1)
-        wait_vmcnt<LPS * (NS - 3)>();
-      else
-        wait_vmcnt<0>();
-    } else if (ks + NS - 2 < NK) {
-      wait_vmcnt<LPS * (NS - 2)>();
-    } else {
-      wait_vmcnt<0>();
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
     if (ks + NS - 1 < NK) issue(ks + NS - 1);
     const unsigned char* st = smem + (ks % NS) * STAGE;
-    const unsigned char* stb = F4B ? smem + BI_OFF + (ks & 1) * SB : st + SA;
+    const unsigned char* stb = st + SA;
     // double-buffered transposed fragment reads (see igemm_conv_kernel)
     constexpr int NSUB = BK / 16;
     uint4 af[2][TM], bfr[2][TN];
@@ -1557,8 +1425,6 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
 #pragma unroll
         for (int b = 0; b < TN; ++b) acc[a][b] = mfma_bf16(af[cs][a], bfr[cs][b], acc[a][b]);
     }
-    if constexpr (F4B)
-      if (ks + 1 < NK) expand(ks + 1);  // image (ks+1)&1: every wave is past its last read
   }
 
   // epilogue.  slab mode: plain stores of this split's partial dW into
@@ -1615,7 +1481,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float4* __restr
       t.z += v.z;
       t.w += v.w;
     }
-    const float4 wv = w[i];
+    const float4 wv = w ? w[i] : make_float4(0.f, 0.f, 0.f, 0.f);  // no w: no mask
     float4 d = dw[i];
     d.x += fabsf(wv.x) <= clip ? t.x : 0.f;
     d.y += fabsf(wv.y) <= clip ? t.y : 0.f;
@@ -1629,8 +1495,10 @@ struct WgradPlan {
   int m_tiles, n_tiles, splits, kps;
 };
 
+// slab: the split-K partials go to slabs (capped by wgrad_slab_mb); otherwise
+// fp32 atomics into dW, where the split count follows the block target alone.
 template <int BM, int BN, int BK>
-bool plan_wgrad(const IGeom& g, int target_blocks, WgradPlan& p) {
+bool plan_wgrad(const IGeom& g, int target_blocks, WgradPlan& p, bool slab) {
   const int NTOT = g.kh * g.kw * g.Cin;
   if (g.Cout % BM || NTOT % BN || g.Cin % 8) return false;
   const long long P = (long long)g.B * g.Ho * g.Wo;
@@ -1641,7 +1509,7 @@ bool plan_wgrad(const IGeom& g, int target_blocks, WgradPlan& p) {
   long long splits = (target_blocks + tiles - 1) / tiles;
   const long long max_splits = (P + 4 * BK - 1) / (4 * BK);  // >= 4 K-steps per split
   if (splits > max_splits) splits = max_splits;
-  splits = cap_splits(splits, (long long)g.Cout * NTOT * 4);
+  if (slab) splits = cap_splits(splits, (long long)g.Cout * NTOT * 4);
   if (splits < 1) splits = 1;
   long long kps = (P + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;
@@ -1650,23 +1518,22 @@ bool plan_wgrad(const IGeom& g, int target_blocks, WgradPlan& p) {
   return true;
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int NS, bool F4B = false>
+template <int BM, int BN, int WM, int WN, int BK, int NS>
 int launch_igemm_wgrad(const void* dy, const void* sx, const void* w, void* dw, const IGeom& g,
                        int pad_ones, float clip, int target_blocks, void* ws, long long ws_bytes,
                        long long* ws_needed, hipStream_t stream) {
   WgradPlan p;
-  if (F4B && g.Cin % 32) return (int)hipErrorInvalidValue;  // 32-channel nibble loads
-  if (!plan_wgrad<BM, BN, BK>(g, target_blocks, p)) return (int)hipErrorInvalidValue;
+  if (!plan_wgrad<BM, BN, BK>(g, target_blocks, p, ws_needed != nullptr || ws != nullptr))
+    return (int)hipErrorInvalidValue;
   const int NTOT = g.kh * g.kw * g.Cin;
   const long long slab_bytes = (long long)p.splits * g.Cout * NTOT * 4;
   if (ws_needed) {  // size query only
     *ws_needed = slab_bytes;
     return 0;
   }
-  constexpr int NW = WM * WN, SNR = (BK * BN / 2 + 1024 * NW - 1) / (1024 * NW) * 1024 * NW;
-  constexpr int LDS = F4B ? NS * (BK * BM * 2 + SNR) + 2 * BK * BN * 2 : NS * BK * (BM + BN) * 2;
+  constexpr int LDS = NS * BK * (BM + BN) * 2;
   static_assert(LDS <= 160 * 1024, "LDS");
-  auto kern = igemm_wgrad_kernel<BM, BN, WM, WN, BK, NS, F4B>;
+  auto kern = igemm_wgrad_kernel<BM, BN, WM, WN, BK, NS>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -1702,18 +1569,12 @@ int launch_igemm_wgrad(const void* dy, const void* sx, const void* w, void* dw, 
 // dy is read 3/TH times per layer instead of 9, sx 3 times instead of 9.
 // The halo costs 2/(W+2) of the K-steps.  Output as igemm_wgrad_kernel.
 // ===========================================================================
-//
-// F4B: sx is the e2m1 sign image [B][H][W][Cin/2] instead of the bf16 one:
-// its segment rows ride the LDS-DMA ring beside dy (a quarter of the bytes)
-// and each K-step expands the next stage's nibbles into one of two bf16
-// segment images (see igemm_wgrad_kernel).
-template <int BM, int BN, int WM, int WN, int BK, int NS, int TH, int OCC, bool F4B = false>
+template <int BM, int BN, int WM, int WN, int BK, int NS, int TH, int OCC>
 __global__ __launch_bounds__(WM * WN * 64, OCC) void igemm_wgrad3_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ sx,
     const float* __restrict__ w, float* __restrict__ dw, float* __restrict__ slab, IGeom g,
     int pad_ones, float clip, int k_per_split, int m_tiles, int n_tiles) {
   constexpr int NWAVES = WM * WN, NT = 3 * TH, TG = 3 / TH;
-  static_assert(!F4B || NS >= 3, "F4B: nibbles of stage ks + 1 must land before stage ks's MFMAs");
   static_assert(TH == 1 || TH == 3, "kernel rows per block");
   constexpr int RA = BM * 2, RBB = BN * 2;
   constexpr int SA = BK * RA;
@@ -1722,18 +1583,10 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void igemm_wgrad3_kernel(
   constexpr int SEG = (BK + 2) * RBB;  // one kernel row's sx segment
   static_assert(SEG % 256 == 0, "segments keep the swizzle period");
   constexpr int B_KB = (TH * SEG + 1023) / 1024;
-  constexpr int B_INS = F4B ? 0 : (B_KB + NWAVES - 1) / NWAVES;  // tail lanes: zero page
-  constexpr int SB = (B_KB + NWAVES - 1) / NWAVES * NWAVES * 1024;
-  // F4B: nibble segments of (BK + 2) rows x RN bytes, linear in LDS; one
-  // expansion item per 16-B nibble chunk
-  constexpr int RN = BN / 2, SEGN = (BK + 2) * RN, SN = TH * SEGN;
-  constexpr int N_INS = F4B ? (SN + 1024 * NWAVES - 1) / (1024 * NWAVES) : 0;
-  constexpr int N_ARR = N_INS > 0 ? N_INS : 1;
-  constexpr int LPS = A_INS + B_INS + N_INS;
-  constexpr int STAGE = SA + (F4B ? N_INS * NWAVES * 1024 : SB);
-  constexpr int BI_OFF = NS * STAGE;  // F4B: two expanded bf16 images of SB bytes
-  constexpr int BPR = BN / 32, BITEMS = TH * (BK + 2) * BPR;
-  constexpr int B_IT = (BITEMS + NWAVES * 64 - 1) / (NWAVES * 64);
+  constexpr int B_INS = (B_KB + NWAVES - 1) / NWAVES;  // tail lanes: zero page
+  constexpr int SB = B_INS * NWAVES * 1024;
+  constexpr int LPS = A_INS + B_INS;
+  constexpr int STAGE = SA + SB;
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
 
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
@@ -1759,8 +1612,6 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void igemm_wgrad3_kernel(
   const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
   const unsigned char* pp = pad_ones ? reinterpret_cast<const unsigned char*>(g_ones_page_bf16)
                                      : zp;
-  const unsigned char* ppn = pad_ones ? reinterpret_cast<const unsigned char*>(g_ones_page_fp4)
-                                      : zp;
   const float invWE = 1.0f / (float)WE, invH = 1.0f / (float)g.H;
 
   int a_row[A_INS], a_byte[A_INS];
@@ -1771,8 +1622,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void igemm_wgrad3_kernel(
     const int slot = (off % RA) >> 4;
     a_byte[j] = m0 * 2 + ((slot ^ tr_swz<RA>(a_row[j])) << 4);
   }
-  constexpr int B_ARR = B_INS > 0 ? B_INS : 1;
-  int b_row[B_ARR], b_th[B_ARR], b_byte[B_ARR];  // b_th < 0: tail lane
+  int b_row[B_INS], b_th[B_INS], b_byte[B_INS];  // b_th < 0: tail lane
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) {
     const int off = ((j * NWAVES + wave) * 64 + lane) * 16;
@@ -1785,20 +1635,6 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void igemm_wgrad3_kernel(
       b_byte[j] = n0 * 2 + ((((o % RBB) >> 4) ^ tr_swz<RBB>(b_row[j])) << 4);
     }
   }
-  int n_row[N_ARR], n_th[N_ARR], n_byte[N_ARR];  // F4B; n_th < 0: tail lane
-#pragma unroll
-  for (int j = 0; j < N_INS; ++j) {
-    const int off = ((j * NWAVES + wave) * 64 + lane) * 16;
-    n_th[j] = -1;
-    n_row[j] = n_byte[j] = 0;
-    if (off < SN) {
-      const int t = off / SEGN, o = off % SEGN;
-      n_th[j] = thg * TH + t;
-      n_row[j] = o / RN;
-      n_byte[j] = n0 / 2 + (o % RN);
-    }
-  }
-
   auto issue = [&](int ks) {
     unsigned char* st = smem + (ks % NS) * STAGE;
     const int e0 = kbeg + ks * BK;
@@ -1829,43 +1665,6 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void igemm_wgrad3_kernel(
       }
       ZK_GLDS16(src, st + SA + (j * NWAVES + wave) * 1024);
     }
-#pragma unroll
-    for (int j = 0; j < N_INS; ++j) {
-      const unsigned char* src = zp;
-      if (n_th[j] >= 0) {
-        src = ppn;  // padding tap
-        const int e = e0 - 1 + n_row[j];
-        if (e >= 0 && e < E) {
-          const int q = fdiv(e, WE, invWE);  // b*H + h
-          const int c = e - q * WE - 1;
-          const int hh = q - fdiv(q, g.H, invH) * g.H + n_th[j] - 1;
-          if (c >= 0 && c < g.W && hh >= 0 && hh < g.H)
-            src = sxb + ((long long)(q + n_th[j] - 1) * g.W + c) * (g.Cin / 2) + n_byte[j];
-        }
-      }
-      ZK_GLDS16(src, st + SA + (j * NWAVES + wave) * 1024);
-    }
-  };
-
-  // F4B: nibbles of stage ks (ring slot) -> bf16 segment image ks & 1
-  auto expand = [&](int ks) {
-    const unsigned char* nb = smem + (ks % NS) * STAGE + SA;
-    unsigned char* bi = smem + BI_OFF + (ks & 1) * SB;
-#pragma unroll
-    for (int j = 0; j < B_IT; ++j) {
-      const int it = j * NWAVES * 64 + tid;
-      if (it < BITEMS) {
-        const int t = it / ((BK + 2) * BPR), o = it % ((BK + 2) * BPR);
-        const int r = o / BPR, hf = o % BPR;
-        const uint4 v = *reinterpret_cast<const uint4*>(nb + it * 16);
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-        unsigned char* rowp = bi + t * SEG + r * RBB;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          *reinterpret_cast<uint4*>(rowp + (((hf * 4 + c) ^ tr_swz<RBB>(r)) << 4)) =
-              e2m1x8_to_bf16(wv[c]);
-      }
-    }
   };
 
   f32x16 acc[NT][TM][TN];
@@ -1881,33 +1680,16 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void igemm_wgrad3_kernel(
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < NK) issue(p);
-  if (F4B && NK > 0) {
-    // stage 0's nibbles -> image 0 (stages 1 .. NS-2 may stay in flight)
-    if (NK - 1 >= NS - 2)
+  for (int ks = 0; ks < NK; ++ks) {
+    if (ks + NS - 2 < NK)
       wait_vmcnt<LPS * (NS - 2)>();
     else
       wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    expand(0);
-  }
-  for (int ks = 0; ks < NK; ++ks) {
-    if constexpr (F4B) {
-      // dy of stage ks and the nibbles of stage ks + 1 (expanded below)
-      if (ks + 1 < NK && ks + NS - 2 <= NK - 1)
-        wait_vmcnt<LPS * (NS - 3)>();
-      else
-        wait_vmcnt<0>();
-    } else if (ks + NS - 2 < NK) {
-      wait_vmcnt<LPS * (NS - 2)>();
-    } else {
-      wait_vmcnt<0>();
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
     if (ks + NS - 1 < NK) issue(ks + NS - 1);
     const unsigned char* st = smem + (ks % NS) * STAGE;
-    const unsigned char* stb = F4B ? smem + BI_OFF + (ks & 1) * SB : st + SA;
+    const unsigned char* stb = st + SA;
 #pragma unroll
     for (int sub = 0; sub < BK / 16; ++sub) {
       uint4 af[TM];
@@ -1927,8 +1709,6 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void igemm_wgrad3_kernel(
           for (int b = 0; b < TN; ++b) acc[t][a][b] = mfma_bf16(af[a], bfr[b], acc[t][a][b]);
       }
     }
-    if constexpr (F4B)
-      if (ks + 1 < NK) expand(ks + 1);  // image (ks+1)&1: every wave is past its last read
   }
 
   const int h = lane >> 5, r32 = lane & 31;
@@ -1957,7 +1737,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void igemm_wgrad3_kernel(
 }
 
 template <int BM, int BN, int BK, int TH>
-bool plan_wgrad3(const IGeom& g, int target_blocks, WgradPlan& p) {
+bool plan_wgrad3(const IGeom& g, int target_blocks, WgradPlan& p, bool slab) {
   if (!conv3_ok(g, 0) || g.Cout % BM || g.Cin % BN) return false;
   const long long E = (long long)g.B * g.H * (g.W + 2);
   if (E >= (1 << 24)) return false;  // fdiv range
@@ -1967,7 +1747,7 @@ bool plan_wgrad3(const IGeom& g, int target_blocks, WgradPlan& p) {
   long long splits = (target_blocks + tiles - 1) / tiles;
   const long long max_splits = (E + 4 * BK - 1) / (4 * BK);
   if (splits > max_splits) splits = max_splits;
-  splits = cap_splits(splits, (long long)g.Cout * g.kh * g.kw * g.Cin * 4);
+  if (slab) splits = cap_splits(splits, (long long)g.Cout * g.kh * g.kw * g.Cin * 4);
   if (splits < 1) splits = 1;
   long long kps = (E + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;
@@ -1976,12 +1756,13 @@ bool plan_wgrad3(const IGeom& g, int target_blocks, WgradPlan& p) {
   return true;
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int NS, int TH, int OCC, bool F4B = false>
+template <int BM, int BN, int WM, int WN, int BK, int NS, int TH, int OCC>
 int launch_igemm_wgrad3(const void* dy, const void* sx, const void* w, void* dw, const IGeom& g,
                         int pad_ones, float clip, int target_blocks, void* ws, long long ws_bytes,
                         long long* ws_needed, hipStream_t stream) {
   WgradPlan p;
-  if (!plan_wgrad3<BM, BN, BK, TH>(g, target_blocks, p)) return (int)hipErrorInvalidValue;
+  if (!plan_wgrad3<BM, BN, BK, TH>(g, target_blocks, p, ws_needed != nullptr || ws != nullptr))
+    return (int)hipErrorInvalidValue;
   const int NTOT = 9 * g.Cin;
   const long long slab_bytes = (long long)p.splits * g.Cout * NTOT * 4;
   if (ws_needed) {
@@ -1990,10 +1771,9 @@ int launch_igemm_wgrad3(const void* dy, const void* sx, const void* w, void* dw,
   }
   constexpr int NW = WM * WN;
   constexpr int SB = ((TH * (BK + 2) * BN * 2 + 1023) / 1024 + NW - 1) / NW * NW * 1024;
-  constexpr int SNR = (TH * (BK + 2) * BN / 2 + 1024 * NW - 1) / (1024 * NW) * 1024 * NW;
-  constexpr int LDS = F4B ? NS * (BK * BM * 2 + SNR) + 2 * SB : NS * (BK * BM * 2 + SB);
+  constexpr int LDS = NS * (BK * BM * 2 + SB);
   static_assert(LDS <= 160 * 1024, "LDS");
-  auto kern = igemm_wgrad3_kernel<BM, BN, WM, WN, BK, NS, TH, OCC, F4B>;
+  auto kern = igemm_wgrad3_kernel<BM, BN, WM, WN, BK, NS, TH, OCC>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -2022,19 +1802,6 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
   return launch_igemm_wgrad<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, ws, wsb, need, st)
 #define ZK_IGW3(...) \
   return launch_igemm_wgrad3<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, ws, wsb, need, st)
-  if (v == 51) {  // conv3rw.hip row-window kernel + the fixed-order slab reduce
-    if (g.s != 1 || g.kh != 3 || g.kw != 3 || g.pt != 1 || g.pl != 1 || g.Ho != g.H ||
-        g.Wo != g.W)
-      return (int)hipErrorInvalidValue;
-    int splits = 0;
-    const int rc = zk_conv3rw_wgrad_impl(dy, sx, w, dw, g.B, g.H, g.W, g.Cin, g.Cout, po, clip,
-                                         ws, wsb, need, &splits, need != nullptr || g_dry_run, st);
-    if (rc || need || g_dry_run || splits == 0) return rc;
-    const long long n4 = (long long)g.Cout * 9 * g.Cin / 4;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st,
-                       (const float4*)ws, splits, n4, (const float4*)w, clip, (float4*)dw);
-    return 0;
-  }
   switch (v) {
     // conv3 family <BM, BN, WM, WN, BK, NS, TH, OCC>
     case 20: ZK_IGW3(64, 64, 2, 2, 32, 4, 3, 1);
@@ -2065,26 +1832,6 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
     case 10: ZK_IGW(256, 128, 4, 2, 32, 2);
     case 11: ZK_IGW(128, 256, 2, 4, 32, 2);
     case 12: ZK_IGW(256, 256, 4, 2, 32, 3);  // 96 KB
-    // e2m1 sx (F4B; sx = the nibble image, >= 3 stages)
-    case 101: ZK_IGW(128, 128, 2, 2, 32, 4, true);
-    case 102: ZK_IGW(128, 192, 2, 2, 32, 4, true);
-    case 104: ZK_IGW(128, 128, 2, 2, 64, 4, true);
-    case 107: ZK_IGW(64, 64, 2, 2, 32, 4, true);
-    case 108: ZK_IGW(256, 256, 4, 2, 32, 4, true);
-    case 109: ZK_IGW(256, 256, 2, 4, 32, 4, true);
-    case 110: ZK_IGW(256, 128, 4, 2, 32, 4, true);
-    case 111: ZK_IGW(128, 128, 2, 2, 32, 3, true);
-    case 114: ZK_IGW(128, 128, 2, 2, 64, 3, true);
-    case 118: ZK_IGW(256, 256, 4, 2, 32, 3, true);
-    case 120: ZK_IGW3(64, 64, 2, 2, 32, 4, 3, 1, true);
-    case 121: ZK_IGW3(64, 64, 2, 2, 32, 4, 1, 2, true);
-    case 122: ZK_IGW3(128, 64, 2, 2, 32, 4, 1, 2, true);
-    case 123: ZK_IGW3(128, 64, 2, 2, 32, 3, 1, 2, true);
-    case 125: ZK_IGW3(64, 64, 2, 2, 64, 3, 3, 1, true);
-    case 126: ZK_IGW3(128, 128, 2, 2, 32, 3, 1, 1, true);
-    case 127: ZK_IGW3(64, 64, 2, 2, 32, 3, 3, 2, true);
-    case 128: ZK_IGW3(128, 64, 2, 2, 64, 3, 1, 1, true);
-    case 132: ZK_IGW3(128, 64, 2, 2, 32, 3, 3, 1, true);
     default: return (int)hipErrorInvalidValue;
   }
 #undef ZK_IGW
@@ -2220,9 +1967,7 @@ void wgrad_defaults(const IGeom& g, int& variant, int& target_blocks) {
     // blocks (329 -> 222 us), 7x7x512 on 128x128 at 2048 blocks (392 vs 400).
     const bool c3 = conv3_ok(g, 0);
     const bool big = g.B >= 512, huge = g.B >= 1024;
-    if (g_opt_wgrad_rw && c3 && g.Cin == 64 && g.Cout == 64 && g.W <= 64) {
-      variant = 51;  // row-window kernel (conv3rw.hip)
-    } else if (c3 && g.Cin == 64 && g.Cout % 64 == 0) {
+    if (c3 && g.Cin == 64 && g.Cout % 64 == 0) {
       variant = 20;
       if (target_blocks <= 0) target_blocks = 512;
     } else if (huge && huge_tiles_env(1) && c3 && g.Cin == 128 && g.Cout % 64 == 0) {
@@ -2271,7 +2016,6 @@ ZK_EXPORT int zk_igemm_wgrad(const void* dy, const void* sx, const void* w, void
                              int target_blocks, int variant, void* workspace,
                              long long ws_bytes, hipStream_t stream) {
   IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
-  if (variant >= 100) return (int)hipErrorInvalidValue;  // e2m1 sx: zk_igemm_wgrad_f4
   wgrad_defaults(g, variant, target_blocks);
   const int rc = igemm_wgrad_variant(variant, dy, sx, w, dw, g, pad_ones, clip, target_blocks,
                                      workspace, ws_bytes, nullptr, stream);
@@ -2280,59 +2024,17 @@ ZK_EXPORT int zk_igemm_wgrad(const void* dy, const void* sx, const void* w, void
   return 0;
 }
 
-// zk_igemm_wgrad with sx as the e2m1 sign image sx4 [B][H][W][Cin/2] (the
-// MX-FP4 forward's operand; channel 2j in the low nibble of byte j) instead
-// of the bf16 +-1 image: F4B variants (100+), Cin % 32 == 0.  variant < 0:
-// the F4B form of the tuned default.
-namespace {
-int wgrad_f4_of(int v) {
-  switch (v) {
-    case 0: case 1: return 101;
-    case 2: return 102;
-    case 4: return 104;
-    case 7: return 107;
-    case 8: case 12: return 108;
-    case 9: return 109;
-    case 10: return 110;
-    case 20: case 29: case 51: return 120;
-    case 21: case 33: return 121;
-    case 22: case 28: case 34: return 122;
-    case 25: return 125;
-    case 23: case 26: return 126;
-    case 27: case 30: return 127;
-    case 32: return 132;
-    default: return v;
-  }
-}
-}  // namespace
-
-ZK_EXPORT int zk_igemm_wgrad_f4(const void* dy, const void* sx4, const void* w, void* dw, int B,
-                                int H, int W, int Cin, int Ho, int Wo, int Cout, int kh, int kw,
-                                int stride, int pt, int pl, int pad_ones, float clip,
-                                int target_blocks, int variant, void* workspace,
-                                long long ws_bytes, hipStream_t stream) {
-  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
-  wgrad_defaults(g, variant, target_blocks);
-  variant = wgrad_f4_of(variant);
-  if (variant < 100) return (int)hipErrorInvalidValue;
-  const int rc = igemm_wgrad_variant(variant, dy, sx4, w, dw, g, pad_ones, clip, target_blocks,
-                                     workspace, ws_bytes, nullptr, stream);
-  if (rc) return rc;
-  if (!g_dry_run) ZK_CHECK_LAUNCH();
+// dw[i] += [|w[i]| <= clip] * sum_s slab[s][i] (w null: no mask), summed in a
+// fixed order: the deterministic-mode reduction of every split-K weight
+// gradient (igemm, small-K convs, depthwise, stem).  n % 4 == 0.
+ZK_EXPORT int zk_wgrad_slab_reduce(const void* slab, int splits, long long n, const void* w,
+                                   float clip, void* dw, hipStream_t stream) {
+  if (n % 4 || splits < 1) return (int)hipErrorInvalidValue;
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, stream,
+                     (const float4*)slab, splits, n4, (const float4*)w, clip, (float4*)dw);
+  ZK_CHECK_LAUNCH();
   return 0;
-}
-
-ZK_EXPORT long long zk_igemm_wgrad_f4_ws_bytes(int B, int Cin, int H, int W, int Ho, int Wo,
-                                               int Cout, int kh, int kw, int stride, int pt,
-                                               int pl, int target_blocks, int variant) {
-  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
-  wgrad_defaults(g, variant, target_blocks);
-  variant = wgrad_f4_of(variant);
-  long long need = -1;
-  if (variant < 100 || igemm_wgrad_variant(variant, nullptr, nullptr, nullptr, nullptr, g, 0, 0.f,
-                                           target_blocks, nullptr, 0, &need, nullptr) != 0)
-    return -1;
-  return need;
 }
 
 // Workspace bytes zk_igemm_wgrad needs for slab mode (-1: shape unsupported).
@@ -2340,7 +2042,6 @@ ZK_EXPORT long long zk_igemm_wgrad_ws_bytes(int B, int Cin, int H, int W, int Ho
                                             int Cout, int kh, int kw, int stride, int pt, int pl,
                                             int target_blocks, int variant) {
   IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
-  if (variant >= 100) return -1;
   wgrad_defaults(g, variant, target_blocks);
   long long need = -1;
   if (igemm_wgrad_variant(variant, nullptr, nullptr, nullptr, nullptr, g, 0, 0.f,
@@ -2491,10 +2192,8 @@ ZK_EXPORT int zk_igemm_fwd_supported(int B, int H, int W, int Cin, int Cout, int
 ZK_EXPORT int zk_set_option(int key, int value) {
   switch (key) {
     case 0: g_opt_tile_huge = value; return 0;
-    case 1: g_opt_korder = value; return 0;
     case 2: g_opt_deterministic = value; return 0;
     case 3: g_opt_dgrad_rw = value; return 0;
-    case 4: g_opt_wgrad_rw = value; return 0;
     case 5: g_opt_wgrad_slab_mb = value; return 0;
     default: return -1;
   }
@@ -2503,10 +2202,8 @@ ZK_EXPORT int zk_set_option(int key, int value) {
 ZK_EXPORT int zk_get_option(int key) {
   switch (key) {
     case 0: return g_opt_tile_huge;
-    case 1: return g_opt_korder;
     case 2: return g_opt_deterministic;
     case 3: return g_opt_dgrad_rw;
-    case 4: return g_opt_wgrad_rw;
     case 5: return g_opt_wgrad_slab_mb;
     default: return -1;
   }

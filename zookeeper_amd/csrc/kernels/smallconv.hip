@@ -132,7 +132,8 @@ template <int KP, bool PW, int NC>
 __global__ __launch_bounds__(256) void smallk_wgrad_kernel(const uint16_t* __restrict__ dy,
                                                            const uint16_t* __restrict__ x,
                                                            const float* __restrict__ w,
-                                                           float* __restrict__ dw, SKGeom g,
+                                                           float* __restrict__ dw,
+                                                           float* __restrict__ slab, SKGeom g,
                                                            int kps, float clip) {
   constexpr int PS = SK_BM + 8;  // pixel stride of the transposed images (16-B aligned rows)
   __shared__ __attribute__((aligned(16))) uint16_t sD[128 * PS];  // dY^T [co][pixel]
@@ -243,7 +244,10 @@ __global__ __launch_bounds__(256) void smallk_wgrad_kernel(const uint16_t* __res
     for (int e = 0; e < 4; ++e) {
       const int co = ct * 16 + 4 * kq + e;
       const long long idx = (((long long)co * g.KH + kh) * g.KW + kw) * g.Cin + c;
-      if (fabsf(w[idx]) <= clip) atomicAdd(dw + idx, acc[i][e]);
+      if (slab)  // deterministic mode: this block's partial, reduced in a fixed order
+        slab[(long long)blockIdx.x * g.Cout * g.K + idx] = acc[i][e];
+      else if (fabsf(w[idx]) <= clip)
+        atomicAdd(dw + idx, acc[i][e]);
     }
   }
 }
@@ -578,11 +582,21 @@ ZK_EXPORT int zk_smallk_conv_fwd(const void* x, const void* wp, void* y, int B, 
 
 // dw fp32 OHWI [Cout][KH][KW][Cin] += dY^T ⊛ x where |w| <= clip (w: the
 // latent fp32 kernel, OHWI); dy bf16 [B][Ho][Wo][Cout].  Split-K over pixel
-// chunks, fp32 atomics (target_blocks <= 0: 1024 blocks).
-ZK_EXPORT int zk_smallk_conv_wgrad(const void* dy, const void* x, const void* w, void* dw, int B,
-                                   int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW,
-                                   int s, int pt, int pl, float clip, int target_blocks,
-                                   hipStream_t st) {
+// chunks (target_blocks <= 0: 1024 blocks), fp32 atomics -- or, with slab
+// (deterministic mode), per-block partials [blocks][Cout*K] (zeroed by the
+// caller; zk_smallk_conv_wgrad_blocks sizes it) summed by zk_wgrad_slab_reduce.
+ZK_EXPORT int zk_smallk_conv_wgrad_blocks(int B, int Ho, int Wo, int target_blocks) {
+  const long long P = (long long)B * Ho * Wo;
+  if (target_blocks <= 0) target_blocks = 1024;
+  long long kps = (P + target_blocks - 1) / target_blocks;
+  kps = (kps + SK_BM - 1) / SK_BM * SK_BM;
+  return (int)((P + kps - 1) / kps);
+}
+
+ZK_EXPORT int zk_smallk_conv_wgrad(const void* dy, const void* x, const void* w, void* dw,
+                                   void* slab, int B, int H, int W, int Cin, int Ho, int Wo,
+                                   int Cout, int KH, int KW, int s, int pt, int pl, float clip,
+                                   int target_blocks, hipStream_t st) {
   SKGeom g{B, H, W, Cin, Ho, Wo, Cout, KH, KW, s, pt, pl, KH * KW * Cin};
   if (!sk_ok(g)) return (int)hipErrorInvalidValue;
   const long long P = (long long)B * Ho * Wo;
@@ -593,8 +607,8 @@ ZK_EXPORT int zk_smallk_conv_wgrad(const void* dy, const void* x, const void* w,
   const bool pw = sk_pw(g);
 #define ZK_SK_WG(KPV, PWV, NCV)                                                                  \
   hipLaunchKernelGGL((smallk_wgrad_kernel<KPV, PWV, NCV>), dim3(blocks), dim3(256), 0, st,       \
-                     (const uint16_t*)dy, (const uint16_t*)x, (const float*)w, (float*)dw, g,    \
-                     (int)kps, clip)
+                     (const uint16_t*)dy, (const uint16_t*)x, (const float*)w, (float*)dw,       \
+                     (float*)slab, g, (int)kps, clip)
 #define ZK_SK_WG_NC(KPV, PWV)                \
   switch (g.Cout >> 4) {                     \
     case 1: ZK_SK_WG(KPV, PWV, 1); break;    \

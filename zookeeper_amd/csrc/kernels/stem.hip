@@ -654,7 +654,7 @@ __global__ __launch_bounds__(256) void stem_dy1_kernel(
 template <int BK, int NS>
 __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(
     const uint16_t* __restrict__ dy1, const unsigned char* __restrict__ xp,
-    float* __restrict__ dw, StemGeom g, int k_per_split) {
+    float* __restrict__ dw, float* __restrict__ slab, StemGeom g, int k_per_split) {
   constexpr int BM = 64, BN = 256, WM = 1, WN = 4, NWAVES = 4;
   constexpr int RA = BM * 2, RBB = BN * 2;
   constexpr int SA = BK * RA, SB = BK * RBB;
@@ -761,8 +761,13 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(
       for (int b = 0; b < TN; ++b) {
         const int n = wn * WTN + b * 32 + r32;
         const int kh = n >> 5, kw = (n >> 2) & 7, c = n & 3;
-        if (kh < g.KH && kw < g.KW && c < g.Cin && co < g.Cout)
-          atomicAdd(dw + ((co * g.KH + kh) * g.KW + kw) * g.Cin + c, acc[a][b][r]);
+        if (kh < g.KH && kw < g.KW && c < g.Cin && co < g.Cout) {
+          const int idx = ((co * g.KH + kh) * g.KW + kw) * g.Cin + c;
+          if (slab)  // deterministic mode: per-split partials, fixed-order reduce
+            slab[(long long)blockIdx.x * g.Cout * g.KH * g.KW * g.Cin + idx] = acc[a][b][r];
+          else
+            atomicAdd(dw + idx, acc[a][b][r]);
+        }
       }
     }
 }
@@ -970,11 +975,23 @@ ZK_EXPORT int zk_stem_dy1(const void* dp, const void* arg, const void* y1, const
   return 0;
 }
 
+// Splits (blocks) of zk_stem_wgrad: its deterministic-mode slab is
+// [splits][Cout*KH*KW*Cin] fp32.
+ZK_EXPORT int zk_stem_wgrad_splits(int B, int Ho, int Wo, int target_blocks) {
+  const long long P = (long long)B * Ho * Wo;
+  if (target_blocks <= 0) target_blocks = 1024;
+  long long kps = (P + target_blocks - 1) / target_blocks;
+  kps = (kps + 31) / 32 * 32;
+  return (int)((P + kps - 1) / kps);
+}
+
 // dw: fp32 OHWI [Cout][KH][KW][Cin], accumulated (zeroed by the caller or the
-// flat gradient buffer).  Cout must be 64.
-ZK_EXPORT int zk_stem_wgrad(const void* dy1, const void* xp, void* dw, int B, int Cin, int Cout,
-                            int KH, int KW, int s, int Ho, int Wo, int Hp, int Wp,
-                            int target_blocks, hipStream_t st) {
+// flat gradient buffer) with fp32 atomics, or with slab (deterministic mode,
+// zeroed by the caller) as per-split partials for zk_wgrad_slab_reduce.
+// Cout must be 64.
+ZK_EXPORT int zk_stem_wgrad(const void* dy1, const void* xp, void* dw, void* slab, int B,
+                            int Cin, int Cout, int KH, int KW, int s, int Ho, int Wo, int Hp,
+                            int Wp, int target_blocks, hipStream_t st) {
   StemGeom g{B, 0, 0, Cin, Cout, KH, KW, s, 0, 0, Ho, Wo, Hp, Wp};
   if (!stem_ok(g) || Cout != 64) return (int)hipErrorInvalidValue;
   const long long P = (long long)B * Ho * Wo;
@@ -988,7 +1005,7 @@ ZK_EXPORT int zk_stem_wgrad(const void* dy1, const void* xp, void* dw, int B, in
   kps = (kps + BK - 1) / BK * BK;
   const long long splits = (P + kps - 1) / kps;
   hipLaunchKernelGGL(kern, dim3((unsigned)splits), dim3(256), lds, st, (const uint16_t*)dy1,
-                     (const unsigned char*)xp, (float*)dw, g, (int)kps);
+                     (const unsigned char*)xp, (float*)dw, (float*)slab, g, (int)kps);
   ZK_CHECK_LAUNCH();
   return 0;
 }

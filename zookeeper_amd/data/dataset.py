@@ -450,14 +450,23 @@ def decode_into(out: np.ndarray, items: Sequence[Any], fn, threads: int) -> np.n
     """``out[k] = fn(items[k])`` for every k, on ``threads`` threads (in
     contiguous chunks, one per thread)."""
     n = len(items)
+    shape = out.shape[1:]
+
+    def one(k):
+        a = fn(items[k])
+        if a.shape != shape:  # no silent broadcast of a 1-channel image into 3
+            raise ValueError(f"decoded example {k} of the batch has shape {a.shape}, the batch "
+                             f"{shape} (mixed image sizes or channel counts)")
+        out[k] = a
+
     if threads <= 1 or n <= 1:
         for k in range(n):
-            out[k] = fn(items[k])
+            one(k)
         return out
 
     def work(lo, hi):
         for k in range(lo, hi):
-            out[k] = fn(items[k])
+            one(k)
 
     step = -(-n // threads)
     futs = [decode_pool(threads).submit(work, lo, min(n, lo + step)) for lo in range(0, n, step)]
@@ -484,6 +493,12 @@ class _HFSource(Source):
                     self._encoded = True
             except Exception:  # older datasets / non-image column: decode row by row
                 pass
+        # one channel layout for the whole dataset, fixed by its first image:
+        # grayscale stays 1-channel only if the dataset starts grayscale; every
+        # other image is converted to it (never per batch, never by order)
+        self._mode = "RGB"
+        if self._encoded and len(self.ds):
+            self._mode = "L" if _encoded_mode(self.ds[0][image_key]) == "L" else "RGB"
 
     def __len__(self) -> int:
         return len(self.ds)
@@ -491,7 +506,8 @@ class _HFSource(Source):
     def get_batch(self, indices: np.ndarray) -> Batch:
         rows = self.ds[np.asarray(indices).tolist()]
         items = rows[self.image_key]
-        decode = (_decode_encoded if self._encoded
+        mode = self._mode
+        decode = ((lambda it: _decode_encoded(it, mode)) if self._encoded
                   else self.decoders.get(self.image_key, _to_uint8_hwc))
         first = decode(items[0])
         out = np.empty((len(items),) + first.shape, dtype=np.uint8)
@@ -505,16 +521,25 @@ def _to_uint8_hwc(im: Any) -> np.ndarray:
     return a[..., None] if a.ndim == 2 else a
 
 
-def _decode_encoded(item: Any) -> np.ndarray:
-    """A datasets ``Image(decode=False)`` cell ({"bytes", "path"}) -> uint8 HWC."""
+def _open_encoded(item: Any):
     import io
 
     from PIL import Image
 
     data = item.get("bytes") if isinstance(item, dict) else None
-    src = io.BytesIO(data) if data is not None else item["path"]
-    with Image.open(src) as im:
-        return _to_uint8_hwc(im.convert("RGB") if im.mode not in ("L", "RGB") else im)
+    return Image.open(io.BytesIO(data) if data is not None else item["path"])
+
+
+def _encoded_mode(item: Any) -> str:
+    with _open_encoded(item) as im:
+        return im.mode
+
+
+def _decode_encoded(item: Any, mode: str = "RGB") -> np.ndarray:
+    """A datasets ``Image(decode=False)`` cell ({"bytes", "path"}) -> uint8 HWC
+    in ``mode`` ("RGB": H x W x 3, "L": H x W x 1)."""
+    with _open_encoded(item) as im:
+        return _to_uint8_hwc(im if im.mode == mode else im.convert(mode))
 
 
 class ImageFolderDataset(SplitDataset):

@@ -26,8 +26,10 @@ class ModelFactory:
     dataset: Dataset = ComponentField()
     input_shape: Tuple[int, int, int] = Field()
 
-    # "auto" picks the fused HIP kernels when the extension is loaded and a GPU
-    # is present, otherwise the pure-PyTorch oracle path.
+    # "auto": the fused HIP kernels on a GPU, the pure-PyTorch oracle path on
+    # the CPU.  On a GPU a missing / stale native library raises instead of
+    # quietly running the library (MIOpen / hipBLASLt) path; "torch" (or
+    # ZK_NATIVE=0) selects that path deliberately.
     backend: str = Field("auto")
 
     @Field
@@ -41,7 +43,16 @@ class ModelFactory:
             return self.backend
         from zookeeper_amd import ops
 
-        return "hip" if (torch.cuda.is_available() and ops.available()) else "torch"
+        if not torch.cuda.is_available():
+            return "torch"
+        if ops.available():
+            return "hip"
+        if ops.native_disabled():
+            return "torch"
+        raise RuntimeError(
+            "backend='auto' on a GPU needs the native library, which did not load: "
+            f"{ops.load_error()} (set model.backend='torch' or ZK_NATIVE=0 to run the "
+            "PyTorch path on purpose)")
 
 
 def count_parameters(model: nn.Module) -> int:

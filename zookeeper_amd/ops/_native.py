@@ -12,6 +12,11 @@ Build: ``python -m zookeeper_amd.csrc.build`` (or ``__graft_entry__.build()``).
 If a GPU is present but the library is missing or fails to load, ``lib()``
 raises: GPU code paths never fall back silently.  Set ``ZK_NATIVE=0`` to
 force the pure-PyTorch path deliberately.
+
+Provenance: the build embeds a digest of every kernel / runtime source and
+header (``zk_build_digest``, ``csrc/build.py:source_digest``).  A library
+whose digest differs from the sources next to it is refused (not loaded):
+a stale ``.so`` cannot run kernels other than the ones in the tree.
 """
 
 from __future__ import annotations
@@ -55,10 +60,46 @@ def _load() -> None:
         return
     try:
         lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
-        _declare(lib)
-        _lib = lib
     except OSError as e:
         _load_error = str(e)
+        return
+    stale = _digest_mismatch(lib)
+    if stale:
+        _load_error = stale
+        return
+    _declare(lib)
+    _lib = lib
+
+
+def _digest_mismatch(lib: ctypes.CDLL) -> Optional[str]:
+    """Why ``lib`` does not match the sources in the tree, or None."""
+    from zookeeper_amd.csrc import build as _build
+
+    tree = _build.source_digest()
+    if tree is None:  # no sources shipped next to the package: nothing to compare
+        return None
+    fn = getattr(lib, "zk_build_digest", None)
+    if fn is None:
+        return f"{LIB_PATH} has no build digest (built before provenance checks); rebuild it"
+    fn.restype = ctypes.c_char_p
+    fn.argtypes = []
+    built = fn().decode()
+    if built != tree:
+        return (f"{LIB_PATH} is stale: built from sources with digest {built[:16]}, the tree has "
+                f"{tree[:16]} (run `python -m zookeeper_amd.csrc.build`)")
+    return None
+
+
+def build_digest() -> Optional[str]:
+    """The source digest the loaded library was built from (None: not loaded)."""
+    if not available():
+        return None
+    return _lib.zk_build_digest().decode()
+
+
+def native_disabled() -> bool:
+    """True if the native path was switched off on purpose (``ZK_NATIVE=0``)."""
+    return os.environ.get("ZK_NATIVE", "1") == "0"
 
 
 def available() -> bool:
@@ -124,6 +165,38 @@ def zeroed_scratch(owner, name: str, shape, dtype: torch.dtype,
         buf = torch.zeros(shape, dtype=dtype, device=device)
         cache[name] = buf
     return buf
+
+
+def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Tensor,
+                geom, pad_ones: int, clip: float, stream: int, what: str = "zk_igemm_wgrad",
+                variant: int = -1) -> None:
+    """Split-K implicit-GEMM weight gradient ``dw += mask(|w| <= clip) *
+    dyᵀ ⊛ x`` (``zk_igemm_wgrad``), with the split-K reduction chosen by the
+    run's options:
+
+    * ``runtime.deterministic``: per-split slabs (plain stores) reduced in a
+      fixed order by ``wgrad_reduce_kernel`` -- bit-reproducible;
+    * otherwise (``runtime.wgrad_atomic``, default): every split adds its
+      tile straight into ``dw`` -- the zeroed flat fp32 gradient buffer --
+      with fp32 atomics: no slab write + re-read, no reduce launch, and no
+      slab cap limiting the split count (which held the deep layers' grids
+      under the CU count).
+
+    ``geom`` = (B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl)."""
+    from zookeeper_amd.ops.options import OPTS
+
+    L = lib()
+    B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl = geom
+    ws, ws_bytes = None, 0
+    if OPTS.deterministic or not OPTS.wgrad_atomic:
+        ws_bytes = max(int(L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Ho, Wo, Cout, kh, kw, s, pt,
+                                                     pl, 0, variant)), 0)
+        if ws_bytes > 0:
+            ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=dy.device)
+    check(L.zk_igemm_wgrad(dy.data_ptr(), x.data_ptr(), w.data_ptr(), dw.data_ptr(), B, H, W,
+                           Cin, Ho, Wo, Cout, kh, kw, s, pt, pl, int(pad_ones), float(clip), 0,
+                           variant, ws.data_ptr() if ws is not None else None, ws_bytes, stream),
+          what)
 
 
 def grad_ready(p) -> None:

@@ -16,6 +16,8 @@ FP = C.POINTER(C.c_float)
 IP = C.POINTER(C.c_int)
 
 SIGNATURES = {
+    # build provenance (csrc/build.py embeds the source digest)
+    "zk_build_digest": (C.c_char_p, []),
     # host runtime
     "zk_gather_rows": (I32, [P, I64, P, I64, P, I32]),
     # preprocessing
@@ -33,8 +35,7 @@ SIGNATURES = {
     "zk_igemm_fwd_fp4": (I32, [P, P, P, P] + [I32] * 16 + [P]),
     "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),
     "zk_igemm_wgrad_ws_bytes": (I64, [I32] * 14),
-    "zk_igemm_wgrad_f4": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),
-    "zk_igemm_wgrad_f4_ws_bytes": (I64, [I32] * 14),
+    "zk_wgrad_slab_reduce": (I32, [P, I32, I64, P, F32, P, P]),
     "zk_igemm_dgrad_supported": (I32, [I32] * 13),
     "zk_set_option": (I32, [I32, I32]),
     "zk_bn_bwd_reduce_blocks": (I32, []),
@@ -51,7 +52,8 @@ SIGNATURES = {
     "zk_bn_bwd_dx_res_bf16": (I32, [P, P, P, P, P, P, I64, I32, P]),
     # small-K convolutions (smallconv.hip)
     "zk_smallk_conv_fwd": (I32, [P, P, P] + [I32] * 12 + [P]),
-    "zk_smallk_conv_wgrad": (I32, [P, P, P, P] + [I32] * 12 + [F32, I32, P]),
+    "zk_smallk_conv_wgrad": (I32, [P, P, P, P, P] + [I32] * 12 + [F32, I32, P]),
+    "zk_smallk_conv_wgrad_blocks": (I32, [I32] * 4),
     "zk_band_conv_ok": (I32, [I32] * 10),
     "zk_band_conv_fwd": (I32, [P, P, P] + [I32] * 12 + [P]),
     "zk_band_conv_wgrad_parts": (I32, [I32] * 4),
@@ -61,7 +63,6 @@ SIGNATURES = {
     "zk_bn_apply": (I32, [P, P, P, P, P, I64, I32, P]),
     "zk_bn_apply_sign": (I32, [P, P, P, P, P, P, P, P, F32, I64, I32, P]),
     "zk_bn_bwd_reduce": (I32, [P, P, P, P, P, I64, I32, I32, P]),
-    "zk_bn_bwd_reduce_coef": (I32, [P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P]),
     "zk_bn_bwd_dx": (I32, [P, P, P, P, I64, I32, I32, P]),
     "zk_ste_combine": (I32, [P, P, P, P, I64, P]),
     "zk_bn_bwd_coef": (I32, [P, P, P, P, C.c_double, I32, I32, P, P, P, P]),
@@ -79,7 +80,8 @@ SIGNATURES = {
     # depthwise convolution
     "zk_dw_fwd": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_dw_dgrad": (I32, [P, P, P] + [I32] * 10 + [P]),
-    "zk_dw_wgrad": (I32, [P, P, P] + [I32] * 10 + [P]),
+    "zk_dw_wgrad": (I32, [P, P, P, P] + [I32] * 10 + [P]),
+    "zk_dw_wgrad_blocks": (I32, [I32] * 4),
     # softmax cross-entropy
     "zk_xent_fwd": (I32, [P, P, P, P, P, I32, I32, F32, P, P]),
     "zk_xent_bwd": (I32, [P, P, P, P, P, I32, I32, F32, P]),
@@ -102,7 +104,8 @@ SIGNATURES = {
     "zk_stem_pool_fwd": (I32, [P, P, P, P, P] + [I32] * 10 + [IP, P]),
     "zk_stem_pool_bwd_sums": (I32, [P, P, P, P, P, P] + [I32] * 10 + [IP, P]),
     "zk_stem_dy1": (I32, [P, P, P, P, P, P] + [I32] * 10 + [P]),
-    "zk_stem_wgrad": (I32, [P, P, P] + [I32] * 11 + [P]),
+    "zk_stem_wgrad": (I32, [P, P, P, P] + [I32] * 11 + [P]),
+    "zk_stem_wgrad_splits": (I32, [I32] * 4),
     # recompute-fused stem (stem_fused.hip)
     "zk_stem_fused_blocks": (I32, [I32] * 6),
     "zk_stem_fused_slab_floats": (I32, []),

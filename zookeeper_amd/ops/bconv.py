@@ -27,8 +27,8 @@ from typing import Optional
 
 import torch
 
-from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
-                                        zeroed_scratch)
+from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, igemm_wgrad, lib,
+                                        stream_ptr, zeroed_scratch)
 
 
 # The forward kernels store the exact +-1 dot product as int16: a reduction
@@ -154,13 +154,8 @@ def _backward(ctx, g: torch.Tensor, need_dx: bool, dw: Optional[torch.Tensor]):
                                dxn.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl,
                                -1, st), "zk_igemm_dgrad(binary conv)")
     if dw is not None:
-        ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Ho, Wo, Cout, kh, kw, s, pt, pl, 0, -1)
-        ws = (torch.empty(ws_bytes // 4, dtype=torch.float32, device=dev)
-              if ws_bytes > 0 else None)
-        check(L.zk_igemm_wgrad(g.data_ptr(), sx.data_ptr(), w_ohwi.data_ptr(), dw.data_ptr(),
-                               B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl, pad_ones, kclip,
-                               0, -1, ws.data_ptr() if ws is not None else None,
-                               max(ws_bytes, 0), st), "zk_igemm_wgrad(binary conv)")
+        igemm_wgrad(g, sx, w_ohwi, dw, (B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl), pad_ones,
+                    kclip, st, "zk_igemm_wgrad(binary conv)")
     return dxn
 
 

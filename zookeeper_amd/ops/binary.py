@@ -37,52 +37,41 @@ import torch
 from zookeeper_amd.nn.layers import same_padding
 from zookeeper_amd.ops import streams
 from zookeeper_amd.ops.options import OPTS
-from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
-                                        zeroed_scratch)
+from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, igemm_wgrad, lib,
+                                        stream_ptr, zeroed_scratch)
 
 
 # Copies of the forward BN statistics the conv blocks add into (block b into
 # copy b % STAT_STRIPES; zk_bn_finalize sums them): one [2][Cout] array took
 # thousands of serialised int64 atomics per cache line on the 56x56 layers.
 STAT_STRIPES = 32
-# Variant switches (ops/options.py, set through the Runtime component):
+# Variant switch (ops/options.py, set through the Runtime component):
 #   bconv_fp4  -- binary forward on MX-FP4 MFMA (4x the bf16 rate); off: the
-#                 bf16 MFMA form (same exact integer outputs);
-#   fuse_bnsum -- the BN-backward reduction (sum g, sum g*yhat) of a block
-#                 whose output only feeds the next block's identity shortcut
-#                 + conv is done in that block's dgrad epilogue, which writes
-#                 exactly this gradient (zk_igemm_dgrad_bnsum).  Off: measured
-#                 on MI355X (E18, batch 256) the extra epilogue work on the
-#                 latency-bound dgrad tiles cost more (33.4k -> 31.0k img/s)
-#                 than the separate reduce kernels it removes;
-#   wgrad_f4   -- weight gradients read the e2m1 sign image the MX-FP4
-#                 forward already uses (zk_igemm_wgrad_f4: a quarter of the
-#                 sx bytes, expanded to bf16 +-1 in LDS), and no bf16 sign
-#                 image is written.  Off: the in-LDS expansion costs more
-#                 than the bytes it saves -- 128x128 tiles 217 -> 352 us,
-#                 whole step 40.6k -> 40.1k img/s (batch 512).
+#                 bf16 MFMA form (same exact integer outputs).
+# The BN-backward reduction of a block whose output only feeds the next
+# block's identity shortcut + 64-channel conv is done in that block's
+# row-window dgrad epilogue (runtime.dgrad_rw, zk_igemm_dgrad_bnsum), which
+# writes exactly this gradient.
 
 
 def bwd_stripes() -> int:
-    """Copies of the BN-backward sums: STAT_STRIPES striped atomic copies, or
-    one per reduce block in the deterministic mode."""
-    if OPTS.deterministic:
-        return int(lib().zk_bn_bwd_reduce_blocks())
-    return STAT_STRIPES
+    """Copies of the BN-backward sums: one per reduce block (plain stores,
+    summed in a fixed order by zk_bn_bwd_coef), in every mode.  The sums feed
+    the BN coefficients of the whole data-gradient chain below the layer;
+    with fp32 atomics their run-to-run rounding noise was amplified by the
+    binary blocks into O(1) gradient differences (profiles/r3/g_dp_forced_diag.md).
+    The copies cost 512 x 2 x C floats of plain stores + one read."""
+    return int(lib().zk_bn_bwd_reduce_blocks())
 
 
 def _fp4() -> bool:
     return OPTS.bconv_fp4
 
 
-def _wgrad_f4() -> bool:
-    return OPTS.bconv_fp4 and OPTS.wgrad_f4
-
-
 def bf16_sign_needed() -> bool:
     """Whether producers of a binary block's input (BN epilogues, the stem)
-    must also write the bf16 +-1 sign image."""
-    return not _wgrad_f4()
+    must also write the bf16 +-1 sign image (the weight gradients' operand)."""
+    return True
 
 
 class _BnSum:
@@ -135,17 +124,17 @@ class _BinaryBlockFn(torch.autograd.Function):
         # (K = kh*kw*Cin <= 32767: the exact dot product is stored as int16)
         mfma = (Cout % 64 == 0 and Cin % 64 == 0 and stride <= 2 and kh <= 4 and kw <= 4
                 and kh * kw * Cin <= 32767)
-        FP4, WGRAD_F4 = _fp4(), _wgrad_f4()
+        FP4 = _fp4()
         fp4 = mfma and FP4
         # The previous block may already have quantised this input in its BN
         # epilogue (zk_bn_apply_sign): reuse its sign images and STE mask.
         cached = getattr(x, "_zk_sign", None)
         sx4 = None
-        need_sx = mfma and not (fp4 and WGRAD_F4)  # bf16 sign image (wgrad / bf16 fwd)
+        need_sx = mfma  # bf16 sign image (wgrad / bf16 fwd)
         if (mfma and cached is not None and cached[0] == clip
                 and tuple(cached[2].shape) == (B * H * W * Cin // 32,)
                 and (not need_sx or cached[1] is not None)
-                and (not (fp4 or WGRAD_F4) or (len(cached) > 3 and cached[3] is not None))):
+                and (not fp4 or (len(cached) > 3 and cached[3] is not None))):
             bits, sx, mask = None, cached[1], cached[2]
             sx4 = cached[3] if fp4 else None
         else:
@@ -240,23 +229,24 @@ class _BinaryBlockFn(torch.autograd.Function):
                                 res.data_ptr() if res is not None else None, out.data_ptr(), P,
                                 Cout, st), "zk_bn_apply")
 
-        # BN-backward fusion hand-off (OPTS.fuse_bnsum): this block's reduction
-        # may be done by its successor; the predecessor's by this block.
+        # BN-backward fusion hand-off: this block's reduction may be done by
+        # its successor's row-window dgrad (64 channels, W <= 64: its
+        # persistent blocks add the sums once per block); the predecessor's
+        # by this block.
         ctx.bnsum = None
-        # Always offered when a successor could take the row-window dgrad
-        # (64 channels, W <= 64: its persistent blocks add the sums once per
-        # block, nothing like the per-tile atomics that made fuse_bnsum lose).
         rw_out = OPTS.dgrad_rw and Cout == 64 and Wo <= 64
-        if ((OPTS.fuse_bnsum or rw_out) and not OPTS.deterministic and will_backward
-                and bn.training):
-            sums_buf = zeroed_scratch(bn, "bwd_sums", (STAT_STRIPES, 2, Cout), torch.float32, dev)
+        if rw_out and not OPTS.deterministic and will_backward and bn.training:
+            # one copy per row-window block (fixed-order combination, below
+            # the reduce's 512 copies): the same buffer as the separate reduce
+            sums_buf = zeroed_scratch(bn, "bwd_sums", (bwd_stripes(), 2, Cout), torch.float32,
+                                      dev)
             ctx.bnsum = _BnSum(y, mean, rstd, sums_buf)
             side["bnsum"] = ctx.bnsum
         pred = side.get("pred")
         rw_in = (OPTS.dgrad_rw and Cin == 64 and Cout == 64 and stride == 1 and kh == kw == 3
                  and W <= 64 and pt == pl == 1)
         ctx.pred = (pred if (pred is not None and identity and mfma
-                             and (OPTS.fuse_bnsum or rw_in)
+                             and rw_in
                              and tuple(pred.y.shape) == (B, H, W, Cin)) else None)
         ctx.save_for_backward(bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx, sx4)
         ctx.params = (weight, gamma, beta)
@@ -294,33 +284,19 @@ class _BinaryBlockFn(torch.autograd.Function):
         dbeta = db_direct if db_direct is not None else (
             torch.zeros(Cout, device=dev) if ctx.has_beta else None)
         coef = torch.empty((3, Cout), dtype=torch.float32, device=dev)
-        coef_done = False
         if not (fused and bs.reduced(dout)):
             if fused:
                 sums.zero_()  # the successor reduced a gradient that was accumulated later
-            if OPTS.bn_coef_tail and not OPTS.deterministic:
-                # reduce + coefficients in one launch (the last block finishes)
-                counter = zeroed_scratch(ctx.bn, "bwd_counter", (1,), torch.int32, dev)
-                check(L.zk_bn_bwd_reduce_coef(
-                    g.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                    sums.data_ptr(), P, Cout, stripes, counter.data_ptr(),
-                    gamma.data_ptr() if gamma is not None else None, coef.data_ptr(),
-                    dgamma.data_ptr() if dgamma is not None else None,
-                    dbeta.data_ptr() if dbeta is not None else None, st),
-                    "zk_bn_bwd_reduce_coef")
-                coef_done = True
-            else:
-                check(L.zk_bn_bwd_reduce(g.data_ptr(), y.data_ptr(), mean.data_ptr(),
-                                         rstd.data_ptr(), sums.data_ptr(), P, Cout, stripes, st),
-                      "zk_bn_bwd_reduce")
+            check(L.zk_bn_bwd_reduce(g.data_ptr(), y.data_ptr(), mean.data_ptr(),
+                                     rstd.data_ptr(), sums.data_ptr(), P, Cout, stripes, st),
+                  "zk_bn_bwd_reduce")
         # else: the successor's dgrad epilogue reduced exactly this gradient
-        if not coef_done:
-            check(L.zk_bn_bwd_coef(sums.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                                   gamma.data_ptr() if gamma is not None else None, float(P),
-                                   Cout, stripes, coef.data_ptr(),
-                                   dgamma.data_ptr() if dgamma is not None else None,
-                                   dbeta.data_ptr() if dbeta is not None else None, st),
-                  "zk_bn_bwd_coef")
+        check(L.zk_bn_bwd_coef(sums.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                               gamma.data_ptr() if gamma is not None else None, float(P),
+                               Cout, stripes, coef.data_ptr(),
+                               dgamma.data_ptr() if dgamma is not None else None,
+                               dbeta.data_ptr() if dbeta is not None else None, st),
+              "zk_bn_bwd_coef")
         if dg_direct is not None:
             grad_ready(gamma_p)
             dgamma = None
@@ -339,8 +315,7 @@ class _BinaryBlockFn(torch.autograd.Function):
             # then overlaps this block's dgrad and the next block's backward
             w_direct = direct_grad(weight_p, channels_last=True)
             dweight = None
-            f4 = _wgrad_f4() and sx4 is not None
-            sxw = sx4 if f4 else sx  # weight-gradient sign operand
+            sxw = sx  # weight-gradient sign operand
             side = streams.active() and w_direct is not None and sxw is not None
             if side:
                 sstream = streams.side_stream(dev)
@@ -349,7 +324,7 @@ class _BinaryBlockFn(torch.autograd.Function):
                 sstream.wait_event(ready)
                 with torch.cuda.stream(sstream):
                     _wgrad(L, dy, sxw, w_ohwi, w_direct.permute(0, 2, 3, 1), ctx,
-                           sstream.cuda_stream, f4)
+                           sstream.cuda_stream)
                     done = torch.cuda.Event()
                     done.record(sstream)
                 streams.keep(dy, sxw, w_ohwi)  # released once the compute stream joins
@@ -357,7 +332,7 @@ class _BinaryBlockFn(torch.autograd.Function):
                 dw = (w_direct.permute(0, 2, 3, 1) if w_direct is not None  # OHWI view
                       else torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev))
                 if sxw is not None:
-                    _wgrad(L, dy, sxw, w_ohwi, dw, ctx, st, f4)
+                    _wgrad(L, dy, sxw, w_ohwi, dw, ctx, st)
                 else:
                     check(L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w_ohwi.data_ptr(),
                                            dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
@@ -376,7 +351,8 @@ class _BinaryBlockFn(torch.autograd.Function):
                                                  dres.data_ptr() if dres is not None else None,
                                                  dx.data_ptr(), pred.y.data_ptr(),
                                                  pred.mean.data_ptr(), pred.rstd.data_ptr(),
-                                                 pred.sums.data_ptr(), STAT_STRIPES, B, H, W, Cin,
+                                                 pred.sums.data_ptr(), pred.sums.shape[0], B, H, W,
+                                                 Cin,
                                                  Ho, Wo, Cout, kh, kw, stride, pt, pl, -1, st),
                           "zk_igemm_dgrad_bnsum")
                     pred.dx, pred.dx_version = dx, dx._version
@@ -406,22 +382,14 @@ class _BinaryBlockFn(torch.autograd.Function):
         return dx, dres_out, dweight, dgamma, dbeta, None, None
 
 
-def _wgrad(L, dy, sx, w_ohwi, dw, ctx, st, f4: bool = False) -> None:
+def _wgrad(L, dy, sx, w_ohwi, dw, ctx, st) -> None:
     """Binary-conv weight gradient (dyᵀ ⊛ sign(x), kernel STE mask) added
-    into ``dw`` (OHWI fp32) on stream ``st``: split-K partial sums go to a
-    workspace slab (plain stores) and one reduce kernel adds them, masked.
-    ``f4``: ``sx`` is the e2m1 sign image (zk_igemm_wgrad_f4)."""
+    into ``dw`` (OHWI fp32) on stream ``st`` (split-K reduction:
+    ``_native.igemm_wgrad``)."""
     (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
     (_, _, clip, pad_ones) = ctx.meta[:4]
-    name = "zk_igemm_wgrad_f4" if f4 else "zk_igemm_wgrad"
-    ws_bytes = getattr(L, name + "_ws_bytes")(B, Cin, H, W, Ho, Wo, Cout, kh, kw, stride, pt,
-                                              pl, 0, -1)
-    ws = (torch.empty(max(ws_bytes, 0) // 4, dtype=torch.float32, device=dy.device)
-          if ws_bytes > 0 else None)
-    check(getattr(L, name)(dy.data_ptr(), sx.data_ptr(), w_ohwi.data_ptr(), dw.data_ptr(), B, H,
-                           W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl, int(pad_ones), clip, 0,
-                           -1, ws.data_ptr() if ws is not None else None, max(ws_bytes, 0), st),
-          name)
+    igemm_wgrad(dy, sx, w_ohwi, dw, (B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl),
+                int(pad_ones), clip, st)
 
 
 def _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx):

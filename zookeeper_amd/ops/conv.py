@@ -25,7 +25,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
+from zookeeper_amd.ops._native import check, direct_grad, grad_ready, igemm_wgrad, lib, stream_ptr
 from zookeeper_amd.ops.options import OPTS
 
 _INF = float("inf")
@@ -113,14 +113,8 @@ class _ConvFn(torch.autograd.Function):
             wf = weight.detach().permute(0, 2, 3, 1)
             if wf.dtype != torch.float32 or not wf.is_contiguous():
                 wf = wf.float().contiguous()
-            ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Ho, Wo, Cout, kh, kw, s, pt, pl,
-                                                 0, -1)
-            ws = (torch.empty(ws_bytes // 4, dtype=torch.float32, device=dev)
-                  if ws_bytes > 0 else None)
-            check(L.zk_igemm_wgrad(g.data_ptr(), xn.data_ptr(), wf.data_ptr(), dw.data_ptr(), B,
-                                   H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl, 0, _INF, 0, -1,
-                                   ws.data_ptr() if ws is not None else None, max(ws_bytes, 0),
-                                   st), "zk_igemm_wgrad(conv)")
+            igemm_wgrad(g, xn, wf, dw, (B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl), 0, _INF,
+                        st, "zk_igemm_wgrad(conv)")
             if target is not None:
                 grad_ready(weight)
             else:

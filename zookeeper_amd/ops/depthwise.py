@@ -12,6 +12,7 @@ import torch
 
 from zookeeper_amd.nn.layers import same_padding
 from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
+from zookeeper_amd.ops.options import OPTS
 
 
 def supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -62,8 +63,16 @@ class _DepthwiseFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             target = direct_grad(ctx.param, channels_last=False)
             buf = target if target is not None else torch.zeros(C, 9, device=dy.device)
-            check(lib().zk_dw_wgrad(g.data_ptr(), xn.data_ptr(), buf.data_ptr(), B, H, W, C, Ho,
-                                    Wo, 3, s, pt, pl, st), "zk_dw_wgrad")
+            L = lib()
+            # deterministic mode: per-block partials + fixed-order reduce
+            slab = (torch.zeros((L.zk_dw_wgrad_blocks(B, Ho, Wo, C), C * 9), device=dy.device)
+                    if OPTS.deterministic else None)
+            check(L.zk_dw_wgrad(g.data_ptr(), xn.data_ptr(), buf.data_ptr(),
+                                slab.data_ptr() if slab is not None else None, B, H, W, C, Ho,
+                                Wo, 3, s, pt, pl, st), "zk_dw_wgrad")
+            if slab is not None:
+                check(L.zk_wgrad_slab_reduce(slab.data_ptr(), slab.shape[0], slab.shape[1], None,
+                                             0.0, buf.data_ptr(), st), "zk_wgrad_slab_reduce")
             if target is not None:
                 grad_ready(ctx.param)
             else:

@@ -115,35 +115,24 @@ class _BatchNormFn(torch.autograd.Function):
         st = stream_ptr(dev)
         L = lib()
         g = _nhwc(dy.to(torch.bfloat16))
-        stripes = 1
-        if OPTS.deterministic:
-            # per-block partials (plain stores), summed in block order by
-            # zk_bn_bwd_coef (stripes = parts): bit-reproducible
-            sums = torch.empty((L.zk_bn_bwd_parts_max(), 2, C), dtype=torch.float32, device=dev)
-            n = ctypes.c_int(0)
-            if ctx.relu_rc:
-                check(L.zk_bn_bwd_reduce_relu_bf16_parts(g.data_ptr(), xn.data_ptr(),
-                                                         coef.data_ptr(), sums.data_ptr(), P, C,
-                                                         ctypes.byref(n), st),
-                      "zk_bn_bwd_reduce_relu_bf16_parts")
-            else:
-                check(L.zk_bn_bwd_reduce_bf16_parts(g.data_ptr(), xn.data_ptr(),
-                                                    y.data_ptr() if y is not None else None,
-                                                    coef.data_ptr(), sums.data_ptr(), P, C,
-                                                    ctypes.byref(n), st),
-                      "zk_bn_bwd_reduce_bf16_parts")
-            stripes = n.value
+        # per-block partials (plain stores), summed in block order by
+        # zk_bn_bwd_coef (stripes = parts): bit-reproducible in every mode --
+        # these sums set the BN coefficients of the whole gradient chain below
+        # (and fp32 atomics of 512 blocks into one [2][C] row also contend)
+        sums = torch.empty((L.zk_bn_bwd_parts_max(), 2, C), dtype=torch.float32, device=dev)
+        n = ctypes.c_int(0)
+        if ctx.relu_rc:
+            check(L.zk_bn_bwd_reduce_relu_bf16_parts(g.data_ptr(), xn.data_ptr(),
+                                                     coef.data_ptr(), sums.data_ptr(), P, C,
+                                                     ctypes.byref(n), st),
+                  "zk_bn_bwd_reduce_relu_bf16_parts")
         else:
-            sums = zeroed_scratch(ctx.bn, "bwd_sums", (2, C), torch.float32, dev)
-            if ctx.relu_rc:
-                check(L.zk_bn_bwd_reduce_relu_bf16(g.data_ptr(), xn.data_ptr(), coef.data_ptr(),
-                                                   sums.data_ptr(), P, C, st),
-                      "zk_bn_bwd_reduce_relu_bf16")
-            else:
-                check(L.zk_bn_bwd_reduce_bf16(g.data_ptr(), xn.data_ptr(),
-                                              y.data_ptr() if y is not None else None,
-                                              coef.data_ptr(), sums.data_ptr(), P, C, st),
-                      "zk_bn_bwd_reduce_bf16")
+            check(L.zk_bn_bwd_reduce_bf16_parts(g.data_ptr(), xn.data_ptr(),
+                                                y.data_ptr() if y is not None else None,
+                                                coef.data_ptr(), sums.data_ptr(), P, C,
+                                                ctypes.byref(n), st),
+                  "zk_bn_bwd_reduce_bf16_parts")
+        stripes = n.value
         gamma_p, beta_p = ctx.params
         dg_direct = direct_grad(gamma_p) if ctx.has_gamma else None
         db_direct = direct_grad(beta_p) if ctx.has_beta else None

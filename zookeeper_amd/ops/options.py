@@ -12,7 +12,8 @@ side of a launch (tile rules, K-step order, deterministic reductions); it is
 pushed through ``zk_set_option`` whenever :func:`set_options` runs.
 
 Defaults are the measured winners (README "Round-2 measurements that decided
-defaults").
+defaults").  Variants that measured slower everywhere were deleted, with
+their measurements kept in ``profiles/`` (``profiles/r4/removed_variants.md``).
 """
 
 from __future__ import annotations
@@ -26,21 +27,10 @@ class KernelOptions:
     # Binary forward on MX-FP4 MFMA (4x the bf16 rate); False selects the
     # bf16 MFMA form (same exact integer outputs).
     bconv_fp4: bool = True
-    # BN-backward sums of a block reduced in its successor's dgrad epilogue
-    # (measured slower: 40.7k -> 37.8k img/s at batch 512).
-    fuse_bnsum: bool = False
-    # Weight gradients on the e2m1 sign image (measured slower, 40.6k -> 40.1k).
-    wgrad_f4: bool = False
     # Binary-conv weight gradients on a side HIP stream (44.9k vs 41.7k off).
     wgrad_side_stream: bool = True
     # HIP priority of that side stream (0 = default, negative = higher).
     wgrad_priority: int = 0
-    # HIP priority of the stream the training step runs on (0: the current
-    # stream; negative: a higher-priority stream, so the data-gradient chain's
-    # small kernels are dispatched ahead of queued side-stream work).  E18:
-    # batch 1024, 60 steps 46.97k vs 46.68k img/s; batch 1536, 200 steps
-    # 47.89k vs 48.00k: no gain, default off.
-    compute_priority: int = 0
     # Recompute-fused ImageNet stem (False: the materialising kernels).
     stem_fused: bool = True
     # Float convolutions on the MFMA implicit-GEMM kernels (False: library).
@@ -50,17 +40,12 @@ class KernelOptions:
     pw_gemm: bool = True
     # Batch >= 1024 tile-rule bitmask (igemm.hip, see tile_rule comments).
     tile_huge: int = 16
-    # K-step order of the implicit GEMMs: 0 tap-major, 1 channel-chunk-major.
-    korder: int = 0
     # Bit-reproducible gradients: split-K weight gradients reduced from slabs
     # in a fixed order, BN / bias sums without float atomics.
     deterministic: bool = False
     # Row-window data gradient for the 64 -> 64 stride-1 3x3 binary conv
     # (conv3rw.hip: resident weights, LDS ring of dY rows).
     dgrad_rw: bool = True
-    # Row-window weight gradient for the same layer (conv3rw.hip: the whole
-    # 64 x 576 dW in registers per persistent block, LDS ring of sign rows).
-    wgrad_rw: bool = False
     # Float conv GEMMs with the LDS epilogue also sum the next BatchNorm's
     # batch statistics (pointwise.forward_with_stats; no statistics pass).
     bn_stats_epilogue: bool = True
@@ -72,21 +57,16 @@ class KernelOptions:
     # Same-box sweep at batch 1536: 28 MB 47.52k, 32 MB 47.79k / 47.71k,
     # 36 MB 47.17k, 40 MB 47.46k img/s.
     wgrad_slab_mb: int = 32
-    # The binary BN-backward reduce's last-arriving block also computes the
-    # coefficients and gamma/beta gradients (zk_bn_bwd_reduce_coef): no
-    # separate coef launch in the data-gradient chain.  Measured slower (E18
-    # batch 1536, interleaved 100-step windows on one box: off 47.60k /
-    # 47.65k, on 47.30k / 47.10k img/s): the agent-scope release in every
-    # block and the last block's serial stripe reads cost more than the coef
-    # launch's wait for a CU slot.  Off.
-    bn_coef_tail: bool = False
+    # Split-K weight gradients add into the flat fp32 gradient buffer with
+    # fp32 atomics (no slabs, no reduce launch, no slab cap); False: slabs +
+    # the fixed-order reduce (what runtime.deterministic always uses).
+    wgrad_atomic: bool = True
 
 
 OPTS = KernelOptions()
 
 # keys the native library reads (zk_set_option); values are ints
-_NATIVE_KEYS = {"tile_huge": 0, "korder": 1, "deterministic": 2, "dgrad_rw": 3, "wgrad_rw": 4,
-                "wgrad_slab_mb": 5}
+_NATIVE_KEYS = {"tile_huge": 0, "deterministic": 2, "dgrad_rw": 3, "wgrad_slab_mb": 5}
 
 
 def _push_native() -> None:

@@ -28,8 +28,8 @@ from typing import Optional
 
 import torch
 
-from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
-                                        zeroed_scratch)
+from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, igemm_wgrad, lib,
+                                        stream_ptr, zeroed_scratch)
 from zookeeper_amd.ops.options import OPTS
 
 _INF = float("inf")
@@ -62,6 +62,12 @@ def forward_with_stats(stats_for, x, wt, y, n: int, geom, st) -> bool:
             or not OPTS.bn_stats_epilogue):
         return False
     parts = zeroed_scratch(stats_for, "fstats", (FSTAT_STRIPES, 2, n), torch.float64, y.device)
+    if stats_for.__dict__.pop("_zk_pending_fstats", None) is not None:
+        # the previous GEMM's statistics were never consumed (its output
+        # reached the BatchNorm some other way, or not at all): the
+        # accumulator was not finalised and re-zeroed -- do it here, or this
+        # epilogue would add onto stale sums
+        parts.zero_()
     rc = lib().zk_igemm_dgrad_fstats(x.data_ptr(), wt.data_ptr(), y.data_ptr(), parts.data_ptr(),
                                      FSTAT_STRIPES, *geom, -1, st)
     if rc == _HIP_INVALID_VALUE:
@@ -132,17 +138,12 @@ class _Conv1x1Fn(torch.autograd.Function):
             target = direct_grad(weight)
             dw = target.view(Cout, Cin) if target is not None else torch.zeros(
                 (Cout, Cin), dtype=torch.float32, device=dev)
-            ws_bytes = L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, H, W, Cout, 1, 1, 1, 0, 0, 0, -1)
-            ws = (torch.empty(ws_bytes // 4, dtype=torch.float32, device=dev)
-                  if ws_bytes > 0 else None)
             wf = weight.detach().reshape(Cout, Cin)
             if wf.dtype != torch.float32 or not wf.is_contiguous():
                 wf = wf.float().contiguous()
             # clip = +inf: the kernel's |w| <= clip gradient mask is all-pass
-            check(L.zk_igemm_wgrad(g2.data_ptr(), x2.data_ptr(), wf.data_ptr(), dw.data_ptr(), B,
-                                   H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0, 0, _INF, 0, -1,
-                                   ws.data_ptr() if ws is not None else None, max(ws_bytes, 0),
-                                   st), "zk_igemm_wgrad(1x1)")
+            igemm_wgrad(g2, x2, wf, dw, (B, H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0), 0, _INF, st,
+                        "zk_igemm_wgrad(1x1)")
             if target is not None:
                 grad_ready(weight)
             else:

@@ -29,6 +29,7 @@ from typing import Optional
 import torch
 
 from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
+from zookeeper_amd.ops.options import OPTS
 
 _INF = float("inf")
 
@@ -148,9 +149,22 @@ class _SmallConvFn(torch.autograd.Function):
                                            Cout, kh, kw, s, pt, pl, clip, 0, st),
                       "zk_band_conv_wgrad")
             else:
+                # deterministic mode: per-block partials + fixed-order reduce
+                # instead of fp32 atomics
+                slab = None
+                if OPTS.deterministic:
+                    nb = L.zk_smallk_conv_wgrad_blocks(B, Ho, Wo, 0)
+                    slab = torch.zeros((nb, Cout * kh * kw * Cin), dtype=torch.float32,
+                                       device=dev)
                 check(L.zk_smallk_conv_wgrad(g.data_ptr(), xn.data_ptr(), wf.data_ptr(),
-                                             dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw, s,
-                                             pt, pl, clip, 0, st), "zk_smallk_conv_wgrad")
+                                             dw.data_ptr(),
+                                             slab.data_ptr() if slab is not None else None,
+                                             B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl, clip,
+                                             0, st), "zk_smallk_conv_wgrad")
+                if slab is not None:
+                    check(L.zk_wgrad_slab_reduce(slab.data_ptr(), slab.shape[0], slab.shape[1],
+                                                 wf.data_ptr(), clip, dw.data_ptr(), st),
+                          "zk_wgrad_slab_reduce")
             if target is not None:
                 grad_ready(weight)
             else:

@@ -314,8 +314,17 @@ class _StemFn(torch.autograd.Function):
                 check(L.zk_stem_dy1(dp.data_ptr(), arg.data_ptr(), y1.data_ptr(),
                                     coef1.data_ptr(), bcoef1.data_ptr(), dy1.data_ptr(), B, Ho,
                                     Wo, Cout, H2, W2, pk, ps, pt2, pl2, st), "zk_stem_dy1")
-                check(L.zk_stem_wgrad(dy1.data_ptr(), xp.data_ptr(), dw.data_ptr(), B, Cin, Cout,
-                                      KH, KW, s, Ho, Wo, Hp, Wp, 0, st), "zk_stem_wgrad")
+                # deterministic mode: per-split partials + fixed-order reduce
+                slab = (torch.zeros((L.zk_stem_wgrad_splits(B, Ho, Wo, 0), Cout * KH * KW * Cin),
+                                    dtype=torch.float32, device=dev)
+                        if OPTS.deterministic else None)
+                check(L.zk_stem_wgrad(dy1.data_ptr(), xp.data_ptr(), dw.data_ptr(),
+                                      slab.data_ptr() if slab is not None else None, B, Cin,
+                                      Cout, KH, KW, s, Ho, Wo, Hp, Wp, 0, st), "zk_stem_wgrad")
+                if slab is not None:
+                    check(L.zk_wgrad_slab_reduce(slab.data_ptr(), slab.shape[0], slab.shape[1],
+                                                 None, 0.0, dw.data_ptr(), st),
+                          "zk_wgrad_slab_reduce")
             if target is not None:
                 grad_ready(weight)
             else:

@@ -62,11 +62,16 @@ from zookeeper_amd.parallel.flat import FlatParams
 class GradBucketer:
     def __init__(self, flat: FlatParams, world: int, bucket_mb: float = 10.0,
                  first_bucket_mb: float = 1.0, group=None, grad_dtype: Optional[torch.dtype] = None,
-                 timing: bool = False, force: bool = False):
+                 timing: bool = False, force: bool = False, high_priority: bool = True,
+                 check_order: bool = False):
         """``force``: stay enabled with one rank (needs an initialised
         process group, e.g. a 1-rank RCCL communicator from
         ``zdist.init(single_group=True)``), so a single-GPU run exercises the
-        exact multi-GPU path: comm stream, events, RCCL kernels."""
+        exact multi-GPU path: comm stream, events, RCCL kernels.
+        ``high_priority``: the comm stream is a high-priority HIP stream.
+        ``check_order``: every step, compare the launched bucket sequence
+        across ranks (a MAX and a MIN all-reduce of its hash; raises on a
+        mismatch) -- a debug check that costs a host sync per step."""
         self.flat, self.world, self.group = flat, world, group
         self.grad_dtype = grad_dtype
         limit0 = int(first_bucket_mb * 2**20 / 4)
@@ -104,7 +109,12 @@ class GradBucketer:
             raise RuntimeError("GradBucketer needs an initialised process group "
                                "(zookeeper_amd.parallel.dist.init(single_group=True) for one rank)")
         self.cuda = flat.grad.is_cuda
-        self.comm_stream = torch.cuda.Stream(flat.grad.device) if (self.enabled and self.cuda) else None
+        self.comm_stream = (torch.cuda.Stream(flat.grad.device, priority=-1 if high_priority else 0)
+                            if (self.enabled and self.cuda) else None)
+        self.check_order = bool(check_order) and self.enabled
+        self._order: List[int] = []  # bucket ids in launch order (this step)
+        self.order_checks = 0        # steps whose order was compared across ranks
+        self.last_order: List[int] = []
         self.timing = bool(timing) and self.comm_stream is not None
         # debugging hook only: ZK_COMM_HOST_SYNC=1 synchronises the device
         # before each collective and after the last (isolates stream-ordering
@@ -165,6 +175,7 @@ class GradBucketer:
         return self._step_events
 
     def _launch(self, b: int) -> None:
+        self._order.append(b)
         lo, hi = self.ranges[b]
         view = self.flat.grad[lo:hi]
         if self.comm_stream is None:  # CPU tensors (gloo): plain async collective
@@ -248,10 +259,26 @@ class GradBucketer:
         if self.timing and self._step_events is not None:
             self._timings.append(self._step_events)
             self._step_events = None
+        self.last_order = list(self._order)
+        self._order.clear()
+        if self.check_order:
+            self._compare_order(self.last_order)
         self._works.clear()
         self._pending = [len(b) for b in self.buckets]
         self._launched = [False] * len(self.buckets)
         self._seen = [False] * len(self.flat.slots)
+
+    def _compare_order(self, order: List[int]) -> None:
+        h = order_hash(order)
+        dev = self.flat.grad.device if dist.get_backend(self.group) == "nccl" else "cpu"
+        t = torch.tensor([h, -h], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        hmax, hmin = int(t[0].item()), -int(t[1].item())
+        self.order_checks += 1
+        if hmax != hmin:
+            raise RuntimeError(
+                f"bucket launch order differs across ranks (this rank: {order}, hash {h}; "
+                f"max {hmax}, min {hmin})")
 
     def pop_timings(self) -> List[Dict[str, float]]:
         """Per recorded step: ``comm_ms`` (first collective start → last end),
@@ -283,6 +310,14 @@ class GradBucketer:
         for s in self.flat.slots:
             if hasattr(s.param, "_zk_grad_ready"):
                 del s.param._zk_grad_ready
+
+
+def order_hash(order: List[int]) -> int:
+    """Position-sensitive hash of a bucket sequence (fits in int64)."""
+    h = 1469598103934665603 % (2**61 - 1)
+    for i, b in enumerate(order):
+        h = (h * 1099511628211 + (b + 1) * 1000003 + i) % (2**61 - 1)
+    return h
 
 
 class _DoneWork:

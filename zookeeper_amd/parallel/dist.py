@@ -10,10 +10,42 @@ from __future__ import annotations
 
 import datetime
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
+
+
+@dataclass
+class CommConfig:
+    """How the data-parallel communicator is set up (``Runtime`` fields
+    ``comm_high_priority``, ``rccl_min_channels``, ``rccl_max_channels``,
+    ``cpu_affinity``, ``check_bucket_order``).
+
+    * ``high_priority``: RCCL's internal streams (``ProcessGroupNCCL.Options
+      .is_high_priority_stream``) and the bucketer's comm stream are created
+      at high HIP priority.  The E18 step keeps the compute stream ~99 % and
+      the weight-gradient side stream ~50 % busy; at default priority the
+      all-reduce kernels would wait for CU slots behind both, and a bucket
+      finishing late is exposed time after backward;
+    * ``min_channels`` / ``max_channels`` (0: RCCL's choice): written to
+      ``NCCL_MIN_NCHANNELS`` / ``NCCL_MAX_NCHANNELS`` before the communicator
+      exists.  Each channel is a workgroup resident on a CU for the whole
+      collective; ≤10 MB buckets over xGMI need few channels, and fewer
+      channels leave more CUs to the backward kernels;
+    * ``cpu_affinity``: pin each rank to its share of the CPUs local to its
+      GPU (``parallel/affinity.py``);
+    * ``check_bucket_order``: debug -- every step all-reduces a hash of the
+      launched bucket sequence (MAX and MIN) and raises if the ranks differ
+      (a rank issuing collectives in another order deadlocks or corrupts RCCL).
+    """
+
+    high_priority: bool = True
+    min_channels: int = 0
+    max_channels: int = 0
+    cpu_affinity: bool = True
+    check_bucket_order: bool = False
 
 
 @dataclass
@@ -23,6 +55,9 @@ class DistInfo:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: str = "none"
+    comm: CommConfig = field(default_factory=CommConfig)
+    cpus: Optional[List[int]] = None  # the CPU affinity set at init (None: untouched)
+    rccl_env: dict = field(default_factory=dict)  # NCCL_* knobs in effect at init
 
     @property
     def is_main(self) -> bool:
@@ -40,8 +75,40 @@ def env_world() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
-def init(backend: str = "auto", timeout_s: float = 600.0, single_group: bool = False) -> DistInfo:
+_RCCL_KEYS = ("NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS")
+
+
+def apply_rccl_env(comm: CommConfig, env=None) -> dict:
+    """Write the channel knobs into the environment (before the communicator
+    is created; RCCL reads them at init) and return the ``NCCL_*`` values in
+    effect.  0 leaves RCCL's own choice (or a value the user exported)."""
+    env = os.environ if env is None else env
+    if comm.min_channels > 0:
+        env["NCCL_MIN_NCHANNELS"] = str(int(comm.min_channels))
+    if comm.max_channels > 0:
+        env["NCCL_MAX_NCHANNELS"] = str(int(comm.max_channels))
+    if comm.min_channels > 0 and comm.max_channels > 0 and comm.min_channels > comm.max_channels:
+        raise ValueError(f"rccl_min_channels {comm.min_channels} > rccl_max_channels "
+                         f"{comm.max_channels}")
+    return {k: env[k] for k in _RCCL_KEYS if k in env}
+
+
+def _pg_options(backend: str, comm: CommConfig):
+    if backend != "nccl" or not comm.high_priority:
+        return None
+    opts = dist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = True
+    return opts
+
+
+def init(backend: str = "auto", timeout_s: float = 600.0, single_group: bool = False,
+         comm: Optional[CommConfig] = None) -> DistInfo:
     """Initialise (once) and return the rank / device binding.
+
+    ``comm``: communicator set-up (:class:`CommConfig`; defaults if None):
+    CPU affinity is applied first (sysfs + ``sched_setaffinity`` only, before
+    any thread of the input pipeline or RCCL exists), then the ``NCCL_*``
+    channel knobs, then the process group with high-priority RCCL streams.
 
     ``single_group``: also create a process group when the job has one rank
     (``force_dp``: a 1-rank RCCL communicator, so the bucketed all-reduce
@@ -52,12 +119,21 @@ def init(backend: str = "auto", timeout_s: float = 600.0, single_group: bool = F
     after it instead of blocking forever, and the launcher then tears the job
     down (failure detection)."""
     timeout_s = float(os.environ.get("ZK_DIST_TIMEOUT_S", timeout_s))
+    comm = comm or CommConfig()
     global _INFO
     if _INFO.backend != "none" or (dist.is_available() and dist.is_initialized()):
         return _INFO
     rank = int(os.environ.get("RANK", "0"))
     world = env_world()
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    cpus = None
+    # a GPU job binds to its GPU's NUMA-local CPUs (gloo CPU rehearsals have
+    # no GPU to be local to); device_count goes through amdsmi, not a HIP init
+    if comm.cpu_affinity and torch.cuda.device_count() > 0:
+        from zookeeper_amd.parallel import affinity
+
+        cpus = affinity.apply(local, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
+    rccl_env = apply_rccl_env(comm)
     use_gpu = torch.cuda.is_available()
     if use_gpu:
         torch.cuda.set_device(local % torch.cuda.device_count())
@@ -79,9 +155,13 @@ def init(backend: str = "auto", timeout_s: float = 600.0, single_group: bool = F
                       timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kwargs["device_id"] = device
+            opts = _pg_options(backend, comm)
+            if opts is not None:
+                kwargs["pg_options"] = opts
         dist.init_process_group(**kwargs)
     grouped = world > 1 or single_group
-    _INFO = DistInfo(rank, world, local, device, backend if grouped else "none")
+    _INFO = DistInfo(rank, world, local, device, backend if grouped else "none", comm, cpus,
+                     rccl_env)
     return _INFO
 
 

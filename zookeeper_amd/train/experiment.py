@@ -94,7 +94,7 @@ class TrainingExperiment(Experiment):
         logit_metrics = {k: f for k, f in resolve_metrics(self.metrics).items() if f is not None}
         rt = self.runtime
         rt.apply()
-        info = zdist.init(single_group=rt.force_dp)
+        info = zdist.init(single_group=rt.force_dp, comm=rt.comm_config())
         torch.manual_seed(self.seed)
         if info.is_main:
             print(self, flush=True)

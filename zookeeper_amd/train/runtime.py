@@ -33,22 +33,17 @@ _KERNEL_FIELDS = tuple(f.name for f in dataclasses.fields(_options.KernelOptions
 class Runtime:
     # --- kernel variants (ops/options.py documents each and its measurement)
     bconv_fp4: bool = Field(True)
-    fuse_bnsum: bool = Field(False)
-    wgrad_f4: bool = Field(False)
     wgrad_side_stream: bool = Field(True)
     wgrad_priority: int = Field(0)
-    compute_priority: int = Field(0)
     stem_fused: bool = Field(True)
     conv_mfma: bool = Field(True)
     conv3_mfma: bool = Field(True)
     pw_gemm: bool = Field(True)
     tile_huge: int = Field(16)
-    korder: int = Field(0)
     dgrad_rw: bool = Field(True)
-    wgrad_rw: bool = Field(False)
     bn_stats_epilogue: bool = Field(True)
     wgrad_slab_mb: int = Field(32)
-    bn_coef_tail: bool = Field(False)
+    wgrad_atomic: bool = Field(True)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
     deterministic: bool = Field(False)
@@ -64,9 +59,24 @@ class Runtime:
     # Time every bucket's collective (comm_ms / exposed_ms in metrics.jsonl).
     comm_timing: bool = Field(True)
 
+    # --- data-parallel communicator (parallel/dist.py CommConfig documents each)
+    # RCCL streams and the comm stream at high HIP priority.
+    comm_high_priority: bool = Field(True)
+    # NCCL_MIN_NCHANNELS / NCCL_MAX_NCHANNELS (0: RCCL's default).
+    rccl_min_channels: int = Field(0)
+    rccl_max_channels: int = Field(0)
+    # Pin each rank to its share of its GPU's NUMA-local CPUs.
+    cpu_affinity: bool = Field(True)
+    # Debug: compare the launched bucket order across ranks every step.
+    check_bucket_order: bool = Field(False)
+
     def __post_configure__(self) -> None:
         if self.graph not in ("off", "on", "auto"):
             raise ValueError(f"runtime.graph must be 'off', 'on' or 'auto', got {self.graph!r}")
+        if self.rccl_min_channels < 0 or self.rccl_max_channels < 0:
+            raise ValueError("runtime.rccl_min_channels / rccl_max_channels must be >= 0")
+        if 0 < self.rccl_max_channels < self.rccl_min_channels:
+            raise ValueError("runtime.rccl_min_channels > rccl_max_channels")
 
     def kernel_options(self) -> Dict[str, Any]:
         return {k: getattr(self, k) for k in _KERNEL_FIELDS}
@@ -78,7 +88,21 @@ class Runtime:
     def trainer_graph(self):
         return {"off": False, "on": True, "auto": "auto"}[self.graph]
 
+    def comm_config(self):
+        """The communicator set-up for ``zdist.init(comm=...)``."""
+        from zookeeper_amd.parallel.dist import CommConfig
+
+        return CommConfig(high_priority=self.comm_high_priority,
+                          min_channels=self.rccl_min_channels,
+                          max_channels=self.rccl_max_channels,
+                          cpu_affinity=self.cpu_affinity,
+                          check_bucket_order=self.check_bucket_order)
+
     def as_dict(self) -> Dict[str, Any]:
         d = self.kernel_options()
-        d.update(graph=self.graph, force_dp=self.force_dp, comm_timing=self.comm_timing)
+        d.update(graph=self.graph, force_dp=self.force_dp, comm_timing=self.comm_timing,
+                 comm_high_priority=self.comm_high_priority,
+                 rccl_min_channels=self.rccl_min_channels,
+                 rccl_max_channels=self.rccl_max_channels, cpu_affinity=self.cpu_affinity,
+                 check_bucket_order=self.check_bucket_order)
         return d

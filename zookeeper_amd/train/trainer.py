@@ -18,7 +18,6 @@ import torch
 import torch.nn as nn
 
 from zookeeper_amd.ops import streams
-from zookeeper_amd.ops.options import OPTS
 from zookeeper_amd.parallel import dist as zdist
 from zookeeper_amd.parallel.ddp import GradBucketer
 from zookeeper_amd.parallel.flat import FlatParams
@@ -67,8 +66,11 @@ class Trainer:
                 zdist.broadcast_(b)
         # force_dp: the bucketed all-reduce stays on with one rank (a 1-rank
         # RCCL group), so one GPU runs the exact data-parallel code path
+        comm = self.info.comm
         self.bucketer = GradBucketer(self.flat, self.info.world, bucket_mb, first_bucket_mb,
-                                     grad_dtype=grad_dtype, timing=comm_timing, force=force_dp)
+                                     grad_dtype=grad_dtype, timing=comm_timing, force=force_dp,
+                                     high_priority=comm.high_priority,
+                                     check_order=comm.check_bucket_order)
         self.optimizer = optimizer.create(self.flat, grad_scale=1.0 / self.info.world)
         # HIP-graph replay of zero-grad + forward + loss + backward: one graph
         # launch instead of ~300 kernel launches and the Python / autograd
@@ -94,7 +96,6 @@ class Trainer:
         self._graph = None
         self._static_in = None
         self._static_out = None
-        self._compute_streams: dict = {}  # runtime.compute_priority -> stream
 
     def _forward_backward(self, x: torch.Tensor, y: torch.Tensor):
         self.flat.zero_grad()
@@ -111,23 +112,7 @@ class Trainer:
     def train_step(self, x: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """One training step.  In graph mode the returned tensors are the
         graph's static outputs: overwritten by the next step (consume or
-        clone them before).  ``runtime.compute_priority`` < 0: the step runs
-        on a higher-priority HIP stream, ordered after / before the caller's
-        stream by stream waits."""
-        prio = OPTS.compute_priority
-        if prio == 0 or self.device.type != "cuda":
-            return self._train_step(x, y)
-        cs = self._compute_streams.get(prio)
-        if cs is None:
-            cs = self._compute_streams[prio] = torch.cuda.Stream(self.device, priority=prio)
-        outer = torch.cuda.current_stream(self.device)
-        cs.wait_stream(outer)
-        with torch.cuda.stream(cs):
-            out = self._train_step(x, y)
-        outer.wait_stream(cs)
-        return out
-
-    def _train_step(self, x: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        clone them before)."""
         if not self.graph or self._eager_steps < self.graph_warmup:
             probe = self._graph_auto and self._eager_steps == self.graph_warmup - 1
             if probe:
