@@ -17,10 +17,11 @@ pytestmark = pytest.mark.gpu
 # accepts (tests/test_tile_support.py pins the rule to the native queries)
 DGRAD_SHAPES = [(64, 64, 1, 12), (64, 128, 2, 12), (128, 128, 1, 7), (256, 512, 2, 8),
                 (128, 64, 1, 9), (128, 256, 2, 15), (64, 64, 1, 28), (256, 256, 1, 6),
-                (64, 64, 1, 14)]
+                (64, 64, 1, 14), (256, 128, 1, 11), (512, 64, 1, 5)]
 WGRAD_SHAPES = [(64, 64, 1, 12, 0), (64, 128, 2, 12, 0), (128, 128, 1, 7, 1), (256, 512, 2, 8, 0),
                 (128, 64, 1, 9, 1), (64, 192, 1, 5, 1), (64, 64, 1, 28, 1), (128, 256, 1, 14, 0),
-                (256, 256, 1, 6, 1), (512, 512, 1, 4, 0), (64, 64, 1, 56, 0)]
+                (256, 256, 1, 6, 1), (512, 512, 1, 4, 0), (64, 64, 1, 56, 0),
+                (256, 512, 1, 9, 1), (512, 256, 1, 7, 0)]
 FWD_SHAPES = [(64, 64, 1, 12, 0, 0), (64, 128, 2, 12, 0, 1), (128, 128, 1, 7, 1, 1),
               (256, 512, 2, 8, 0, 0), (128, 64, 1, 9, 1, 0), (512, 128, 1, 5, 0, 1)]
 

@@ -26,6 +26,8 @@ DGRAD: Dict[int, Tuple[int, int, bool]] = {
     32: (64, 64, True), 33: (128, 32, True), 34: (128, 32, True),
     # row-window kernel (conv3rw.hip): 64 -> 64 only, stride 1
     50: (64, 64, True),
+    # phased 256x256 kernel (deep_gemm.hip): stride 1, Cin % 256 == 0
+    60: (256, 128, True),
     # LDS-staged (coalesced) epilogue variants
     40: (128, 128, False), 41: (128, 64, False), 42: (64, 128, False), 43: (64, 64, False),
     44: (128, 128, False), 45: (256, 128, False), 46: (128, 64, False), 47: (256, 64, False),
@@ -53,6 +55,8 @@ WGRAD: Dict[int, Tuple[int, int, bool]] = {
     24: (64, 128, True), 25: (64, 64, True), 26: (128, 128, True), 27: (64, 64, True),
     28: (128, 64, True), 29: (64, 64, True), 30: (64, 64, True), 32: (128, 64, True),
     33: (64, 64, True), 34: (128, 64, True),
+    # phased 256x256 kernel (deep_gemm.hip): stride 1, Cin and Cout % 256 == 0
+    60: (256, 256, True),
 }
 
 
@@ -72,6 +76,8 @@ def dgrad_ok(v: int, cin: int, cout: int, stride: int) -> bool:
     bn, cb, c3 = DGRAD[v]
     if v == 50:
         return stride == 1 and cin == 64 and cout == 64
+    if v == 60:
+        return stride == 1 and cin % 256 == 0 and cout % 64 == 0
     if c3 and not conv3_ok(stride):
         return False
     return (2 * cout) % cb == 0 and cin % bn == 0 and stride <= 2
@@ -90,6 +96,8 @@ def wgrad_ok(v: int, cin: int, cout: int, stride: int) -> bool:
     if v not in WGRAD:
         return False
     bm, bn, c3 = WGRAD[v]
+    if v == 60:
+        return stride == 1 and cin % 256 == 0 and cout % 256 == 0
     if c3:
         return conv3_ok(stride) and cout % bm == 0 and cin % bn == 0
     return cout % bm == 0 and (9 * cin) % bn == 0 and cin % 8 == 0

@@ -51,6 +51,9 @@ def main():
     ap.add_argument("--shapes", default="all", help="all or H+W+Cin+Cout+s/... ('+' or ',')")
     ap.add_argument("--dvariants", default=None, help="dgrad variants to compare (+-separated)")
     ap.add_argument("--wvariants", default=None, help="wgrad variants to compare (+-separated)")
+    ap.add_argument("--wgrad-mode", default="atomic", choices=["atomic", "slab"],
+                    help="split-K reduction: fp32 atomics into dW (default mode) or slabs + "
+                         "the fixed-order reduce (deterministic mode)")
     args = ap.parse_args()
     from zookeeper_amd.models.binary_resnet import stage_shapes
     from zookeeper_amd.nn.layers import same_padding
@@ -58,6 +61,7 @@ def main():
 
     L, st = lib(), stream_ptr()
     B = args.batch
+    slab = args.wgrad_mode == "slab"
     if args.shapes == "all":
         shapes = sorted(set(stage_shapes((224, 224, 3))), key=lambda s: (-s[0], s[2], s[4]))
     else:
@@ -110,7 +114,8 @@ def main():
         def wgrad():
             assert L.zk_igemm_wgrad(dy.data_ptr(), sx.data_ptr(), w.data_ptr(), dw.data_ptr(), B,
                                     H, W, cin, Ho, Ho, cout, 3, 3, s, pt, pt, 0, 1.0, 0,
-                                    args.wvariant, ws.data_ptr(), ws.numel() * 4, st) == 0
+                                    args.wvariant, ws.data_ptr() if slab else None,
+                                    ws.numel() * 4 if slab else 0, st) == 0
 
         # bytes each pass must move through HBM at least
         need = {"fwd4": (S_in / 4 + S_out, FP4_PEAK),        # sx4 in, int16 y out

@@ -28,6 +28,13 @@
 //   * XCD-aware tile order: consecutive M tiles of one N tile share an XCD.
 #include "mfma_common.h"
 
+// deep_gemm.hip: phased 256x256 wgrad of the stride-1 3x3 convs with Cin and
+// Cout % 256 == 0 (variant 60 of the wgrad dispatch)
+int zk_wgrad_deep_impl(const void* dy, const void* sx, const void* w, void* dw, int B, int H,
+                       int W, int Cin, int Cout, int pad_ones, float clip, int target_blocks,
+                       void* slab, long long slab_bytes, long long* need, int* splits, bool dry,
+                       hipStream_t st);
+
 namespace {
 
 // Support queries (zk_igemm_*_supported): every launcher validates the
@@ -95,6 +102,12 @@ int g_opt_dgrad_rw = 1;
 // (splits <= cap / |dW|); 0 = no cap (splits from the block target alone).
 // Default 32 MB (ops/options.py has the measurements).
 int g_opt_wgrad_slab_mb = 32;
+// dgrad_deep (key 6): the phased 256x256 kernel (deep_gemm.hip, variant 60)
+// for stride-1 3x3 data gradients with Cin % 256 == 0.
+int g_opt_dgrad_deep = 1;
+// wgrad_deep (key 7): the same for stride-1 3x3 weight gradients with
+// Cin % 256 == 0 and Cout % 256 == 0 (variant 60 of the wgrad dispatch).
+int g_opt_wgrad_deep = 1;
 
 // splits limited by the slab cap (plan_wgrad / plan_wgrad3)
 inline long long cap_splits(long long splits, long long dw_bytes) {
@@ -1802,6 +1815,17 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
   return launch_igemm_wgrad<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, ws, wsb, need, st)
 #define ZK_IGW3(...) \
   return launch_igemm_wgrad3<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, ws, wsb, need, st)
+  if (v == 60) {  // deep_gemm.hip phased 256x256 kernel + the fixed-order slab reduce
+    if (!conv3_ok(g, 0)) return (int)hipErrorInvalidValue;
+    int splits = 0;
+    const int rc = zk_wgrad_deep_impl(dy, sx, w, dw, g.B, g.H, g.W, g.Cin, g.Cout, po, clip, tb,
+                                      ws, wsb, need, &splits, need != nullptr || g_dry_run, st);
+    if (rc || need || g_dry_run || splits == 0) return rc;
+    const long long n4 = (long long)g.Cout * 9 * g.Cin / 4;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st,
+                       (const float4*)ws, splits, n4, (const float4*)w, clip, (float4*)dw);
+    return 0;
+  }
   switch (v) {
     // conv3 family <BM, BN, WM, WN, BK, NS, TH, OCC>
     case 20: ZK_IGW3(64, 64, 2, 2, 32, 4, 3, 1);
@@ -1840,6 +1864,11 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
 
 }  // namespace
 
+// deep_gemm.hip: phased 256x256 dgrad of the stride-1 3x3 convs with
+// Cin % 256 == 0 (variant 60)
+int zk_dgrad_deep_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
+                       int B, int H, int W, int Cin, int Cout, bool dry, hipStream_t st);
+
 // conv3rw.hip: row-window dgrad of the 64 -> 64 stride-1 3x3 conv (variant 50)
 int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres,
                           void* dx, int B, int H, int W, int Cin, int Cout, const void* ypred,
@@ -1868,7 +1897,9 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     const bool c3 = conv3_ok(g, 0);
     const bool le = bs.sums == nullptr;
     const int v256 = le ? 45 : 14;
-    if (le && g.kh == 1 && g.kw == 1 && stride == 1 && Cin % 64 == 0)
+    if (g_opt_dgrad_deep && le && !bs.fstats && c3 && Cin % 256 == 0 && g.Cout % 64 == 0)
+      variant = 60;  // phased 256x256 schedule (deep_gemm.hip)
+    else if (le && g.kh == 1 && g.kw == 1 && stride == 1 && Cin % 64 == 0)
       variant = Cin % 256 == 0 ? 45 : Cin % 128 == 0 ? 41 : 43;
     else if (Cin == 256 && stride == 1)
       variant = v256;
@@ -1886,6 +1917,11 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
       variant = 0;
     else
       variant = 7;
+  }
+  if (variant == 60) {  // deep_gemm.hip (explicit, or the default above)
+    if (bs.fstats || bs.sums || !conv3_ok(g, 0)) return (int)hipErrorInvalidValue;
+    return zk_dgrad_deep_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Cout, g_dry_run,
+                              stream);
   }
   if (variant == 50) {  // conv3rw.hip (explicit, or the default above)
     if (bs.fstats) return (int)hipErrorInvalidValue;
@@ -1967,7 +2003,10 @@ void wgrad_defaults(const IGeom& g, int& variant, int& target_blocks) {
     // blocks (329 -> 222 us), 7x7x512 on 128x128 at 2048 blocks (392 vs 400).
     const bool c3 = conv3_ok(g, 0);
     const bool big = g.B >= 512, huge = g.B >= 1024;
-    if (c3 && g.Cin == 64 && g.Cout % 64 == 0) {
+    if (g_opt_wgrad_deep && c3 && g.Cin % 256 == 0 && g.Cout % 256 == 0) {
+      variant = 60;  // phased 256x256 schedule (deep_gemm.hip)
+      if (target_blocks <= 0) target_blocks = 512;
+    } else if (c3 && g.Cin == 64 && g.Cout % 64 == 0) {
       variant = 20;
       if (target_blocks <= 0) target_blocks = 512;
     } else if (huge && huge_tiles_env(1) && c3 && g.Cin == 128 && g.Cout % 64 == 0) {
@@ -2195,6 +2234,8 @@ ZK_EXPORT int zk_set_option(int key, int value) {
     case 2: g_opt_deterministic = value; return 0;
     case 3: g_opt_dgrad_rw = value; return 0;
     case 5: g_opt_wgrad_slab_mb = value; return 0;
+    case 6: g_opt_dgrad_deep = value; return 0;
+    case 7: g_opt_wgrad_deep = value; return 0;
     default: return -1;
   }
 }
@@ -2205,6 +2246,8 @@ ZK_EXPORT int zk_get_option(int key) {
     case 2: return g_opt_deterministic;
     case 3: return g_opt_dgrad_rw;
     case 5: return g_opt_wgrad_slab_mb;
+    case 6: return g_opt_dgrad_deep;
+    case 7: return g_opt_wgrad_deep;
     default: return -1;
   }
 }

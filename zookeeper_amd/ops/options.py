@@ -61,12 +61,19 @@ class KernelOptions:
     # fp32 atomics (no slabs, no reduce launch, no slab cap); False: slabs +
     # the fixed-order reduce (what runtime.deterministic always uses).
     wgrad_atomic: bool = True
+    # Phased 256x256 data-gradient kernel (deep_gemm.hip) for the stride-1
+    # 3x3 binary convs with >= 256 input channels.
+    dgrad_deep: bool = True
+    # ... and weight-gradient kernel for the stride-1 3x3 convs with >= 256
+    # input and output channels.
+    wgrad_deep: bool = True
 
 
 OPTS = KernelOptions()
 
 # keys the native library reads (zk_set_option); values are ints
-_NATIVE_KEYS = {"tile_huge": 0, "deterministic": 2, "dgrad_rw": 3, "wgrad_slab_mb": 5}
+_NATIVE_KEYS = {"tile_huge": 0, "deterministic": 2, "dgrad_rw": 3, "wgrad_slab_mb": 5,
+                "dgrad_deep": 6, "wgrad_deep": 7}
 
 
 def _push_native() -> None:

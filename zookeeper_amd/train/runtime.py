@@ -44,6 +44,8 @@ class Runtime:
     bn_stats_epilogue: bool = Field(True)
     wgrad_slab_mb: int = Field(32)
     wgrad_atomic: bool = Field(True)
+    dgrad_deep: bool = Field(True)
+    wgrad_deep: bool = Field(True)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
     deterministic: bool = Field(False)
