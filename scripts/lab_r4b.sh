@@ -12,8 +12,8 @@ timeout -k 10 400 python -u -m pytest tests/gpu/test_bconv_bwd_kernels.py -x -q 
   > "$OUT/r4b_tests.log" 2>&1 || { echo "tests failed $?" >> "$P"; exit 1; }
 echo "tests ok $(date +%T)" >> "$P"
 SH="14+14+256+256+1/7+7+512+512+1"
-timeout -k 10 300 python -u tools/gemm_roofline.py --batch 1536 --ops dgrad --shapes "$SH" \
-  --dvariants=60+45+14 > "$OUT/r4b_dgrad.log" 2>&1 || exit $?
+timeout -k 10 300 python -u tools/gemm_roofline.py --batch 1536 --ops dgrad --shapes "$SH/28+28+128+128+1" \
+  --dvariants=60+45+27 > "$OUT/r4b_dgrad.log" 2>&1 || exit $?
 echo "dgrad done $(date +%T)" >> "$P"
 timeout -k 10 300 python -u tools/gemm_roofline.py --batch 1536 --ops wgrad --shapes "$SH" \
   --wvariants=60+8+12 > "$OUT/r4b_wgrad_atomic.log" 2>&1 || exit $?

@@ -62,7 +62,17 @@ struct DeepDgradArgs {
   int m_tiles;           // 256-pixel tiles
 };
 
+// BNC: input channels per block (256, or 128 for the 128-channel stage):
+// the weight pieces hold BNC rows, a wave's A rows are BNC / 2 in two phase
+// halves of FA = BNC / 64 fragments.
+template <int BNC>
 __global__ __launch_bounds__(DP_NT, 1) void dgrad_deep_kernel(DeepDgradArgs a) {
+  constexpr int WP = BNC * 64;              // weight piece bytes
+  constexpr int BUF = 2 * WP + 2 * DP_PIECE;
+  constexpr int WINS = BNC / 16 / 8;        // weight-piece glds per wave
+  constexpr int FA = BNC / 64;              // A fragments per phase half
+  constexpr int OFF_K1 = WP + DP_PIECE;     // buffer layout: W k0 | dY k0 | W k1 | dY k1
+  constexpr int VM2 = WINS + 2;             // vm ops per wave of one (S, dY) piece pair
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 2, wn = wave & 3;  // ci half, pixel quarter
@@ -71,24 +81,28 @@ __global__ __launch_bounds__(DP_NT, 1) void dgrad_deep_kernel(DeepDgradArgs a) {
   const int mt = L % a.m_tiles, ct = L / a.m_tiles;
   const long long P = (long long)a.B * a.H * a.W;
   const long long m0 = (long long)mt * 256;
-  const int n0 = ct * 256;
+  const int n0 = ct * BNC;
   const int KC = a.Cout >> 6;  // K-tiles per tap
   const int NKT = 9 * KC;
   const long long rowb = (long long)a.Cout * 2;  // bytes per dY / S row
 
-  // ---- loader: instruction i (0, 1) of wave w fills piece rows (i*8 + w)*16
-  // .. +15; lane l -> row l >> 2, LDS slot l & 3 holding global chunk
+  // ---- loader: instruction i of wave w fills piece rows (i*8 + w)*16 ..
+  // +15; lane l -> row l >> 2, LDS slot l & 3 holding global chunk
   // (l & 3) ^ f(row)
   const int lrow = lane >> 2, lslot = lane & 3;
   const int gch = lslot ^ dp_swz(lrow);
   const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page) + gch * 16;
-  const unsigned char* wsrc[2];  // S row ci, tap 0, k 0
-  const unsigned char* dsrc[2];  // dY row of the pixel itself (tap (1, 1)), k 0
-  uint32_t vh[2], vw[2];         // bit th / tw: the tap's source row / column is inside the image
+  const unsigned char* wsrc[WINS];  // S row ci, tap 0, k 0
+  const unsigned char* dsrc[2];     // dY row of the pixel itself (tap (1, 1)), k 0
+  uint32_t vh[2], vw[2];            // bit th / tw: the tap's source row / column is inside the image
+#pragma unroll
+  for (int i = 0; i < WINS; ++i) {
+    const int r = (i * 8 + wave) * 16 + lrow;
+    wsrc[i] = reinterpret_cast<const unsigned char*>(a.wt) + (long long)(n0 + r) * rowb + gch * 16;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int r = (i * 8 + wave) * 16 + lrow;
-    wsrc[i] = reinterpret_cast<const unsigned char*>(a.wt) + (long long)(n0 + r) * rowb + gch * 16;
     const long long m = m0 + r;
     vh[i] = vw[i] = 0;
     dsrc[i] = reinterpret_cast<const unsigned char*>(a.dy) + gch * 16;
@@ -105,51 +119,53 @@ __global__ __launch_bounds__(DP_NT, 1) void dgrad_deep_kernel(DeepDgradArgs a) {
     }
   }
   const long long wtap = (long long)a.Cin * rowb;  // S bytes per tap
-  // piece p of K-tile kt into buffer kt & 1
+  // piece p of K-tile kt into buffer kt & 1: p even = S, odd = dY; p >> 1 =
+  // which 32 output channels of the 64
   auto issue = [&](int kt, int p) {
     const int tap = kt / KC, kc = kt - tap * KC;
     const int th = tap / 3, tw = tap - th * 3;
     const int koff = kc * 128 + (p >> 1) * 64;
-    unsigned char* dst = smem + (kt & 1) * DP_BUF + p * DP_PIECE;
+    unsigned char* buf = smem + (kt & 1) * BUF + (p >> 1) * OFF_K1;
     if ((p & 1) == 0) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) glds16(wsrc[i] + tap * wtap + koff, dst + (i * 8 + wave) * 1024);
+      for (int i = 0; i < WINS; ++i)
+        glds16(wsrc[i] + tap * wtap + koff, buf + (i * 8 + wave) * 1024);
     } else {
       const long long toff = ((long long)(1 - th) * a.W + (1 - tw)) * rowb;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const bool ok = (vh[i] >> th) & (vw[i] >> tw) & 1u;
-        glds16(ok ? dsrc[i] + toff + koff : zp, dst + (i * 8 + wave) * 1024);
+        glds16(ok ? dsrc[i] + toff + koff : zp, buf + WP + (i * 8 + wave) * 1024);
       }
     }
   };
 
   // ---- fragments: lane l reads row l & 15, chunk l >> 4 of a 16-row block
   const int foff = (lane & 15) * 64 + (((lane >> 4) ^ dp_swz(lane & 15)) << 4);
-  const int arow0 = wm * 128, brow0 = wn * 64;
-  f32x4 acc[8][4];
+  const int arow0 = wm * (BNC / 2), brow0 = wn * 64;
+  f32x4 acc[2 * FA][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 2 * FA; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 a1[4], a2[4], b1[4], b2[4];
-  auto readA = [&](uint4 (&d)[4], int kt, int kh, int mh) {
+  uint4 a1[FA], a2[FA], b1[4], b2[4];
+  auto readA = [&](uint4 (&d)[FA], int kt, int kh, int mh) {
     const unsigned char* base =
-        smem + (kt & 1) * DP_BUF + (kh * 2) * DP_PIECE + (arow0 + mh * 64) * 64 + foff;
+        smem + (kt & 1) * BUF + kh * OFF_K1 + (arow0 + mh * (BNC / 4)) * 64 + foff;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) d[i] = *reinterpret_cast<const uint4*>(base + i * 1024);
+    for (int i = 0; i < FA; ++i) d[i] = *reinterpret_cast<const uint4*>(base + i * 1024);
   };
   auto readB = [&](uint4 (&d)[4], int kt, int kh) {
-    const unsigned char* base = smem + (kt & 1) * DP_BUF + (kh * 2 + 1) * DP_PIECE + brow0 * 64 + foff;
+    const unsigned char* base = smem + (kt & 1) * BUF + kh * OFF_K1 + WP + brow0 * 64 + foff;
 #pragma unroll
     for (int j = 0; j < 4; ++j) d[j] = *reinterpret_cast<const uint4*>(base + j * 1024);
   };
-  auto mma = [&](const uint4 (&x)[4], const uint4 (&y)[4], int mh) {
+  auto mma = [&](const uint4 (&x)[FA], const uint4 (&y)[4], int mh) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FA; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[mh * 4 + i][j] = dp_mfma(x[i], y[j], acc[mh * 4 + i][j]);
+      for (int j = 0; j < 4; ++j) acc[mh * FA + i][j] = dp_mfma(x[i], y[j], acc[mh * FA + i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -157,22 +173,22 @@ __global__ __launch_bounds__(DP_NT, 1) void dgrad_deep_kernel(DeepDgradArgs a) {
   // waits for its first two pieces
 #pragma unroll
   for (int p = 0; p < 4; ++p) issue(0, p);
-  wait_vmcnt<4>();
+  wait_vmcnt<VM2>();
   dp_barrier();
   readA(a1, 0, 0, 0);
   readB(b1, 0, 0);
   for (int kt = 0; kt < NKT; ++kt) {
     const bool more = kt + 1 < NKT;
-    // phase 0: (k0, ci rows 0-63 of the wave) with a1 b1
+    // phase 0: (k0, first half of the wave's ci rows) with a1 b1
     if (more) issue(kt + 1, 0);
     readA(a2, kt, 0, 1);
     __builtin_amdgcn_sched_barrier(0);
     mma(a1, b1, 0);
     __builtin_amdgcn_sched_barrier(0);
-    // phase 1: (k0, rows 64-127) with a2 b1; pieces 2, 3 of K-tile kt land
+    // phase 1: (k0, second half) with a2 b1; pieces 2, 3 of K-tile kt land
     if (more) {
       issue(kt + 1, 1);
-      wait_vmcnt<4>();
+      wait_vmcnt<VM2>();
     } else {
       wait_vmcnt<0>();
     }
@@ -182,16 +198,16 @@ __global__ __launch_bounds__(DP_NT, 1) void dgrad_deep_kernel(DeepDgradArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     mma(a2, b1, 1);
     __builtin_amdgcn_sched_barrier(0);
-    // phase 2: (k1, rows 0-63) with a1 b2
+    // phase 2: (k1, first half) with a1 b2
     if (more) issue(kt + 1, 2);
     readA(a2, kt, 1, 1);
     __builtin_amdgcn_sched_barrier(0);
     mma(a1, b2, 0);
     __builtin_amdgcn_sched_barrier(0);
-    // phase 3: (k1, rows 64-127) with a2 b2; pieces 0, 1 of K-tile kt + 1 land
+    // phase 3: (k1, second half) with a2 b2; pieces 0, 1 of K-tile kt + 1 land
     if (more) {
       issue(kt + 1, 3);
-      wait_vmcnt<4>();
+      wait_vmcnt<VM2>();
       dp_barrier();
       readA(a1, kt + 1, 0, 0);
       readB(b1, kt + 1, 0);
@@ -209,17 +225,17 @@ __global__ __launch_bounds__(DP_NT, 1) void dgrad_deep_kernel(DeepDgradArgs a) {
   for (int j = 0; j < 4; ++j) {
     const long long pix = m0 + brow0 + 16 * j + (lane & 15);
     if (pix >= P) continue;
-    uint32_t mw[4];
-    uint2 dv[8];
+    uint32_t mw[FA];
+    uint2 dv[2 * FA];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 2 * FA; ++i) {
       const int ci = n0 + arow0 + 16 * i + cq;
       if ((i & 1) == 0) mw[i >> 1] = a.mask ? a.mask[pix * CW + (ci >> 5)] : 0xFFFFFFFFu;
       dv[i] = a.dres ? *reinterpret_cast<const uint2*>(a.dres + pix * a.Cin + ci)
                      : make_uint2(0u, 0u);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 2 * FA; ++i) {
       const int ci = n0 + arow0 + 16 * i + cq;
       const uint32_t bits = mw[i >> 1] >> (ci & 31);
       float v[4];
@@ -436,6 +452,7 @@ __global__ __launch_bounds__(DP_NT, 1) void wgrad_deep_kernel(DeepWgradArgs a) {
 }
 
 bool g_dp_attr = false;
+bool g_dp_attr128 = false;
 bool g_wp_attr = false;
 
 }  // namespace
@@ -493,27 +510,40 @@ int zk_wgrad_deep_impl(const void* dy, const void* sx, const void* w, void* dw, 
 }
 
 // Entry used by igemm.hip's dgrad dispatch (variant 60): stride-1 3x3 'same'
-// (pad 1) data gradient, Cin % 256 == 0, Cout % 64 == 0; mask / dres
-// optional.  dry: validate only.
+// (pad 1) data gradient, Cin % 128 == 0 (256-channel blocks when Cin % 256 ==
+// 0), Cout % 64 == 0; mask / dres optional.  dry: validate only.
 int zk_dgrad_deep_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
                        int B, int H, int W, int Cin, int Cout, bool dry, hipStream_t st) {
-  if (Cin % 256 || Cout % 64 || Cout < 64 || B < 1 || H < 1 || W < 1)
+  if (Cin % 128 || Cout % 64 || Cout < 64 || B < 1 || H < 1 || W < 1)
     return (int)hipErrorInvalidValue;
   const long long P = (long long)B * H * W;
   if (P * Cin >= (1LL << 40) || P * Cout >= (1LL << 40)) return (int)hipErrorInvalidValue;
+  const int bnc = Cin % 256 == 0 ? 256 : 128;
   const long long m_tiles = (P + 255) / 256;
-  const long long blocks = m_tiles * (Cin / 256);
+  const long long blocks = m_tiles * (Cin / bnc);
   if (blocks >= (1LL << 31)) return (int)hipErrorInvalidValue;
   if (dry) return 0;
-  if (!g_dp_attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)dgrad_deep_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, DP_LDS);
-    if (e != hipSuccess) return (int)e;
-    g_dp_attr = true;
-  }
   DeepDgradArgs a{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
                   (const uint16_t*)dres, (uint16_t*)dx, B, H, W, Cin, Cout, (int)m_tiles};
   (void)hipGetLastError();
-  hipLaunchKernelGGL(dgrad_deep_kernel, dim3((unsigned)blocks), dim3(DP_NT), DP_LDS, st, a);
+  if (bnc == 256) {
+    constexpr int lds = 2 * (2 * 256 * 64 + 2 * DP_PIECE);
+    if (!g_dp_attr) {
+      const hipError_t e = hipFuncSetAttribute((const void*)dgrad_deep_kernel<256>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e != hipSuccess) return (int)e;
+      g_dp_attr = true;
+    }
+    hipLaunchKernelGGL(dgrad_deep_kernel<256>, dim3((unsigned)blocks), dim3(DP_NT), lds, st, a);
+  } else {
+    constexpr int lds = 2 * (2 * 128 * 64 + 2 * DP_PIECE);
+    if (!g_dp_attr128) {
+      const hipError_t e = hipFuncSetAttribute((const void*)dgrad_deep_kernel<128>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e != hipSuccess) return (int)e;
+      g_dp_attr128 = true;
+    }
+    hipLaunchKernelGGL(dgrad_deep_kernel<128>, dim3((unsigned)blocks), dim3(DP_NT), lds, st, a);
+  }
   return (int)hipGetLastError();
 }

@@ -102,8 +102,8 @@ int g_opt_dgrad_rw = 1;
 // (splits <= cap / |dW|); 0 = no cap (splits from the block target alone).
 // Default 32 MB (ops/options.py has the measurements).
 int g_opt_wgrad_slab_mb = 32;
-// dgrad_deep (key 6): the phased 256x256 kernel (deep_gemm.hip, variant 60)
-// for stride-1 3x3 data gradients with Cin % 256 == 0.
+// dgrad_deep (key 6): the phased kernel (deep_gemm.hip, variant 60) for
+// stride-1 3x3 data gradients with Cin % 128 == 0.
 int g_opt_dgrad_deep = 1;
 // wgrad_deep (key 7): the same for stride-1 3x3 weight gradients with
 // Cin % 256 == 0 and Cout % 256 == 0 (variant 60 of the wgrad dispatch).
@@ -1864,8 +1864,8 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
 
 }  // namespace
 
-// deep_gemm.hip: phased 256x256 dgrad of the stride-1 3x3 convs with
-// Cin % 256 == 0 (variant 60)
+// deep_gemm.hip: phased 256x256 (256x128) dgrad of the stride-1 3x3 convs
+// with Cin % 128 == 0 (variant 60)
 int zk_dgrad_deep_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
                        int B, int H, int W, int Cin, int Cout, bool dry, hipStream_t st);
 
@@ -1897,7 +1897,7 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     const bool c3 = conv3_ok(g, 0);
     const bool le = bs.sums == nullptr;
     const int v256 = le ? 45 : 14;
-    if (g_opt_dgrad_deep && le && !bs.fstats && c3 && Cin % 256 == 0 && g.Cout % 64 == 0)
+    if (g_opt_dgrad_deep && le && !bs.fstats && c3 && Cin % 128 == 0 && g.Cout % 64 == 0)
       variant = 60;  // phased 256x256 schedule (deep_gemm.hip)
     else if (le && g.kh == 1 && g.kw == 1 && stride == 1 && Cin % 64 == 0)
       variant = Cin % 256 == 0 ? 45 : Cin % 128 == 0 ? 41 : 43;

@@ -61,8 +61,8 @@ class KernelOptions:
     # fp32 atomics (no slabs, no reduce launch, no slab cap); False: slabs +
     # the fixed-order reduce (what runtime.deterministic always uses).
     wgrad_atomic: bool = True
-    # Phased 256x256 data-gradient kernel (deep_gemm.hip) for the stride-1
-    # 3x3 binary convs with >= 256 input channels.
+    # Phased data-gradient kernel (deep_gemm.hip) for the stride-1 3x3
+    # binary convs with >= 128 input channels.
     dgrad_deep: bool = True
     # ... and weight-gradient kernel for the stride-1 3x3 convs with >= 256
     # input and output channels.
