@@ -43,6 +43,14 @@ def test_bench_self_spawns_ranks(n):
     # a gloo/CPU rehearsal never carries the bare headline metric string
     assert rec["metric"].startswith("rehearsal")
     assert rec["config"]["dist_backend"] == "gloo"
+    # the driver-timed default streams data through the host pipeline, and
+    # the communicator set-up is recorded
+    assert rec["config"]["data_path"] == "stream"
+    comm = rec["config"]["comm"]
+    assert comm["bucket_mb"] == 10.0 and sum(comm["bucket_sizes_mb"]) > 0
+    for k in ("comm_high_priority", "rccl_min_channels", "rccl_max_channels", "cpu_affinity",
+              "check_bucket_order"):
+        assert k in rec["config"]["runtime"]
 
 
 @pytest.mark.timeout(120)
