@@ -53,7 +53,8 @@ def run(mode: str, out: str) -> None:
                        else int(v)})
     # ZK_TEST_CHECK_ORDER=1: every step compares the launched bucket order
     # across ranks (runtime.check_bucket_order)
-    comm = zdist.CommConfig(check_bucket_order=os.environ.get("ZK_TEST_CHECK_ORDER", "0") == "1")
+    comm = zdist.CommConfig(check_bucket_order=os.environ.get("ZK_TEST_CHECK_ORDER", "0") == "1",
+                            backend=os.environ.get("ZK_TEST_COMM", "torch"))
     if world > 1 or force:
         info = zdist.init(backend, single_group=force, comm=comm)
     else:
@@ -93,6 +94,7 @@ def run(mode: str, out: str) -> None:
                 "slots": [(sl.name, sl.offset, sl.numel) for sl in tr.flat.slots],
                 "ranges": list(tr.bucketer.ranges),
                 "order_checks": tr.bucketer.order_checks,
+                "native": tr.bucketer.native is not None,
                 "last_order": list(tr.bucketer.last_order)},
                os.path.join(out, f"{mode}_w{world}{'dp' if force else ''}_r{info.rank}.pt"))
     zdist.shutdown()

@@ -25,10 +25,10 @@ WORKER = os.path.join(os.path.dirname(HERE), "dp_gpu_worker.py")
 
 
 def _run(mode, out, nproc, side="1", graph="0", force="0", backend="gloo", rt="",
-         check_order="0"):
+         check_order="0", comm="torch"):
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4", ZK_TEST_SIDE=side,
                ZK_TEST_GRAPH=graph, ZK_TEST_FORCE_DP=force, ZK_TEST_BACKEND=backend,
-               ZK_TEST_RT=rt, ZK_TEST_CHECK_ORDER=check_order)
+               ZK_TEST_RT=rt, ZK_TEST_CHECK_ORDER=check_order, ZK_TEST_COMM=comm)
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     if nproc == 1:
@@ -127,3 +127,22 @@ def test_rccl_single_rank_forced_dp_matches_plain_run(tmp_path, side, graph, mod
     assert (ref["params"] - ref["init"]).norm().item() > 0
     # a 1-rank all-reduce is the identity and nothing else differs
     _close(dp["params"], ref["params"], exact)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("graph", ["0", "1"], ids=["eager", "graph"])
+def test_native_rccl_communicator_forced_dp_matches_plain_run(tmp_path, graph):
+    """runtime.comm_backend="native": the bucketed all-reduce through the
+    in-tree RCCL communicator (parallel/rccl.py, runtime/comm.cpp), issued
+    straight onto the comm stream; with graph replay the collectives are
+    captured INTO the graph with the backward.  One rank (a 1-rank RCCL
+    communicator), deterministic mode: bit-equal to the plain run."""
+    rt = "deterministic=1"
+    assert _run("same", tmp_path, 1, "1", graph, rt=rt) == 0
+    assert _run("same", tmp_path, 1, "1", graph, force="1", backend="nccl", rt=rt,
+                comm="native") == 0
+    ref = torch.load(tmp_path / "same_w1_r0.pt", weights_only=True)
+    dp = torch.load(tmp_path / "same_w1dp_r0.pt", weights_only=True)
+    assert dp["native"] and dp["bucketer"]
+    assert dp["graph"] == (graph == "1")
+    torch.testing.assert_close(dp["params"], ref["params"], atol=0, rtol=0)

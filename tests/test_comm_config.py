@@ -127,3 +127,32 @@ def test_bucket_order_check_two_ranks(tmp_path):
     assert r[0]["checks"] == r[1]["checks"] == 3  # one per training step
     assert r[0]["order"] == r[1]["order"] and len(r[0]["order"]) > 1
     assert r[0]["flagged"] and r[1]["flagged"]
+
+
+def test_native_communicator_binding_on_cpu():
+    """The in-tree RCCL binding resolves torch's bundled librccl by path and
+    creates unique ids without a GPU (the communicator itself needs one:
+    tests/gpu/test_native_comm.py)."""
+    from zookeeper_amd.ops import _native
+    from zookeeper_amd.parallel import rccl
+
+    if not _native.available():
+        pytest.skip(_native.load_error())
+    if rccl.rccl_path() is None:
+        pytest.skip("torch ships no librccl")
+    rccl.load()
+    assert _native.lib().zk_comm_loaded() == 1
+    a, b = rccl.unique_id(), rccl.unique_id()
+    assert len(a) == 128 and a != b
+    assert rccl.DTYPES[torch.float32] == 7 and rccl.OPS["sum"] == 0
+
+
+def test_runtime_comm_backend_field():
+    from zookeeper_amd import configure
+    from zookeeper_amd.train.runtime import Runtime
+
+    rt = Runtime()
+    configure(rt, {"comm_backend": "native"})
+    assert rt.comm_config().backend == "native" and rt.as_dict()["comm_backend"] == "native"
+    with pytest.raises(ValueError):
+        configure(Runtime(), {"comm_backend": "mpi"})

@@ -150,7 +150,7 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
     if force or not _key_ok(OUT, link_key):
         tmp = OUT + ".tmp"
         cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp, *objs,
-               "-lpthread"]
+               "-lpthread", "-ldl"]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")

@@ -20,6 +20,17 @@ SIGNATURES = {
     "zk_build_digest": (C.c_char_p, []),
     # host runtime
     "zk_gather_rows": (I32, [P, I64, P, I64, P, I32]),
+    # native RCCL communicator (runtime/comm.cpp; parallel/rccl.py)
+    "zk_comm_load": (I32, [C.c_char_p]),
+    "zk_comm_loaded": (I32, []),
+    "zk_comm_unique_id": (I32, [P]),
+    "zk_comm_init": (I32, [P, I32, I32, P]),
+    "zk_comm_count": (I32, [P, P]),
+    "zk_comm_all_reduce": (I32, [P, P, P, I64, I32, I32, P]),
+    "zk_comm_broadcast": (I32, [P, P, P, I64, I32, I32, P]),
+    "zk_comm_group_start": (I32, []),
+    "zk_comm_group_end": (I32, []),
+    "zk_comm_destroy": (I32, [P, I32]),
     # preprocessing
     "zk_normalize_flip_c3": (I32, [P, P, I32, I32, I32, FP, FP, I32, U64, P]),
     # binary convolution

@@ -63,7 +63,7 @@ class GradBucketer:
     def __init__(self, flat: FlatParams, world: int, bucket_mb: float = 10.0,
                  first_bucket_mb: float = 1.0, group=None, grad_dtype: Optional[torch.dtype] = None,
                  timing: bool = False, force: bool = False, high_priority: bool = True,
-                 check_order: bool = False):
+                 check_order: bool = False, native_comm=None):
         """``force``: stay enabled with one rank (needs an initialised
         process group, e.g. a 1-rank RCCL communicator from
         ``zdist.init(single_group=True)``), so a single-GPU run exercises the
@@ -71,7 +71,11 @@ class GradBucketer:
         ``high_priority``: the comm stream is a high-priority HIP stream.
         ``check_order``: every step, compare the launched bucket sequence
         across ranks (a MAX and a MIN all-reduce of its hash; raises on a
-        mismatch) -- a debug check that costs a host sync per step."""
+        mismatch) -- a debug check that costs a host sync per step.
+        ``native_comm``: a :class:`~zookeeper_amd.parallel.rccl.NativeComm`
+        that issues the all-reduces onto the comm stream itself (instead of
+        ProcessGroupNCCL); the collectives are then graph-capturable
+        (:attr:`capturable`)."""
         self.flat, self.world, self.group = flat, world, group
         self.grad_dtype = grad_dtype
         limit0 = int(first_bucket_mb * 2**20 / 4)
@@ -112,6 +116,7 @@ class GradBucketer:
         self.comm_stream = (torch.cuda.Stream(flat.grad.device, priority=-1 if high_priority else 0)
                             if (self.enabled and self.cuda) else None)
         self.check_order = bool(check_order) and self.enabled
+        self.native = native_comm if (self.enabled and self.cuda) else None
         self._order: List[int] = []  # bucket ids in launch order (this step)
         self.order_checks = 0        # steps whose order was compared across ranks
         self.last_order: List[int] = []
@@ -129,7 +134,8 @@ class GradBucketer:
         # staging streams raced with the compute stream on this ROCm build,
         # tools/dp_order_diag.py)
         self._stager = None
-        if self.enabled and self.cuda and dist.get_backend(group) != "nccl":
+        if (self.enabled and self.cuda and self.native is None
+                and dist.get_backend(group) != "nccl"):
             self._stager = _HostStager(flat.total, group)
         if self.enabled:
             for i, s in enumerate(flat.slots):
@@ -142,6 +148,22 @@ class GradBucketer:
     @property
     def num_buckets(self) -> int:
         return len(self.buckets)
+
+    @property
+    def capturable(self) -> bool:
+        """The collectives can be captured into a HIP graph with the backward
+        (native communicator: plain stream work, no work objects)."""
+        return self.native is not None
+
+    @contextlib.contextmanager
+    def untimed(self):
+        """No timing events (they cannot be recorded inside a graph capture)."""
+        old = self.timing
+        self.timing = False
+        try:
+            yield
+        finally:
+            self.timing = old
 
     @contextlib.contextmanager
     def suspended(self):
@@ -216,6 +238,11 @@ class GradBucketer:
         self._launched[b] = True
 
     def _issue(self, view: torch.Tensor):
+        if self.native is not None:
+            # onto the comm stream (current here): ordered by the stream alone
+            buf = view if self.grad_dtype in (None, view.dtype) else view.to(self.grad_dtype)
+            self.native.all_reduce_(buf, stream=self.comm_stream)
+            return (_DoneWork(), buf if buf is not view else None)
         if self.grad_dtype is not None and self.grad_dtype != view.dtype:
             tmp = view.to(self.grad_dtype)
             return (dist.all_reduce(tmp, group=self.group, async_op=True), tmp)

@@ -38,7 +38,11 @@ class CommConfig:
       GPU (``parallel/affinity.py``);
     * ``check_bucket_order``: debug -- every step all-reduces a hash of the
       launched bucket sequence (MAX and MIN) and raises if the ranks differ
-      (a rank issuing collectives in another order deadlocks or corrupts RCCL).
+      (a rank issuing collectives in another order deadlocks or corrupts RCCL);
+    * ``backend``: ``"torch"`` -- the gradient all-reduce through
+      ProcessGroupNCCL (RCCL behind work objects); ``"native"`` -- through the
+      in-tree RCCL communicator (``parallel/rccl.py``), straight onto the comm
+      stream, which also lets a HIP graph capture the collectives.
     """
 
     high_priority: bool = True
@@ -46,6 +50,7 @@ class CommConfig:
     max_channels: int = 0
     cpu_affinity: bool = True
     check_bucket_order: bool = False
+    backend: str = "torch"
 
 
 @dataclass

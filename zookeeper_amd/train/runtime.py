@@ -71,6 +71,9 @@ class Runtime:
     cpu_affinity: bool = Field(True)
     # Debug: compare the launched bucket order across ranks every step.
     check_bucket_order: bool = Field(False)
+    # Gradient all-reduce transport: "torch" (ProcessGroupNCCL) or "native"
+    # (parallel/rccl.py: the in-tree RCCL communicator; graph-capturable).
+    comm_backend: str = Field("torch")
 
     def __post_configure__(self) -> None:
         if self.graph not in ("off", "on", "auto"):
@@ -79,6 +82,9 @@ class Runtime:
             raise ValueError("runtime.rccl_min_channels / rccl_max_channels must be >= 0")
         if 0 < self.rccl_max_channels < self.rccl_min_channels:
             raise ValueError("runtime.rccl_min_channels > rccl_max_channels")
+        if self.comm_backend not in ("torch", "native"):
+            raise ValueError(f"runtime.comm_backend must be 'torch' or 'native', "
+                             f"got {self.comm_backend!r}")
 
     def kernel_options(self) -> Dict[str, Any]:
         return {k: getattr(self, k) for k in _KERNEL_FIELDS}
@@ -98,7 +104,8 @@ class Runtime:
                           min_channels=self.rccl_min_channels,
                           max_channels=self.rccl_max_channels,
                           cpu_affinity=self.cpu_affinity,
-                          check_bucket_order=self.check_bucket_order)
+                          check_bucket_order=self.check_bucket_order,
+                          backend=self.comm_backend)
 
     def as_dict(self) -> Dict[str, Any]:
         d = self.kernel_options()
@@ -106,5 +113,5 @@ class Runtime:
                  comm_high_priority=self.comm_high_priority,
                  rccl_min_channels=self.rccl_min_channels,
                  rccl_max_channels=self.rccl_max_channels, cpu_affinity=self.cpu_affinity,
-                 check_bucket_order=self.check_bucket_order)
+                 check_bucket_order=self.check_bucket_order, comm_backend=self.comm_backend)
         return d

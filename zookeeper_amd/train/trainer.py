@@ -67,10 +67,16 @@ class Trainer:
         # force_dp: the bucketed all-reduce stays on with one rank (a 1-rank
         # RCCL group), so one GPU runs the exact data-parallel code path
         comm = self.info.comm
+        native = None
+        if (comm.backend == "native" and self.device.type == "cuda"
+                and (self.info.world > 1 or force_dp)):
+            from zookeeper_amd.parallel.rccl import NativeComm
+
+            native = NativeComm(self.info.rank, self.info.world)
         self.bucketer = GradBucketer(self.flat, self.info.world, bucket_mb, first_bucket_mb,
                                      grad_dtype=grad_dtype, timing=comm_timing, force=force_dp,
                                      high_priority=comm.high_priority,
-                                     check_order=comm.check_bucket_order)
+                                     check_order=comm.check_bucket_order, native_comm=native)
         self.optimizer = optimizer.create(self.flat, grad_scale=1.0 / self.info.world)
         # HIP-graph replay of zero-grad + forward + loss + backward: one graph
         # launch instead of ~300 kernel launches and the Python / autograd
@@ -140,6 +146,7 @@ class Trainer:
                 self.graph_probe = (t_host, t_gpu)
                 self.graph = t_host > 0.85 * t_gpu  # host-bound: replay
             return out
+        capture_comm = self.bucketer.enabled and self.bucketer.capturable
         if self._graph is None:
             self._static_in = (x.clone(), y.clone())  # clone keeps x's channels_last strides
             self._graph = torch.cuda.CUDAGraph()
@@ -148,14 +155,23 @@ class Trainer:
             # capture, which a global-mode capture turns into
             # hipErrorStreamCaptureUnsupported (found on the 1-rank RCCL test)
             torch.cuda.synchronize(self.device)
-            with self.bucketer.suspended(), torch.cuda.graph(self._graph,
-                                                             capture_error_mode="thread_local"):
-                self._static_out = self._forward_backward(*self._static_in)
+            if capture_comm:
+                # native communicator: the bucketed all-reduce is captured with
+                # the backward (same overlap as eager, one graph launch)
+                with self.bucketer.untimed(), torch.cuda.graph(
+                        self._graph, capture_error_mode="thread_local"):
+                    self._static_out = self._forward_backward(*self._static_in)
+                    self.bucketer.finish()
+            else:
+                with self.bucketer.suspended(), torch.cuda.graph(
+                        self._graph, capture_error_mode="thread_local"):
+                    self._static_out = self._forward_backward(*self._static_in)
         else:
             self._static_in[0].copy_(x)
             self._static_in[1].copy_(y)
         self._graph.replay()
-        self.bucketer.finish()  # DP: all buckets all-reduced after the replay
+        if not capture_comm:
+            self.bucketer.finish()  # DP: all buckets all-reduced after the replay
         self.optimizer.step()
         return self._static_out
 
