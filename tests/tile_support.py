@@ -77,7 +77,7 @@ def dgrad_ok(v: int, cin: int, cout: int, stride: int) -> bool:
     if v == 50:
         return stride == 1 and cin == 64 and cout == 64
     if v == 60:
-        return stride == 1 and cin % 128 == 0 and cout % 64 == 0
+        return stride <= 2 and cin % 128 == 0 and cout % 64 == 0
     if c3 and not conv3_ok(stride):
         return False
     return (2 * cout) % cb == 0 and cin % bn == 0 and stride <= 2

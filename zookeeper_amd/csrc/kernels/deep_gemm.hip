@@ -53,13 +53,14 @@ __device__ __forceinline__ f32x4 dp_mfma(const uint4& a, const uint4& b, const f
 __device__ __forceinline__ void dp_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
 struct DeepDgradArgs {
-  const uint16_t* dy;    // [B][H][W][Cout]
-  const uint16_t* wt;    // S^T [9][Cin][Cout] bf16 +-1
+  const uint16_t* dy;    // [B][Ho][Wo][Cout]
+  const uint16_t* wt;    // S^T [kh*kw][Cin][Cout] bf16
   const uint32_t* mask;  // STE mask bits [B*H*W][Cin/32] (optional)
   const uint16_t* dres;  // residual gradient [B][H][W][Cin] (optional)
   uint16_t* dx;          // [B][H][W][Cin]
   int B, H, W, Cin, Cout;
-  int m_tiles;           // 256-pixel tiles
+  int Ho, Wo, kh, kw, s, pt, pl;
+  int m_tiles;           // 256-pixel tiles of the largest stride-parity class
 };
 
 // BNC: input channels per block (256, or 128 for the 128-channel stage):
@@ -79,11 +80,20 @@ __global__ __launch_bounds__(DP_NT, 1) void dgrad_deep_kernel(DeepDgradArgs a) {
   // XCD-aware order: consecutive logical ids = pixel tiles of one ci tile
   const int L = xcd_linear(blockIdx.x, gridDim.x);
   const int mt = L % a.m_tiles, ct = L / a.m_tiles;
-  const long long P = (long long)a.B * a.H * a.W;
+  // stride-parity class (blockIdx.y) of the input pixels: h = hc*s + ph.  Its
+  // taps are th = th0 + i*s (i < nth), reading output row ho = hc + dh0 - i
+  const int s = a.s;
+  const int ph = blockIdx.y / s, pw = blockIdx.y - (blockIdx.y / s) * s;
+  const int Hc = (a.H - ph + s - 1) / s, Wc = (a.W - pw + s - 1) / s;
+  const int th0 = (ph + a.pt) % s, tw0 = (pw + a.pl) % s;
+  const int nth = (a.kh - th0 + s - 1) / s, ntw = (a.kw - tw0 + s - 1) / s;
+  const int dh0 = (ph + a.pt - th0) / s, dw0 = (pw + a.pl - tw0) / s;
+  const long long P = (long long)a.B * Hc * Wc;  // pixels of the class
   const long long m0 = (long long)mt * 256;
+  if (m0 >= P || nth <= 0 || ntw <= 0) return;  // block-uniform
   const int n0 = ct * BNC;
   const int KC = a.Cout >> 6;  // K-tiles per tap
-  const int NKT = 9 * KC;
+  const int NKT = nth * ntw * KC;
   const long long rowb = (long long)a.Cout * 2;  // bytes per dY / S row
 
   // ---- loader: instruction i of wave w fills piece rows (i*8 + w)*16 ..
@@ -93,8 +103,8 @@ __global__ __launch_bounds__(DP_NT, 1) void dgrad_deep_kernel(DeepDgradArgs a) {
   const int gch = lslot ^ dp_swz(lrow);
   const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page) + gch * 16;
   const unsigned char* wsrc[WINS];  // S row ci, tap 0, k 0
-  const unsigned char* dsrc[2];     // dY row of the pixel itself (tap (1, 1)), k 0
-  uint32_t vh[2], vw[2];            // bit th / tw: the tap's source row / column is inside the image
+  const unsigned char* dsrc[2];     // dY row of tap (th0, tw0), k 0
+  uint32_t vh[2], vw[2];            // bit i / j: tap (i, j)'s dY row / column is inside the image
 #pragma unroll
   for (int i = 0; i < WINS; ++i) {
     const int r = (i * 8 + wave) * 16 + lrow;
@@ -107,23 +117,23 @@ __global__ __launch_bounds__(DP_NT, 1) void dgrad_deep_kernel(DeepDgradArgs a) {
     vh[i] = vw[i] = 0;
     dsrc[i] = reinterpret_cast<const unsigned char*>(a.dy) + gch * 16;
     if (m < P) {
-      const int w = (int)(m % a.W);
-      const long long q = m / a.W;
-      const int h = (int)(q % a.H);
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        vh[i] |= (uint32_t)((unsigned)(h + 1 - t) < (unsigned)a.H) << t;
-        vw[i] |= (uint32_t)((unsigned)(w + 1 - t) < (unsigned)a.W) << t;
-      }
-      dsrc[i] += m * rowb;
+      const int wc = (int)(m % Wc);
+      const long long q = m / Wc;
+      const int hc = (int)(q % Hc);
+      const long long b = q / Hc;
+      const int ho0 = hc + dh0, wo0 = wc + dw0;
+      for (int t = 0; t < nth; ++t) vh[i] |= (uint32_t)((unsigned)(ho0 - t) < (unsigned)a.Ho) << t;
+      for (int t = 0; t < ntw; ++t) vw[i] |= (uint32_t)((unsigned)(wo0 - t) < (unsigned)a.Wo) << t;
+      dsrc[i] += ((b * a.Ho + ho0) * a.Wo + wo0) * rowb;
     }
   }
   const long long wtap = (long long)a.Cin * rowb;  // S bytes per tap
   // piece p of K-tile kt into buffer kt & 1: p even = S, odd = dY; p >> 1 =
   // which 32 output channels of the 64
   auto issue = [&](int kt, int p) {
-    const int tap = kt / KC, kc = kt - tap * KC;
-    const int th = tap / 3, tw = tap - th * 3;
+    const int ti = kt / KC, kc = kt - ti * KC;
+    const int ih = ti / ntw, iw = ti - ih * ntw;  // tap (th0 + ih*s, tw0 + iw*s)
+    const int tap = (th0 + ih * s) * a.kw + tw0 + iw * s;
     const int koff = kc * 128 + (p >> 1) * 64;
     unsigned char* buf = smem + (kt & 1) * BUF + (p >> 1) * OFF_K1;
     if ((p & 1) == 0) {
@@ -131,10 +141,10 @@ __global__ __launch_bounds__(DP_NT, 1) void dgrad_deep_kernel(DeepDgradArgs a) {
       for (int i = 0; i < WINS; ++i)
         glds16(wsrc[i] + tap * wtap + koff, buf + (i * 8 + wave) * 1024);
     } else {
-      const long long toff = ((long long)(1 - th) * a.W + (1 - tw)) * rowb;
+      const long long toff = -((long long)ih * a.Wo + iw) * rowb;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const bool ok = (vh[i] >> th) & (vw[i] >> tw) & 1u;
+        const bool ok = (vh[i] >> ih) & (vw[i] >> iw) & 1u;
         glds16(ok ? dsrc[i] + toff + koff : zp, buf + WP + (i * 8 + wave) * 1024);
       }
     }
@@ -218,13 +228,19 @@ __global__ __launch_bounds__(DP_NT, 1) void dgrad_deep_kernel(DeepDgradArgs a) {
   }
 
   // ---- epilogue: acc[i][j] reg e = D[ci][pixel], ci = n0 + arow0 + 16 i +
-  // 4 (lane >> 4) + e, pixel = m0 + brow0 + 16 j + (lane & 15)
+  // 4 (lane >> 4) + e, class pixel m = m0 + brow0 + 16 j + (lane & 15)
   const int CW = a.Cin >> 5;
   const int cq = 4 * (lane >> 4);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const long long pix = m0 + brow0 + 16 * j + (lane & 15);
-    if (pix >= P) continue;
+    const long long m = m0 + brow0 + 16 * j + (lane & 15);
+    if (m >= P) continue;
+    long long pix = m;  // input pixel index
+    if (s != 1) {
+      const int wc = (int)(m % Wc);
+      const long long q = m / Wc;
+      pix = ((q / Hc) * a.H + (q % Hc) * s + ph) * a.W + (long long)wc * s + pw;
+    }
     uint32_t mw[FA];
     uint2 dv[2 * FA];
 #pragma unroll
@@ -509,22 +525,32 @@ int zk_wgrad_deep_impl(const void* dy, const void* sx, const void* w, void* dw, 
   return (int)hipGetLastError();
 }
 
-// Entry used by igemm.hip's dgrad dispatch (variant 60): stride-1 3x3 'same'
-// (pad 1) data gradient, Cin % 128 == 0 (256-channel blocks when Cin % 256 ==
+// Entry used by igemm.hip's dgrad dispatch (variant 60): data gradient of a
+// conv with kh, kw <= 3, stride 1 or 2 (one grid row per stride-parity class
+// of the input pixels), Cin % 128 == 0 (256-channel blocks when Cin % 256 ==
 // 0), Cout % 64 == 0; mask / dres optional.  dry: validate only.
 int zk_dgrad_deep_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
-                       int B, int H, int W, int Cin, int Cout, bool dry, hipStream_t st) {
-  if (Cin % 128 || Cout % 64 || Cout < 64 || B < 1 || H < 1 || W < 1)
+                       int B, int H, int W, int Cin, int Cout, int Ho, int Wo, int kh, int kw,
+                       int s, int pt, int pl, bool dry, hipStream_t st) {
+  if (Cin % 128 || Cout % 64 || Cout < 64 || B < 1 || H < 1 || W < 1 || Ho < 1 || Wo < 1)
+    return (int)hipErrorInvalidValue;
+  if (kh < 1 || kh > 3 || kw < 1 || kw > 3 || s < 1 || s > 2 || pt < 0 || pl < 0 || pt >= kh ||
+      pl >= kw)
     return (int)hipErrorInvalidValue;
   const long long P = (long long)B * H * W;
-  if (P * Cin >= (1LL << 40) || P * Cout >= (1LL << 40)) return (int)hipErrorInvalidValue;
+  if (P * Cin >= (1LL << 40) || (long long)B * Ho * Wo * Cout >= (1LL << 40))
+    return (int)hipErrorInvalidValue;
   const int bnc = Cin % 256 == 0 ? 256 : 128;
-  const long long m_tiles = (P + 255) / 256;
+  // the largest parity class: ceil(H / s) x ceil(W / s) pixels per image
+  const long long Pc = (long long)B * ((H + s - 1) / s) * ((W + s - 1) / s);
+  const long long m_tiles = (Pc + 255) / 256;
   const long long blocks = m_tiles * (Cin / bnc);
   if (blocks >= (1LL << 31)) return (int)hipErrorInvalidValue;
   if (dry) return 0;
   DeepDgradArgs a{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
-                  (const uint16_t*)dres, (uint16_t*)dx, B, H, W, Cin, Cout, (int)m_tiles};
+                  (const uint16_t*)dres, (uint16_t*)dx, B, H, W, Cin, Cout, Ho, Wo, kh, kw,
+                  s, pt, pl, (int)m_tiles};
+  const dim3 grid((unsigned)blocks, (unsigned)(s * s));
   (void)hipGetLastError();
   if (bnc == 256) {
     constexpr int lds = 2 * (2 * 256 * 64 + 2 * DP_PIECE);
@@ -534,7 +560,7 @@ int zk_dgrad_deep_impl(const void* dy, const void* wt, const void* mask, const v
       if (e != hipSuccess) return (int)e;
       g_dp_attr = true;
     }
-    hipLaunchKernelGGL(dgrad_deep_kernel<256>, dim3((unsigned)blocks), dim3(DP_NT), lds, st, a);
+    hipLaunchKernelGGL(dgrad_deep_kernel<256>, grid, dim3(DP_NT), lds, st, a);
   } else {
     constexpr int lds = 2 * (2 * 128 * 64 + 2 * DP_PIECE);
     if (!g_dp_attr128) {
@@ -543,7 +569,7 @@ int zk_dgrad_deep_impl(const void* dy, const void* wt, const void* mask, const v
       if (e != hipSuccess) return (int)e;
       g_dp_attr128 = true;
     }
-    hipLaunchKernelGGL(dgrad_deep_kernel<128>, dim3((unsigned)blocks), dim3(DP_NT), lds, st, a);
+    hipLaunchKernelGGL(dgrad_deep_kernel<128>, grid, dim3(DP_NT), lds, st, a);
   }
   return (int)hipGetLastError();
 }

@@ -1867,7 +1867,8 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
 // deep_gemm.hip: phased 256x256 (256x128) dgrad of the stride-1 3x3 convs
 // with Cin % 128 == 0 (variant 60)
 int zk_dgrad_deep_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
-                       int B, int H, int W, int Cin, int Cout, bool dry, hipStream_t st);
+                       int B, int H, int W, int Cin, int Cout, int Ho, int Wo, int kh, int kw,
+                       int s, int pt, int pl, bool dry, hipStream_t st);
 
 // conv3rw.hip: row-window dgrad of the 64 -> 64 stride-1 3x3 conv (variant 50)
 int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres,
@@ -1876,6 +1877,14 @@ int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, cons
                           bool dry, hipStream_t st);
 
 namespace {
+// Shapes the phased dgrad (variant 60) takes by default: 3x3 stride 1 / 2 and
+// 1x1 stride 1 with Cin % 128 == 0 and Cout % 64 == 0.
+bool deep_dgrad_ok(const IGeom& g) {
+  const bool k3 = g.kh == 3 && g.kw == 3 && (g.s == 1 || g.s == 2);
+  const bool k1 = g.kh == 1 && g.kw == 1 && g.s == 1 && g.pt == 0 && g.pl == 0;
+  return (k3 || k1) && g.Cin % 128 == 0 && g.Cout % 64 == 0 && g.pt < g.kh && g.pl < g.kw;
+}
+
 int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
                      const IGeom& g, const BnSum& bs, int variant, hipStream_t stream) {
   if (variant < 0) {
@@ -1897,7 +1906,7 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     const bool c3 = conv3_ok(g, 0);
     const bool le = bs.sums == nullptr;
     const int v256 = le ? 45 : 14;
-    if (g_opt_dgrad_deep && le && !bs.fstats && c3 && Cin % 128 == 0 && g.Cout % 64 == 0)
+    if (g_opt_dgrad_deep && le && !bs.fstats && deep_dgrad_ok(g))
       variant = 60;  // phased 256x256 schedule (deep_gemm.hip)
     else if (le && g.kh == 1 && g.kw == 1 && stride == 1 && Cin % 64 == 0)
       variant = Cin % 256 == 0 ? 45 : Cin % 128 == 0 ? 41 : 43;
@@ -1919,9 +1928,9 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
       variant = 7;
   }
   if (variant == 60) {  // deep_gemm.hip (explicit, or the default above)
-    if (bs.fstats || bs.sums || !conv3_ok(g, 0)) return (int)hipErrorInvalidValue;
-    return zk_dgrad_deep_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Cout, g_dry_run,
-                              stream);
+    if (bs.fstats || bs.sums) return (int)hipErrorInvalidValue;
+    return zk_dgrad_deep_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Cout, g.Ho, g.Wo,
+                              g.kh, g.kw, g.s, g.pt, g.pl, g_dry_run, stream);
   }
   if (variant == 50) {  // conv3rw.hip (explicit, or the default above)
     if (bs.fstats) return (int)hipErrorInvalidValue;
