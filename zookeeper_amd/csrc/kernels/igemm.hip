@@ -1877,14 +1877,6 @@ int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, cons
                           bool dry, hipStream_t st);
 
 namespace {
-// Shapes the phased dgrad (variant 60) takes by default: 3x3 stride 1 / 2 and
-// 1x1 stride 1 with Cin % 128 == 0 and Cout % 64 == 0.
-bool deep_dgrad_ok(const IGeom& g) {
-  const bool k3 = g.kh == 3 && g.kw == 3 && (g.s == 1 || g.s == 2);
-  const bool k1 = g.kh == 1 && g.kw == 1 && g.s == 1 && g.pt == 0 && g.pl == 0;
-  return (k3 || k1) && g.Cin % 128 == 0 && g.Cout % 64 == 0 && g.pt < g.kh && g.pl < g.kw;
-}
-
 int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
                      const IGeom& g, const BnSum& bs, int variant, hipStream_t stream) {
   if (variant < 0) {
@@ -1906,8 +1898,13 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     const bool c3 = conv3_ok(g, 0);
     const bool le = bs.sums == nullptr;
     const int v256 = le ? 45 : 14;
-    if (g_opt_dgrad_deep && le && !bs.fstats && deep_dgrad_ok(g))
-      variant = 60;  // phased 256x256 schedule (deep_gemm.hip)
+    if (g_opt_dgrad_deep && le && !bs.fstats && c3 && Cin % 256 == 0 && g.Cout % 64 == 0)
+      // phased 256x256 schedule (deep_gemm.hip).  Measured at batch 1536 it
+      // ties the 256x256 implicit GEMM (14x14x256: 428-484 vs 495 us; 7x7x512
+      // 432-462 vs 406 us) and loses for 128 channels (769 vs 594 us) and the
+      // stride-2 transitions, so only the stride-1 >= 256-channel layers take it
+      // by default (profiles/r4/b_deep_gemm.md)
+      variant = 60;
     else if (le && g.kh == 1 && g.kw == 1 && stride == 1 && Cin % 64 == 0)
       variant = Cin % 256 == 0 ? 45 : Cin % 128 == 0 ? 41 : 43;
     else if (Cin == 256 && stride == 1)
@@ -2083,6 +2080,22 @@ ZK_EXPORT int zk_wgrad_slab_reduce(const void* slab, int splits, long long n, co
                      (const float4*)slab, splits, n4, (const float4*)w, clip, (float4*)dw);
   ZK_CHECK_LAUNCH();
   return 0;
+}
+
+// 1 if the split-K reduction of this weight gradient is faster with fp32
+// atomics than with slabs + the reduce kernel (runtime.wgrad_reduce="auto").
+// Measured standalone at batch 1536 (profiles/r4/a_wgrad_atomic_vs_slab.md):
+// only the conv3 kernels with 64 input channels win with atomics (56x56x64:
+// 630 vs 909 us: their slabs hit the slab cap, which cuts the grid below the
+// CU count); every other E18 shape is faster with slabs (the deep kernel's
+// 256 / 512-channel layers 545 / 540 vs 648 / 695 us).
+ZK_EXPORT int zk_igemm_wgrad_prefers_atomic(int B, int Cin, int H, int W, int Ho, int Wo,
+                                            int Cout, int kh, int kw, int stride, int pt, int pl,
+                                            int variant) {
+  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+  int tb = 0;
+  wgrad_defaults(g, variant, tb);
+  return (variant >= 20 && variant < 40 && g.Cin == 64) ? 1 : 0;
 }
 
 // Workspace bytes zk_igemm_wgrad needs for slab mode (-1: shape unsupported).

@@ -174,13 +174,14 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Te
     dyᵀ ⊛ x`` (``zk_igemm_wgrad``), with the split-K reduction chosen by the
     run's options:
 
-    * ``runtime.deterministic``: per-split slabs (plain stores) reduced in a
-      fixed order by ``wgrad_reduce_kernel`` -- bit-reproducible;
-    * otherwise (``runtime.wgrad_atomic``, default): every split adds its
-      tile straight into ``dw`` -- the zeroed flat fp32 gradient buffer --
-      with fp32 atomics: no slab write + re-read, no reduce launch, and no
-      slab cap limiting the split count (which held the deep layers' grids
-      under the CU count).
+    * ``runtime.deterministic`` or ``runtime.wgrad_reduce="slab"``: per-split
+      slabs (plain stores) reduced in a fixed order by ``wgrad_reduce_kernel``
+      -- bit-reproducible;
+    * ``"atomic"``: every split adds its tile straight into ``dw`` -- the
+      zeroed flat fp32 gradient buffer -- with fp32 atomics: no slab write +
+      re-read, no reduce launch, and no slab cap limiting the split count;
+    * ``"auto"`` (default): the measured winner for the shape
+      (``zk_igemm_wgrad_prefers_atomic``).
 
     ``geom`` = (B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl)."""
     from zookeeper_amd.ops.options import OPTS
@@ -188,7 +189,11 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Te
     L = lib()
     B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl = geom
     ws, ws_bytes = None, 0
-    if OPTS.deterministic or not OPTS.wgrad_atomic:
+    mode = OPTS.wgrad_reduce
+    if mode == "auto":
+        mode = "atomic" if L.zk_igemm_wgrad_prefers_atomic(B, Cin, H, W, Ho, Wo, Cout, kh, kw, s,
+                                                            pt, pl, variant) else "slab"
+    if OPTS.deterministic or mode == "slab":
         ws_bytes = max(int(L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Ho, Wo, Cout, kh, kw, s, pt,
                                                      pl, 0, variant)), 0)
         if ws_bytes > 0:

@@ -47,6 +47,7 @@ SIGNATURES = {
     "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),
     "zk_igemm_wgrad_ws_bytes": (I64, [I32] * 14),
     "zk_wgrad_slab_reduce": (I32, [P, I32, I64, P, F32, P, P]),
+    "zk_igemm_wgrad_prefers_atomic": (I32, [I32] * 13),
     "zk_igemm_dgrad_supported": (I32, [I32] * 13),
     "zk_set_option": (I32, [I32, I32]),
     "zk_bn_bwd_reduce_blocks": (I32, []),

@@ -57,10 +57,16 @@ class KernelOptions:
     # Same-box sweep at batch 1536: 28 MB 47.52k, 32 MB 47.79k / 47.71k,
     # 36 MB 47.17k, 40 MB 47.46k img/s.
     wgrad_slab_mb: int = 32
-    # Split-K weight gradients add into the flat fp32 gradient buffer with
-    # fp32 atomics (no slabs, no reduce launch, no slab cap); False: slabs +
-    # the fixed-order reduce (what runtime.deterministic always uses).
-    wgrad_atomic: bool = True
+    # Split-K reduction of the weight gradients: "atomic" (fp32 atomics into
+    # the flat gradient buffer: no slabs, no reduce launch, no slab cap),
+    # "slab" (per-split slabs + the fixed-order reduce kernel; what
+    # runtime.deterministic always uses), or "auto": per layer shape, the
+    # measured winner (zk_igemm_wgrad_prefers_atomic).  Standalone at batch
+    # 1536 (profiles/r4/a_wgrad_atomic_vs_slab.md): 56x56x64 atomic 630 vs
+    # slab 909 us (the slab cap starves its grid); the deep 256 / 512-channel
+    # layers slab 545 / 540 vs atomic 648 / 695 us (fp32 atomics run at
+    # ~1.3 TB/s of added bytes, slab stores at ~6 TB/s).
+    wgrad_reduce: str = "auto"
     # Phased data-gradient kernel (deep_gemm.hip) for the stride-1 3x3
     # binary convs with >= 128 input channels.
     dgrad_deep: bool = True

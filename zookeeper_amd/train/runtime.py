@@ -43,7 +43,7 @@ class Runtime:
     dgrad_rw: bool = Field(True)
     bn_stats_epilogue: bool = Field(True)
     wgrad_slab_mb: int = Field(32)
-    wgrad_atomic: bool = Field(True)
+    wgrad_reduce: str = Field("auto")
     dgrad_deep: bool = Field(True)
     wgrad_deep: bool = Field(True)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
@@ -82,6 +82,9 @@ class Runtime:
             raise ValueError("runtime.rccl_min_channels / rccl_max_channels must be >= 0")
         if 0 < self.rccl_max_channels < self.rccl_min_channels:
             raise ValueError("runtime.rccl_min_channels > rccl_max_channels")
+        if self.wgrad_reduce not in ("auto", "atomic", "slab"):
+            raise ValueError(f"runtime.wgrad_reduce must be 'auto', 'atomic' or 'slab', "
+                             f"got {self.wgrad_reduce!r}")
         if self.comm_backend not in ("torch", "native"):
             raise ValueError(f"runtime.comm_backend must be 'torch' or 'native', "
                              f"got {self.comm_backend!r}")
