@@ -102,7 +102,9 @@ def _compile_cmd(src: str, obj: str, extra: List[str]) -> List[str]:
     if src.endswith(".hip"):
         cmd += [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
     else:
-        cmd += ["-x", "c++"]
+        # host C++: the HIP runtime API headers (no device code, no offload)
+        rocm = os.path.dirname(os.path.dirname(os.path.realpath(hipcc())))
+        cmd += ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(rocm, "include")]
     return cmd + extra + ["-c", src, "-o", obj]
 
 

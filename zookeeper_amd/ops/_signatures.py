@@ -20,6 +20,8 @@ SIGNATURES = {
     "zk_build_digest": (C.c_char_p, []),
     # host runtime
     "zk_gather_rows": (I32, [P, I64, P, I64, P, I32]),
+    # CU-masked streams (runtime/cu_mask.cpp; ops/streams.py)
+    "zk_cu_masked_stream": (I32, [I32, I32, I32, P, P]),
     # native RCCL communicator (runtime/comm.cpp; parallel/rccl.py)
     "zk_comm_load": (I32, [C.c_char_p]),
     "zk_comm_loaded": (I32, []),

@@ -31,6 +31,9 @@ class KernelOptions:
     wgrad_side_stream: bool = True
     # HIP priority of that side stream (0 = default, negative = higher).
     wgrad_priority: int = 0
+    # Share of the CUs the side stream may use (hipExtStreamCreateWithCUMask;
+    # 0 = all of them): the rest stay free for the data-gradient chain.
+    wgrad_cu_share: float = 0.0
     # Recompute-fused ImageNet stem (False: the materialising kernels).
     stem_fused: bool = True
     # Float convolutions on the MFMA implicit-GEMM kernels (False: library).

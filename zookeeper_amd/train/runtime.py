@@ -35,6 +35,7 @@ class Runtime:
     bconv_fp4: bool = Field(True)
     wgrad_side_stream: bool = Field(True)
     wgrad_priority: int = Field(0)
+    wgrad_cu_share: float = Field(0.0)
     stem_fused: bool = Field(True)
     conv_mfma: bool = Field(True)
     conv3_mfma: bool = Field(True)
@@ -82,6 +83,8 @@ class Runtime:
             raise ValueError("runtime.rccl_min_channels / rccl_max_channels must be >= 0")
         if 0 < self.rccl_max_channels < self.rccl_min_channels:
             raise ValueError("runtime.rccl_min_channels > rccl_max_channels")
+        if not 0.0 <= self.wgrad_cu_share <= 1.0:
+            raise ValueError("runtime.wgrad_cu_share must be in [0, 1]")
         if self.wgrad_reduce not in ("auto", "atomic", "slab"):
             raise ValueError(f"runtime.wgrad_reduce must be 'auto', 'atomic' or 'slab', "
                              f"got {self.wgrad_reduce!r}")
