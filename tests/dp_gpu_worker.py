@@ -54,7 +54,9 @@ def run(mode: str, out: str) -> None:
     # ZK_TEST_CHECK_ORDER=1: every step compares the launched bucket order
     # across ranks (runtime.check_bucket_order)
     comm = zdist.CommConfig(check_bucket_order=os.environ.get("ZK_TEST_CHECK_ORDER", "0") == "1",
-                            backend=os.environ.get("ZK_TEST_COMM", "torch"))
+                            backend=os.environ.get("ZK_TEST_COMM", "torch"),
+                            high_priority=os.environ.get("ZK_TEST_COMM_PRIO", "1") == "1",
+                            cpu_affinity=os.environ.get("ZK_TEST_AFFINITY", "1") == "1")
     if world > 1 or force:
         info = zdist.init(backend, single_group=force, comm=comm)
     else:

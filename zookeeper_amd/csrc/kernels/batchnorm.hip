@@ -184,9 +184,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     red[1][threadIdx.x][k] = sgy[k];
   }
   __syncthreads();
-  float* out = sums + (long long)(blockIdx.x % stripes) * 2 * C;  // striped copies
-  // one copy per block (stripes >= blocks, the deterministic mode): plain
-  // stores, summed in a fixed order by bn_bwd_coef
+  // copies in channel-major layout [2][C][stripes]: copy j of channel c's
+  // statistic s at (s*C + c)*stripes + j (bn_bwd_coef reads a channel's
+  // copies as contiguous float4s).  One copy per block (stripes >= blocks,
+  // the default): plain stores, summed in a fixed order by bn_bwd_coef.
+  const int copy = (int)(blockIdx.x % stripes);
   const bool own = stripes >= (int)gridDim.x;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const int gcg = c / 8, k = c % 8;
@@ -195,12 +197,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       a += red[0][rr * CG + gcg][k];
       b += red[1][rr * CG + gcg][k];
     }
+    float* o0 = sums + (long long)c * stripes + copy;
+    float* o1 = sums + (long long)(C + c) * stripes + copy;
     if (own) {
-      out[c] = a;
-      out[C + c] = b;
+      *o0 = a;
+      *o1 = b;
     } else {
-      atomicAdd(out + c, a);
-      atomicAdd(out + C + c, b);
+      atomicAdd(o0, a);
+      atomicAdd(o1, b);
     }
   }
 }
@@ -249,32 +253,47 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const uint16_t* __restri
 // Per-channel backward coefficients from the reductions (one tiny launch
 // instead of a chain of framework ops), plus gamma/beta gradients
 // accumulated straight into the parameters' gradient buffers:
-//   sums = [stripes][sum g, sum g*yhat] (copies summed and re-zeroed here);
+//   sums = channel-major copies [2][C][stride] of (sum g, sum g*yhat): the
+//   first `stripes` copies of a channel are contiguous, read as float4s by
+//   32 lanes (4 per lane at 512 copies) and summed in a fixed order (lane
+//   partials, then a butterfly), then re-zeroed;
 //   coef = [k1, k0, k3];  dgamma += sum g*yhat,  dbeta += sum g.
-// A group of 32 lanes owns one channel (lane k reads copies k, k+32, ...).
+// A group of 32 lanes owns one channel.  (The [stripe][2][C] layout this
+// replaced made each lane walk its copies 2C floats apart, 16 dependent
+// loads per lane at 512 copies: ~90 us per call on a busy chip.)
+__device__ __forceinline__ float coef_row_sum(float* __restrict__ row, int stripes, int k) {
+  float acc = 0.f;
+  const int n4 = (reinterpret_cast<uintptr_t>(row) & 15) ? 0 : stripes >> 2;
+  float4* r4 = reinterpret_cast<float4*>(row);
+#pragma unroll 4
+  for (int j = k; j < n4; j += 32) {
+    const float4 q = r4[j];
+    acc += (q.x + q.y) + (q.z + q.w);
+    r4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int j = n4 * 4 + k; j < stripes; j += 32) {
+    acc += row[j];
+    row[j] = 0.f;
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 32);
+  return acc;
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_coef_kernel(float* __restrict__ sums,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ rstd,
                                                           const float* __restrict__ gamma,
                                                           double P, int C, int stripes,
+                                                          int stride,
                                                           float* __restrict__ coef,
                                                           float* __restrict__ dgamma,
                                                           float* __restrict__ dbeta) {
   const int k = threadIdx.x & 31;
   const int c = blockIdx.x * 8 + (threadIdx.x >> 5);
   if (c >= C) return;  // uniform over the 32-lane group
-  float sg = 0.f, sgy = 0.f;
-  for (int j = k; j < stripes; j += 32) {
-    sg += sums[(2LL * j) * C + c];
-    sgy += sums[(2LL * j + 1) * C + c];
-    sums[(2LL * j) * C + c] = 0.f;
-    sums[(2LL * j + 1) * C + c] = 0.f;
-  }
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) {
-    sg += __shfl_xor(sg, o, 32);
-    sgy += __shfl_xor(sgy, o, 32);
-  }
+  const float sg = coef_row_sum(sums + (long long)c * stride, stripes, k);
+  const float sgy = coef_row_sum(sums + (long long)(C + c) * stride, stripes, k);
   if (k != 0) return;
   const float rs = rstd[c];
   const float k1 = (gamma ? gamma[c] : 1.f) * rs;
@@ -394,7 +413,8 @@ ZK_EXPORT int zk_bn_apply_sign(const void* y, const void* scale, const void* shi
   return 0;
 }
 
-// sums: [stripes][2][C] fp32 copies (block b adds into copy b % stripes).
+// sums: [2][C][stripes] fp32 channel-major copies (block b writes / adds
+// into copy b % stripes).
 ZK_EXPORT int zk_bn_bwd_reduce_blocks() { return 512; }
 
 namespace {
@@ -446,12 +466,16 @@ ZK_EXPORT int zk_bn_bwd_dx(const void* g, const void* y, const void* coef, void*
   return 0;
 }
 
+// sums: channel-major copies [2][C][stride] (stride >= stripes; the first
+// `stripes` copies of each row are summed in a fixed order and re-zeroed).
 ZK_EXPORT int zk_bn_bwd_coef(const void* sums, const void* mean, const void* rstd,
-                             const void* gamma, double P, int C, int stripes, void* coef,
-                             void* dgamma, void* dbeta, hipStream_t stream) {
+                             const void* gamma, double P, int C, int stripes, int stride,
+                             void* coef, void* dgamma, void* dbeta, hipStream_t stream) {
+  if (stripes < 1) stripes = 1;
+  if (stride < stripes) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 7) / 8), dim3(256), 0, stream, (float*)sums,
                      (const float*)mean, (const float*)rstd, (const float*)gamma, P, C,
-                     stripes < 1 ? 1 : stripes, (float*)coef, (float*)dgamma, (float*)dbeta);
+                     stripes, stride, (float*)coef, (float*)dgamma, (float*)dbeta);
   ZK_CHECK_LAUNCH();
   return 0;
 }

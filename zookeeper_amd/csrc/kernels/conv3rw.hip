@@ -61,8 +61,8 @@ struct RWArgs {
   uint16_t* dx;          // [B][H][W][64]
   int B, H, W, ngroups, ipb, slot;
   // optional: the predecessor block's BN-backward reduction over the stored
-  // dx (its output gradient): psums[stripe][0][c] += sum dx,
-  // [1][c] += sum dx * (ypred - mean[c]) * rstd[c]  (ypred int16 [B][H][W][64])
+  // dx (its output gradient): psums[0][c][stripe] += sum dx,
+  // [1][c][stripe] += sum dx * (ypred - mean[c]) * rstd[c]  (ypred int16 [B][H][W][64])
   const int16_t* ypred;
   const float* pmean;
   const float* prstd;
@@ -335,23 +335,23 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
         }
       }
       __syncthreads();
-      if (wave == 0) {
-        float* ps = a.psums + (long long)blockIdx.x * 2 * 64;
+      if (wave == 0) {  // channel-major copies [2][64][stripes] (zk_bn_bwd_coef)
 #pragma unroll
         for (int v = lane; v < 128; v += 64) {
           const int which = v >> 6, c = v & 63, half = c >> 5, cc = c & 31;
           float t = 0.f;
 #pragma unroll
           for (int m = 0; m < RW_NW / 2; ++m) t += red[((2 * m + half) * 2 + which) * 32 + cc];
-          ps[which * 64 + c] = t;
+          a.psums[(long long)(which * 64 + c) * a.stripes + blockIdx.x] = t;
         }
       }
     } else if (r16 == 0) {
-      float* ps = a.psums + (long long)(blockIdx.x % a.stripes) * 2 * 64;
+      const long long copy = blockIdx.x % a.stripes;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        atomicAdd(ps + nh * 32 + kq * 8 + e, s1[e]);
-        atomicAdd(ps + 64 + nh * 32 + kq * 8 + e, s2[e]);
+        const int c = nh * 32 + kq * 8 + e;
+        atomicAdd(a.psums + (long long)c * a.stripes + copy, s1[e]);
+        atomicAdd(a.psums + (long long)(64 + c) * a.stripes + copy, s2[e]);
       }
     }
   }

@@ -69,7 +69,8 @@ struct ConvArgs {
   int stripes;           // copies of stats / psums; block b adds into copy b % stripes
   // dgrad (optional): fused BN-backward reduction of the PREVIOUS block, whose
   // output gradient is exactly the dx this kernel writes (identity shortcut,
-  // single consumer): psums[stripe][0][c] += sum dx, [1][c] += sum dx * yhat,
+  // single consumer): psums[0][c][stripe] += sum dx, [1][c][stripe] += sum dx * yhat
+  // (channel-major copies, the layout zk_bn_bwd_coef reads),
   // yhat = (ypred - pmean[c]) * prstd[c] -- the zk_bn_bwd_reduce of that block.
   const int16_t* ypred;
   const float* pmean;
@@ -148,9 +149,9 @@ __device__ __forceinline__ void dgrad_store_block(const ConvArgs& args, const IG
 #pragma unroll
   for (int a = 0; a < TM; ++a)
     mw[a] = (args.mask && pix[a] >= 0) ? args.mask[pix[a] * CW + (nb >> 5)] : 0xFFFFFFFFu;
+  // channel-major copies [2][Cin][stripes] (zk_bn_bwd_coef)
   float* ps = nullptr;
-  if (args.psums)
-    ps = args.psums + (long long)(args.stripes > 1 ? blockIdx.x % args.stripes : 0) * 2 * g.Cin;
+  if (args.psums) ps = args.psums + (args.stripes > 1 ? blockIdx.x % args.stripes : 0);
   float vals[32];  // value j = s*16 + q*4 + e: sum (s = 0) / sum * yhat (s = 1) of channel (q, e)
 #pragma unroll
   for (int j = 0; j < 32; ++j) vals[j] = 0.f;
@@ -201,7 +202,7 @@ __device__ __forceinline__ void dgrad_store_block(const ConvArgs& args, const IG
     rs_step<2>(vals, r32);
     rs_step<1>(vals, r32);
     const int c = nb + 8 * ((r32 >> 2) & 3) + 4 * h + (r32 & 3);
-    atomicAdd(ps + (r32 >> 4) * g.Cin + c, vals[0]);
+    atomicAdd(ps + (long long)((r32 >> 4) * g.Cin + c) * args.stripes, vals[0]);
   }
 }
 
@@ -1956,7 +1957,7 @@ ZK_EXPORT int zk_igemm_dgrad(const void* dy, const void* wt, const void* mask, c
 }
 
 // zk_igemm_dgrad + the previous block's BN-backward reduction fused into the
-// epilogue: sums [stripes][2][Cin] fp32 += (sum dx, sum dx * (ypred - mean) *
+// epilogue: sums [2][Cin][stripes] fp32 (channel-major) += (sum dx, sum dx * (ypred - mean) *
 // rstd) over the stored bf16 dx (ypred int16 [B][H][W][Cin]; mean / rstd
 // [Cin]).  Valid when dx is that block's whole output gradient.
 ZK_EXPORT int zk_igemm_dgrad_bnsum(const void* dy, const void* wt, const void* mask,

@@ -194,9 +194,11 @@ __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __re
   }
 }
 
-// PARTS: per-block partial sums [block][2][C] with plain stores (summed in a
-// fixed order by zk_bn_bwd_coef with stripes = blocks: run-to-run
-// deterministic) instead of fp32 atomics into one [2][C] row.
+constexpr int kBnBwdParts = 512;  // copy capacity of the PARTS reduce (red_grid <= it)
+
+// PARTS: per-block partial sums with plain stores, channel-major [2][C][512]
+// (summed in a fixed order by zk_bn_bwd_coef with stripes = blocks, stride =
+// 512: run-to-run deterministic) instead of fp32 atomics into one [2][C] row.
 // RC: BN + ReLU without a stored output: the ReLU mask is recomputed from x
 // and the forward coefficients (relu_live(bn_pre(...))), saving a read of y.
 template <int CG, bool PARTS = false, bool RC = false>
@@ -265,9 +267,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
       a += red[0][rr * CG + c / 8][c % 8];
       b += red[1][rr * CG + c / 8][c % 8];
     }
-    if (PARTS) {
-      sums[(2LL * blockIdx.x) * C + c] = a;
-      sums[(2LL * blockIdx.x + 1) * C + c] = b;
+    if (PARTS) {  // channel-major copies [2][C][kBnBwdParts] (zk_bn_bwd_coef)
+      sums[(long long)c * kBnBwdParts + blockIdx.x] = a;
+      sums[(long long)(C + c) * kBnBwdParts + blockIdx.x] = b;
     } else {
       atomicAdd(sums + c, a);
       atomicAdd(sums + C + c, b);
@@ -640,10 +642,10 @@ ZK_EXPORT int zk_bn_bwd_reduce_bf16(const void* g, const void* x, const void* y,
   return 0;
 }
 
-// Deterministic form: parts [zk_bn_bwd_parts_max()][2][C] receives one row
-// pair per block (*nparts of them); pass parts and *nparts as sums / stripes
-// to zk_bn_bwd_coef.
-ZK_EXPORT int zk_bn_bwd_parts_max() { return 512; }
+// Deterministic form: parts [2][C][zk_bn_bwd_parts_max()] (channel-major)
+// receives one copy per block (*nparts of them); pass parts, *nparts and
+// zk_bn_bwd_parts_max() as sums / stripes / stride to zk_bn_bwd_coef.
+ZK_EXPORT int zk_bn_bwd_parts_max() { return kBnBwdParts; }
 
 ZK_EXPORT int zk_bn_bwd_reduce_bf16_parts(const void* g, const void* x, const void* y,
                                           const void* coef, void* parts, long long P, int C,

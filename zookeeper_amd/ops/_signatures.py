@@ -79,7 +79,7 @@ SIGNATURES = {
     "zk_bn_bwd_reduce": (I32, [P, P, P, P, P, I64, I32, I32, P]),
     "zk_bn_bwd_dx": (I32, [P, P, P, P, I64, I32, I32, P]),
     "zk_ste_combine": (I32, [P, P, P, P, I64, P]),
-    "zk_bn_bwd_coef": (I32, [P, P, P, P, C.c_double, I32, I32, P, P, P, P]),
+    "zk_bn_bwd_coef": (I32, [P, P, P, P, C.c_double, I32, I32, I32, P, P, P, P]),
     # batch norm (bf16) and pooling
     "zk_bn_stats_bf16": (I32, [P, P, I64, I32, P]),
     "zk_bn_finalize_f64": (I32, [P, I32, C.c_double, P, P, F32, F32, P, P, P, P]),

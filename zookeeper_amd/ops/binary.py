@@ -238,7 +238,7 @@ class _BinaryBlockFn(torch.autograd.Function):
         if rw_out and not OPTS.deterministic and will_backward and bn.training:
             # one copy per row-window block (fixed-order combination, below
             # the reduce's 512 copies): the same buffer as the separate reduce
-            sums_buf = zeroed_scratch(bn, "bwd_sums", (bwd_stripes(), 2, Cout), torch.float32,
+            sums_buf = zeroed_scratch(bn, "bwd_sums", (2, Cout, bwd_stripes()), torch.float32,
                                       dev)
             ctx.bnsum = _BnSum(y, mean, rstd, sums_buf)
             side["bnsum"] = ctx.bnsum
@@ -272,7 +272,9 @@ class _BinaryBlockFn(torch.autograd.Function):
         # deterministic mode: one copy of the sums per reduce block (plain
         # stores, fixed-order sum in zk_bn_bwd_coef) instead of striped atomics
         stripes = bwd_stripes()
-        sums = zeroed_scratch(ctx.bn, "bwd_sums", (stripes, 2, Cout), torch.float32, dev)
+        # channel-major copies [2][C][stripes]: zk_bn_bwd_coef reads each
+        # channel's copies as one contiguous row
+        sums = zeroed_scratch(ctx.bn, "bwd_sums", (2, Cout, stripes), torch.float32, dev)
         bs = ctx.bnsum
         fused = bs is not None and bs.dx is not None
         # BN coefficients + gamma/beta gradients; gradients go straight into
@@ -293,7 +295,7 @@ class _BinaryBlockFn(torch.autograd.Function):
         # else: the successor's dgrad epilogue reduced exactly this gradient
         check(L.zk_bn_bwd_coef(sums.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                                gamma.data_ptr() if gamma is not None else None, float(P),
-                               Cout, stripes, coef.data_ptr(),
+                               Cout, stripes, stripes, coef.data_ptr(),
                                dgamma.data_ptr() if dgamma is not None else None,
                                dbeta.data_ptr() if dbeta is not None else None, st),
               "zk_bn_bwd_coef")
@@ -351,7 +353,7 @@ class _BinaryBlockFn(torch.autograd.Function):
                                                  dres.data_ptr() if dres is not None else None,
                                                  dx.data_ptr(), pred.y.data_ptr(),
                                                  pred.mean.data_ptr(), pred.rstd.data_ptr(),
-                                                 pred.sums.data_ptr(), pred.sums.shape[0], B, H, W,
+                                                 pred.sums.data_ptr(), pred.sums.shape[2], B, H, W,
                                                  Cin,
                                                  Ho, Wo, Cout, kh, kw, stride, pt, pl, -1, st),
                           "zk_igemm_dgrad_bnsum")

@@ -119,7 +119,8 @@ class _BatchNormFn(torch.autograd.Function):
         # zk_bn_bwd_coef (stripes = parts): bit-reproducible in every mode --
         # these sums set the BN coefficients of the whole gradient chain below
         # (and fp32 atomics of 512 blocks into one [2][C] row also contend)
-        sums = torch.empty((L.zk_bn_bwd_parts_max(), 2, C), dtype=torch.float32, device=dev)
+        # channel-major copies [2][C][parts_max]
+        sums = torch.empty((2, C, L.zk_bn_bwd_parts_max()), dtype=torch.float32, device=dev)
         n = ctypes.c_int(0)
         if ctx.relu_rc:
             check(L.zk_bn_bwd_reduce_relu_bf16_parts(g.data_ptr(), xn.data_ptr(),
@@ -143,7 +144,7 @@ class _BatchNormFn(torch.autograd.Function):
         bcoef = torch.empty((3, C), dtype=torch.float32, device=dev)
         check(L.zk_bn_bwd_coef(sums.data_ptr(), coef[2].data_ptr(), coef[3].data_ptr(),
                                gamma.data_ptr() if gamma is not None else None, float(P), C,
-                               stripes,
+                               stripes, sums.shape[2],
                                bcoef.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
                                dbeta.data_ptr() if dbeta is not None else None, st),
               "zk_bn_bwd_coef")

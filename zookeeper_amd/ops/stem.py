@@ -74,9 +74,12 @@ def _bn_eval_coef(bn, C, dev):
     return coef
 
 
-def _bn_bwd_coef(L, st, sums, coef, gamma_p, beta_p, P, C, dev, stripes: int = 1):
-    """BN backward coefficients [k1, k0, k3]; γ/β gradients go into the flat
-    buffer when the trainer manages it, else are returned."""
+def _bn_bwd_coef(L, st, sums, coef, gamma_p, beta_p, P, C, dev, stripes: int = 1,
+                 stride: int = 1):
+    """BN backward coefficients [k1, k0, k3] from channel-major copies
+    ``sums`` [2][C][stride] (the first ``stripes`` of each row are summed);
+    γ/β gradients go into the flat buffer when the trainer manages it, else
+    are returned."""
     dg = direct_grad(gamma_p) if gamma_p is not None else None
     db = direct_grad(beta_p) if beta_p is not None else None
     dgamma = dg if dg is not None else (torch.zeros(C, device=dev) if gamma_p is not None else None)
@@ -84,7 +87,7 @@ def _bn_bwd_coef(L, st, sums, coef, gamma_p, beta_p, P, C, dev, stripes: int = 1
     bcoef = torch.empty((3, C), dtype=torch.float32, device=dev)
     check(L.zk_bn_bwd_coef(sums.data_ptr(), coef[2].data_ptr(), coef[3].data_ptr(),
                            gamma_p.data_ptr() if gamma_p is not None else None, float(P), C,
-                           stripes,
+                           stripes, stride,
                            bcoef.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
                            dbeta.data_ptr() if dbeta is not None else None, st), "zk_bn_bwd_coef")
     if dg is not None:
@@ -254,15 +257,15 @@ class _StemFn(torch.autograd.Function):
             # per-block partials summed in a fixed order: the stem's BN-1 / conv
             # gradients amplify run-to-run noise of these sums (BN-2 makes
             # dL/dgamma1 a near-total cancellation)
-            sums2 = torch.empty((L.zk_bn_bwd_parts_max(), 2, Cout), dtype=torch.float32,
-                                device=dev)
+            sums2 = torch.empty((2, Cout, L.zk_bn_bwd_parts_max()), dtype=torch.float32,
+                                device=dev)  # channel-major copies
             nb2 = ctypes.c_int(0)
             check(L.zk_bn_bwd_reduce_bf16_parts(g.data_ptr(), p.data_ptr(), None,
                                                 coef2.data_ptr(), sums2.data_ptr(), P2, Cout,
                                                 ctypes.byref(nb2), st),
                   "zk_bn_bwd_reduce_bf16_parts")
             bcoef2, dg2, db2 = _bn_bwd_coef(L, st, sums2, coef2, g2p, b2p, P2, Cout, dev,
-                                            stripes=nb2.value)
+                                            stripes=nb2.value, stride=sums2.shape[2])
             dp = torch.empty_like(g)
             check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), p.data_ptr(), None, bcoef2.data_ptr(),
                                       dp.data_ptr(), P2, Cout, st), "zk_bn_bwd_dx_bf16")

@@ -104,6 +104,8 @@ class GradBucketer:
                 self.slot_bucket[i] = bi
         self._pending = [len(b) for b in buckets]
         self._works: List = []
+        # events a stream wait refers to, held for two steps (see _launch)
+        self._held_events: List = [[], []]
         self._launched = [False] * len(buckets)
         self._hooks = []
         self._seen = [False] * len(flat.slots)
@@ -206,12 +208,21 @@ class GradBucketer:
             return
         if self._sync_launch:
             torch.cuda.synchronize(view.device)
+        dbg = os.environ.get("ZK_COMM_DEBUG_WAIT", "")
+        if dbg == "compute":
+            torch.cuda.current_stream(view.device).synchronize()
+        elif dbg == "side":
+            for ev in side_streams.unwaited_events():
+                ev.synchronize()
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(view.device))
         self.comm_stream.wait_event(ready)
         # weight gradients still running on the side stream (ops/streams.py)
-        for ev in side_streams.unwaited_events():
+        side_evs = list(side_streams.unwaited_events())
+        for ev in side_evs:
             self.comm_stream.wait_event(ev)
+        if os.environ.get("ZK_COMM_HOLD_EVENTS", "0") == "1":
+            self._held_events[-1].extend([ready] + side_evs)
         with torch.cuda.stream(self.comm_stream):
             if self.timing:
                 ev = self._events()
@@ -291,6 +302,7 @@ class GradBucketer:
         if self.check_order:
             self._compare_order(self.last_order)
         self._works.clear()
+        self._held_events = [self._held_events[1], []]
         self._pending = [len(b) for b in self.buckets]
         self._launched = [False] * len(self.buckets)
         self._seen = [False] * len(self.flat.slots)
@@ -389,7 +401,12 @@ class _HostStager:
                 return
             lo, hi, ev, done, box = item
             try:
-                ev.synchronize()
+                if isinstance(ev, tuple):  # (view, stream): blocking copy here
+                    view, stream = ev
+                    with torch.cuda.stream(stream):
+                        self.host[lo:hi].copy_(view, non_blocking=False)
+                else:
+                    ev.synchronize()
                 dist.all_reduce(self.host[lo:hi], group=self.group)
             except Exception as e:  # surfaced by wait()
                 box.append(e)
@@ -397,9 +414,12 @@ class _HostStager:
 
     def submit(self, b: int, lo: int, hi: int, view: torch.Tensor, stream) -> tuple:
         host = self.host[lo:hi]
-        host.copy_(view, non_blocking=True)  # on the comm stream (current)
-        ev = torch.cuda.Event()
-        ev.record(stream)
+        if os.environ.get("ZK_STAGER_SYNC_COPY", "0") == "1":
+            ev = (view, stream)
+        else:
+            host.copy_(view, non_blocking=True)  # on the comm stream (current)
+            ev = torch.cuda.Event()
+            ev.record(stream)
         done, box = threading.Event(), []
         self.q.put((lo, hi, ev, done, box))
         return _StagedWork(done, box), host
