@@ -31,7 +31,6 @@ semantics.  ``runtime.wgrad_side_stream=False`` disables it.
 from __future__ import annotations
 
 import contextlib
-import os
 from typing import Dict, List, Tuple
 
 import torch
@@ -52,9 +51,6 @@ _unwaited: List[torch.cuda.Event] = []
 # which runs a step ahead of the GPU: ~2.5 fresh device allocations per E18
 # step, memory growth and multi-second hipMalloc stalls.)
 _keep: List[torch.Tensor] = []
-# diagnostics: events held for two sessions after their last wait
-_held: List[List[torch.cuda.Event]] = [[], []]
-_HOLD = os.environ.get("ZK_COMM_HOLD_EVENTS", "0") == "1"
 
 
 def active() -> bool:
@@ -121,8 +117,6 @@ def flush(wait: bool = True) -> None:
     cur = torch.cuda.current_stream()
     items = list(_pending)
     _pending.clear()
-    if _HOLD:
-        _held[-1].extend(ev for ev, _ in items)
     if wait:
         for ev in _unwaited:
             cur.wait_event(ev)
@@ -147,7 +141,6 @@ def session(device: torch.device):
     _pending.clear()
     _unwaited.clear()
     _keep.clear()
-    _held[:] = [_held[1], []]
     _active = use
     try:
         yield

@@ -104,8 +104,6 @@ class GradBucketer:
                 self.slot_bucket[i] = bi
         self._pending = [len(b) for b in buckets]
         self._works: List = []
-        # events a stream wait refers to, held for two steps (see _launch)
-        self._held_events: List = [[], []]
         self._launched = [False] * len(buckets)
         self._hooks = []
         self._seen = [False] * len(flat.slots)
@@ -208,21 +206,12 @@ class GradBucketer:
             return
         if self._sync_launch:
             torch.cuda.synchronize(view.device)
-        dbg = os.environ.get("ZK_COMM_DEBUG_WAIT", "")
-        if dbg == "compute":
-            torch.cuda.current_stream(view.device).synchronize()
-        elif dbg == "side":
-            for ev in side_streams.unwaited_events():
-                ev.synchronize()
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(view.device))
         self.comm_stream.wait_event(ready)
         # weight gradients still running on the side stream (ops/streams.py)
-        side_evs = list(side_streams.unwaited_events())
-        for ev in side_evs:
+        for ev in side_streams.unwaited_events():
             self.comm_stream.wait_event(ev)
-        if os.environ.get("ZK_COMM_HOLD_EVENTS", "0") == "1":
-            self._held_events[-1].extend([ready] + side_evs)
         with torch.cuda.stream(self.comm_stream):
             if self.timing:
                 ev = self._events()
@@ -302,7 +291,6 @@ class GradBucketer:
         if self.check_order:
             self._compare_order(self.last_order)
         self._works.clear()
-        self._held_events = [self._held_events[1], []]
         self._pending = [len(b) for b in self.buckets]
         self._launched = [False] * len(self.buckets)
         self._seen = [False] * len(self.flat.slots)
@@ -379,17 +367,27 @@ class _StagedWork:
 class _HostStager:
     """gloo all-reduce of GPU gradient ranges through a pinned host mirror.
 
-    On the comm stream: D2H of the range into the mirror (after the
-    bucket-ready event), then an event.  A worker thread waits for that
-    event (the compute stream never blocks), all-reduces the host range over
-    gloo — one thread, so every rank issues the collectives in the same
-    bucket order — and signals.  :meth:`GradBucketer.finish` then copies the
-    result back H2D on the comm stream, which the compute stream waits on.
-    The mirror range is reused next step only after this H2D (same stream)."""
+    The main thread records an event on the comm stream after the bucket's
+    readiness waits and queues the range.  A worker thread (one, so every
+    rank issues the collectives in the same bucket order) orders its own
+    copy stream after that event, copies the range D2H into the mirror with
+    a BLOCKING copy, all-reduces the host range over gloo and signals;
+    the compute stream never blocks.  :meth:`GradBucketer.finish` then copies
+    the result back H2D on the comm stream, which the compute stream waits
+    on; next step's D2H of the range is ordered after that H2D (its event is
+    recorded on the comm stream later).
+
+    The copy used to be an async D2H on the comm stream followed by an event
+    the worker synchronised on.  With the comm stream at high priority the
+    worker then all-reduced host data that did not yet hold the whole copy
+    in ~1 of 3 two-rank runs (tests/gpu/test_dp_gpu.py, deterministic mode,
+    side stream on: a partially stale weight gradient, identical on both
+    ranks); with the blocking copy: 0 of 12 (scripts/diag_dp.py)."""
 
     def __init__(self, total: int, group):
         self.host = torch.empty(total, dtype=torch.float32, pin_memory=True)
         self.group = group
+        self.copy_stream = None  # created by the worker on first use
         self.q: "queue.Queue" = queue.Queue()
         self.thread = threading.Thread(target=self._run, daemon=True)
         self.thread.start()
@@ -399,14 +397,13 @@ class _HostStager:
             item = self.q.get()
             if item is None:
                 return
-            lo, hi, ev, done, box = item
+            lo, hi, view, ready, done, box = item
             try:
-                if isinstance(ev, tuple):  # (view, stream): blocking copy here
-                    view, stream = ev
-                    with torch.cuda.stream(stream):
-                        self.host[lo:hi].copy_(view, non_blocking=False)
-                else:
-                    ev.synchronize()
+                if self.copy_stream is None:
+                    self.copy_stream = torch.cuda.Stream(view.device)
+                self.copy_stream.wait_event(ready)
+                with torch.cuda.stream(self.copy_stream):
+                    self.host[lo:hi].copy_(view, non_blocking=False)
                 dist.all_reduce(self.host[lo:hi], group=self.group)
             except Exception as e:  # surfaced by wait()
                 box.append(e)
@@ -414,14 +411,10 @@ class _HostStager:
 
     def submit(self, b: int, lo: int, hi: int, view: torch.Tensor, stream) -> tuple:
         host = self.host[lo:hi]
-        if os.environ.get("ZK_STAGER_SYNC_COPY", "0") == "1":
-            ev = (view, stream)
-        else:
-            host.copy_(view, non_blocking=True)  # on the comm stream (current)
-            ev = torch.cuda.Event()
-            ev.record(stream)
+        ready = torch.cuda.Event()
+        ready.record(stream)  # after the bucket's readiness waits
         done, box = threading.Event(), []
-        self.q.put((lo, hi, ev, done, box))
+        self.q.put((lo, hi, view, ready, done, box))
         return _StagedWork(done, box), host
 
 
