@@ -134,6 +134,7 @@ SIGNATURES = {
     "zk_avgpool2_bwd": (I32, [P, P] + [I32] * 6 + [P]),
     "zk_avgpool2_bwd_add": (I32, [P, P, P] + [I32] * 6 + [P]),
     # optimizers
-    "zk_adam_step": (I32, [P, P, P, P, P, I32, F32, F32, F32, F32, F32, F32, F32, F32, P]),
-    "zk_sgd_step": (I32, [P, P, P, P, I32, F32, F32, F32, F32, I32, P]),
+    "zk_adam_step": (I32, [P, P, P, P, P, I32, F32, F32, F32, F32, F32, F32, F32, F32, P, P]),
+    "zk_sgd_step": (I32, [P, P, P, P, I32, F32, F32, F32, F32, I32, P, P]),
+    "zk_weight_images": (I32, [P, P, I32, I64, P]),
 }

@@ -25,6 +25,7 @@ from typing import Optional, Tuple
 
 import torch
 
+from zookeeper_amd.ops import weight_images
 from zookeeper_amd.ops._native import check, direct_grad, grad_ready, igemm_wgrad, lib, stream_ptr
 from zookeeper_amd.ops.options import OPTS
 
@@ -68,12 +69,18 @@ class _ConvFn(torch.autograd.Function):
         pt, pl, Ho, Wo = geometry(H, W, kh, kw, stride, padding)
         T = kh * kw
         xn = _nhwc(x)
-        wf = weight.detach().permute(2, 3, 0, 1).reshape(T, Cout, Cin).to(torch.bfloat16)
-        wf = wf.contiguous()
+        st = stream_ptr(x.device)
+        imgs = weight_images.images(weight, False, st)  # kept by the optimizer
+        if imgs is not None:
+            wf = imgs[0]
+        else:
+            wf = weight.detach().permute(2, 3, 0, 1).reshape(T, Cout, Cin).to(torch.bfloat16)
+            wf = wf.contiguous()
+        ctx.wt = imgs[1] if imgs is not None else None
         y = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x.device)
         check(lib().zk_igemm_fwd_bf16(xn.data_ptr(), wf.data_ptr(), y.data_ptr(), B, H, W, Cin,
-                                      Cout, kh, kw, stride, pt, pl, Ho, Wo, 0, -1,
-                                      stream_ptr(x.device)), "zk_igemm_fwd_bf16")
+                                      Cout, kh, kw, stride, pt, pl, Ho, Wo, 0, -1, st),
+              "zk_igemm_fwd_bf16")
         ctx.save_for_backward(xn)
         ctx.weight = weight
         ctx.geom = (B, Cin, H, W, Cout, kh, kw, stride, pt, pl, Ho, Wo)
@@ -94,8 +101,10 @@ class _ConvFn(torch.autograd.Function):
         # + x's other gradient, left by a consumer that ran first (ResidualHandoff)
         dres = ctx.handoff.take() if ctx.handoff is not None else None
         if ctx.needs_input_grad[0]:
-            wt = weight.detach().permute(2, 3, 1, 0).reshape(T, Cin, Cout).to(torch.bfloat16)
-            wt = wt.contiguous()
+            wt = ctx.wt
+            if wt is None:
+                wt = weight.detach().permute(2, 3, 1, 0).reshape(T, Cin, Cout).to(torch.bfloat16)
+                wt = wt.contiguous()
             dxn = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
             if dres is not None and (tuple(dres.shape) != (B, H, W, Cin)
                                      or not dres.is_contiguous()):

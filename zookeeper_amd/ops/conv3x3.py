@@ -27,6 +27,7 @@ from typing import Optional
 import torch
 
 from zookeeper_amd.ops import pointwise
+from zookeeper_amd.ops import weight_images
 from zookeeper_amd.ops._native import check, direct_grad, grad_ready, igemm_wgrad, lib, stream_ptr
 from zookeeper_amd.ops.options import OPTS
 
@@ -55,14 +56,19 @@ class _Conv3x3Fn(torch.autograd.Function):
         B, Cin, H, W = x.shape
         Cout = weight.shape[0]
         xn = _nhwc(x)
-        wd = weight.detach()
+        st = stream_ptr(x.device)
         # forward as a dgrad: flipped taps, [T][N = Cout][K = Cin]
-        wf = wd.flip(2, 3).permute(2, 3, 0, 1).reshape(9, Cout, Cin).to(torch.bfloat16)
-        wf = wf.contiguous()
+        imgs = weight_images.images(weight, True, st)
+        if imgs is not None:  # kept by the optimizer
+            wf = imgs[0]
+        else:
+            wd = weight.detach()
+            wf = wd.flip(2, 3).permute(2, 3, 0, 1).reshape(9, Cout, Cin).to(torch.bfloat16)
+            wf = wf.contiguous()
+        ctx.wt = imgs[1] if imgs is not None else None
         y = torch.empty((B, H, W, Cout), dtype=torch.bfloat16, device=x.device)
         # dgrad geometry with roles renamed: "Cin" = Cout (N), "Cout" = Cin (K),
         # mirrored pads kh - 1 - 1 = 1
-        st = stream_ptr(x.device)
         if not pointwise.forward_with_stats(stats_for, xn, wf, y, Cout,
                                             (B, H, W, Cout, H, W, Cin, 3, 3, 1, 1, 1), st):
             check(lib().zk_igemm_dgrad(xn.data_ptr(), wf.data_ptr(), None, None, y.data_ptr(), B,
@@ -84,8 +90,10 @@ class _Conv3x3Fn(torch.autograd.Function):
         st = stream_ptr(dev)
         dx = dweight = None
         if ctx.needs_input_grad[0]:
-            wt = weight.detach().permute(2, 3, 1, 0).reshape(9, Cin, Cout).to(torch.bfloat16)
-            wt = wt.contiguous()
+            wt = ctx.wt
+            if wt is None:
+                wt = weight.detach().permute(2, 3, 1, 0).reshape(9, Cin, Cout).to(torch.bfloat16)
+                wt = wt.contiguous()
             dxn = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
             check(L.zk_igemm_dgrad(g.data_ptr(), wt.data_ptr(), None, None, dxn.data_ptr(), B, H,
                                    W, Cin, H, W, Cout, 3, 3, 1, 1, 1, -1, st),

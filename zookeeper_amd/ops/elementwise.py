@@ -37,33 +37,44 @@ def normalize_flip(image: torch.Tensor, mean: Sequence[float], std: Sequence[flo
 CHUNK = 16384
 
 
-def chunk_table(flat) -> torch.Tensor:
+def chunk_table(flat, images=None) -> torch.Tensor:
     """Split every parameter of a FlatParams into ≤CHUNK-element chunks:
-    rows of ``[offset, numel, clip_bits, decay]`` (int64)."""
+    rows of ``[offset, numel, clip_bits, flags]`` (int64); flags = decay
+    (bit 0) | (1 + the parameter's weight-image row) << 8."""
     import struct
 
     rows = []
     for s in flat.slots:
         clip_bits = struct.unpack("<i", struct.pack("<f", s.clip))[0]
+        img = images.row_of(s.param) if images is not None else -1
+        flags = int(s.decay) | ((img + 1) << 8)
         for lo in range(0, s.numel, CHUNK):
-            rows.append([s.offset + lo, min(CHUNK, s.numel - lo), clip_bits, int(s.decay)])
+            rows.append([s.offset + lo, min(CHUNK, s.numel - lo), clip_bits, flags])
     return torch.tensor(rows, dtype=torch.int64)
 
 
 def fused_optimizer_step(opt, lr: float) -> None:
-    """One launch: Adam/SGD + decay + 1/world grad scaling + weight_clip."""
+    """One launch: Adam/SGD + decay + 1/world grad scaling + weight_clip,
+    plus the bf16 weight images of the float convs (ops/weight_images.py)."""
     flat, sp = opt.flat, opt.spec
-    if getattr(opt, "_chunks", None) is None:
-        opt._chunks = chunk_table(flat).to(flat.data.device)
+    reg = getattr(flat, "images", None)
+    gen = reg.generation if reg is not None else -1
+    if getattr(opt, "_chunks", None) is None or getattr(opt, "_chunks_gen", None) != gen:
+        opt._chunks = chunk_table(flat, reg).to(flat.data.device)
+        opt._chunks_gen = gen
     ch = opt._chunks
     st = stream_ptr(flat.data.device)
+    table = reg.table() if reg is not None else None
+    tptr = table.data_ptr() if table is not None else None
     if sp.kind == "adam":
         t = opt.step_count
         check(lib().zk_adam_step(flat.data.data_ptr(), flat.grad.data_ptr(), opt.m.data_ptr(),
                                  opt.v.data_ptr(), ch.data_ptr(), ch.shape[0], lr, sp.beta_1,
                                  sp.beta_2, sp.eps_effective(t), sp.weight_decay, 1 - sp.beta_1**t,
-                                 1 - sp.beta_2**t, opt.grad_scale, st), "zk_adam_step")
+                                 1 - sp.beta_2**t, opt.grad_scale, tptr, st), "zk_adam_step")
     else:
         check(lib().zk_sgd_step(flat.data.data_ptr(), flat.grad.data_ptr(), opt.m.data_ptr(),
                                 ch.data_ptr(), ch.shape[0], lr, sp.momentum, sp.weight_decay,
-                                opt.grad_scale, int(sp.nesterov), st), "zk_sgd_step")
+                                opt.grad_scale, int(sp.nesterov), tptr, st), "zk_sgd_step")
+    if reg is not None and table is not None:
+        reg.valid = True  # every registered image was rewritten from the new parameters

@@ -76,6 +76,10 @@ class KernelOptions:
     # ... and weight-gradient kernel for the stride-1 3x3 convs with >= 256
     # input and output channels.
     wgrad_deep: bool = True
+    # Float conv weights as persistent bf16 GEMM-layout images written by the
+    # fused optimizer (ops/weight_images.py) instead of a cast / transpose
+    # per conv and pass.
+    weight_images: bool = True
 
 
 OPTS = KernelOptions()

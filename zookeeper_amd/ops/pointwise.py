@@ -28,6 +28,7 @@ from typing import Optional
 
 import torch
 
+from zookeeper_amd.ops import weight_images
 from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, igemm_wgrad, lib,
                                         stream_ptr, zeroed_scratch)
 from zookeeper_amd.ops.options import OPTS
@@ -92,10 +93,14 @@ class _Conv1x1Fn(torch.autograd.Function):
         B, Cin, H, W = x.shape
         Cout = weight.shape[0]
         x2 = _rows(x)
-        w2 = weight.detach().reshape(Cout, Cin).to(torch.bfloat16)
-        y2 = torch.empty((x2.shape[0], Cout), dtype=torch.bfloat16, device=x.device)
         L = lib()
         st = stream_ptr(x.device)
+        imgs = weight_images.images(weight, False, st)
+        if imgs is not None:  # kept by the optimizer: [1][Cout][Cin], [1][Cin][Cout]
+            w2, wt = imgs[0].view(Cout, Cin), imgs[1].view(Cin, Cout)
+        else:
+            w2, wt = weight.detach().reshape(Cout, Cin).to(torch.bfloat16), None
+        y2 = torch.empty((x2.shape[0], Cout), dtype=torch.bfloat16, device=x.device)
         # dgrad kernel, roles renamed: N = Cout ("Cin"), K = Cin ("Cout")
         if not forward_with_stats(stats_for, x2, w2, y2, Cout, (B, H, W, Cout, H, W, Cin,
                                                                  1, 1, 1, 0, 0), st):
@@ -103,6 +108,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                                    B, H, W, Cout, H, W, Cin, 1, 1, 1, 0, 0, -1, st),
                   "zk_igemm_dgrad(1x1 fwd)")
         ctx.save_for_backward(x2, w2)
+        ctx.wt = wt
         ctx.weight = weight
         ctx.handoff, ctx.give = handoff, give
         ctx.shape = (B, Cin, H, W, Cout)
@@ -122,7 +128,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         dres = ctx.handoff.take() if ctx.handoff is not None else None
         if ctx.needs_input_grad[0]:
             dx2 = torch.empty((g2.shape[0], Cin), dtype=torch.bfloat16, device=dev)
-            wt = w2.t().contiguous()  # [Cin][Cout]
+            wt = ctx.wt if ctx.wt is not None else w2.t().contiguous()  # [Cin][Cout]
             if dres is not None and tuple(dres.shape) != (B, H, W, Cin):
                 raise RuntimeError(f"residual gradient {tuple(dres.shape)} does not match the "
                                    f"1x1 conv input {(B, H, W, Cin)}")

@@ -1,0 +1,163 @@
+"""bf16 GEMM-layout images of the float conv weights, kept by the optimizer.
+
+The float convs' MFMA kernels (``ops/pointwise.py``, ``ops/conv3x3.py``,
+``ops/conv.py``) read their weights as bf16 in GEMM layouts:
+
+* forward: ``[T][Cout][Cin]`` (the 3×3 "same" conv runs as a dgrad, so its
+  taps are flipped);
+* data gradient: ``[T][Cin][Cout]``.
+
+Building them per pass costs a framework cast / transpose launch per conv and
+pass (~140 ``at::native`` copy kernels per ResNet-50 step).  Under the
+:class:`~zookeeper_amd.train.trainer.Trainer`, a :class:`WeightImages`
+registry instead keeps one persistent image pair per conv weight:
+
+* the first use of a weight registers it and builds its images
+  (``zk_weight_images``, one launch for every registered weight);
+* the fused optimizer step (``optimizer.hip``) writes the images of every
+  parameter it updates in the same pass, so they stay current for free;
+* any other change of the parameters (initial broadcast, checkpoint restore,
+  a non-fused optimizer) must call :meth:`WeightImages.invalidate`; the next
+  use rebuilds every image in one launch.
+
+Ops call :func:`images` and fall back to building the images themselves when
+the weight has no registry (direct use outside the trainer) or
+``runtime.weight_images`` is off.  The images are bit-identical to
+``weight.to(torch.bfloat16)`` in the same layout (round to nearest even).
+SURVEY §2 N7 (the fused optimizer); VERDICT r3 item 3.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from zookeeper_amd.ops._native import check, lib
+
+
+@dataclass
+class _Entry:
+    row: int
+    param: torch.nn.Parameter
+    offset: int  # flat offset (elements)
+    flip: bool
+    fwd: torch.Tensor  # bf16 [T][Cout][Cin]
+    bwd: torch.Tensor  # bf16 [T][Cin][Cout]
+
+
+class WeightImages:
+    def __init__(self, flat):
+        self.flat = flat
+        self._offsets = {id(s.param): s.offset for s in flat.slots}
+        self.entries: Dict[int, _Entry] = {}
+        self.generation = 0  # bumped on registration (the optimizer rebuilds its chunk table)
+        self.valid = False
+        self._table: Optional[torch.Tensor] = None
+        self._max_numel = 0
+        self.builds = 0  # full rebuilds (tests / diagnostics)
+        self.row_builds = 0  # single-weight builds at registration
+
+    # -- registration ---------------------------------------------------------
+    def attach(self) -> None:
+        """Mark every 4-D parameter of the flat buffer as served by this
+        registry (``p._zk_images``)."""
+        for s in self.flat.slots:
+            if s.param.dim() == 4:
+                s.param._zk_images = self
+
+    def detach(self) -> None:
+        for s in self.flat.slots:
+            if getattr(s.param, "_zk_images", None) is self:
+                del s.param._zk_images
+
+    def invalidate(self) -> None:
+        """The parameters changed outside the fused optimizer."""
+        self.valid = False
+
+    def row_of(self, param) -> int:
+        e = self.entries.get(id(param))
+        return -1 if e is None else e.row
+
+    def table(self) -> Optional[torch.Tensor]:
+        """Device image table (int64 [rows][8]), or None without entries."""
+        if not self.entries:
+            return None
+        if self._table is None:
+            rows = []
+            for e in sorted(self.entries.values(), key=lambda e: e.row):
+                p = e.param
+                Cout, Cin, KH, KW = p.shape
+                ohwi = (not p.is_contiguous()) and p.is_contiguous(
+                    memory_format=torch.channels_last)
+                flags = (1 if ohwi else 0) | (2 if e.flip else 0)
+                rows.append([e.offset, Cout, Cin, KH, KW, flags, e.fwd.data_ptr(),
+                             e.bwd.data_ptr()])
+            self._table = torch.tensor(rows, dtype=torch.int64).to(self.flat.data.device)
+            self._max_numel = max(e.param.numel() for e in self.entries.values())
+        return self._table
+
+    def _register(self, param, flip: bool) -> _Entry:
+        Cout, Cin, KH, KW = param.shape
+        dev = self.flat.data.device
+        T = KH * KW
+        e = _Entry(len(self.entries), param, self._offsets[id(param)], flip,
+                   torch.empty((T, Cout, Cin), dtype=torch.bfloat16, device=dev),
+                   torch.empty((T, Cin, Cout), dtype=torch.bfloat16, device=dev))
+        self.entries[id(param)] = e
+        self.generation += 1
+        self._table = None
+        return e
+
+    def refresh(self, stream: int) -> None:
+        """Rebuild every image from the current parameters (one launch)."""
+        t = self.table()
+        if t is None:
+            return
+        check(lib().zk_weight_images(self.flat.data.data_ptr(), t.data_ptr(), t.shape[0],
+                                     self._max_numel, stream), "zk_weight_images")
+        self.builds += 1
+        self.valid = True
+
+    def get(self, param, flip: bool, stream: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        e = self.entries.get(id(param))
+        if e is None:
+            e = self._register(param, flip)
+            if self.valid:  # the others are current: build just this one
+                t = self.table()[e.row:e.row + 1]
+                check(lib().zk_weight_images(self.flat.data.data_ptr(), t.data_ptr(), 1,
+                                             param.numel(), stream), "zk_weight_images")
+                self.row_builds += 1
+        elif e.flip != flip:
+            raise RuntimeError("a conv weight was requested with two forward tap orders")
+        if not self.valid:
+            self.refresh(stream)
+        return e.fwd, e.bwd
+
+
+def invalidate_model(model: torch.nn.Module) -> None:
+    """Parameters of ``model`` were overwritten (checkpoint restore): rebuild
+    their weight images at the next use."""
+    for p in model.parameters():
+        reg = getattr(p, "_zk_images", None)
+        if reg is not None:
+            reg.invalidate()
+
+
+def _usable(weight) -> bool:
+    if weight.dim() != 4 or weight.dtype != torch.float32 or not weight.is_cuda:
+        return False
+    return weight.is_contiguous() or weight.is_contiguous(memory_format=torch.channels_last)
+
+
+def images(weight, flip: bool, stream: int) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+    """(forward image [T][Cout][Cin], data-gradient image [T][Cin][Cout]) of a
+    float conv weight kept by the trainer's registry, or None (build them in
+    the op)."""
+    from zookeeper_amd.ops.options import OPTS
+
+    reg = getattr(weight, "_zk_images", None)
+    if reg is None or not OPTS.weight_images or not _usable(weight):
+        return None
+    return reg.get(weight, flip, stream)

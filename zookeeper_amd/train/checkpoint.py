@@ -103,6 +103,9 @@ def load(path: str, model: torch.nn.Module, optimizer=None, rank: int = 0) -> Di
         own = model.state_dict()
         for k, v in state.items():
             own[k].copy_(v)
+    from zookeeper_amd.ops.weight_images import invalidate_model
+
+    invalidate_model(model)  # the bf16 weight images no longer match
     if optimizer is not None and os.path.exists(os.path.join(path, "optimizer.pt")):
         ostate = torch.load(os.path.join(path, "optimizer.pt"), map_location="cpu",
                             weights_only=True)

@@ -172,6 +172,9 @@ class FlatOptimizer:
             ops.fused_optimizer_step(self, lr)
         else:
             self._step_torch(lr)
+            reg = getattr(self.flat, "images", None)
+            if reg is not None:
+                reg.invalidate()  # parameters changed without their weight images
         return lr
 
     def state_dict(self) -> Dict[str, Any]:

@@ -47,6 +47,7 @@ class Runtime:
     wgrad_reduce: str = Field("auto")
     dgrad_deep: bool = Field(True)
     wgrad_deep: bool = Field(True)
+    weight_images: bool = Field(True)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
     deterministic: bool = Field(False)

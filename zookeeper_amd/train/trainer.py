@@ -59,11 +59,20 @@ class Trainer:
         self.last_metrics: dict = {}
         self.eval_metrics: dict = {}  # eval_step's (kept apart: graph replays reuse last_metrics)
         self.flat = FlatParams(self.model, self.device)
+        if self.device.type == "cuda":
+            # bf16 GEMM-layout images of the float conv weights, kept current
+            # by the fused optimizer (ops/weight_images.py)
+            from zookeeper_amd.ops.weight_images import WeightImages
+
+            self.flat.images = WeightImages(self.flat)
+            self.flat.images.attach()
         if self.info.world > 1:
             # One broadcast of the flat parameter buffer + the BN buffers.
             zdist.broadcast_(self.flat.data)
             for b in self.model.buffers():
                 zdist.broadcast_(b)
+            if getattr(self.flat, "images", None) is not None:
+                self.flat.images.invalidate()
         # force_dp: the bucketed all-reduce stays on with one rank (a 1-rank
         # RCCL group), so one GPU runs the exact data-parallel code path
         comm = self.info.comm
