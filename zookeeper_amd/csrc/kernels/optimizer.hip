@@ -189,6 +189,13 @@ ZK_EXPORT int zk_sgd_step(void* p, const void* g, void* m, const void* chunks, i
   return 0;
 }
 
+// Zero `bytes` of device memory on `stream` (the per-step gradient-buffer
+// clear: a runtime memset instead of a framework fill kernel).
+ZK_EXPORT int zk_zero(void* p, long long bytes, hipStream_t stream) {
+  if (bytes <= 0) return 0;
+  return (int)hipMemsetAsync(p, 0, (size_t)bytes, stream);
+}
+
 // Weight images of `rows` image-table rows (see the top of this file) from
 // the flat parameter buffer; max_numel = the largest row's element count.
 ZK_EXPORT int zk_weight_images(const void* flat, const void* images, int rows,

@@ -100,7 +100,27 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(const float* __restrict__
   }
 }
 
+// Mean loss and hit count out of the accumulators, which are re-zeroed for
+// the next call (no framework fill / divide / cast kernels around the op).
+__global__ void xent_finalize_kernel(float* __restrict__ acc, float* __restrict__ loss,
+                                     long long* __restrict__ hits, int B) {
+  if (threadIdx.x != 0) return;
+  loss[0] = __fdiv_rn(acc[0], (float)B);
+  hits[0] = (long long)__float_as_int(acc[1]);
+  acc[0] = 0.f;
+  acc[1] = 0.f;  // int 0 bits
+}
+
 }  // namespace
+
+// acc = [loss_sum fp32, correct int32 bits] -> loss = loss_sum / B (fp32),
+// hits (int64); acc re-zeroed.
+ZK_EXPORT int zk_xent_finalize(void* acc, void* loss, void* hits, int B, hipStream_t st) {
+  hipLaunchKernelGGL(xent_finalize_kernel, dim3(1), dim3(64), 0, st, (float*)acc, (float*)loss,
+                     (long long*)hits, B);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
 
 // loss_sum (fp32) and correct (int32) are accumulated (zeroed by the caller).
 // row_loss (optional, [B] fp32): per-row losses summed in a fixed order

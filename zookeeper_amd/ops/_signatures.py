@@ -137,4 +137,6 @@ SIGNATURES = {
     "zk_adam_step": (I32, [P, P, P, P, P, I32, F32, F32, F32, F32, F32, F32, F32, F32, P, P]),
     "zk_sgd_step": (I32, [P, P, P, P, I32, F32, F32, F32, F32, I32, P, P]),
     "zk_weight_images": (I32, [P, P, I32, I64, P]),
+    "zk_zero": (I32, [P, I64, P]),
+    "zk_xent_finalize": (I32, [P, P, P, I32, P]),
 }

@@ -8,6 +8,19 @@ from zookeeper_amd.ops._native import check, lib, stream_ptr
 from zookeeper_amd.ops.options import OPTS
 
 
+# Per-device accumulator [loss_sum, correct (int32 bits)], zero between calls
+# (zk_xent_finalize reads and re-zeroes it).
+_ACC = {}
+
+
+def _acc(dev: torch.device) -> torch.Tensor:
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    a = _ACC.get(key)
+    if a is None:
+        a = _ACC[key] = torch.zeros(2, dtype=torch.float32, device=dev)
+    return a
+
+
 class _SoftmaxXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, eps):
@@ -16,7 +29,7 @@ class _SoftmaxXentFn(torch.autograd.Function):
         y = labels.to(torch.int64).contiguous()
         dev = x.device
         lse = torch.empty(B, dtype=torch.float32, device=dev)
-        acc = torch.zeros(2, dtype=torch.float32, device=dev)  # [loss_sum, correct (int bits)]
+        acc = _acc(dev)
         correct = acc[1:].view(torch.int32)
         # deterministic mode: per-row losses summed in a fixed order
         row_loss = torch.empty(B, dtype=torch.float32, device=dev) if OPTS.deterministic else None
@@ -25,15 +38,20 @@ class _SoftmaxXentFn(torch.autograd.Function):
                                 row_loss.data_ptr() if row_loss is not None else None,
                                 stream_ptr(dev)),
               "zk_xent_fwd")
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        hits = torch.empty((), dtype=torch.int64, device=dev)
+        check(lib().zk_xent_finalize(acc.data_ptr(), loss.data_ptr(), hits.data_ptr(), B,
+                                     stream_ptr(dev)), "zk_xent_finalize")
         ctx.save_for_backward(x, y, lse)
         ctx.eps, ctx.in_dtype = float(eps), logits.dtype
-        loss = acc[0] / B
-        hits = correct.reshape(()).to(torch.int64)
         ctx.mark_non_differentiable(hits)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the hit count
         return loss, hits
 
     @staticmethod
     def backward(ctx, gloss, _ghits):
+        if gloss is None:
+            return None, None, None
         x, y, lse = ctx.saved_tensors
         B, C = x.shape
         g = gloss.float().reshape(1).contiguous()

@@ -79,6 +79,15 @@ class FlatParams:
         self.slots = slots
 
     def zero_grad(self) -> None:
+        if self.grad.is_cuda:
+            from zookeeper_amd.ops import _native
+
+            if _native.available():  # a runtime memset, not a framework fill kernel
+                _native.check(_native.lib().zk_zero(self.grad.data_ptr(),
+                                                    self.grad.numel() * 4,
+                                                    _native.stream_ptr(self.grad.device)),
+                              "zk_zero")
+                return
         self.grad.zero_()
 
     def rebind_grads(self) -> None:

@@ -121,7 +121,14 @@ class Trainer:
                 self.last_metrics = {k: f(logits.detach(), y) for k, f in self.metric_fns.items()}
         # binary-conv weight gradients on a side stream, ordered by events
         with streams.session(self.device):
-            loss.backward()
+            if loss.is_cuda:
+                # a persistent seed gradient: no fill kernel for ones_like(loss)
+                one = getattr(self, "_one", None)
+                if one is None or one.device != loss.device or one.dtype != loss.dtype:
+                    one = self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
+                torch.autograd.backward(loss, one)
+            else:
+                loss.backward()
         return loss.detach(), correct
 
     def train_step(self, x: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
