@@ -86,3 +86,11 @@ def test_invalidate_rebuilds_images():
     fwd, bwd = _expected(e.param, e.flip)
     assert torch.equal(e.fwd, fwd) and torch.equal(e.bwd, bwd)
     assert reg.builds == 2
+    # an in-place edit without invalidate() is caught by the version counters
+    with torch.no_grad():
+        e.param.mul_(2.0)
+    reg.get(e.param, e.flip, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    fwd, bwd = _expected(e.param, e.flip)
+    assert torch.equal(e.fwd, fwd) and torch.equal(e.bwd, bwd)
+    assert reg.builds == 3

@@ -77,4 +77,4 @@ def fused_optimizer_step(opt, lr: float) -> None:
                                 ch.data_ptr(), ch.shape[0], lr, sp.momentum, sp.weight_decay,
                                 opt.grad_scale, int(sp.nesterov), tptr, st), "zk_sgd_step")
     if reg is not None and table is not None:
-        reg.valid = True  # every registered image was rewritten from the new parameters
+        reg._mark_current()  # every registered image was rewritten from the new parameters

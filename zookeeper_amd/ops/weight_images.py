@@ -18,7 +18,10 @@ registry instead keeps one persistent image pair per conv weight:
   parameter it updates in the same pass, so they stay current for free;
 * any other change of the parameters (initial broadcast, checkpoint restore,
   a non-fused optimizer) must call :meth:`WeightImages.invalidate`; the next
-  use rebuilds every image in one launch.
+  use rebuilds every image in one launch.  As a safety net, an in-place
+  change that bumps the autograd version counter of the weight or of the
+  flat buffer (``with torch.no_grad(): w.mul_(2)``, ``copy_``) is detected
+  at the next use as well; the optimizer's raw-pointer writes bump neither.
 
 Ops call :func:`images` and fall back to building the images themselves when
 the weight has no registry (direct use outside the trainer) or
@@ -45,6 +48,7 @@ class _Entry:
     flip: bool
     fwd: torch.Tensor  # bf16 [T][Cout][Cin]
     bwd: torch.Tensor  # bf16 [T][Cin][Cout]
+    version: int = -1  # param._version the images were built from
 
 
 class WeightImages:
@@ -54,6 +58,7 @@ class WeightImages:
         self.entries: Dict[int, _Entry] = {}
         self.generation = 0  # bumped on registration (the optimizer rebuilds its chunk table)
         self.valid = False
+        self._flat_version = -1  # flat.data._version at the last build
         self._table: Optional[torch.Tensor] = None
         self._max_numel = 0
         self.builds = 0  # full rebuilds (tests / diagnostics)
@@ -118,7 +123,18 @@ class WeightImages:
         check(lib().zk_weight_images(self.flat.data.data_ptr(), t.data_ptr(), t.shape[0],
                                      self._max_numel, stream), "zk_weight_images")
         self.builds += 1
+        self._mark_current()
+
+    def _mark_current(self) -> None:
+        """Every image matches the parameters as they are now."""
         self.valid = True
+        self._flat_version = self.flat.data._version
+        for e in self.entries.values():
+            e.version = e.param._version
+
+    def _stale(self, e: _Entry) -> bool:
+        return (not self.valid or e.version != e.param._version
+                or self._flat_version != self.flat.data._version)
 
     def get(self, param, flip: bool, stream: int) -> Tuple[torch.Tensor, torch.Tensor]:
         e = self.entries.get(id(param))
@@ -129,9 +145,10 @@ class WeightImages:
                 check(lib().zk_weight_images(self.flat.data.data_ptr(), t.data_ptr(), 1,
                                              param.numel(), stream), "zk_weight_images")
                 self.row_builds += 1
+                e.version = param._version
         elif e.flip != flip:
             raise RuntimeError("a conv weight was requested with two forward tap orders")
-        if not self.valid:
+        if self._stale(e):
             self.refresh(stream)
         return e.fwd, e.bwd
 
