@@ -68,8 +68,11 @@ class KernelOptions:
     # 1536 (profiles/r4/a_wgrad_atomic_vs_slab.md): 56x56x64 atomic 630 vs
     # slab 909 us (the slab cap starves its grid); the deep 256 / 512-channel
     # layers slab 545 / 540 vs atomic 648 / 695 us (fp32 atomics run at
-    # ~1.3 TB/s of added bytes, slab stores at ~6 TB/s).
-    wgrad_reduce: str = "auto"
+    # ~1.3 TB/s of added bytes, slab stores at ~6 TB/s).  In the E18 step
+    # all-slab beat "auto" on every box measured (interleaved 80-100-step
+    # windows at batch 1536: 46.9-47.0k vs 46.85k; 47.13k / 47.02k vs
+    # 46.91k / 46.68k), so slabs are the default.
+    wgrad_reduce: str = "slab"
     # Phased data-gradient kernel (deep_gemm.hip) for the stride-1 3x3
     # binary convs with >= 128 input channels.
     dgrad_deep: bool = True

@@ -44,7 +44,7 @@ class Runtime:
     dgrad_rw: bool = Field(True)
     bn_stats_epilogue: bool = Field(True)
     wgrad_slab_mb: int = Field(32)
-    wgrad_reduce: str = Field("auto")
+    wgrad_reduce: str = Field("slab")
     dgrad_deep: bool = Field(True)
     wgrad_deep: bool = Field(True)
     weight_images: bool = Field(True)
