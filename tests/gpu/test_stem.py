@@ -190,3 +190,48 @@ def test_two_pass_finalize_matches_one_pass(nb):
         outs.append((coef, rm, rv))
     for a, b in zip(outs[0], outs[1]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_bn2_sums_from_the_first_binary_block(monkeypatch):
+    """E18's stem hands its BN-2 to the first binary block like the binary
+    blocks do among themselves: the block's row-window dgrad epilogue sums
+    (dx, dx * yhat) over the stem output's gradient, and the stem backward
+    skips its own reduce.  Same BN-2 gradients as the stem's own reduce
+    (up to summation order)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from zookeeper_amd.models.binary_resnet import BinaryResNetE
+    from zookeeper_amd.ops import stem as stem_mod
+
+    torch.manual_seed(3)
+    x = torch.randn(8, 3, 64, 64, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+
+    def run(handoff: bool):
+        torch.manual_seed(5)
+        model = BinaryResNetE((64, 64, 3), 10, 18, backend="hip").cuda()
+        for p in model.parameters():
+            if p.dim() == 4:
+                p.data = p.data.contiguous(memory_format=torch.channels_last)
+        model.train()
+        if not handoff:
+            orig = stem_mod.fused_stem
+
+            def no_handoff(*a, **k):
+                out = orig(*a, **k)
+                out.__dict__.pop("_zk_bnsum", None)
+                return out
+            monkeypatch.setattr(stem_mod, "fused_stem", no_handoff)
+        before = stem_mod.FUSED_BN2_SUMS[0]
+        out = model(x)
+        out.float().square().mean().backward()
+        used = stem_mod.FUSED_BN2_SUMS[0] - before
+        monkeypatch.undo()
+        bn2 = model.stem[3]
+        return used, bn2.weight.grad.clone(), bn2.bias.grad.clone()
+
+    used, gw, gb = run(True)
+    used0, gw0, gb0 = run(False)
+    assert used == 1 and used0 == 0
+    torch.testing.assert_close(gw, gw0, rtol=1e-4, atol=1e-4 * gw0.abs().max().item())
+    torch.testing.assert_close(gb, gb0, rtol=1e-4, atol=1e-4 * gb0.abs().max().item())

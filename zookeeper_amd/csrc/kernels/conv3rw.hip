@@ -62,12 +62,14 @@ struct RWArgs {
   int B, H, W, ngroups, ipb, slot;
   // optional: the predecessor block's BN-backward reduction over the stored
   // dx (its output gradient): psums[0][c][stripe] += sum dx,
-  // [1][c][stripe] += sum dx * (ypred - mean[c]) * rstd[c]  (ypred int16 [B][H][W][64])
+  // [1][c][stripe] += sum dx * (ypred - mean[c]) * rstd[c]  (ypred int16, or bf16
+  // with ypred_bf16, [B][H][W][64])
   const int16_t* ypred;
   const float* pmean;
   const float* prstd;
   float* psums;
   int stripes;
+  int ypred_bf16;  // ypred holds bf16 values (the stem's pooled BN-2 input), not int16
 };
 
 // vmcnt(0) through the builtin (expcnt / lgkmcnt left at their maxima), so
@@ -301,7 +303,8 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void conv3rw_dgrad_kernel(RWArgs a) 
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float gv = zk::bf16_to_f32((uint16_t)(pw4[e >> 1] >> (16 * (e & 1))));
-          const float yv = (float)(int16_t)(uint16_t)(y4[e >> 1] >> (16 * (e & 1)));
+          const uint16_t yb = (uint16_t)(y4[e >> 1] >> (16 * (e & 1)));
+          const float yv = a.ypred_bf16 ? zk::bf16_to_f32(yb) : (float)(int16_t)yb;
           s1[e] += gv;
           s2[e] += gv * (yv - mu[e]) * rs[e];
         }
@@ -370,7 +373,7 @@ int g_lds_attr = 0;
 int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres,
                           void* dx, int B, int H, int W, int Cin, int Cout, const void* ypred,
                           const void* pmean, const void* prstd, void* psums, int stripes,
-                          bool dry, hipStream_t st) {
+                          int ypred_bf16, bool dry, hipStream_t st) {
   if (Cin != 64 || Cout != 64 || W < 1 || W > 64 || H < 1 || B < 1) return (int)hipErrorInvalidValue;
   if (psums && (!ypred || !pmean || !prstd)) return (int)hipErrorInvalidValue;
   if ((long long)B * H * W * 64 >= (1LL << 40)) return (int)hipErrorInvalidValue;
@@ -394,7 +397,7 @@ int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, cons
   RWArgs a{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
            (const uint16_t*)dres, (uint16_t*)dx, B, H, W, (H + RW_TR - 1) / RW_TR, 0, slot,
            (const int16_t*)ypred, (const float*)pmean, (const float*)prstd, (float*)psums,
-           stripes < 1 ? 1 : stripes};
+           stripes < 1 ? 1 : stripes, ypred_bf16};
   const int nitems = B * a.ngroups;
   a.ipb = (nitems + g_num_cus - 1) / g_num_cus;
   const int grid = (nitems + a.ipb - 1) / a.ipb;

@@ -1046,7 +1046,8 @@ struct BnSum {
   const void* rstd;
   void* sums;
   int stripes;
-  void* fstats;  // LE variants only: ConvArgs::fstats (float forward statistics)
+  void* fstats = nullptr;  // LE variants only: ConvArgs::fstats (float forward statistics)
+  int ypred_bf16 = 0;      // ypred bf16 (the stem's pooled BN-2 input): variant 50 only
 };
 
 template <int BM, int BN, int WM, int WN, int NS, int CB = 128, bool LE = false>
@@ -1875,7 +1876,7 @@ int zk_dgrad_deep_impl(const void* dy, const void* wt, const void* mask, const v
 int zk_conv3rw_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres,
                           void* dx, int B, int H, int W, int Cin, int Cout, const void* ypred,
                           const void* pmean, const void* prstd, void* psums, int stripes,
-                          bool dry, hipStream_t st);
+                          int ypred_bf16, bool dry, hipStream_t st);
 
 namespace {
 int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
@@ -1936,8 +1937,11 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
         g.Wo != g.W)
       return (int)hipErrorInvalidValue;
     return zk_conv3rw_dgrad_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Cout, bs.ypred,
-                                 bs.mean, bs.rstd, bs.sums, bs.stripes, g_dry_run, stream);
+                                 bs.mean, bs.rstd, bs.sums, bs.stripes, bs.ypred_bf16, g_dry_run,
+                                 stream);
   }
+  // bf16 predecessor outputs: only the row-window epilogue converts them
+  if (bs.ypred_bf16) return (int)hipErrorInvalidValue;
   const int rc = igemm_dgrad_variant(variant, dy, wt, mask, dres, dx, g, bs, stream);
   if (rc) return rc;
   if (!g_dry_run) ZK_CHECK_LAUNCH();
@@ -1962,14 +1966,16 @@ ZK_EXPORT int zk_igemm_dgrad(const void* dy, const void* wt, const void* mask, c
 // [Cin]).  Valid when dx is that block's whole output gradient.
 ZK_EXPORT int zk_igemm_dgrad_bnsum(const void* dy, const void* wt, const void* mask,
                                    const void* dres, void* dx, const void* ypred, const void* mean,
-                                   const void* rstd, void* sums, int stripes, int B, int H, int W,
-                                   int Cin, int Ho, int Wo, int Cout, int kh, int kw, int stride,
-                                   int pt, int pl, int variant, hipStream_t stream) {
+                                   const void* rstd, void* sums, int stripes, int ypred_bf16,
+                                   int B, int H, int W, int Cin, int Ho, int Wo, int Cout, int kh,
+                                   int kw, int stride, int pt, int pl, int variant,
+                                   hipStream_t stream) {
   IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
   if (!ypred || !mean || !rstd || !sums || Cin % 32) return (int)hipErrorInvalidValue;
   return igemm_dgrad_impl(dy, wt, mask, dres, dx, g,
-                          BnSum{ypred, mean, rstd, sums, stripes < 1 ? 1 : stripes}, variant,
-                          stream);
+                          BnSum{ypred, mean, rstd, sums, stripes < 1 ? 1 : stripes, nullptr,
+                                ypred_bf16 ? 1 : 0},
+                          variant, stream);
 }
 
 // Float 1x1 forward as this GEMM (roles renamed as in ops/pointwise.py:

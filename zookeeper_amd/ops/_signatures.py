@@ -42,7 +42,7 @@ SIGNATURES = {
     "zk_bconv_fwd": (I32, [P, P, P, P, P] + [I32] * 14 + [P]),
     "zk_bconv_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
     "zk_igemm_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
-    "zk_igemm_dgrad_bnsum": (I32, [P] * 9 + [I32] * 14 + [P]),
+    "zk_igemm_dgrad_bnsum": (I32, [P] * 9 + [I32] * 15 + [P]),
     "zk_igemm_dgrad_fstats": (I32, [P] * 4 + [I32] * 14 + [P]),
     "zk_igemm_fwd": (I32, [P, P, P, P] + [I32] * 16 + [P]),
     "zk_igemm_fwd_fp4": (I32, [P, P, P, P] + [I32] * 16 + [P]),

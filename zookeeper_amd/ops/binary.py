@@ -76,13 +76,15 @@ def bf16_sign_needed() -> bool:
 
 class _BnSum:
     """What the successor's dgrad needs to reduce this block's BN gradient:
-    the int16 conv output, BN mean / rstd, the striped sums buffer, and (set
-    by the successor's backward) the dx it reduced and its version."""
+    the BN input (the int16 conv output of a binary block, or the bf16 pooled
+    tensor of the stem: ``bf16``), BN mean / rstd, the striped sums buffer,
+    and (set by the successor's backward) the dx it reduced and its version."""
 
-    __slots__ = ("y", "mean", "rstd", "sums", "dx", "dx_version")
+    __slots__ = ("y", "mean", "rstd", "sums", "bf16", "dx", "dx_version")
 
-    def __init__(self, y, mean, rstd, sums):
+    def __init__(self, y, mean, rstd, sums, bf16: bool = False):
         self.y, self.mean, self.rstd, self.sums = y, mean, rstd, sums
+        self.bf16 = bool(bf16)
         self.dx = self.dx_version = None
 
     def reduced(self, dout: torch.Tensor) -> bool:
@@ -353,7 +355,8 @@ class _BinaryBlockFn(torch.autograd.Function):
                                                  dres.data_ptr() if dres is not None else None,
                                                  dx.data_ptr(), pred.y.data_ptr(),
                                                  pred.mean.data_ptr(), pred.rstd.data_ptr(),
-                                                 pred.sums.data_ptr(), pred.sums.shape[2], B, H, W,
+                                                 pred.sums.data_ptr(), pred.sums.shape[2],
+                                                 int(pred.bf16), B, H, W,
                                                  Cin,
                                                  Ho, Wo, Cout, kh, kw, stride, pt, pl, -1, st),
                           "zk_igemm_dgrad_bnsum")

@@ -99,10 +99,15 @@ def _bn_bwd_coef(L, st, sums, coef, gamma_p, beta_p, P, C, dev, stripes: int = 1
     return bcoef, dgamma, dbeta
 
 
+# BN-2 backward sums taken from the first binary block's dgrad epilogue
+# (backward passes; tests / diagnostics)
+FUSED_BN2_SUMS = [0]
+
+
 class _StemFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, g1, b1, g2, b2, bn1, bn2, pool):
-        pk, ps, sign_clip, holder = pool
+        pk, ps, sign_clip, holder, bnsum_holder = pool
         B, Cin, H, W = x.shape
         Cout, _, KH, KW = weight.shape
         s = 2
@@ -233,6 +238,19 @@ class _StemFn(torch.autograd.Function):
             else:
                 check(L.zk_bn_apply_bf16(p.data_ptr(), coef2.data_ptr(), out.data_ptr(), P2,
                                          Cout, 0, st), "zk_bn_apply_bf16")
+        # BN-2's backward sums reduced by the first binary block's row-window
+        # dgrad epilogue (its dx is exactly this output's gradient: identity
+        # shortcut, single consumer), as between binary blocks
+        ctx.bnsum = None
+        if (bnsum_holder is not None and bn2 is not None and bn2.training
+                and OPTS.dgrad_rw and not OPTS.deterministic
+                and Cout == 64 and W2 <= 64):
+            from zookeeper_amd.ops.binary import _BnSum, bwd_stripes
+
+            sums_buf = zeroed_scratch(bn2, "bwd_sums", (2, Cout, bwd_stripes()), torch.float32,
+                                      dev)
+            ctx.bnsum = _BnSum(p, coef2[2], coef2[3], sums_buf, bf16=True)
+            bnsum_holder.append(ctx.bnsum)
         ctx.save_for_backward(xp, ws, y1 if y1 is not None else ya, arg, p, coef1, coef2, g1,
                               g2)
         ctx.fused = fused
@@ -254,18 +272,31 @@ class _StemFn(torch.autograd.Function):
         g = dout.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
         dg2 = db2 = None
         if ctx.has_bn2:
-            # per-block partials summed in a fixed order: the stem's BN-1 / conv
-            # gradients amplify run-to-run noise of these sums (BN-2 makes
-            # dL/dgamma1 a near-total cancellation)
-            sums2 = torch.empty((2, Cout, L.zk_bn_bwd_parts_max()), dtype=torch.float32,
-                                device=dev)  # channel-major copies
-            nb2 = ctypes.c_int(0)
-            check(L.zk_bn_bwd_reduce_bf16_parts(g.data_ptr(), p.data_ptr(), None,
-                                                coef2.data_ptr(), sums2.data_ptr(), P2, Cout,
-                                                ctypes.byref(nb2), st),
-                  "zk_bn_bwd_reduce_bf16_parts")
-            bcoef2, dg2, db2 = _bn_bwd_coef(L, st, sums2, coef2, g2p, b2p, P2, Cout, dev,
-                                            stripes=nb2.value, stride=sums2.shape[2])
+            bs = ctx.bnsum
+            touched = bs is not None and bs.dx is not None  # the successor wrote the sums
+            if touched and bs.reduced(dout):
+                # the first binary block's row-window dgrad epilogue reduced
+                # exactly this gradient (one copy per block, fixed order)
+                n = bs.sums.shape[2]
+                FUSED_BN2_SUMS[0] += 1
+                bcoef2, dg2, db2 = _bn_bwd_coef(L, st, bs.sums, coef2, g2p, b2p, P2, Cout, dev,
+                                                stripes=n, stride=n)
+            else:
+                if touched:
+                    bs.dx = None
+                    bs.sums.zero_()  # a gradient that was accumulated after the reduction
+                # per-block partials summed in a fixed order: the stem's BN-1 /
+                # conv gradients amplify run-to-run noise of these sums (BN-2
+                # makes dL/dgamma1 a near-total cancellation)
+                sums2 = torch.empty((2, Cout, L.zk_bn_bwd_parts_max()), dtype=torch.float32,
+                                    device=dev)  # channel-major copies
+                nb2 = ctypes.c_int(0)
+                check(L.zk_bn_bwd_reduce_bf16_parts(g.data_ptr(), p.data_ptr(), None,
+                                                    coef2.data_ptr(), sums2.data_ptr(), P2, Cout,
+                                                    ctypes.byref(nb2), st),
+                      "zk_bn_bwd_reduce_bf16_parts")
+                bcoef2, dg2, db2 = _bn_bwd_coef(L, st, sums2, coef2, g2p, b2p, P2, Cout, dev,
+                                                stripes=nb2.value, stride=sums2.shape[2])
             dp = torch.empty_like(g)
             check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), p.data_ptr(), None, bcoef2.data_ptr(),
                                       dp.data_ptr(), P2, Cout, st), "zk_bn_bwd_dx_bf16")
@@ -343,10 +374,15 @@ def fused_stem(x: torch.Tensor, conv, bn1, pool_k: int = 3, pool_s: int = 2, bn2
     image and STE mask (|y| <= sign_clip) of the output, attached as
     ``_zk_sign`` for the first binary block (see ``ops.binary_block``)."""
     holder = [] if (sign_clip is not None and bn2 is not None) else None
+    # consumer: a binary block; only when a backward will run (grad mode is
+    # off inside the autograd function's forward)
+    bnsum = [] if holder is not None and torch.is_grad_enabled() else None
     out = _StemFn.apply(x, conv.weight, bn1.weight, bn1.bias,
                         bn2.weight if bn2 is not None else None,
                         bn2.bias if bn2 is not None else None, bn1, bn2,
-                        (pool_k, pool_s, float(sign_clip or 0.0), holder))
+                        (pool_k, pool_s, float(sign_clip or 0.0), holder, bnsum))
     if holder:
         out._zk_sign = tuple(holder)
+    if bnsum:
+        out._zk_bnsum = bnsum[0]
     return out
