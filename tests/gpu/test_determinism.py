@@ -300,3 +300,22 @@ def test_default_mode_runs_stay_close_over_training_steps():
 # Stated run-to-run tolerance of the default mode (relative L2 difference of
 # all parameters after 5 Adam steps at lr 1e-3; README "Determinism").
 DEFAULT_MODE_BOUND = 1e-3
+
+
+def test_default_mode_e18_gradients_bit_identical():
+    """Default mode (runtime.deterministic=False) on E18: the split-K weight
+    gradients reduce through slabs by default and every BN-backward sum is
+    fixed-order in every mode, so repeated forward + backward passes give
+    bit-identical gradients and loss (the only remaining atomics on E18's path
+    are the exact int64 BN statistics and the fp64 statistics of the float
+    shortcut convs, whose order reaches the fp32 mean / variance only at a
+    rounding tie)."""
+    from zookeeper_amd.ops.options import OPTS
+
+    assert not OPTS.deterministic and OPTS.wgrad_reduce == "slab"
+    batch = _batch()
+    l0, g0, _ = _e18_grads(batch)
+    l1, g1, _ = _e18_grads(batch)
+    assert torch.equal(l0, l1)
+    diff = (g0 != g1).nonzero()
+    assert diff.numel() == 0, f"{diff.shape[0]} gradient elements differ, first at {diff[:5]}"
