@@ -302,20 +302,22 @@ def test_default_mode_runs_stay_close_over_training_steps():
 DEFAULT_MODE_BOUND = 1e-3
 
 
-def test_default_mode_e18_gradients_bit_identical():
-    """Default mode (runtime.deterministic=False) on E18: the split-K weight
-    gradients reduce through slabs by default and every BN-backward sum is
-    fixed-order in every mode, so repeated forward + backward passes give
-    bit-identical gradients and loss (the only remaining atomics on E18's path
-    are the exact int64 BN statistics and the fp64 statistics of the float
-    shortcut convs, whose order reaches the fp32 mean / variance only at a
-    rounding tie)."""
+@pytest.mark.parametrize("model", ["e18", "quicknet"])
+def test_default_mode_gradients_bit_identical(model):
+    """Default mode (runtime.deterministic=False): every split-K weight
+    gradient (igemm, small-K stem convs, depthwise, fused stem) reduces through
+    slabs by default and every BN-backward sum is fixed-order in every mode, so
+    repeated forward + backward passes give bit-identical gradients and loss
+    (the only remaining atomics on these paths are the exact int64 BN
+    statistics and the fp64 statistics of the float convs, whose order reaches
+    the fp32 mean / variance only at a rounding tie)."""
     from zookeeper_amd.ops.options import OPTS
 
     assert not OPTS.deterministic and OPTS.wgrad_reduce == "slab"
+    fn = _e18_grads if model == "e18" else _quicknet_grads
     batch = _batch()
-    l0, g0, _ = _e18_grads(batch)
-    l1, g1, _ = _e18_grads(batch)
+    l0, g0, _ = fn(batch)
+    l1, g1, _ = fn(batch)
     assert torch.equal(l0, l1)
     diff = (g0 != g1).nonzero()
     assert diff.numel() == 0, f"{diff.shape[0]} gradient elements differ, first at {diff[:5]}"

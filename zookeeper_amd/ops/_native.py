@@ -193,7 +193,7 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Te
     if mode == "auto":
         mode = "atomic" if L.zk_igemm_wgrad_prefers_atomic(B, Cin, H, W, Ho, Wo, Cout, kh, kw, s,
                                                             pt, pl, variant) else "slab"
-    if OPTS.deterministic or mode == "slab":
+    if slab_reduce() or mode == "slab":
         ws_bytes = max(int(L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Ho, Wo, Cout, kh, kw, s, pt,
                                                      pl, 0, variant)), 0)
         if ws_bytes > 0:
@@ -202,6 +202,28 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Te
                            Cin, Ho, Wo, Cout, kh, kw, s, pt, pl, int(pad_ones), float(clip), 0,
                            variant, ws.data_ptr() if ws is not None else None, ws_bytes, stream),
           what)
+
+
+def slab_reduce() -> bool:
+    """Split-K weight gradients through per-split slabs and the fixed-order
+    reduce (``runtime.deterministic``, or the default ``wgrad_reduce="slab"``)
+    rather than fp32 atomics: the policy of every weight-gradient op
+    (igemm, small-K convs, depthwise, stem)."""
+    from zookeeper_amd.ops.options import OPTS
+
+    return OPTS.deterministic or OPTS.wgrad_reduce == "slab"
+
+
+def zeroed(shape, device, dtype=torch.float32) -> torch.Tensor:
+    """A zero-filled scratch tensor cleared by a runtime memset (no framework
+    fill kernel in the training step)."""
+    t = torch.empty(shape, dtype=dtype, device=device)
+    if t.is_cuda and available():
+        check(lib().zk_zero(t.data_ptr(), t.numel() * t.element_size(), stream_ptr(t.device)),
+              "zk_zero")
+    else:
+        t.zero_()
+    return t
 
 
 def grad_ready(p) -> None:

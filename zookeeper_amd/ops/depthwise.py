@@ -11,8 +11,8 @@ from __future__ import annotations
 import torch
 
 from zookeeper_amd.nn.layers import same_padding
-from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
-from zookeeper_amd.ops.options import OPTS
+from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, slab_reduce,
+                                        stream_ptr, zeroed)
 
 
 def supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -64,9 +64,10 @@ class _DepthwiseFn(torch.autograd.Function):
             target = direct_grad(ctx.param, channels_last=False)
             buf = target if target is not None else torch.zeros(C, 9, device=dy.device)
             L = lib()
-            # deterministic mode: per-block partials + fixed-order reduce
-            slab = (torch.zeros((L.zk_dw_wgrad_blocks(B, Ho, Wo, C), C * 9), device=dy.device)
-                    if OPTS.deterministic else None)
+            # slab policy (default / deterministic): per-block partials +
+            # fixed-order reduce instead of fp32 atomics
+            slab = (zeroed((L.zk_dw_wgrad_blocks(B, Ho, Wo, C), C * 9), dy.device)
+                    if slab_reduce() else None)
             check(L.zk_dw_wgrad(g.data_ptr(), xn.data_ptr(), buf.data_ptr(),
                                 slab.data_ptr() if slab is not None else None, B, H, W, C, Ho,
                                 Wo, 3, s, pt, pl, st), "zk_dw_wgrad")

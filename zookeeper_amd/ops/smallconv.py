@@ -28,8 +28,8 @@ from typing import Optional
 
 import torch
 
-from zookeeper_amd.ops._native import check, direct_grad, grad_ready, lib, stream_ptr
-from zookeeper_amd.ops.options import OPTS
+from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, slab_reduce,
+                                        stream_ptr, zeroed)
 
 _INF = float("inf")
 
@@ -149,13 +149,12 @@ class _SmallConvFn(torch.autograd.Function):
                                            Cout, kh, kw, s, pt, pl, clip, 0, st),
                       "zk_band_conv_wgrad")
             else:
-                # deterministic mode: per-block partials + fixed-order reduce
-                # instead of fp32 atomics
+                # slab policy (default / deterministic): per-block partials +
+                # fixed-order reduce instead of fp32 atomics
                 slab = None
-                if OPTS.deterministic:
+                if slab_reduce():
                     nb = L.zk_smallk_conv_wgrad_blocks(B, Ho, Wo, 0)
-                    slab = torch.zeros((nb, Cout * kh * kw * Cin), dtype=torch.float32,
-                                       device=dev)
+                    slab = zeroed((nb, Cout * kh * kw * Cin), dev)
                 check(L.zk_smallk_conv_wgrad(g.data_ptr(), xn.data_ptr(), wf.data_ptr(),
                                              dw.data_ptr(),
                                              slab.data_ptr() if slab is not None else None,

@@ -28,8 +28,8 @@ import torch
 
 from zookeeper_amd.nn.layers import same_padding
 from zookeeper_amd.ops.options import OPTS
-from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, stream_ptr,
-                                        zeroed_scratch)
+from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, slab_reduce,
+                                        stream_ptr, zeroed, zeroed_scratch)
 
 # The recompute-fused kernels of stem_fused.hip are the default
 # (``runtime.stem_fused=False`` selects the materialising kernels of stem.hip): they never write the
@@ -348,10 +348,10 @@ class _StemFn(torch.autograd.Function):
                 check(L.zk_stem_dy1(dp.data_ptr(), arg.data_ptr(), y1.data_ptr(),
                                     coef1.data_ptr(), bcoef1.data_ptr(), dy1.data_ptr(), B, Ho,
                                     Wo, Cout, H2, W2, pk, ps, pt2, pl2, st), "zk_stem_dy1")
-                # deterministic mode: per-split partials + fixed-order reduce
-                slab = (torch.zeros((L.zk_stem_wgrad_splits(B, Ho, Wo, 0), Cout * KH * KW * Cin),
-                                    dtype=torch.float32, device=dev)
-                        if OPTS.deterministic else None)
+                # slab policy (default / deterministic): per-split partials +
+                # fixed-order reduce
+                slab = (zeroed((L.zk_stem_wgrad_splits(B, Ho, Wo, 0), Cout * KH * KW * Cin), dev)
+                        if slab_reduce() else None)
                 check(L.zk_stem_wgrad(dy1.data_ptr(), xp.data_ptr(), dw.data_ptr(),
                                       slab.data_ptr() if slab is not None else None, B, Cin,
                                       Cout, KH, KW, s, Ho, Wo, Hp, Wp, 0, st), "zk_stem_wgrad")
