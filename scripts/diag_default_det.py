@@ -14,12 +14,34 @@ import torch  # noqa: E402
 import test_determinism as td  # noqa: E402
 
 
+def _resnet_grads(steps_x, model_seed=1234):
+    from zookeeper_amd.models.resnet import ResNetModule
+    from zookeeper_amd.ops import streams
+    from zookeeper_amd.parallel.flat import FlatParams
+    from zookeeper_amd.train.losses import get_loss
+    from zookeeper_amd.train.trainer import prepare_model
+
+    torch.manual_seed(model_seed)
+    dev = torch.device("cuda", 0)
+    model = prepare_model(ResNetModule((64, 64, 3), 10, blocks=(1, 1, 1, 1)), dev).train()
+    flat = FlatParams(model, dev)
+    loss_fn = get_loss("sparse_categorical_crossentropy")
+    x, y = steps_x
+    flat.zero_grad()
+    loss, _ = loss_fn(model(x), y)
+    with streams.session(dev):
+        loss.backward()
+    torch.cuda.synchronize()
+    return loss.detach().clone(), flat.grad.clone(), [b.clone() for b in model.buffers()]
+
+
 def main():
     from zookeeper_amd.ops.options import set_options
 
     set_options(deterministic=False)
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    for name, fn in (("e18", td._e18_grads), ("quicknet", td._quicknet_grads)):
+    for name, fn in (("e18", td._e18_grads), ("quicknet", td._quicknet_grads),
+                     ("resnet", _resnet_grads)):
         batch = td._batch()
         l0, g0, _ = fn(batch)
         worst = 0
