@@ -45,9 +45,9 @@ def _gpu():
         pytest.skip("needs a GPU")
 
 
-# Default mode (fp32 split-K atomics in the conv weight gradients; every
-# BN-backward sum fixed-order): stated run-to-run tolerance of the parameters
-# after the worker's SGD steps, relative L2.
+# Stated run-to-run tolerance of the parameters after the worker's SGD steps
+# (relative L2) for a default mode with fp32 split-K atomics
+# (runtime.wgrad_reduce="atomic"); the default slab policy is exact.
 DEFAULT_MODE_REL = 1e-4
 
 
@@ -66,10 +66,11 @@ def _close(a, b, exact):
 def test_two_ranks_match_single_process_on_same_data(tmp_path, side, graph, mode):
     """Deterministic mode: two ranks on the same batches average identical
     gradients (g + g = 2g, times 1/2, is exact in fp32), so the result must
-    equal the single-process run bit for bit.  Default mode: equal up to the
-    weight gradients' atomic-ordering noise (DEFAULT_MODE_REL)."""
-    exact = mode == "deterministic"
-    rt = "deterministic=1" if exact else ""
+    equal the single-process run bit for bit.  The default mode is
+    gradient-reproducible too since round 4 (slab split-K, fixed-order BN and
+    loss sums), so it must match bit for bit as well."""
+    exact = True
+    rt = "deterministic=1" if mode == "deterministic" else ""
     assert _run("same", tmp_path, 1, side, graph, rt=rt) == 0
     assert _run("same", tmp_path, 2, side, graph, rt=rt) == 0
     ref = torch.load(tmp_path / "same_w1_r0.pt", weights_only=True)
@@ -106,12 +107,13 @@ def test_two_ranks_disjoint_data_stay_identical(tmp_path):
 def test_rccl_single_rank_forced_dp_matches_plain_run(tmp_path, side, graph, mode):
     """Deterministic mode (``runtime.deterministic``: no float atomics on the
     gradient path): the forced 1-rank RCCL run must equal the plain run BIT
-    FOR BIT.  Default mode: within DEFAULT_MODE_REL (round 3's default mode
-    used fp32 atomics in the BN-backward sums, whose noise the binary blocks
-    amplified into O(1) differences between any two runs after two steps:
-    profiles/r3/g_dp_forced_diag.md; those sums are fixed-order now)."""
-    exact = mode == "deterministic"
-    rt = "deterministic=1" if exact else ""
+    FOR BIT, and so must the default mode since round 4 (round 3's default
+    mode used fp32 atomics in the BN-backward sums, whose noise the binary
+    blocks amplified into O(1) differences between any two runs after two
+    steps: profiles/r3/g_dp_forced_diag.md; those sums, the split-K weight
+    gradients and the loss sum are fixed-order now)."""
+    exact = True
+    rt = "deterministic=1" if mode == "deterministic" else ""
     assert _run("same", tmp_path, 1, side, graph, rt=rt) == 0
     assert _run("same", tmp_path, 1, side, graph, force="1", backend="nccl", rt=rt) == 0
     ref = torch.load(tmp_path / "same_w1_r0.pt", weights_only=True)
