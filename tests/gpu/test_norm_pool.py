@@ -81,6 +81,27 @@ def test_maxpool(k, s, padding, hw):
     torch.testing.assert_close(xh.grad.float(), xr.grad, atol=2e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("k,s,padding", [(2, 1, "valid"), (3, 2, "same")])
+def test_maxpool_relu(k, s, padding):
+    """relu(max_pool(x)) in one pass (QuickNet transitions): exact forward,
+    and no gradient through outputs the ReLU clipped (window max <= 0)."""
+    from zookeeper_amd.ops.norm_pool import max_pool
+
+    torch.manual_seed(3)
+    x = _cl(torch.randn(2, 64, 9, 9, device="cuda") - 0.7).to(torch.bfloat16)
+    x[0, :, :4, :4] = 0  # windows whose max is exactly 0: clipped, no gradient
+    xh = x.clone().requires_grad_(True)
+    yh = max_pool(xh, k, s, padding, relu=True)
+    xr = x.float().clone().requires_grad_(True)
+    yr = F.relu(MaxPool2d(k, s, padding)(xr))
+    torch.testing.assert_close(yh.float(), yr, atol=0, rtol=0)
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    yh.backward(g)
+    yr.backward(g.float())
+    torch.testing.assert_close(xh.grad.float(), xr.grad, atol=2e-2, rtol=1e-2)
+    assert (xh.grad[0, :, :3, :3] == 0).all()
+
+
 def test_avgpool2():
     torch.manual_seed(2)
     x = _cl(torch.randn(2, 128, 14, 14, device="cuda")).to(torch.bfloat16)

@@ -323,12 +323,16 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_bf16_kernel(
 // ---------------------------------------------------------------------------
 // Max pooling (NHWC bf16), window k, stride s, TF padding (pt, pl) with -inf.
 // One thread = 8 channels of one output pixel; argmax tap (uint8) saved.
+// relu: relu(max(window)) == max(0, window) -- the running max starts at 0
+// with the tap sentinel 255 (k*k <= 255 taps never reach it), so an output
+// clipped to 0 passes no gradient, as ReLU's backward (x <= 0 -> 0) does.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x,
                                                           uint16_t* __restrict__ y,
                                                           uint8_t* __restrict__ arg, int B,
                                                           int H, int W, int C, int Ho, int Wo,
-                                                          int k, int s, int pt, int pl) {
+                                                          int k, int s, int pt, int pl,
+                                                          int relu) {
   const int CG = C / 8;
   const long long total = (long long)B * Ho * Wo * CG;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -342,8 +346,8 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
     uint8_t bi[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      best[q] = -INFINITY;
-      bi[q] = 0;
+      best[q] = relu ? 0.f : -INFINITY;
+      bi[q] = relu ? 255 : 0;
     }
     for (int dh = 0; dh < k; ++dh) {
       const int hi = ho * s - pt + dh;
@@ -748,13 +752,15 @@ ZK_EXPORT int zk_bn_bwd_dx_res_bf16(const void* g, const void* x, const void* y,
   return 0;
 }
 
+// relu != 0: y = relu(maxpool(x)) in the same pass (QuickNet transitions).
 ZK_EXPORT int zk_maxpool_fwd(const void* x, void* y, void* arg, int B, int H, int W, int C,
-                             int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st) {
+                             int Ho, int Wo, int k, int s, int pt, int pl, int relu,
+                             hipStream_t st) {
   if (C % 8 || k * k > 255) return (int)hipErrorInvalidValue;
   const long long work = (long long)B * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(flat_grid(work)), dim3(256), 0, st,
                      (const uint16_t*)x, (uint16_t*)y, (uint8_t*)arg, B, H, W, C, Ho, Wo, k, s,
-                     pt, pl);
+                     pt, pl, relu);
   ZK_CHECK_LAUNCH();
   return 0;
 }

@@ -94,7 +94,7 @@ class Transition(nn.Module):
         if _use_native(x) and x.shape[1] % 8 == 0:
             from zookeeper_amd.ops.norm_pool import max_pool
 
-            x = F.relu(max_pool(x, 2, 1, "valid"))  # relu∘max == max∘relu
+            x = max_pool(x, 2, 1, "valid", relu=True)  # relu∘max == max∘relu, one pass
         else:
             x = F.max_pool2d(F.relu(x), 2, 1)
         # (BN statistics from the 1x1 GEMM's epilogue where it runs one: stats_for)

@@ -128,7 +128,7 @@ SIGNATURES = {
     "zk_stem_fwd_pool": (I32, [P] * 7 + [I32] * 11 + [IP, P]),
     "zk_stem_pool_bwd_sums_ya": (I32, [P, P, P, P, I64, IP, P]),
     "zk_stem_bwd_fused": (I32, [P] * 8 + [I32] * 11 + [P]),
-    "zk_maxpool_fwd": (I32, [P, P, P] + [I32] * 10 + [P]),
+    "zk_maxpool_fwd": (I32, [P, P, P] + [I32] * 11 + [P]),
     "zk_maxpool_bwd": (I32, [P, P, P] + [I32] * 10 + [P]),
     "zk_avgpool2_fwd": (I32, [P, P] + [I32] * 6 + [P]),
     "zk_avgpool2_bwd": (I32, [P, P] + [I32] * 6 + [P]),

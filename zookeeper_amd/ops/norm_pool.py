@@ -227,7 +227,7 @@ def batch_norm(x: torch.Tensor, bn, relu: bool = False,
 
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s, padding):
+    def forward(ctx, x, k, s, padding, relu):
         B, C, H, W = x.shape
         if padding == "same":
             pt, pb = same_padding(H, k, s)
@@ -239,7 +239,8 @@ class _MaxPoolFn(torch.autograd.Function):
         y = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=x.device)
         arg = torch.empty((B, Ho, Wo, C), dtype=torch.uint8, device=x.device)
         check(lib().zk_maxpool_fwd(xn.data_ptr(), y.data_ptr(), arg.data_ptr(), B, H, W, C, Ho,
-                                   Wo, k, s, pt, pl, stream_ptr(x.device)), "zk_maxpool_fwd")
+                                   Wo, k, s, pt, pl, int(relu), stream_ptr(x.device)),
+              "zk_maxpool_fwd")
         ctx.save_for_backward(arg)
         ctx.geom = (B, H, W, C, Ho, Wo, k, s, pt, pl)
         return y.permute(0, 3, 1, 2)
@@ -252,11 +253,14 @@ class _MaxPoolFn(torch.autograd.Function):
         dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
         check(lib().zk_maxpool_bwd(g.data_ptr(), arg.data_ptr(), dx.data_ptr(), B, H, W, C, Ho,
                                    Wo, k, s, pt, pl, stream_ptr(dy.device)), "zk_maxpool_bwd")
-        return dx.permute(0, 3, 1, 2), None, None, None
+        return dx.permute(0, 3, 1, 2), None, None, None, None
 
 
-def max_pool(x: torch.Tensor, k: int, s: int, padding: str = "valid") -> torch.Tensor:
-    return _MaxPoolFn.apply(x, k, s, padding)
+def max_pool(x: torch.Tensor, k: int, s: int, padding: str = "valid",
+             relu: bool = False) -> torch.Tensor:
+    """Max pooling; ``relu=True`` returns ``relu(max_pool(x))`` from the same
+    pass (no separate ReLU forward / backward launch)."""
+    return _MaxPoolFn.apply(x, k, s, padding, relu)
 
 
 class _AvgPool2Fn(torch.autograd.Function):
