@@ -185,3 +185,27 @@ def test_binarynet_runs_native_and_matches_fp32_oracle():
     assert abs(loss.item() - loss_r.item()) < 0.1 * abs(loss_r.item()) + 0.05
     for p in m.parameters():
         assert torch.isfinite(p.grad).all() and p.grad.abs().sum() > 0
+
+
+@pytest.mark.parametrize("shape,sign,transposed,cl", [
+    ((64, 16, 1, 1), False, False, False), ((64, 16, 1, 1), True, True, True),
+    ((16, 3, 3, 3), False, False, True), ((32, 1, 3, 3), True, False, False),
+    ((48, 40, 1, 1), False, True, False)])
+def test_smallk_native_pack_matches_torch_pack(shape, sign, transposed, cl):
+    """zk_smallk_pack (one launch) == the torch fill + cast + copy pack."""
+    from zookeeper_amd.ops import smallconv
+
+    torch.manual_seed(5)
+    w = torch.randn(shape, device="cuda")
+    w[0, 0] = 0.0  # sign(0) = +1
+    if cl:
+        w = w.contiguous(memory_format=torch.channels_last)
+    Cout, Cin, kh, kw = shape
+    w2 = w.permute(0, 2, 3, 1).reshape(Cout, kh * kw * Cin)
+    if transposed:
+        w2 = w.reshape(Cout, Cin).t()
+    if sign:
+        w2 = torch.where(w2 >= 0, 1.0, -1.0)
+    KP = 32 if w2.shape[1] <= 32 else 64
+    got = smallconv._pack_native(w, KP, sign, transposed)
+    torch.testing.assert_close(got, smallconv._pack(w2, KP), atol=0, rtol=0)

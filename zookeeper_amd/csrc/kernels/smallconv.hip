@@ -714,3 +714,40 @@ ZK_EXPORT int zk_band_conv_wgrad(const void* dy, const void* x, const void* w, v
   ZK_CHECK_LAUNCH();
   return 0;
 }
+
+namespace {
+
+// Weight operand of the small-K / band convs: out[n][k] (bf16, row stride KP)
+// = w[n*sn + k1*t1 + k2*t2 + k3*t3] for k = (k1*d2 + k2)*d3 + k3 < d1*d2*d3,
+// zero up to KP; sign: the ste_sign kernel (w >= 0 -> +1, else -1).  One
+// launch instead of the framework's fill + cast + strided copy.
+__global__ __launch_bounds__(256) void sk_pack_kernel(const float* __restrict__ w,
+                                                      uint16_t* __restrict__ out, int N, int KP,
+                                                      int d2, int d3, int K, long long sn,
+                                                      long long t1, long long t2, long long t3,
+                                                      int sign) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)N * KP) return;
+  const int n = (int)(i / KP), k = (int)(i % KP);
+  float v = 0.f;
+  if (k < K) {
+    const int k3 = k % d3, k2 = (k / d3) % d2, k1 = k / (d3 * d2);
+    v = w[n * sn + k1 * t1 + k2 * t2 + k3 * t3];
+    if (sign) v = v >= 0.f ? 1.f : -1.f;
+  }
+  out[i] = zk::f32_to_bf16(v);
+}
+
+}  // namespace
+
+ZK_EXPORT int zk_smallk_pack(const void* w, void* out, int N, int KP, int d1, int d2, int d3,
+                             long long sn, long long t1, long long t2, long long t3, int sign,
+                             hipStream_t st) {
+  const int K = d1 * d2 * d3;
+  if (N < 1 || d1 < 1 || d2 < 1 || d3 < 1 || K > KP) return (int)hipErrorInvalidValue;
+  const long long n = (long long)N * KP;
+  hipLaunchKernelGGL(sk_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     (const float*)w, (uint16_t*)out, N, KP, d2, d3, K, sn, t1, t2, t3, sign);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}

@@ -66,6 +66,7 @@ SIGNATURES = {
     "zk_bn_bwd_dx_res_bf16": (I32, [P, P, P, P, P, P, I64, I32, P]),
     # small-K convolutions (smallconv.hip)
     "zk_smallk_conv_fwd": (I32, [P, P, P] + [I32] * 12 + [P]),
+    "zk_smallk_pack": (I32, [P, P] + [I32] * 5 + [I64] * 4 + [I32, P]),
     "zk_smallk_conv_wgrad": (I32, [P, P, P, P, P] + [I32] * 12 + [F32, I32, P]),
     "zk_smallk_conv_wgrad_blocks": (I32, [I32] * 4),
     "zk_band_conv_ok": (I32, [I32] * 10),

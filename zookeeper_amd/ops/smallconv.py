@@ -87,6 +87,26 @@ def _pack(w2: torch.Tensor, KP: int) -> torch.Tensor:
     return out
 
 
+def _pack_native(weight: torch.Tensor, KP: int, sign: bool, transposed: bool):
+    """The same operand from the [Cout][Cin][kh][kw] weight in one native
+    launch (``zk_smallk_pack``): rows Cout with K in (kh, kw, Cin) order, or
+    (``transposed``, 1x1 only) rows Cin with K = Cout; ``sign``: ±1.  None
+    when the weight is not an fp32 CUDA tensor (the caller packs in torch)."""
+    w = weight.detach()
+    if w.dtype != torch.float32 or not w.is_cuda:
+        return None
+    Cout, Cin, kh, kw = w.shape
+    s0, s1, s2, s3 = w.stride()
+    if transposed:
+        N, dims, strides, sn = Cin, (1, 1, Cout), (0, 0, s0), s1
+    else:
+        N, dims, strides, sn = Cout, (kh, kw, Cin), (s2, s3, s1), s0
+    out = torch.empty((N, KP), dtype=torch.bfloat16, device=w.device)
+    check(lib().zk_smallk_pack(w.data_ptr(), out.data_ptr(), N, KP, *dims, sn, *strides,
+                               int(sign), stream_ptr(w.device)), "zk_smallk_pack")
+    return out
+
+
 class _SmallConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride, padding, kclip):
@@ -95,10 +115,12 @@ class _SmallConvFn(torch.autograd.Function):
         pt, pl, Ho, Wo = _geometry(H, W, kh, kw, stride, padding)
         K = kh * kw * Cin
         KP = 32 if K <= 32 else 64
-        w2 = weight.detach().permute(0, 2, 3, 1).reshape(Cout, K).float()
-        if kclip is not None:  # ste_sign kernel: ±1 (sign(0) = +1)
-            w2 = torch.where(w2 >= 0, 1.0, -1.0)
-        wp = _pack(w2, KP)
+        wp = _pack_native(weight, KP, kclip is not None, False)
+        if wp is None:
+            w2 = weight.detach().permute(0, 2, 3, 1).reshape(Cout, K).float()
+            if kclip is not None:  # ste_sign kernel: ±1 (sign(0) = +1)
+                w2 = torch.where(w2 >= 0, 1.0, -1.0)
+            wp = _pack(w2, KP)
         xn = x.permute(0, 2, 3, 1).contiguous()
         y = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x.device)
         band = _band(B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride)
@@ -124,10 +146,13 @@ class _SmallConvFn(torch.autograd.Function):
         dx = dweight = None
         if ctx.needs_input_grad[0]:
             # 1x1 stride 1: dx = dY · W  (a K = Cout conv with Cin outputs)
-            w2 = weight.detach().reshape(Cout, Cin).float()
-            if kclip is not None:
-                w2 = torch.where(w2 >= 0, 1.0, -1.0)
-            wpT = _pack(w2.t(), 32 if Cout <= 32 else 64)
+            KPT = 32 if Cout <= 32 else 64
+            wpT = _pack_native(weight, KPT, kclip is not None, True)
+            if wpT is None:
+                w2 = weight.detach().reshape(Cout, Cin).float()
+                if kclip is not None:
+                    w2 = torch.where(w2 >= 0, 1.0, -1.0)
+                wpT = _pack(w2.t(), KPT)
             dxn = torch.empty((B, H, W, Cin), dtype=torch.bfloat16, device=dev)
             check(L.zk_smallk_conv_fwd(g.data_ptr(), wpT.data_ptr(), dxn.data_ptr(), B, H, W, Cout,
                                        H, W, Cin, 1, 1, 1, 0, 0, st), "zk_smallk_conv_fwd(dgrad)")
