@@ -1,17 +1,21 @@
 """Determinism of the reductions.
 
+Every mode is bit-reproducible run to run:
+
 * binary-conv forward: exact int16 outputs and exact int64 BN statistics
-  (striped integer atomics commute) -> bit-identical across runs;
-* data gradient: no atomics -> bit-identical;
-* weight gradient in slab mode: fixed-order split-K reduction ->
-  bit-identical; in atomic mode only last-bit differences;
-* whole model, default mode: the E18 forward (outputs, BN running
-  statistics) is bit-identical, and so are the data-gradient chain and the BN
-  gamma / beta gradients (every BN-backward sum is a per-block copy summed in
-  a fixed order); only the split-K weight gradients of the convolutions add
-  with fp32 atomics (ordering noise ~1e-7 relative, bounded here);
-* deterministic mode: everything bit-identical, E18 and QuickNet (small-K
-  stem convs, depthwise convs: per-block partials + fixed-order reduce).
+  (striped integer atomics commute);
+* data gradient: no atomics;
+* weight gradients: split-K partials summed in a fixed order -- per-split slabs
+  + the reduce kernel, or the in-launch fixed-order tree of the row-streaming
+  3x3 kernel (wgrad_rows.hip); small-K stem, depthwise and fused-stem weight
+  gradients through per-block partials;
+* BN-backward sums and the loss: per-block copies summed in a fixed order;
+* BN statistics of the float convs (fp64 atomics in the GEMM epilogue): every
+  block's partial is rounded to a fixed grid first, so the fp64 additions are
+  exact and their order cannot change the result;
+* E18, QuickNet and a ResNet (float convs, BN statistics in the epilogues)
+  repeat forward + backward bit for bit, and two 5-step default-mode training
+  runs end with identical parameters.
 """
 
 import pytest
@@ -96,7 +100,7 @@ def test_wgrad_reduction_order(slab):
             assert err < 1e-6, err  # fp32 atomics: ordering noise only
 
 
-def test_model_forward_bit_identical_and_gradient_noise_bounded():
+def test_model_forward_and_gradients_bit_identical():
     from zookeeper_amd.models.binary_resnet import BinaryResNetE
     from zookeeper_amd.parallel.flat import FlatParams
     from zookeeper_amd.train.losses import get_loss
@@ -133,9 +137,8 @@ def test_model_forward_bit_identical_and_gradient_noise_bounded():
             a = g0[s.offset:s.offset + s.numel]
             b = g1[s.offset:s.offset + s.numel]
             assert torch.equal(a, b), s.name
-    # conv weight gradients: fp32 split-K atomics, ordering noise only (no
-    # amplification: the data-gradient chain they are computed from is exact)
-    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5
+    # conv weight gradients: fixed-order split-K sums -> bit-identical too
+    assert torch.equal(g0, g1)
 
 
 @pytest.fixture
@@ -261,13 +264,11 @@ def test_deterministic_resume_matches_uninterrupted_run(tmp_path, deterministic)
 
 
 @pytest.mark.timeout(300)
-def test_default_mode_runs_stay_close_over_training_steps():
+def test_default_mode_training_runs_bit_identical():
     """Two default-mode E18 training runs (64x64, batch 8, Adam, 5 steps,
-    same init and batches).  Before round 4 the BN-backward sums used fp32
-    atomics and the two runs differed at O(1) after two steps
-    (profiles/r3/g_dp_forced_diag.md).  Now only the conv weight gradients
-    carry atomic-ordering noise (~1e-7 relative); the bound below is the
-    stated run-to-run tolerance of the default mode after 5 steps."""
+    same init and batches) end with bit-identical parameters and losses.
+    Before round 4 the BN-backward sums used fp32 atomics and the two runs
+    differed at O(1) after two steps (profiles/r3/g_dp_forced_diag.md)."""
     from zookeeper_amd.core import configure
     from zookeeper_amd.models.binary_resnet import BinaryResNetE
     from zookeeper_amd.train import Adam, Trainer
@@ -289,35 +290,48 @@ def test_default_mode_runs_stay_close_over_training_steps():
 
     p0, l0 = run()
     p1, l1 = run()
-    rel = ((p1 - p0).norm() / p0.norm()).item()
-    print(f"default-mode run-to-run after 5 steps: params rel diff {rel:.3e}, "
-          f"losses {l0} vs {l1}")
-    assert rel < DEFAULT_MODE_BOUND, rel
-    for a, b in zip(l0, l1):
-        assert abs(a - b) <= 1e-2 * abs(a) + 1e-3, (l0, l1)
+    assert l0 == l1, (l0, l1)
+    assert torch.equal(p0, p1), ((p1 - p0).norm() / p0.norm()).item()
 
 
-# Stated run-to-run tolerance of the default mode (relative L2 difference of
-# all parameters after 5 Adam steps at lr 1e-3; README "Determinism").
-DEFAULT_MODE_BOUND = 1e-3
+def _resnet_grads(steps_x, model_seed=1234):
+    from zookeeper_amd.models.resnet import ResNetModule
+    from zookeeper_amd.ops import streams
+    from zookeeper_amd.parallel.flat import FlatParams
+    from zookeeper_amd.train.losses import get_loss
+    from zookeeper_amd.train.trainer import prepare_model
+
+    torch.manual_seed(model_seed)
+    dev = torch.device("cuda", 0)
+    model = prepare_model(ResNetModule((64, 64, 3), 10, blocks=(1, 1)), dev).train()
+    flat = FlatParams(model, dev)
+    loss_fn = get_loss("sparse_categorical_crossentropy")
+    x, y = steps_x
+    flat.zero_grad()
+    loss, _ = loss_fn(model(x), y)
+    with streams.session(dev):
+        loss.backward()
+    torch.cuda.synchronize()
+    return loss.detach().clone(), flat.grad.clone(), [b.clone() for b in model.buffers()]
 
 
-@pytest.mark.parametrize("model", ["e18", "quicknet"])
+@pytest.mark.parametrize("model", ["e18", "quicknet", "resnet"])
 def test_default_mode_gradients_bit_identical(model):
     """Default mode (runtime.deterministic=False): every split-K weight
-    gradient (igemm, small-K stem convs, depthwise, fused stem) reduces through
-    slabs by default and every BN-backward sum is fixed-order in every mode, so
-    repeated forward + backward passes give bit-identical gradients and loss
-    (the only remaining atomics on these paths are the exact int64 BN
-    statistics and the fp64 statistics of the float convs, whose order reaches
-    the fp32 mean / variance only at a rounding tie)."""
+    gradient is summed in a fixed order, every BN-backward sum is fixed-order,
+    and the float convs' fp64 BN statistics are grid-rounded per block (exact
+    fp64 additions), so repeated forward + backward passes give bit-identical
+    gradients, loss and BN running statistics -- also for the float ResNet,
+    whose 1x1 / 3x3 GEMM epilogues carry those statistics."""
     from zookeeper_amd.ops.options import OPTS
 
-    assert not OPTS.deterministic and OPTS.wgrad_reduce == "slab"
-    fn = _e18_grads if model == "e18" else _quicknet_grads
+    assert not OPTS.deterministic
+    fn = {"e18": _e18_grads, "quicknet": _quicknet_grads, "resnet": _resnet_grads}[model]
     batch = _batch()
-    l0, g0, _ = fn(batch)
-    l1, g1, _ = fn(batch)
+    l0, g0, b0 = fn(batch)
+    l1, g1, b1 = fn(batch)
     assert torch.equal(l0, l1)
     diff = (g0 != g1).nonzero()
     assert diff.numel() == 0, f"{diff.shape[0]} gradient elements differ, first at {diff[:5]}"
+    for a, b in zip(b0, b1):
+        assert torch.equal(a, b)

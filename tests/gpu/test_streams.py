@@ -72,25 +72,3 @@ def test_side_stream_wgrad_bit_exact_in_deterministic_mode(monkeypatch):
     finally:
         options.set_options(deterministic=old)
     assert torch.equal(g_side, g_one), ((g_side - g_one).norm() / g_one.norm()).item()
-
-
-def test_cu_masked_side_stream_runs_work():
-    """runtime.wgrad_cu_share: the side stream is created with a CU mask
-    (runtime/cu_mask.cpp, hipExtStreamCreateWithCUMask) holding that share of
-    the CUs, and work queued on it completes with the right result."""
-    from zookeeper_amd.ops import options, streams
-
-    options.set_options(wgrad_cu_share=0.5)
-    try:
-        s = streams.side_stream(torch.device("cuda", 0))
-        ncu = torch.cuda.get_device_properties(0).multi_processor_count
-        assert abs(s.zk_cus - ncu // 2) <= 1
-        x = torch.randn(1 << 20, device="cuda")
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            y = x * 2 + 1
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        assert torch.equal(y, x * 2 + 1)
-    finally:
-        options.reset()

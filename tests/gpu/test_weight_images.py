@@ -22,7 +22,7 @@ def _gpu():
         pytest.skip("needs a GPU")
 
 
-def _run(images: bool, opt: str, steps: int = 3):
+def _run(images: bool, opt: str, steps: int = 3, graph=False, edit_at=None):
     from zookeeper_amd.core import configure
     from zookeeper_amd.models.resnet import ResNetModule
     from zookeeper_amd.ops.options import OPTS, set_options
@@ -35,9 +35,16 @@ def _run(images: bool, opt: str, steps: int = 3):
         model = ResNetModule((64, 64, 3), 10, blocks=(1, 1))
         spec = SGD() if opt == "sgd" else Adam()
         configure(spec, {"learning_rate": 1e-2})
-        tr = Trainer(model, "sparse_categorical_crossentropy", spec, None, graph=False)
+        tr = Trainer(model, "sparse_categorical_crossentropy", spec, None, graph=graph,
+                     graph_warmup=1)
         g = torch.Generator().manual_seed(3)
-        for _ in range(steps):
+        for step in range(steps):
+            if step == edit_at:
+                # a parameter change outside the fused optimizer (after the
+                # graph was captured): an in-place edit of one conv weight
+                p = next(p for p in tr.model.parameters() if p.dim() == 4 and p.shape[2] == 3)
+                with torch.no_grad():
+                    p.mul_(0.5)
             x = torch.randn(4, 3, 64, 64, generator=g).cuda().to(torch.bfloat16).contiguous(
                 memory_format=torch.channels_last)
             y = torch.randint(0, 10, (4,), generator=g).cuda()
@@ -94,3 +101,13 @@ def test_invalidate_rebuilds_images():
     fwd, bwd = _expected(e.param, e.flip)
     assert torch.equal(e.fwd, fwd) and torch.equal(e.bwd, bwd)
     assert reg.builds == 3
+
+
+def test_graph_replay_refreshes_stale_images():
+    """a replayed graph never calls images(); the trainer checks
+    the registry before each replay, so an in-place weight edit after capture
+    gives the same training as the eager run with the same edit."""
+    eager = _run(True, "sgd", steps=4, graph=False, edit_at=2)
+    graph = _run(True, "sgd", steps=4, graph=True, edit_at=2)
+    assert graph._graph is not None  # steps 1.. replayed
+    torch.testing.assert_close(graph.flat.data, eager.flat.data, atol=0, rtol=0)

@@ -15,28 +15,54 @@ import collections
 import csv
 
 
+# (substring, family), first match wins.  Kernel names are matched on the
+# demangled name; every kernel of csrc/kernels has a rule here
+# (tests/test_prof_summary.py checks a fixture of every name in a step).
+FAMILY_RULES = [
+    ("stem_", "stem (fused 7x7 conv / BN / pool)"),
+    ("wgrad_rows_kernel", "weight gradient (MFMA)"),
+    ("wgrad_deep_kernel", "weight gradient (MFMA)"),
+    ("igemm_wgrad", "weight gradient (MFMA)"),
+    ("wgrad_reduce", "weight gradient (MFMA)"),
+    ("smallk_wgrad", "weight gradient (MFMA)"),
+    ("band_wgrad", "weight gradient (MFMA)"),
+    ("bconv_wgrad", "weight gradient (MFMA)"),
+    ("dgrad_deep_kernel", "data gradient (MFMA)"),
+    ("conv3rw_dgrad", "data gradient (MFMA)"),
+    ("bconv_dgrad", "data gradient (MFMA)"),
+    ("igemm_conv3_kernel<true", "conv forward (MFMA; binary ±1 or float)"),
+    ("igemm_conv_kernel<true", "conv forward (MFMA; binary ±1 or float)"),
+    ("bconv_fwd", "conv forward (MFMA; binary ±1 or float)"),
+    # FWD=false: the data gradients and the float 1x1 forward GEMMs
+    ("igemm_conv", "data gradient / float 1x1 forward (MFMA)"),
+    ("smallk_fwd", "small-K / band conv forward (MFMA)"),
+    ("band_fwd", "small-K / band conv forward (MFMA)"),
+    ("sk_pack", "sign / weight packing"),
+    ("bn_", "batch norm (apply / stats / backward)"),
+    ("ste_combine", "batch norm (apply / stats / backward)"),
+    ("reduce_partials", "batch norm (apply / stats / backward)"),
+    ("partials_colsum", "batch norm (apply / stats / backward)"),
+    ("dw_", "depthwise conv"),
+    ("pool", "pooling"),
+    ("gap_", "classifier head (GAP + dense)"),
+    ("head_", "classifier head (GAP + dense)"),
+    ("sgemm", "classifier head (GAP + dense)"),
+    ("weight_pack", "sign / weight packing"),
+    ("sign_pack", "sign / weight packing"),
+    ("unpack_sign", "sign / weight packing"),
+    ("weight_images", "optimizer"),
+    ("adam", "optimizer"),
+    ("sgd", "optimizer"),
+    ("xent", "softmax cross-entropy"),
+    ("normalize_flip", "input preprocessing"),
+]
+
+
 def family(name: str) -> str:
     n = name
-    if "stem_" in n:
-        return "stem (fused 7x7 conv / BN / pool)"
-    if "igemm_wgrad" in n or "wgrad_reduce" in n:
-        return "binary/1x1 conv weight gradient (MFMA)"
-    if "igemm_conv3_kernel<true" in n or "igemm_conv_kernel<true" in n:
-        return "binary conv forward (MFMA)"
-    if "igemm_conv" in n:
-        return "conv data gradient / 1x1 forward (MFMA)"
-    if "bn_" in n[:80]:
-        return "batch norm (apply / stats / backward)"
-    if "dw_" in n[:60]:
-        return "depthwise conv"
-    if "pool" in n[:60]:
-        return "pooling"
-    if "weight_pack" in n or "sign_pack" in n:
-        return "sign / weight packing"
-    if "adam" in n or "sgd" in n:
-        return "optimizer"
-    if "xent" in n:
-        return "softmax cross-entropy"
+    for key, fam in FAMILY_RULES:
+        if key in n[:120]:
+            return fam
     if n.startswith("Cijk") or "gtc" in n or "MIOpen" in n or "ck::" in n or "SubTensor" in n:
         return "library (hipBLASLt / MIOpen)"
     if "at::native" in n:
@@ -44,11 +70,43 @@ def family(name: str) -> str:
     return "other"
 
 
+def is_step_end(name: str) -> bool:
+    """The fused optimizer launch that ends every training step."""
+    return "adam_chunks" in name or "sgd_chunks" in name
+
+
+def refamily_md(path: str) -> str:
+    """A family table recomputed with :data:`FAMILY_RULES` from the per-kernel
+    rows (``| ms/step | calls/step | avg us | `name` |``) of a kept profile
+    summary: for summaries written before the rules covered every kernel."""
+    fam = collections.Counter()
+    listed = 0.0
+    total = None
+    for line in open(path):
+        if line.startswith("Total kernel time per step:"):
+            total = float(line.split(":")[1].split()[0])
+        cells = [c.strip() for c in line.strip().strip("|").split("|")]
+        if len(cells) == 4 and cells[3].startswith("`"):
+            try:
+                ms = float(cells[0])
+            except ValueError:
+                continue
+            fam[family(cells[3].strip("`"))] += ms
+            listed += ms
+    out = ["| ms/step | share | family |", "|---:|---:|---|"]
+    total = total or listed
+    for k, v in fam.most_common():
+        out.append(f"| {v:.3f} | {100 * v / total:.1f}% | {k} |")
+    if total > listed + 1e-9:
+        out.append(f"| {total - listed:.3f} | {100 * (total - listed) / total:.1f}% | "
+                   "kernels below the listed rows |")
+    return "\n".join(out)
+
+
 def _trace_window(trace, k: int):
     """Aggregate a kernel trace over the last ``k`` optimizer-delimited steps
     into rows shaped like ``run_kernel_stats.csv``."""
-    opt = sorted(int(r["End_Timestamp"]) for r in trace
-                 if family(r["Kernel_Name"]) == "optimizer")
+    opt = sorted(int(r["End_Timestamp"]) for r in trace if is_step_end(r["Kernel_Name"]))
     if len(opt) < k + 1:
         raise SystemExit(f"trace has {len(opt)} optimizer launches, need {k + 1}")
     lo, hi = opt[-k - 1], opt[-1]

@@ -96,6 +96,14 @@ def _write_key(path: str, key: str) -> None:
         f.write(key)
 
 
+# Per-file code-generation flags.  wgrad_rows.hip: keep the MFMA accumulators
+# in VGPRs (the default AGPR form made the compiler copy all 144 loop-carried
+# accumulator registers AGPR <-> VGPR on every step of the main loop).
+FILE_FLAGS = {
+    "wgrad_rows.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+}
+
+
 def _compile_cmd(src: str, obj: str, extra: List[str]) -> List[str]:
     cmd = [hipcc(), "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
            "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
@@ -105,7 +113,7 @@ def _compile_cmd(src: str, obj: str, extra: List[str]) -> List[str]:
         # host C++: the HIP runtime API headers (no device code, no offload)
         rocm = os.path.dirname(os.path.dirname(os.path.realpath(hipcc())))
         cmd += ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(rocm, "include")]
-    return cmd + extra + ["-c", src, "-o", obj]
+    return cmd + FILE_FLAGS.get(os.path.basename(src), []) + extra + ["-c", src, "-o", obj]
 
 
 def compile_one(src: str, extra: List[str], hdr_digest: str = "") -> str:

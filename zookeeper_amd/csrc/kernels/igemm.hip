@@ -104,7 +104,7 @@ int g_opt_dgrad_rw = 1;
 // Default 32 MB (ops/options.py has the measurements).
 int g_opt_wgrad_slab_mb = 32;
 // dgrad_deep (key 6): the phased kernel (deep_gemm.hip, variant 60) for
-// stride-1 3x3 data gradients with Cin % 128 == 0.
+// stride-1 3x3 data gradients with Cin % 256 == 0 (igemm_dgrad_impl).
 int g_opt_dgrad_deep = 1;
 // wgrad_deep (key 7): the same for stride-1 3x3 weight gradients with
 // Cin % 256 == 0 and Cout % 256 == 0 (variant 60 of the wgrad dispatch).
@@ -326,7 +326,12 @@ __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeo
       float t = 0.f;
 #pragma unroll 4
       for (int r = 0; r < RPT; ++r) t += red[(r * JC + j) * 16 + which * 8 + k];
-      atomicAdd(so + which * g.Cin + n0 + nl, (double)t);
+      // the block's partial rounded to a fixed grid (2^-20 for sums, 2^-8 for
+      // sums of squares): every addend is an integer number of grid units and
+      // the totals stay far below 2^53 units, so the fp64 atomics are exact
+      // and their order cannot change the statistics (bit-reproducible)
+      const double q = which ? 256.0 : 1048576.0;
+      atomicAdd(so + which * g.Cin + n0 + nl, rint((double)t * q) / q);
     }
   }
 }
@@ -2087,22 +2092,6 @@ ZK_EXPORT int zk_wgrad_slab_reduce(const void* slab, int splits, long long n, co
                      (const float4*)slab, splits, n4, (const float4*)w, clip, (float4*)dw);
   ZK_CHECK_LAUNCH();
   return 0;
-}
-
-// 1 if the split-K reduction of this weight gradient is faster with fp32
-// atomics than with slabs + the reduce kernel (runtime.wgrad_reduce="auto").
-// Measured standalone at batch 1536 (profiles/r4/a_wgrad_atomic_vs_slab.md):
-// only the conv3 kernels with 64 input channels win with atomics (56x56x64:
-// 630 vs 909 us: their slabs hit the slab cap, which cuts the grid below the
-// CU count); every other E18 shape is faster with slabs (the deep kernel's
-// 256 / 512-channel layers 545 / 540 vs 648 / 695 us).
-ZK_EXPORT int zk_igemm_wgrad_prefers_atomic(int B, int Cin, int H, int W, int Ho, int Wo,
-                                            int Cout, int kh, int kw, int stride, int pt, int pl,
-                                            int variant) {
-  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
-  int tb = 0;
-  wgrad_defaults(g, variant, tb);
-  return (variant >= 20 && variant < 40 && g.Cin == 64) ? 1 : 0;
 }
 
 // Workspace bytes zk_igemm_wgrad needs for slab mode (-1: shape unsupported).

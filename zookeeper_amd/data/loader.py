@@ -12,9 +12,10 @@ Design (MI355X-first):
   multi-threaded row gather straight into pinned memory) or by a Python
   thread otherwise;
 * each filled slot is copied with ``non_blocking`` H2D on a **side HIP
-  stream** and published with an event; the compute stream waits on the
-  event only when it consumes the batch, so the copy of batch *i+1* overlaps
-  compute on batch *i* (double/triple buffering);
+  stream** into one of a ring of preallocated device batches and published
+  with an event; the compute stream waits on the event only when it consumes
+  the batch, so the copy of batch *i+1* overlaps compute on batch *i*
+  (double/triple buffering), and the steady state allocates no device memory;
 * slots are recycled through an event-carrying free list: the consumer never
   blocks on a copy — the producer thread waits for a slot's last copy event
   before it refills that slot;
@@ -180,7 +181,23 @@ class DeviceLoader:
 
         copy_stream = torch.cuda.Stream(self.device) if use_pin else None
         ahead = max(1, self.slots - 2)  # H2D copies kept in flight ahead of the consumer
-        in_flight: list = []  # (slot, device batch, event)
+        # A ring of preallocated device batches, reused round-robin: no device
+        # allocation (and no record_stream, which made the caching allocator
+        # hold blocks a step longer) per batch.  Each device slot carries two
+        # reusable events: `copied` (its H2D landed, recorded on the copy
+        # stream; the compute stream waits for it) and `consumed` (recorded on
+        # the compute stream when the consumer asks for the following batch,
+        # i.e. after it enqueued every use of this one; the copy stream waits
+        # for it before overwriting the slot).  A yielded batch therefore stays
+        # valid until the consumer has requested two more.
+        ndev = ahead + 2 if copy_stream is not None else 0
+        dev_slots = [{k: torch.empty(v.shape, dtype=v.dtype, device=self.device)
+                      for k, v in pinned[0].items()} for _ in range(ndev)]
+        copied = [torch.cuda.Event() for _ in range(ndev)]
+        consumed = [torch.cuda.Event() for _ in range(ndev)]
+        used = [False] * ndev
+        free_dev = list(range(ndev))
+        in_flight: list = []  # (pinned slot, device slot or batch, event)
         try:
             while True:
                 while len(in_flight) < ahead:
@@ -189,26 +206,34 @@ class DeviceLoader:
                         raise item
                     slot = item
                     if copy_stream is not None:
+                        d = free_dev.pop(0)
                         with torch.cuda.stream(copy_stream):
-                            dev = {k: v.to(self.device, non_blocking=True)
-                                   for k, v in pinned[slot].items()}
-                            ev = torch.cuda.Event()
-                            ev.record(copy_stream)
+                            if used[d]:
+                                copy_stream.wait_event(consumed[d])
+                            for k, v in pinned[slot].items():
+                                dev_slots[d][k].copy_(v, non_blocking=True)
+                            copied[d].record(copy_stream)
+                        used[d] = True
+                        in_flight.append((slot, d, copied[d]))
                     else:
-                        dev = {k: v.clone() for k, v in pinned[slot].items()}
-                        ev = None
-                    in_flight.append((slot, dev, ev))
-                slot, dev, ev = in_flight.pop(0)
+                        in_flight.append((slot, {k: v.clone() for k, v in pinned[slot].items()},
+                                          None))
+                slot, d, ev = in_flight.pop(0)
                 if ev is not None:
                     # the compute stream (not the host) waits for the copy
                     cur = torch.cuda.current_stream(self.device)
                     cur.wait_event(ev)
-                    for v in dev.values():
-                        v.record_stream(cur)
-                # recycled through the free list with its copy event: the
-                # producer thread waits on it before refilling the slot
-                free_q.put((slot, ev))
-                yield dev
+                    # recycled through the free list with its copy event: the
+                    # producer thread waits on it before refilling the slot
+                    free_q.put((slot, ev))
+                    yield dev_slots[d]
+                    # the consumer is back for the next batch: every use of
+                    # this one is enqueued on its stream
+                    consumed[d].record(torch.cuda.current_stream(self.device))
+                    free_dev.append(d)
+                else:
+                    free_q.put((slot, None))
+                    yield d
         finally:
             self.close()
 

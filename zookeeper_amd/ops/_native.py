@@ -23,7 +23,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Optional
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -167,37 +167,74 @@ def zeroed_scratch(owner, name: str, shape, dtype: torch.dtype,
     return buf
 
 
-def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Tensor,
-                geom, pad_ones: int, clip: float, stream: int, what: str = "zk_igemm_wgrad",
-                variant: int = -1) -> None:
-    """Split-K implicit-GEMM weight gradient ``dw += mask(|w| <= clip) *
-    dyᵀ ⊛ x`` (``zk_igemm_wgrad``), with the split-K reduction chosen by the
-    run's options:
+# Arrival counters of the in-launch split-K trees (zk_wgrad_rows), one buffer
+# per (device, stream): launches on one stream never overlap and every launch
+# leaves its counters zero, so a stream's launches can share one buffer.
+_COUNTERS: Dict[Tuple[int, int], torch.Tensor] = {}
+_OLD_COUNTERS: List[torch.Tensor] = []  # outgrown buffers (queued kernels may still use them)
 
-    * ``runtime.deterministic`` or ``runtime.wgrad_reduce="slab"``: per-split
-      slabs (plain stores) reduced in a fixed order by ``wgrad_reduce_kernel``
-      -- bit-reproducible;
-    * ``"atomic"``: every split adds its tile straight into ``dw`` -- the
-      zeroed flat fp32 gradient buffer -- with fp32 atomics: no slab write +
-      re-read, no reduce launch, and no slab cap limiting the split count;
-    * ``"auto"`` (default): the measured winner for the shape
-      (``zk_igemm_wgrad_prefers_atomic``).
 
-    ``geom`` = (B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl)."""
+def tree_counters(nbytes: int, device: torch.device, stream: int) -> torch.Tensor:
+    key = (device.index if device.index is not None else torch.cuda.current_device(), stream)
+    buf = _COUNTERS.get(key)
+    if buf is None or buf.numel() * 4 < nbytes:
+        if buf is not None:
+            _OLD_COUNTERS.append(buf)
+        n = max(1024, (nbytes + 3) // 4)
+        buf = torch.empty(n, dtype=torch.int32, device=device)
+        check(lib().zk_zero(buf.data_ptr(), n * 4, stream), "zk_zero")
+        _COUNTERS[key] = buf
+    return buf
+
+
+def wgrad_rows_ok(geom) -> bool:
+    """Whether ``zk_wgrad_rows`` (row-streaming 3x3 weight gradient with the
+    in-launch fixed-order split-K tree) takes this layer."""
     from zookeeper_amd.ops.options import OPTS
 
+    B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl = geom
+    if not (OPTS.wgrad_rows and kh == 3 and kw == 3 and s == 1 and pt == 1 and pl == 1
+            and Ho == H and Wo == W):
+        return False
+    return lib().zk_wgrad_rows_plan(B, H, W, Cin, Cout, 0, None, None) == 0
+
+
+def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Tensor,
+                geom, pad_ones: int, clip: float, stream: int, what: str = "zk_igemm_wgrad",
+                variant: int = -1, sign_act: bool = False) -> None:
+    """Implicit-GEMM weight gradient ``dw += mask(|w| <= clip) * dyᵀ ⊛ x``.
+
+    * 3x3 stride-1 layers the row-streaming kernel takes (``wgrad_rows_ok``):
+      ``zk_wgrad_rows``, split-K combined inside the launch by a fixed-order
+      tree (no reduce launch);
+    * otherwise ``zk_igemm_wgrad``: per-split slabs (plain stores) summed in a
+      fixed order by ``wgrad_reduce_kernel``.
+
+    Both are bit-reproducible.  ``sign_act``: ``x`` is the bf16 activation
+    and the kernel takes its sign (``zk_wgrad_rows`` only; needs pad_ones).
+    ``geom`` = (B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl)."""
     L = lib()
     B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl = geom
+    if variant < 0 and wgrad_rows_ok(geom) and (pad_ones or not sign_act):
+        sb, cb = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(L.zk_wgrad_rows_plan(B, H, W, Cin, Cout, 0, ctypes.byref(sb), ctypes.byref(cb)),
+              what + " (plan)")
+        slab = (torch.empty(sb.value // 4, dtype=torch.float32, device=dy.device)
+                if sb.value > 0 else None)
+        cnt = tree_counters(cb.value, dy.device, stream) if cb.value > 0 else None
+        check(L.zk_wgrad_rows(dy.data_ptr(), x.data_ptr(), w.data_ptr() if w is not None else None,
+                              dw.data_ptr(), slab.data_ptr() if slab is not None else None,
+                              sb.value, cnt.data_ptr() if cnt is not None else None, cb.value,
+                              B, H, W, Cin, Cout, int(pad_ones), int(sign_act), float(clip), 0,
+                              stream), what)
+        return
+    if sign_act:
+        raise ValueError(f"{what}: the sign-of-activation operand needs zk_wgrad_rows")
     ws, ws_bytes = None, 0
-    mode = OPTS.wgrad_reduce
-    if mode == "auto":
-        mode = "atomic" if L.zk_igemm_wgrad_prefers_atomic(B, Cin, H, W, Ho, Wo, Cout, kh, kw, s,
-                                                            pt, pl, variant) else "slab"
-    if slab_reduce() or mode == "slab":
-        ws_bytes = max(int(L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Ho, Wo, Cout, kh, kw, s, pt,
-                                                     pl, 0, variant)), 0)
-        if ws_bytes > 0:
-            ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=dy.device)
+    ws_bytes = max(int(L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Ho, Wo, Cout, kh, kw, s, pt,
+                                                 pl, 0, variant)), 0)
+    if ws_bytes > 0:
+        ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=dy.device)
     check(L.zk_igemm_wgrad(dy.data_ptr(), x.data_ptr(), w.data_ptr(), dw.data_ptr(), B, H, W,
                            Cin, Ho, Wo, Cout, kh, kw, s, pt, pl, int(pad_ones), float(clip), 0,
                            variant, ws.data_ptr() if ws is not None else None, ws_bytes, stream),
@@ -205,13 +242,12 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Te
 
 
 def slab_reduce() -> bool:
-    """Split-K weight gradients through per-split slabs and the fixed-order
-    reduce (``runtime.deterministic``, or the default ``wgrad_reduce="slab"``)
-    rather than fp32 atomics: the policy of every weight-gradient op
-    (igemm, small-K convs, depthwise, stem)."""
-    from zookeeper_amd.ops.options import OPTS
-
-    return OPTS.deterministic or OPTS.wgrad_reduce == "slab"
+    """Split-K weight gradients through per-split slabs and a fixed-order
+    reduce rather than fp32 atomics: the policy of every weight-gradient op
+    (igemm, small-K convs, depthwise, stem), in every mode (fp32-atomic
+    reductions measured slower in the E18 step and were removed,
+    profiles/r4/removed_variants.md)."""
+    return True
 
 
 def zeroed(shape, device, dtype=torch.float32) -> torch.Tensor:

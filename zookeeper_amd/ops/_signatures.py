@@ -20,8 +20,6 @@ SIGNATURES = {
     "zk_build_digest": (C.c_char_p, []),
     # host runtime
     "zk_gather_rows": (I32, [P, I64, P, I64, P, I32]),
-    # CU-masked streams (runtime/cu_mask.cpp; ops/streams.py)
-    "zk_cu_masked_stream": (I32, [I32, I32, I32, P, P]),
     # native RCCL communicator (runtime/comm.cpp; parallel/rccl.py)
     "zk_comm_load": (I32, [C.c_char_p]),
     "zk_comm_loaded": (I32, []),
@@ -49,7 +47,10 @@ SIGNATURES = {
     "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),
     "zk_igemm_wgrad_ws_bytes": (I64, [I32] * 14),
     "zk_wgrad_slab_reduce": (I32, [P, I32, I64, P, F32, P, P]),
-    "zk_igemm_wgrad_prefers_atomic": (I32, [I32] * 13),
+    # row-streaming 3x3 weight gradient (wgrad_rows.hip)
+    "zk_wgrad_rows_plan": (I32, [I32] * 6 + [P, P]),
+    "zk_wgrad_rows_lab": (I32, [I32, P]),
+    "zk_wgrad_rows": (I32, [P] * 5 + [I64, P, I64] + [I32] * 7 + [F32, I32, P]),
     "zk_igemm_dgrad_supported": (I32, [I32] * 13),
     "zk_set_option": (I32, [I32, I32]),
     "zk_bn_bwd_reduce_blocks": (I32, []),

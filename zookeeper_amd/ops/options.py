@@ -29,11 +29,6 @@ class KernelOptions:
     bconv_fp4: bool = True
     # Binary-conv weight gradients on a side HIP stream (44.9k vs 41.7k off).
     wgrad_side_stream: bool = True
-    # HIP priority of that side stream (0 = default, negative = higher).
-    wgrad_priority: int = 0
-    # Share of the CUs the side stream may use (hipExtStreamCreateWithCUMask;
-    # 0 = all of them): the rest stay free for the data-gradient chain.
-    wgrad_cu_share: float = 0.0
     # Recompute-fused ImageNet stem (False: the materialising kernels).
     stem_fused: bool = True
     # Float convolutions on the MFMA implicit-GEMM kernels (False: library).
@@ -60,19 +55,10 @@ class KernelOptions:
     # Same-box sweep at batch 1536: 28 MB 47.52k, 32 MB 47.79k / 47.71k,
     # 36 MB 47.17k, 40 MB 47.46k img/s.
     wgrad_slab_mb: int = 32
-    # Split-K reduction of the weight gradients: "atomic" (fp32 atomics into
-    # the flat gradient buffer: no slabs, no reduce launch, no slab cap),
-    # "slab" (per-split slabs + the fixed-order reduce kernel; what
-    # runtime.deterministic always uses), or "auto": per layer shape, the
-    # measured winner (zk_igemm_wgrad_prefers_atomic).  Standalone at batch
-    # 1536 (profiles/r4/a_wgrad_atomic_vs_slab.md): 56x56x64 atomic 630 vs
-    # slab 909 us (the slab cap starves its grid); the deep 256 / 512-channel
-    # layers slab 545 / 540 vs atomic 648 / 695 us (fp32 atomics run at
-    # ~1.3 TB/s of added bytes, slab stores at ~6 TB/s).  In the E18 step
-    # all-slab beat "auto" on every box measured (interleaved 80-100-step
-    # windows at batch 1536: 46.9-47.0k vs 46.85k; 47.13k / 47.02k vs
-    # 46.91k / 46.68k), so slabs are the default.
-    wgrad_reduce: str = "slab"
+    # Row-streaming weight gradient for the 3x3 stride-1 layers it takes
+    # (wgrad_rows.hip: every dY / S row loaded once per block, split-K summed
+    # inside the launch by a fixed-order tree; 64 / 128-channel stages).
+    wgrad_rows: bool = True
     # Phased data-gradient kernel (deep_gemm.hip) for the stride-1 3x3
     # binary convs with >= 128 input channels.
     dgrad_deep: bool = True

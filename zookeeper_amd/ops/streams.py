@@ -39,7 +39,7 @@ from zookeeper_amd.ops._native import grad_ready
 from zookeeper_amd.ops.options import OPTS
 
 _active = False
-_streams: Dict[Tuple[int, int], torch.cuda.Stream] = {}
+_streams: Dict[int, torch.cuda.Stream] = {}
 _pending: List[Tuple[torch.cuda.Event, object]] = []
 # side-stream events whose gradients were signalled ready without the
 # compute stream waiting for them (flush(wait=False)); joined at session exit
@@ -58,36 +58,14 @@ def active() -> bool:
 
 
 def side_stream(device: torch.device) -> torch.cuda.Stream:
+    """The weight-gradient side stream of ``device`` (default priority: a
+    higher-priority side stream and a CU-masked one both measured slower,
+    profiles/r4/removed_variants.md)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    prio = OPTS.wgrad_priority
-    share = float(OPTS.wgrad_cu_share)
-    key = (idx, prio, share)
-    s = _streams.get(key)
+    s = _streams.get(idx)
     if s is None:
-        if 0.0 < share < 1.0:
-            # runtime.wgrad_cu_share: a stream restricted to that share of the
-            # CUs (runtime/cu_mask.cpp); the compute stream keeps the rest
-            s = _cu_masked_stream(idx, share)
-        else:
-            # runtime.wgrad_priority: HIP stream priority of the side stream (0
-            # = the default / lowest, negative = higher than the compute stream)
-            s = torch.cuda.Stream(device=idx, priority=prio)
-        _streams[key] = s
-    return s
-
-
-def _cu_masked_stream(idx: int, share: float) -> torch.cuda.Stream:
-    import ctypes
-
-    from zookeeper_amd.ops._native import check, lib
-
-    den = 1024
-    num = max(1, min(den, int(round(share * den))))
-    ptr, n = ctypes.c_void_p(), ctypes.c_int(0)
-    check(lib().zk_cu_masked_stream(idx, num, den, ctypes.byref(ptr), ctypes.byref(n)),
-          "zk_cu_masked_stream")
-    s = torch.cuda.ExternalStream(ptr.value, device=torch.device("cuda", idx))
-    s.zk_cus = n.value  # CUs in the mask (reported by bench / tests)
+        s = torch.cuda.Stream(device=idx)
+        _streams[idx] = s
     return s
 
 

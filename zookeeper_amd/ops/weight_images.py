@@ -136,6 +136,16 @@ class WeightImages:
         return (not self.valid or e.version != e.param._version
                 or self._flat_version != self.flat.data._version)
 
+    def ensure_current(self, stream: int) -> bool:
+        """Rebuild the images if any parameter changed outside the fused
+        optimizer (invalidate(), or an in-place edit that bumped a version
+        counter).  A replayed HIP graph never calls :meth:`get`, so the
+        trainer calls this before every replay; returns True if it rebuilt."""
+        if self.entries and any(self._stale(e) for e in self.entries.values()):
+            self.refresh(stream)
+            return True
+        return False
+
     def get(self, param, flip: bool, stream: int) -> Tuple[torch.Tensor, torch.Tensor]:
         e = self.entries.get(id(param))
         if e is None:

@@ -7,13 +7,16 @@ import torch
 from zookeeper_amd.ops._native import check, lib, stream_ptr
 
 
-# Per-device accumulator [loss_sum, correct (int32 bits)], zero between calls
-# (zk_xent_finalize reads and re-zeroes it).
+# Accumulator [loss_sum, correct (int32 bits)] per (device, stream), zero
+# between calls: zk_xent_finalize reads and re-zeroes it right after the
+# zk_xent_fwd that fills it, on the same stream, so work on two streams (a
+# training step and an eval pass) never shares one.  If the launch pair fails
+# half-way the accumulator is re-zeroed (zk_zero) before the error propagates.
 _ACC = {}
 
 
-def _acc(dev: torch.device) -> torch.Tensor:
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
+def _acc(dev: torch.device, stream: int) -> torch.Tensor:
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), stream)
     a = _ACC.get(key)
     if a is None:
         a = _ACC[key] = torch.zeros(2, dtype=torch.float32, device=dev)
@@ -28,21 +31,25 @@ class _SoftmaxXentFn(torch.autograd.Function):
         y = labels.to(torch.int64).contiguous()
         dev = x.device
         lse = torch.empty(B, dtype=torch.float32, device=dev)
-        acc = _acc(dev)
+        st = stream_ptr(dev)
+        acc = _acc(dev, st)
         correct = acc[1:].view(torch.int32)
         # per-row losses summed in a fixed order (every mode: a reproducible
         # loss value for one extra single-block launch; the hit count stays an
         # exact integer atomic)
         row_loss = torch.empty(B, dtype=torch.float32, device=dev)
-        check(lib().zk_xent_fwd(x.data_ptr(), y.data_ptr(), lse.data_ptr(), acc.data_ptr(),
-                                correct.data_ptr(), B, C, float(eps),
-                                row_loss.data_ptr() if row_loss is not None else None,
-                                stream_ptr(dev)),
-              "zk_xent_fwd")
         loss = torch.empty((), dtype=torch.float32, device=dev)
         hits = torch.empty((), dtype=torch.int64, device=dev)
-        check(lib().zk_xent_finalize(acc.data_ptr(), loss.data_ptr(), hits.data_ptr(), B,
-                                     stream_ptr(dev)), "zk_xent_finalize")
+        try:
+            check(lib().zk_xent_fwd(x.data_ptr(), y.data_ptr(), lse.data_ptr(), acc.data_ptr(),
+                                    correct.data_ptr(), B, C, float(eps),
+                                    row_loss.data_ptr() if row_loss is not None else None, st),
+                  "zk_xent_fwd")
+            check(lib().zk_xent_finalize(acc.data_ptr(), loss.data_ptr(), hits.data_ptr(), B, st),
+                  "zk_xent_finalize")
+        except RuntimeError:
+            lib().zk_zero(acc.data_ptr(), acc.numel() * 4, st)  # no partial sums leak
+            raise
         ctx.save_for_backward(x, y, lse)
         ctx.eps, ctx.in_dtype = float(eps), logits.dtype
         ctx.mark_non_differentiable(hits)

@@ -62,7 +62,7 @@ from zookeeper_amd.parallel.flat import FlatParams
 class GradBucketer:
     def __init__(self, flat: FlatParams, world: int, bucket_mb: float = 10.0,
                  first_bucket_mb: float = 1.0, group=None, grad_dtype: Optional[torch.dtype] = None,
-                 timing: bool = False, force: bool = False, high_priority: bool = True,
+                 timing: bool = False, force: bool = False, high_priority: bool = False,
                  check_order: bool = False, native_comm=None):
         """``force``: stay enabled with one rank (needs an initialised
         process group, e.g. a 1-rank RCCL communicator from

@@ -45,7 +45,7 @@ class CommConfig:
       stream, which also lets a HIP graph capture the collectives.
     """
 
-    high_priority: bool = True
+    high_priority: bool = False
     min_channels: int = 0
     max_channels: int = 0
     cpu_affinity: bool = True

@@ -34,8 +34,6 @@ class Runtime:
     # --- kernel variants (ops/options.py documents each and its measurement)
     bconv_fp4: bool = Field(True)
     wgrad_side_stream: bool = Field(True)
-    wgrad_priority: int = Field(0)
-    wgrad_cu_share: float = Field(0.0)
     stem_fused: bool = Field(True)
     conv_mfma: bool = Field(True)
     conv3_mfma: bool = Field(True)
@@ -44,7 +42,7 @@ class Runtime:
     dgrad_rw: bool = Field(True)
     bn_stats_epilogue: bool = Field(True)
     wgrad_slab_mb: int = Field(32)
-    wgrad_reduce: str = Field("slab")
+    wgrad_rows: bool = Field(True)
     dgrad_deep: bool = Field(True)
     wgrad_deep: bool = Field(True)
     weight_images: bool = Field(True)
@@ -64,8 +62,11 @@ class Runtime:
     comm_timing: bool = Field(True)
 
     # --- data-parallel communicator (parallel/dist.py CommConfig documents each)
-    # RCCL streams and the comm stream at high HIP priority.
-    comm_high_priority: bool = Field(True)
+    # RCCL streams and the comm stream at high HIP priority.  Off by default:
+    # with it on, the two-rank gloo GPU test exposed a stale-gradient race in
+    # the (since fixed) host stager (profiles/r4/d_dp_stager_race.md), and the
+    # high-priority RCCL ordering has no multi-rank GPU verification yet.
+    comm_high_priority: bool = Field(False)
     # NCCL_MIN_NCHANNELS / NCCL_MAX_NCHANNELS (0: RCCL's default).
     rccl_min_channels: int = Field(0)
     rccl_max_channels: int = Field(0)
@@ -84,14 +85,14 @@ class Runtime:
             raise ValueError("runtime.rccl_min_channels / rccl_max_channels must be >= 0")
         if 0 < self.rccl_max_channels < self.rccl_min_channels:
             raise ValueError("runtime.rccl_min_channels > rccl_max_channels")
-        if not 0.0 <= self.wgrad_cu_share <= 1.0:
-            raise ValueError("runtime.wgrad_cu_share must be in [0, 1]")
-        if self.wgrad_reduce not in ("auto", "atomic", "slab"):
-            raise ValueError(f"runtime.wgrad_reduce must be 'auto', 'atomic' or 'slab', "
-                             f"got {self.wgrad_reduce!r}")
         if self.comm_backend not in ("torch", "native"):
             raise ValueError(f"runtime.comm_backend must be 'torch' or 'native', "
                              f"got {self.comm_backend!r}")
+        if self.check_bucket_order and self.comm_backend == "native" and self.graph != "off":
+            # the order check all-reduces and reads a hash on the host inside
+            # bucketer.finish(), which the native backend captures into the graph
+            raise ValueError("runtime.check_bucket_order needs runtime.graph='off' with "
+                             "runtime.comm_backend='native'")
 
     def kernel_options(self) -> Dict[str, Any]:
         return {k: getattr(self, k) for k in _KERNEL_FIELDS}

@@ -163,6 +163,12 @@ class Trainer:
                 self.graph = t_host > 0.85 * t_gpu  # host-bound: replay
             return out
         capture_comm = self.bucketer.enabled and self.bucketer.capturable
+        images = getattr(self.flat, "images", None)
+        if images is not None:
+            # the replay reads the bf16 weight images as captured: rebuild them
+            # if a parameter changed outside the fused optimizer (checkpoint
+            # restore, an in-place edit) -- eagerly, before the replay
+            images.ensure_current(torch.cuda.current_stream(self.device).cuda_stream)
         if self._graph is None:
             self._static_in = (x.clone(), y.clone())  # clone keeps x's channels_last strides
             self._graph = torch.cuda.CUDAGraph()
