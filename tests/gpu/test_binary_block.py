@@ -41,6 +41,8 @@ def _run(block, x, backend, g):
 CASES = [
     # (cin, cout, stride, H)  — E18 shapes (reduced batch)
     (64, 64, 1, 14),
+    (64, 64, 1, 28),     # weight gradient on the e2m1 image (wgrad_rows op 2)
+    (128, 128, 1, 28),
     (64, 128, 2, 14),
     (128, 128, 1, 7),
     (256, 512, 2, 8),
@@ -210,3 +212,45 @@ def test_fused_bn_backward_sums_match_separate_reduce(monkeypatch, second_consum
         res.append([xx.grad.float()] + [p.grad.clone() for b in bs for p in b.parameters()])
     for a, b in zip(*res):
         assert ((a - b).norm() / b.norm().clamp_min(1e-12)).item() < 2e-3
+
+
+@pytest.mark.parametrize("hw", [28, 56])
+def test_fp4_weight_gradient_skips_bf16_sign_image(monkeypatch, hw):
+    """With the consumer links of the model (``sign_consumer``) a block whose
+    next conv's weight gradient reads the e2m1 image (wgrad_rows operand 2)
+    writes no bf16 sign image, and the gradients equal the bf16-image run
+    (runtime.wgrad_fp4 off) -- the weight gradients bit for bit: same products,
+    same fixed summation order."""
+    _setup()
+    from zookeeper_amd import ops
+
+    torch.manual_seed(21)
+    blocks = [BinaryResBlock(64, 64, 1).cuda().to(memory_format=torch.channels_last)
+              for _ in range(3)]
+    with torch.no_grad():
+        for b in blocks:
+            b.bn.weight.uniform_(0.5, 1.5)
+            b.bn.bias.uniform_(-0.5, 0.5)
+    x = (torch.randn(2, 64, hw, hw, device="cuda") * 1.5).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    g = torch.randn(2, 64, hw, hw, device="cuda").to(torch.bfloat16)
+    res = []
+    for fp4 in (True, False):
+        monkeypatch.setattr(OPTS, "wgrad_fp4", fp4)
+        monkeypatch.setattr(OPTS, "wgrad_side_stream", False)
+        bs = [copy.deepcopy(b) for b in blocks]
+        xx = x.clone().requires_grad_(True)
+        h = xx
+        for i, b in enumerate(bs):
+            nxt = bs[i + 1].conv if i + 1 < len(bs) else None
+            h = ops.binary_block(h, h, b.conv, b.bn, sign_consumer=nxt)
+            if nxt is not None:
+                # (clip, bf16 sign image, mask, e2m1 image)
+                assert (h._zk_sign[1] is None) == fp4
+                assert h._zk_sign[3] is not None
+        (h.float() * g.float()).sum().backward()
+        res.append([xx.grad.float()] + [b.conv.weight.grad.clone() for b in bs])
+    (dx1, *w1), (dx2, *w2) = res
+    assert ((dx1 - dx2).norm() / dx2.norm()).item() < 1e-3
+    for a, b in zip(w1, w2):
+        assert torch.equal(a, b)

@@ -74,3 +74,37 @@ def test_stream_overlaps_compute():
     assert b["image"].shape == (128, 224, 224, 3)
     # the GPU work was still running when next() returned
     assert t_gpu > 0.002, (t_next, t_gpu)
+
+
+@pytest.mark.timeout(120)
+def test_device_slots_reused_under_slow_consumer():
+    """The device batches come from a preallocated ring (no allocation per
+    batch), and a slot is not overwritten while a slow consumer's queued work
+    still reads it: each batch is summed on the compute stream only after a
+    long sleep kernel, and every sum must equal its host reference."""
+    from zookeeper_amd.data.dataset import ArraySource
+    from zookeeper_amd.data.loader import DeviceLoader, IndexSampler
+
+    arr = np.random.default_rng(5).integers(0, 255, (512, 32, 32, 3), dtype=np.uint8)
+    src = ArraySource(arr, np.arange(512) % 11)
+    dev = torch.device("cuda", 0)
+    loader = DeviceLoader(src, 32, dev, shuffle=True, seed=2, slots=4)
+    sampler = IndexSampler(len(src), 32, True, 2)
+    it, ref = iter(loader), sampler.batches()
+    sums, want, ptrs = [], [], set()
+    for i in range(24):
+        got, idx = next(it), next(ref)
+        if i == 4:
+            torch.cuda.synchronize()
+            allocs0 = torch.cuda.memory_stats(dev).get("num_device_alloc", 0)
+        ptrs.add(got["image"].data_ptr())
+        torch.cuda._sleep(2_000_000)  # the consumer's "step": the copy stream runs ahead
+        sums.append(got["image"].sum(dtype=torch.int64))
+        want.append(int(src.get_batch(idx)["image"].astype(np.int64).sum()))
+    torch.cuda.synchronize()
+    allocs1 = torch.cuda.memory_stats(dev).get("num_device_alloc", 0)
+    loader.close()
+    assert [int(s) for s in sums] == want
+    assert len(ptrs) <= 4  # ahead + 2 device slots, round-robin
+    # (the sum results are the only allocations; the caching allocator reuses them)
+    assert allocs1 == allocs0

@@ -43,3 +43,51 @@ def test_one_rank_all_reduce_broadcast_and_graph_capture():
     # ((0+1)*2 + 1)*2 ... : 2, 6, 14
     assert torch.all(y == 14), y[:4]
     comm.close()
+
+
+@pytest.mark.timeout(120)
+def test_missing_peer_raises_instead_of_hanging():
+    """NativeComm(0, 2) with no second rank: the set-up rendezvous raises
+    within its deadline (before ncclCommInitRank could hang)."""
+    import time
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    from zookeeper_amd.parallel.rccl import NativeComm
+
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    store = dist.TCPStore("127.0.0.1", port, 2, True, timedelta(seconds=30),
+                          wait_for_workers=False)
+    t0 = time.monotonic()
+    with pytest.raises(TimeoutError):
+        NativeComm(0, 2, store=store, tag="zk_test_no_peer", timeout_s=3)
+    assert time.monotonic() - t0 < 30
+
+
+@pytest.mark.timeout(120)
+def test_watchdog_flags_a_collective_past_its_deadline():
+    """The watchdog follows an event that never completes in time (a stream
+    blocked behind a long kernel stands in for a hung collective): it aborts
+    the communicator and check() raises in the calling thread."""
+    import time
+
+    from zookeeper_amd.parallel.rccl import NativeComm
+
+    comm = NativeComm(0, 1, tag="zk_test_watchdog", timeout_s=0.5)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(int(3e9))  # ~1.5 s of a spinning kernel
+        ev = torch.cuda.Event()
+        ev.record(s)
+    comm.watch(ev, "test collective")
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError, match="did not complete"):
+        while time.monotonic() - t0 < 20:
+            comm.check()
+            time.sleep(0.05)
+    comm._stop.set()
+    torch.cuda.synchronize()

@@ -1,9 +1,12 @@
 """Row-streaming 3x3 weight gradient (csrc/kernels/wgrad_rows.hip) against an
 fp64 oracle.
 
-* both operand modes: the bf16 +-1 sign image, and (sign_act) the bf16
+* the three operand modes: the bf16 +-1 sign image, (sign_act) the bf16
   activation whose sign the kernel takes in registers -- with exact zeros in
-  the activation (sign(0) = +1, larq's ste_sign) and +1 padding;
+  the activation (sign(0) = +1, larq's ste_sign) and +1 padding -- and the
+  e2m1 (FP4) sign image the binary forward reads, expanded in LDS, with +1
+  and zero padding (bit-identical to the bf16 image: same products, same
+  summation order);
 * the image mode with zero padding (the float 3x3 convs of ResNet-50);
 * every shape of the dispatch (W = 56 / 28, 64 / 128 channels, Cin != Cout),
   and split counts that exercise each depth of the in-launch fixed-order tree
@@ -42,9 +45,17 @@ def _oracle(s, dy, w, pad, clip):
     return gw.permute(0, 2, 3, 1) * mask
 
 
+def _fp4(s):
+    """e2m1 image of a +-1 tensor [..., C] -> [..., C/2] bytes (channel 2j in
+    the low nibble of byte j: +1 = 0x2, -1 = 0xA), zk_sign_pack's layout."""
+    code = torch.where(s.float() >= 0, 2, 10).to(torch.uint8)
+    return (code[..., 0::2] | (code[..., 1::2] << 4)).contiguous()
+
+
 def _run(dy, s, w, dw, pad_ones, sign_act, clip, tb):
     L = _lib()
     B, H, W, Cin = s.shape
+    Cin *= 2 if sign_act == 2 else 1  # operand 2: e2m1, two channels per byte
     Cout = dy.shape[3]
     sb, cb = ctypes.c_int64(0), ctypes.c_int64(0)
     assert L.zk_wgrad_rows_plan(B, H, W, Cin, Cout, tb, ctypes.byref(sb), ctypes.byref(cb)) == 0
@@ -122,6 +133,23 @@ def test_sign_mode_equals_image_mode():
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("pad_ones", [True, False])
+@pytest.mark.parametrize("tb", [3, 256])
+def test_fp4_operand_equals_image_mode(shape, pad_ones, tb):
+    """op 2 (e2m1 image, expanded in LDS) gives the bits of op 0 on the bf16
+    image, and matches the fp64 oracle with either padding value."""
+    B, H, W, Cin, Cout = shape
+    _, s, dy, w = _data(B, H, W, Cin, Cout, seed=11)
+    a, b = torch.zeros_like(w), torch.zeros_like(w)
+    _run(dy, s, w, a, pad_ones, 0, 1.0, tb)
+    _run(dy, _fp4(s), w, b, pad_ones, 2, 1.0, tb)
+    assert torch.equal(a, b)
+    ref = _oracle(s, dy, w, 1.0 if pad_ones else 0.0, 1.0)
+    err = (b.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+
+
 def test_unsupported_shapes_rejected():
     L = _lib()
     assert L.zk_wgrad_rows_plan(8, 14, 14, 256, 256, 0, None, None) != 0  # W not 56 / 28
@@ -133,6 +161,9 @@ def test_unsupported_shapes_rejected():
     rc = L.zk_wgrad_rows(dy.data_ptr(), dy.data_ptr(), None, dw.data_ptr(), None, 0, None, 0,
                          2, 56, 56, 64, 64, 0, 1, 1.0, 1, torch.cuda.current_stream().cuda_stream)
     assert rc != 0
+    rc = L.zk_wgrad_rows(dy.data_ptr(), dy.data_ptr(), None, dw.data_ptr(), None, 0, None, 0,
+                         2, 56, 56, 64, 64, 1, 3, 1.0, 1, torch.cuda.current_stream().cuda_stream)
+    assert rc != 0  # no operand mode 3
 
 
 def test_dispatch_routes_3x3_stride1_layers():
@@ -147,18 +178,21 @@ def test_dispatch_routes_3x3_stride1_layers():
     assert _native.wgrad_rows_ok(geom)
     st = torch.cuda.current_stream().cuda_stream
     a, b = torch.zeros_like(w), torch.zeros_like(w)
-    _native.igemm_wgrad(dy, x, w, a, geom, 1, 1.0, st, sign_act=True)
+    _native.igemm_wgrad(dy, x, w, a, geom, 1, 1.0, st, operand="sign")
+    c = torch.zeros_like(w)
+    _native.igemm_wgrad(dy, _fp4(s), w, c, geom, 1, 1.0, st, operand="fp4")
     old = OPTS.wgrad_rows
     set_options(wgrad_rows=False)
     try:
         assert not _native.wgrad_rows_ok(geom)
         _native.igemm_wgrad(dy, s, w, b, geom, 1, 1.0, st)
-        with pytest.raises(ValueError):
-            _native.igemm_wgrad(dy, x, w, b, geom, 1, 1.0, st, sign_act=True)
+        for op in ("sign", "fp4"):
+            with pytest.raises(ValueError):
+                _native.igemm_wgrad(dy, x, w, b, geom, 1, 1.0, st, operand=op)
     finally:
         set_options(wgrad_rows=old)
     torch.cuda.synchronize()
     ref = _oracle(s, dy, w, 1.0, 1.0)
-    for d in (a, b):
+    for d in (a, b, c):
         err = (d.double() - ref).abs().max().item() / ref.abs().max().item()
         assert err < 2e-6, err

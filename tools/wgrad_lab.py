@@ -31,6 +31,12 @@ def make(B, H, Cin, Cout, dev, seed=0):
     return x, sx, dy, w
 
 
+def fp4(sx):
+    """e2m1 sign image (channel 2j in the low nibble of byte j)."""
+    code = torch.where(sx.float() >= 0, 2, 10).to(torch.uint8)
+    return (code[..., 0::2] | (code[..., 1::2] << 4)).contiguous()
+
+
 def oracle(sx, dy, w, pad_ones, clip):
     xp = torch.nn.functional.pad(sx.float().permute(0, 3, 1, 2), (1, 1, 1, 1),
                                  value=1.0 if pad_ones else 0.0)
@@ -122,11 +128,12 @@ def main():
         ref = oracle(sx, dy, w, True, 1.0)
         scale = ref.abs().max().item()
         rec = {"shape": [H, H, Cin, Cout], "check_batch": B}
+        sx4 = fp4(sx)
         for tb in tbs + [8, 3]:
             k = Rows(L, B, H, Cin, Cout, tb, dev)
-            for sign in (0, 1):
+            for sign in (0, 1, 2):
                 dw = torch.full_like(w, 0.25)  # accumulates into existing values
-                k(dy, x if sign else sx, w, dw, sign, st)
+                k(dy, (sx, x, sx4)[sign], w, dw, sign, st)
                 torch.cuda.synchronize()
                 err = ((dw - 0.25 * (w.abs() <= 1.0).float() - 0.25 * (w.abs() > 1.0).float()
                         - ref).abs().max().item()) / scale
@@ -135,10 +142,11 @@ def main():
         old_wgrad(L, dy, sx, w, dw, B, H, Cin, Cout, st)
         torch.cuda.synchronize()
         rec["old_relerr"] = (dw - ref).abs().max().item() / scale
-        del x, sx, dy, w, ref
+        del x, sx, sx4, dy, w, ref
         # --- full batch: determinism, new vs old, timings
         B = args.batch
         x, sx, dy, w = make(B, H, Cin, Cout, dev, seed=1)
+        sx4 = fp4(sx)
         ks = {tb: Rows(L, B, H, Cin, Cout, tb, dev) for tb in tbs}
         outs = []
         for rep in range(2):
@@ -149,12 +157,18 @@ def main():
         old_wgrad(L, dy, sx, w, dwo, B, H, Cin, Cout, st)
         torch.cuda.synchronize()
         rec["rows_bitwise_repeat"] = bool(torch.equal(outs[0], outs[1]))
+        d4 = torch.zeros_like(w)
+        ks[tbs[0]](dy, sx4, w, d4, 2, st)
+        torch.cuda.synchronize()
+        rec["rows_fp4_equals_sign"] = bool(torch.equal(outs[0], d4))
+        del d4
         rec["rows_vs_old_rel"] = ((outs[0] - dwo).abs().max() / dwo.abs().max()).item()
         dw = torch.zeros_like(w)
         fns = {"old": lambda: old_wgrad(L, dy, sx, w, dw, B, H, Cin, Cout, st)}
         for tb in tbs:
             fns[f"rows_tb{tb}_img"] = (lambda k=ks[tb]: k(dy, sx, w, dw, 0, st))
             fns[f"rows_tb{tb}_sign"] = (lambda k=ks[tb]: k(dy, x, w, dw, 1, st))
+            fns[f"rows_tb{tb}_fp4"] = (lambda k=ks[tb]: k(dy, sx4, w, dw, 2, st))
 
         dbg = torch.zeros(4096 * 4 * 8, dtype=torch.int64, device=dev)
 
@@ -168,8 +182,9 @@ def main():
         fns["rows_compute_only"] = lambda: ablate(2)
         fns["rows_lds_reads_only"] = lambda: ablate(3)
         fns["rows_mfma_no_s_reads"] = lambda: ablate(4)
-        fns["rows_fd3"] = lambda: ablate(5)
-        fns["rows_fd7"] = lambda: ablate(6)
+        fns["rows_nosplit_sign"] = lambda: ablate(5)
+        fns["rows_fd4_sign"] = lambda: ablate(6)
+        fns["rows_burst_issue_sign"] = lambda: ablate(8)
         times = {n: [] for n in fns}
         for _ in range(args.rounds):
             for n, fn in fns.items():
@@ -178,6 +193,27 @@ def main():
             rec[f"{n}_us_med"] = round(statistics.median(t), 1)
             rec[f"{n}_us_min"] = round(min(t), 1)
         if H == 56:
+            dbg.zero_()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            ev0.record()
+            ablate(7)
+            ev1.record()
+            torch.cuda.synchronize()
+            ends = dbg.view(-1, 8)
+            ends = ends[ends[:, 3] > 0]
+            # wall_clock64 ticks of the whole launch vs its event time (us):
+            # calibrates the tick rate (events add the launch latency)
+            span_ticks = float(ends[:, 7].max() - ends[:, 4].min())
+            rec["lab7_event_us"] = round(ev0.elapsed_time(ev1) * 1e3, 1)
+            rec["wall_clock_mhz_upper"] = round(span_ticks / (ev0.elapsed_time(ev1) * 1e3), 2)
+            dbg.zero_()
+            ablate(7)
+            torch.cuda.synchronize()
+            ends = dbg.view(-1, 8)
+            ends = ends[ends[:, 3] > 0]
+            rec["tree_tail_us"] = round(float((ends[:, 7].max() - ends[:, 5].max()) / 100.0), 1)
+            rec["kernel_span_us"] = round(float((ends[:, 7].max() - ends[:, 4].min()) / 100.0), 1)
             dbg.zero_()
             ablate(7)
             torch.cuda.synchronize()
@@ -205,7 +241,7 @@ def main():
         rec["hbm_floor_us_at_6TBs"] = round(gbytes / 6.0e3 * 1e6, 1)
         rows.append(rec)
         print(json.dumps(rec), flush=True)
-        del x, sx, dy, w, dw, dwo, outs, ks
+        del x, sx, sx4, dy, w, dw, dwo, outs, ks
         torch.cuda.empty_cache()
     if args.out:
         with open(args.out, "w") as f:

@@ -55,28 +55,44 @@ constexpr int WR_MAXLV = 8;
 constexpr int WR_RW = 112;     // pixels per step
 constexpr int WR_NK = WR_RW / 16;
 constexpr int WR_NSLOT = 3;
+constexpr int WR_SC1 = 16;     // buffer-op cache policy: sc1 (agent-coherent)
 
-template <int W>
+// Operand modes of S: the bf16 image (OP_IMG: a +-1 sign image, or a float
+// activation), the bf16 activation whose sign is taken in registers
+// (OP_SIGN), or the e2m1 (FP4) sign image the binary forward already reads
+// (OP_FP4): staged at a quarter of the bytes and expanded in LDS
+// (v_cvt_scalef32_pk_bf16_fp4, one instruction per bf16 pair) one step ahead,
+// so padding keeps its value (0 or +1) and the forward need not write a bf16
+// sign image for these layers.
+enum { OP_IMG = 0, OP_SIGN = 1, OP_FP4 = 2 };
+
+template <int W, int OP>
 struct WrGeo {
   static constexpr int R = WR_RW / W;           // image rows per step
   static constexpr int PW = W + 2;              // S window row pitch (pixels)
   static constexpr int RB = PW * 64;            // S window row bytes in one plane
   static constexpr int SPLANE = (R + 2) * RB;   // window rows h0-1 .. h0+R
-  static constexpr int SBYTES = 2 * SPLANE;
+  static constexpr int SBYTES = 2 * SPLANE;     // bf16 window, 2 planes of 32 channels
+  static constexpr int S4BYTES = (R + 2) * PW * 32;  // e2m1 window, 32 B per pixel
   static constexpr int DPLANE = WR_RW * 64;
   static constexpr int DBYTES = 2 * DPLANE;     // 14 KB
   static constexpr int DINS = DBYTES / 1024;
-  static constexpr int TOT = (DINS + (SBYTES + 1023) / 1024 + 3) / 4 * 4;  // DMA pieces
+  // staged per step: dY + the S window (bf16, or e2m1 for OP_FP4)
+  static constexpr int STAGED = OP == OP_FP4 ? S4BYTES : SBYTES;
+  static constexpr int TOT = (DINS + (STAGED + 1023) / 1024 + 3) / 4 * 4;  // DMA pieces
   static constexpr int NI = TOT / 4;            // DMA pieces per wave per step
   static constexpr int SLOT = TOT * 1024;
-  static constexpr int FLAG = WR_NSLOT * SLOT;  // arrival broadcast word
+  // OP_FP4: two expanded bf16 windows after the slots (step j's, step j+1's)
+  static constexpr int SBF = WR_NSLOT * SLOT;
+  static constexpr int FLAG = SBF + (OP == OP_FP4 ? 2 * SBYTES : 0);  // arrival word
   static constexpr int LDS = FLAG + 16;
+  static constexpr int CHUNKS = SBYTES / 16;    // OP_FP4 expansion: 16-B bf16 chunks
   static_assert(WR_RW % W == 0 && LDS <= 160 * 1024, "row-stream geometry");
 };
 
 struct WrArgs {
   const uint16_t* dy;  // [B][H][W][Cout] bf16
-  const uint16_t* sx;  // [B][H][W][Cin] bf16 (sign image, or the activation with SIGN)
+  const uint16_t* sx;  // [B][H][W][Cin] bf16 (OP_IMG / OP_SIGN) or [B][H][W][Cin/2] e2m1 (OP_FP4)
   const float* w;      // [Cout][9][Cin] latent weights (kernel STE mask), or null
   float* dw;           // [Cout][9][Cin] fp32, accumulated
   float* slab;         // tree levels 0 .. levels-1, full-dW layout per node
@@ -115,15 +131,51 @@ __device__ __forceinline__ uint32_t sign_bf16x2(uint32_t v, uint32_t ones) {
   return (v & 0x80008000u) | (ones & 0x7FFF7FFFu);
 }
 
+// Unit schedules of the main loop (a unit = one S fragment: K-step kk, tap t).
+// M 0 / 1: the SPLIT pair members (taps 0-3 / 5-8 of every K-step, tap 4 of
+// K-steps 0-3 / 4-6: 32 / 31 units); M 2: all 63 units in (kk, t) order.
+__host__ __device__ constexpr int wr_units(int m) { return m == 2 ? 63 : (m == 0 ? 32 : 31); }
+// (closed forms, so unrolled loops fold them to constants: M 0 has 5 units
+// per K-step below kk 4 and 4 above, M 1 the reverse)
+__host__ __device__ constexpr int wr_unit_kk(int m, int n) {
+  return m == 2 ? n / 9
+       : m == 0 ? (n < 20 ? n / 5 : 4 + (n - 20) / 4)
+                : (n < 16 ? n / 4 : 4 + (n - 16) / 5);
+}
+__host__ __device__ constexpr int wr_unit_tap(int m, int n) {
+  return m == 2 ? n % 9
+       : m == 0 ? (n < 20 ? n % 5 : (n - 20) % 4)
+                : (n < 16 ? 5 + n % 4 : ((n - 16) % 5 == 4 ? 4 : 5 + (n - 16) % 5));
+}
+// accumulator slot of tap t, and back (M 1 keeps tap 4 in slot 0)
+__host__ __device__ constexpr int wr_tap_slot(int m, int t) {
+  return m == 1 ? (t == 4 ? 0 : t - 4) : t;
+}
+__host__ __device__ constexpr int wr_slot_tap(int m, int s) {
+  return m == 1 ? (s == 0 ? 4 : s + 4) : s;
+}
+static_assert(wr_unit_kk(0, 31) == 6 && wr_unit_tap(0, 31) == 3 && wr_unit_tap(0, 4) == 4 &&
+                  wr_unit_kk(1, 30) == 6 && wr_unit_tap(1, 30) == 4 && wr_unit_tap(1, 3) == 8 &&
+                  wr_unit_kk(1, 4) == 1,
+              "unit schedule");
+
 // LAB: ablation builds for tools/wgrad_lab.py (0 = the kernel; 1 loads only,
 // 2 compute only, 3 compute only without MFMAs, 4 compute only without the S
 // fragment reads; results are garbage in 1-4)
 // FD: how many MFMAs ahead each S fragment is read (one wave per SIMD: only
 // this lookahead hides the LDS latency)
-template <int W, bool SIGN, int LAB = 0, int FD = 6>
+// SPLIT: wave tile 64(co) x 32(ci) x 9 taps, the two waves of a ci half
+// splitting the step's 63 (K-step, tap) units 32 / 31 (each S fragment feeds
+// both co halves: half the LDS fragment reads per MFMA); partial tiles of the
+// pair combined through LDS after the loop.  Otherwise 32 x 32 x 9 per wave.
+template <int W, int OP, bool SPLIT, int LAB = 0, int FD0 = 0>
 __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
-  using G = WrGeo<W>;
+  // lookahead: 5 units (SPLIT: 10 S + up to 4 dY reads in flight, under the
+  // 15 lgkmcnt can count) or 6 MFMAs
+  constexpr int FD = FD0 > 0 ? FD0 : (SPLIT ? 5 : 6);
+  using G = WrGeo<W, OP>;
   constexpr int R = G::R, PW = G::PW, RB = G::RB, NI = G::NI;
+  constexpr bool FP4 = OP == OP_FP4, SIGN = OP == OP_SIGN;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
@@ -139,8 +191,13 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
   const unsigned char* sxb = reinterpret_cast<const unsigned char*>(a.sx);
   const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
   const unsigned char* pp =
-      (a.pad_ones && !SIGN) ? reinterpret_cast<const unsigned char*>(g_ones_page_bf16) : zp;
-  constexpr bool do_load = LAB < 2, do_mma = LAB != 1;
+      !a.pad_ones || SIGN ? zp
+      : FP4 ? reinterpret_cast<const unsigned char*>(g_ones_page_fp4)
+            : reinterpret_cast<const unsigned char*>(g_ones_page_bf16);
+  constexpr bool do_load = LAB < 2 || LAB > 4, do_mma = LAB != 1;
+  // the next step's LDS-DMA pieces spread over the MFMA units (LAB 8: all
+  // issued at the top of the step, before the first MFMA)
+  constexpr bool spread = LAB != 8;
   constexpr bool lab_reads = LAB != 4, lab_mfma = LAB != 3;
 
   // per-lane LDS-DMA sources of a slot's NI pieces per wave (piece t = k*4 +
@@ -156,39 +213,89 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
       const int plane = b / G::DPLANE, rem = b % G::DPLANE;
       const int p = rem >> 6, ch = (rem & 63) >> 4;
       src[k] = (p * a.Cout + co0 + plane * 32 + ch * 8) * 2;
-    } else if (b - G::DBYTES < G::SBYTES) {
+    } else if (b - G::DBYTES < G::STAGED) {
       const int bs = b - G::DBYTES;
-      const int plane = bs / G::SPLANE, rem = bs % G::SPLANE;
-      const int wr = rem / RB, col = (rem % RB) >> 6, ch = (rem & 63) >> 4;
-      if (col >= 1 && col <= W)
-        src[k] = ((((wr - 1) * W + col - 1) * a.Cin + ci0 + plane * 32 + ch * 8) * 2) | (1 + wr);
-      else
-        src[k] = 14;
+      int wr, col, off;
+      if constexpr (FP4) {  // [window pixel][32 B]: the tile's 64 channels as nibbles
+        const int pix = bs >> 5, half = (bs & 31) >> 4;
+        wr = pix / PW;
+        col = pix % PW;
+        off = ((wr - 1) * W + col - 1) * (a.Cin / 2) + ci0 / 2 + half * 16;
+      } else {  // [plane][window pixel][32 channels]
+        const int plane = bs / G::SPLANE, rem = bs % G::SPLANE;
+        const int ch = (rem & 63) >> 4;
+        wr = rem / RB;
+        col = (rem % RB) >> 6;
+        off = (((wr - 1) * W + col - 1) * a.Cin + ci0 + plane * 32 + ch * 8) * 2;
+      }
+      src[k] = (col >= 1 && col <= W) ? (off | (1 + wr)) : 14;
     } else {
       src[k] = 15;
     }
   }
   const long long dy_step = (long long)WR_RW * a.Cout * 2;
-  const long long sx_step = (long long)WR_RW * a.Cin * 2;
-  auto issue = [&](int j, int slot) {
+  const long long sx_step = (long long)WR_RW * a.Cin * (FP4 ? 1 : 4) / 2;
+  // stage dY of step jd and the S window of step js into `slot` (OP_FP4
+  // stages the window one step ahead: js = jd + 1); out-of-range steps read
+  // zeros / padding
+  // (steps past the end stage zeros / padding: the loop issues two steps
+  // ahead unconditionally, branch-free)
+  struct Stage {
+    uint64_t dyu, sxu;
+    int top, bot;
+    bool dok, sok;
+    unsigned char* dst;
+  };
+  auto prep = [&](int jd, int js, int slot) -> Stage {
+    Stage t;
+    t.dok = jd >= 0 && jd < a.nsteps;
+    t.sok = js >= 0 && js < a.nsteps;
+    t.dyu = (uint64_t)(uintptr_t)(dyb + (long long)(t.dok ? jd : 0) * dy_step);
+    t.sxu = (uint64_t)(uintptr_t)(sxb + (long long)(t.sok ? js : 0) * sx_step);
+    const int h0 = t.sok ? (int)(((long long)js * R) % H) : 0;
+    t.top = h0 == 0 ? 1 : -100;          // window row 0 is above the image
+    t.bot = h0 + R == H ? R + 2 : -100;  // window row R + 1 is below it
+    t.dst = smem + slot * G::SLOT + wave * 1024;
+    return t;
+  };
+  const uint64_t ppu = (uint64_t)(uintptr_t)pp, zpu = (uint64_t)(uintptr_t)zp;
+  auto piece = [&](const Stage& t, int k) {
     if constexpr (!do_load) return;
-    const unsigned char* dyp = dyb + (long long)j * dy_step;
-    const unsigned char* sxp = sxb + (long long)j * sx_step;
-    const int h0 = (int)(((long long)j * R) % H);
-    const int top = h0 == 0 ? 1 : -100;           // window row 0 is above the image
-    const int bot = h0 + R == H ? R + 2 : -100;   // window row R + 1 is below it
-    unsigned char* dst = smem + slot * G::SLOT + wave * 1024;
     // branch-free source selection (selects, no divergent branches)
-    const uint64_t dyu = (uint64_t)(uintptr_t)dyp, sxu = (uint64_t)(uintptr_t)sxp;
-    const uint64_t ppu = (uint64_t)(uintptr_t)pp, zpu = (uint64_t)(uintptr_t)zp;
+    const int kd = src[k] & 15, off = src[k] & ~15;
+    const bool pad = kd >= 14 || kd == t.top || kd == t.bot || (kd == 0 ? !t.dok : !t.sok);
+    const uint64_t real = (kd == 0 ? t.dyu : t.sxu) + (uint64_t)(int64_t)off;
+    const uint64_t fill = kd == 15 || kd == 0 || !t.sok ? zpu : ppu;
+    ZK_GLDS16((const void*)(uintptr_t)(pad ? fill : real), t.dst + k * 4096);
+  };
+  auto issue = [&](int jd, int js, int slot) {
+    const Stage t = prep(jd, js, slot);
 #pragma unroll
-    for (int k = 0; k < NI; ++k) {
-      const int kd = src[k] & 15, off = src[k] & ~15;
-      const bool pad = kd >= 14 || kd == top || kd == bot;
-      const uint64_t real = (kd == 0 ? dyu : sxu) + (uint64_t)(int64_t)off;
-      const uint64_t fill = kd == 15 ? zpu : ppu;
-      ZK_GLDS16((const void*)(uintptr_t)(pad ? fill : real), dst + k * 4096);
-    }
+    for (int k = 0; k < NI; ++k) piece(t, k);
+  };
+
+  // OP_FP4: expand the e2m1 window staged in `slot` into bf16 window buffer
+  // `buf` (chunks c0, c0 + 256, ... of this thread; `part` of the NPART parts
+  // this is split into so it can interleave with the MFMAs)
+  constexpr int CPT = (G::CHUNKS + WR_NT - 1) / WR_NT;  // chunks per thread
+  constexpr int CPP = (R + 2) * PW * 4;                  // chunks per plane
+  auto expand_read = [&](int slot, int c) -> uint32_t {
+    const int o = min(c * WR_NT + tid, G::CHUNKS - 1);
+    const int plane = o / CPP, rem = o % CPP;
+    const int pix = rem >> 2, q = rem & 3;
+    return *reinterpret_cast<const uint32_t*>(smem + slot * G::SLOT + G::DBYTES + pix * 32 +
+                                              plane * 16 + q * 4);
+  };
+  // (lanes past the last chunk redo the last one: same bytes, no branch)
+  auto expand_write = [&](int buf, int c, uint32_t v) {
+    const int o = min(c * WR_NT + tid, G::CHUNKS - 1);
+    typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+    uint4 out;
+    out.x = __builtin_bit_cast(uint32_t, (bf2)__builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(v, 1.0f, 0));
+    out.y = __builtin_bit_cast(uint32_t, (bf2)__builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(v, 1.0f, 1));
+    out.z = __builtin_bit_cast(uint32_t, (bf2)__builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(v, 1.0f, 2));
+    out.w = __builtin_bit_cast(uint32_t, (bf2)__builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(v, 1.0f, 3));
+    *reinterpret_cast<uint4*>(smem + G::SBF + buf * G::SBYTES + o * 16) = out;
   };
 
   // fragment offsets: lane group gq = lane >> 4 reads pixels p = kk*16 +
@@ -200,8 +307,9 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
   const int gq = lane >> 4, qi = lane & 15, qq = qi >> 2, pq = qi & 3;
   const int colb = (gq & 1) * 32 + pq * 8;
   const int p0 = 8 * (gq >> 1) + qq;  // 0 .. 11
-  const int offD = wm * G::DPLANE + p0 * 64 + colb;
-  const int offS0 = G::DBYTES + wn * G::SPLANE + p0 * 64 + colb;
+  const int offDp = p0 * 64 + colb;  // SPLIT: both co halves (+ h * DPLANE)
+  const int offD = wm * G::DPLANE + offDp;
+  const int offS0 = wn * G::SPLANE + p0 * 64 + colb;  // from the S window base
   int xS[WR_NK][2];  // per (kk, hf): offS0 + 128 * (r - r_min) (used where lanes straddle)
 #pragma unroll
   for (int kk = 0; kk < WR_NK; ++kk)
@@ -213,138 +321,265 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
 
   uint32_t ones;
   asm volatile("v_mov_b32 %0, 0x3f803f80" : "=v"(ones));
-  f32x16 acc[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
-
-  long long t_wait = 0, t_issue = 0, t_mma = 0, t_prev = 0, t_start = 0;
-  if constexpr (LAB == 7) {
-    t_prev = clock64();
-    t_start = wall_clock64();
-  }
-  if (j0 < j1) issue(j0, 0);
-  if (j0 + 1 < j1) issue(j0 + 1, 1);
-  for (int j = j0; j < j1; ++j) {
-    const int slot = (j - j0) % WR_NSLOT;
-    if constexpr (LAB == 7) {
-      const long long t = clock64();
-      t_mma += t - t_prev;
-      t_prev = t;
-    }
-    if (j + 1 < j1)
-      wait_vmcnt<NI>();  // step j landed (this wave's pieces); j + 1 in flight
-    else
-      wait_vmcnt<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if constexpr (LAB == 7) {
-      const long long t = clock64();
-      t_wait += t - t_prev;
-      t_prev = t;
-    }
-    if (j + 2 < j1) issue(j + 2, (j + 2 - j0) % WR_NSLOT);
-    if constexpr (LAB == 7) {
-      const long long t = clock64();
-      t_issue += t - t_prev;
-      t_prev = t;
-    }
-    if constexpr (!do_mma) continue;
-    const int base = slot * G::SLOT;
-    // the step's 63 MFMAs (K-step kk = i / 9, tap t = i % 9) with each
-    // fragment read FD MFMAs ahead into a small rotating buffer (one wave per
-    // SIMD: only this lookahead hides the LDS latency; few registers, so the
-    // accumulators never leave their registers)
-    constexpr int NB = FD + 1, NM = WR_NK * 9;
-    uint4 fb[NB], fa[2];
-    auto read_b = [&](int i) {
-      const int kk = i / 9, t = i % 9, kh = t / 3, kw = t % 3;
-      if constexpr (!lab_reads) {
-        fb[i % NB] = make_uint4(i, kk, t, lane);
-        return;
-      }
-      int o[2];
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const int q0 = kk * 16 + 4 * hf;
-        // lanes p0 = 0 .. 11 of this K-step in one image row: a constant offset
-        const bool one_row = q0 / W == (q0 + 11) / W;
-        o[hf] = (one_row ? base + offS0 : base + xS[kk][hf]) + (q0 + 2 * (q0 / W)) * 64 +
-                kh * RB + kw * 64;
-      }
-      fb[i % NB] = tr_read2(smem, o[0], o[1]);
-    };
-    auto read_a = [&](int kk) {
-      const int aD = base + offD + kk * 1024;
-      fa[kk % 2] = tr_read2(smem, aD, aD + 256);
-    };
-    read_a(0);
-#pragma unroll
-    for (int i = 0; i < FD; ++i) read_b(i);
-#pragma unroll
-    for (int i = 0; i < NM; ++i) {
-      if (i + FD < NM) {
-        if ((i + FD) % 9 == 0) read_a((i + FD) / 9);
-        read_b(i + FD);
-      }
-      uint4 b = fb[i % NB];
-      if constexpr (SIGN) {
-        b.x = sign_bf16x2(b.x, ones);
-        b.y = sign_bf16x2(b.y, ones);
-        b.z = sign_bf16x2(b.z, ones);
-        b.w = sign_bf16x2(b.w, ones);
-      }
-      if constexpr (lab_mfma)
-        acc[i % 9] = mfma_bf16(fa[(i / 9) % 2], b, acc[i % 9]);
-      else
-        asm volatile("" ::"v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w));
-      // keep the issue order: reads FD MFMAs ahead (the scheduler would
-      // otherwise sink them next to their MFMA and expose the LDS latency)
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-
-  if constexpr (LAB == 7) {
-    t_mma += clock64() - t_prev;
-    if (lane == 0) {
-      long long* d = a.dbg + ((long long)blockIdx.x * 4 + wave) * 8;
-      d[0] = t_wait;
-      d[1] = t_issue;
-      d[2] = t_mma;
-      d[3] = j1 - j0;
-      d[4] = t_start;
-      d[5] = wall_clock64();
-      d[6] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID
-      d[7] = clock64();
-    }
-  }
-  // ---- epilogue: D[co][ci] of tap t in acc[t]: co = co0 + wm*32 + (e&3) +
-  // 8*(e>>2) + 4*(lane>>5), ci = ci0 + wn*32 + (lane&31)
+  long long* dbg = LAB == 7 ? a.dbg + ((long long)blockIdx.x * 4 + wave) * 8 : nullptr;
+  // LAB 7: wall clock when this block leaves (after its tree work)
+  auto lab_end = [&]() {
+    if constexpr (LAB == 7)
+      if (lane == 0) dbg[7] = wall_clock64();
+  };
   const int h = lane >> 5, r32 = lane & 31;
   const long long NT9 = 9LL * a.Cin;
-  const int ci = ci0 + wn * 32 + r32;
-  if (a.levels == 0) {  // one split: straight into dW
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int co = co0 + wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const long long idx = (long long)co * NT9 + (long long)t * a.Cin + ci;
-        if (!a.w || fabsf(a.w[idx]) <= a.clip) a.dw[idx] += acc[t][e];
-      }
-    return;
-  }
   const long long DWN = (long long)a.Cout * NT9;
-  {
+  const int ci = ci0 + wn * 32 + r32;
+
+  // The main loop and the partial-tile stores, per member M of the wave's
+  // schedule (a wave-uniform branch around all of it, so each path keeps its
+  // own accumulators in registers: no copies at the join):
+  //   SPLIT: M = 0 (waves 0, 1) / 1 (waves 2, 3) of the ci half wn; a wave
+  //     covers both co halves (64 x 32) on taps 0-3 (M 0) or 5-8 (M 1) of
+  //     every K-step and tap 4 of K-steps 0-3 (M 0) or 4-6 (M 1): 32 / 31
+  //     (K-step, tap) units of two MFMAs that share one S fragment; the two
+  //     tap-4 partials are combined through LDS in a fixed order.
+  //   else:  M = 2, the 32 x 32 tile (wm, wn) on all 9 taps.
+  // Returns false if the block is done (no tree work).
+  auto body = [&](auto mc) -> bool {
+    constexpr int M = decltype(mc)::value;
+    constexpr int NH = M < 2 ? 2 : 1;      // co halves per wave
+    constexpr int NT = M < 2 ? 5 : 9;      // taps held
+    constexpr int NU = wr_units(M);        // units per step
+    f32x16 acc[NH][NT];
+#pragma unroll
+    for (int hh = 0; hh < NH; ++hh)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[hh][t][e] = 0.f;
+
+    long long t_wait = 0, t_issue = 0, t_mma = 0, t_prev = 0, t_start = 0;
+    if constexpr (LAB == 7) {
+      t_prev = clock64();
+      t_start = wall_clock64();
+    }
+    // slot of step j: (j - j0 + FP4) % 3 (OP_FP4: a prologue slot holds the
+    // window of step j0, each later slot dY(j) + the window of step j + 1)
+    if constexpr (FP4) {
+      issue(-1, j0, 0);
+      issue(j0, j0 + 1, 1);
+      issue(j0 + 1, j0 + 2, 2);
+      wait_vmcnt<2 * NI>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) expand_write(j0 & 1, c, expand_read(0, c));
+    } else {
+      issue(j0, j0, 0);
+      issue(j0 + 1, j0 + 1, 1);
+    }
+    for (int j = j0; j < j1; ++j) {
+      const int slot = (j - j0 + (FP4 ? 1 : 0)) % WR_NSLOT;
+      if constexpr (LAB == 7) {
+        const long long t = clock64();
+        t_mma += t - t_prev;
+        t_prev = t;
+      }
+      wait_vmcnt<NI>();  // step j landed (this wave's pieces); j + 1 in flight
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if constexpr (LAB == 7) {
+        const long long t = clock64();
+        t_wait += t - t_prev;
+        t_prev = t;
+      }
+      // step j + 2 into the slot step j - 1 used (every wave is past it)
+      const Stage nx = prep(j + 2, j + 2 + (FP4 ? 1 : 0), (j + 2 - j0 + (FP4 ? 1 : 0)) % WR_NSLOT);
+      if constexpr (!spread || !do_mma) {
+#pragma unroll
+        for (int k = 0; k < NI; ++k) piece(nx, k);
+      }
+      if constexpr (LAB == 7) {
+        const long long t = clock64();
+        t_issue += t - t_prev;
+        t_prev = t;
+      }
+      if constexpr (!do_mma) continue;
+      const int base = slot * G::SLOT;
+      const int sbase = FP4 ? G::SBF + (j & 1) * G::SBYTES : base + G::DBYTES;
+      // OP_FP4: the window of step j + 1 is expanded for the next iteration
+      // (unconditionally: after the last step it fills a buffer nobody reads).
+      // Each S fragment is read FD units ahead into a small rotating buffer
+      // (one wave per SIMD: only this lookahead hides the LDS latency; few
+      // registers, so the accumulators never leave their registers).
+      constexpr int NB = FD + 1;
+      uint4 fb[NB], fa[3][NH];
+      uint32_t xv[2] = {0u, 0u};
+      auto read_b = [&](int n) {
+        const int kk = wr_unit_kk(M, n), t = wr_unit_tap(M, n), kh = t / 3, kw = t % 3;
+        if constexpr (!lab_reads) {
+          fb[n % NB] = make_uint4(n, kk, t, lane);
+          return;
+        }
+        int o[2];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          const int q0 = kk * 16 + 4 * hf;
+          // lanes p0 = 0 .. 11 of this K-step in one image row: a constant offset
+          const bool one_row = q0 / W == (q0 + 11) / W;
+          o[hf] = (one_row ? sbase + offS0 : sbase + xS[kk][hf]) + (q0 + 2 * (q0 / W)) * 64 +
+                  kh * RB + kw * 64;
+        }
+        fb[n % NB] = tr_read2(smem, o[0], o[1]);
+      };
+      auto read_a = [&](int kk) {
+#pragma unroll
+        for (int hh = 0; hh < NH; ++hh) {
+          const int aD = base + (M < 2 ? hh * G::DPLANE + offDp : offD) + kk * 1024;
+          fa[kk % 3][hh] = tr_read2(smem, aD, aD + 256);
+        }
+      };
+      // (a unit whose K-step differs from its predecessor's reads that K-step's dY)
+      auto first_of_kk = [](int n) { return n == 0 || wr_unit_kk(M, n) != wr_unit_kk(M, n - 1); };
+#pragma unroll
+      for (int n = 0; n < FD; ++n) {
+        if (first_of_kk(n)) read_a(wr_unit_kk(M, n));
+        read_b(n);
+      }
+      // FP4 expansion chunks spread over the units: chunk c read at unit
+      // c * XS, converted and stored XS / 2 units later
+      constexpr int XS = NU / CPT >= 2 ? NU / CPT : 2;
+#pragma unroll
+      for (int n = 0; n < NU; ++n) {
+        if constexpr (spread && do_mma) {
+          // DMA piece k at unit k * NU / NI
+#pragma unroll
+          for (int k = 0; k < NI; ++k)
+            if (n == k * NU / NI) piece(nx, k);
+        }
+        if (n + FD < NU) {
+          if (first_of_kk(n + FD)) read_a(wr_unit_kk(M, n + FD));
+          read_b(n + FD);
+        }
+        if constexpr (FP4) {
+          if (n % XS == 0 && n / XS < CPT) xv[(n / XS) & 1] = expand_read(slot, n / XS);
+          if (n % XS == XS / 2 && n / XS < CPT) expand_write((j + 1) & 1, n / XS, xv[(n / XS) & 1]);
+        }
+        uint4 b = fb[n % NB];
+        if constexpr (SIGN) {
+          b.x = sign_bf16x2(b.x, ones);
+          b.y = sign_bf16x2(b.y, ones);
+          b.z = sign_bf16x2(b.z, ones);
+          b.w = sign_bf16x2(b.w, ones);
+        }
+        const int kk = wr_unit_kk(M, n), ti = wr_tap_slot(M, wr_unit_tap(M, n));
+        if constexpr (lab_mfma) {
+#pragma unroll
+          for (int hh = 0; hh < NH; ++hh) acc[hh][ti] = mfma_bf16(fa[kk % 3][hh], b, acc[hh][ti]);
+        } else {
+          asm volatile("" ::"v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w));
+        }
+        // keep the issue order: reads FD units ahead (the scheduler would
+        // otherwise sink them next to their MFMA and expose the LDS latency)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (FP4) {
+        // chunks beyond the units' slots: finish them here
+#pragma unroll
+        for (int c = (NU + XS - 1) / XS; c < CPT; ++c)
+          expand_write((j + 1) & 1, c, expand_read(slot, c));
+      }
+    }
+
+    wait_vmcnt<0>();  // the DMA issued past the last step (its LDS is reused below)
+    if constexpr (LAB == 7) {
+      t_mma += clock64() - t_prev;
+      if (lane == 0) {
+        dbg[0] = t_wait;
+        dbg[1] = t_issue;
+        dbg[2] = t_mma;
+        dbg[3] = j1 - j0;
+        dbg[4] = t_start;
+        dbg[5] = wall_clock64();
+        dbg[6] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID
+      }
+    }
+    if constexpr (M < 2) {
+      // tap 4: member 1 hands its partial to member 0 through LDS (fixed
+      // order: member 0's + member 1's); 8 KB per wave
+      float4* cb = reinterpret_cast<float4*>(smem);
+      __syncthreads();  // every wave is past its last LDS read of the loop
+      if constexpr (M == 1) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            cb[((wn * 2 + hh) * 4 + q) * 64 + lane] =
+                make_float4(acc[hh][0][4 * q], acc[hh][0][4 * q + 1], acc[hh][0][4 * q + 2],
+                            acc[hh][0][4 * q + 3]);
+      }
+      __syncthreads();
+      if constexpr (M == 0) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 v = cb[((wn * 2 + hh) * 4 + q) * 64 + lane];
+            acc[hh][4][4 * q] += v.x;
+            acc[hh][4][4 * q + 1] += v.y;
+            acc[hh][4][4 * q + 2] += v.z;
+            acc[hh][4][4 * q + 3] += v.w;
+          }
+      }
+    }
+    // ---- this wave's final partial taps: D[co][ci] of tap t: co = co0 + 32*cw
+    // + (e&3) + 8*(e>>2) + 4*(lane>>5) with cw = hh (SPLIT) or wm, ci = ci0 +
+    // wn*32 + (lane&31).  Member 1's tap 4 went to member 0.
+    constexpr int TLO = M == 1 ? 1 : 0;
+    if (a.levels == 0) {  // one split: straight into dW
+#pragma unroll
+      for (int hh = 0; hh < NH; ++hh)
+#pragma unroll
+        for (int ti = TLO; ti < NT; ++ti)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int t = wr_slot_tap(M, ti);
+            const int co = co0 + (M < 2 ? hh : wm) * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const long long idx = (long long)co * NT9 + (long long)t * a.Cin + ci;
+            if (!a.w || fabsf(a.w[idx]) <= a.clip) a.dw[idx] += acc[hh][ti][e];
+          }
+      return false;
+    }
+    // Partial tiles cross XCDs (each has its own L2): slab stores and loads
+    // are agent-scope (sc1: written through to, and read from, the coherent
+    // level), so publishing needs only the stores' completion before the
+    // counter atomic -- no agent-scope release / acquire fence, which writes
+    // back / invalidates the WHOLE L2 of the XCD (buffer_wbl2 / buffer_inv)
+    // and, with 32 blocks per XCD arriving together, serialised into ~180 us
+    // at b1536.
     float* sl = a.slab + a.slab_off[0] + (long long)split * DWN;
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+    for (int hh = 0; hh < NH; ++hh)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int co = co0 + wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        sl[(long long)co * NT9 + (long long)t * a.Cin + ci] = acc[t][e];
-      }
+      for (int ti = TLO; ti < NT; ++ti)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int t = wr_slot_tap(M, ti);
+          const int co = co0 + (M < 2 ? hh : wm) * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          __hip_atomic_store(sl + (long long)co * NT9 + (long long)t * a.Cin + ci, acc[hh][ti][e],
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    return true;
+  };
+  bool more;
+  if constexpr (SPLIT) {
+    if (wave < 2)
+      more = body(std::integral_constant<int, 0>{});
+    else
+      more = body(std::integral_constant<int, 1>{});
+  } else {
+    more = body(std::integral_constant<int, 2>{});
+  }
+  if (!more) {
+    lab_end();
+    return;
   }
 
   // ---- fixed-order tree over the splits of this tile
@@ -354,75 +589,88 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
     const int parent = node / WR_G;
     const int first = parent * WR_G;
     const int nchild = min(WR_G, a.nodes[l - 1] - first);
-    // publish this block's slab: every wave's stores done, one agent release
+    // publish this block's slab: every wave's (write-through) stores complete
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       int* c = a.cnt + a.cnt_off[l] + tile * a.nodes[l] + parent;
       const int t = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = t == nchild - 1;
-      if (last) {
-        __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
       *flag = last;
     }
     __syncthreads();
-    if (!*flag) return;
+    if (!*flag) {
+      lab_end();
+      return;
+    }
     node = parent;
-    // sum the children in index order; this tile's 64 x 9 x 64 floats as
-    // 9216 float4, 36 per thread, in 3 chunks of 12
+    // sum the children in index order.  This tile's 64 x 9 x 64 floats are
+    // 9216 float4, 36 per thread, taken 4 at a time from all 8 children at
+    // once (32 loads in flight per thread: the reducer is latency-bound
+    // otherwise).  Missing children (the last group) re-read the group's last
+    // child and are dropped by a select, not a branch around the load.
     const float* src = a.slab + a.slab_off[l - 1];
     const bool root = l == a.levels;
     float* dst = root ? a.dw : a.slab + a.slab_off[l] + (long long)node * DWN;
-    for (int i0 = 0; i0 < 36; i0 += 12) {
-      int idx[12];
+    __amdgpu_buffer_rsrc_t rs[WR_G];
 #pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        const int e = (i0 + i) * WR_NT + tid;
+    for (int c = 0; c < WR_G; ++c)
+      rs[c] = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(src + (long long)(first + min(c, nchild - 1)) * DWN), (short)0,
+          (int)(DWN * 4), 0x00020000);
+    for (int i0 = 0; i0 < 36; i0 += 4) {
+      int idx[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = (i0 + u) * WR_NT + tid;
         const int co = e / 144, rem = e - co * 144;
-        idx[i] = ((co0 + co) * 9 + (rem >> 4)) * a.Cin + ci0 + (rem & 15) * 4;
+        idx[u] = ((co0 + co) * 9 + (rem >> 4)) * a.Cin + ci0 + (rem & 15) * 4;
       }
-      float4 s[12];
+      float4 v[4][WR_G];
 #pragma unroll
-      for (int i = 0; i < 12; ++i) s[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int c = 0; c < nchild; ++c) {
-        const float* cs = src + (long long)(first + c) * DWN;
+      for (int c = 0; c < WR_G; ++c)
 #pragma unroll
-        for (int i = 0; i < 12; ++i) {
-          const float4 v = *reinterpret_cast<const float4*>(cs + idx[i]);
-          s[i].x += v.x;
-          s[i].y += v.y;
-          s[i].z += v.z;
-          s[i].w += v.w;
+        for (int u = 0; u < 4; ++u)
+          v[u][c] = __builtin_bit_cast(
+              float4, __builtin_amdgcn_raw_buffer_load_b128(rs[c], idx[u] * 4, 0, WR_SC1));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float4 t = v[u][0];
+#pragma unroll
+        for (int c = 1; c < WR_G; ++c) {
+          const bool in = c < nchild;
+          t.x += in ? v[u][c].x : 0.f;
+          t.y += in ? v[u][c].y : 0.f;
+          t.z += in ? v[u][c].z : 0.f;
+          t.w += in ? v[u][c].w : 0.f;
         }
-      }
-#pragma unroll
-      for (int i = 0; i < 12; ++i) {
         if (root) {
-          float4 d = *reinterpret_cast<float4*>(dst + idx[i]);
+          float4 d = *reinterpret_cast<float4*>(dst + idx[u]);
           if (a.w) {
-            const float4 wv = *reinterpret_cast<const float4*>(a.w + idx[i]);
-            d.x += fabsf(wv.x) <= a.clip ? s[i].x : 0.f;
-            d.y += fabsf(wv.y) <= a.clip ? s[i].y : 0.f;
-            d.z += fabsf(wv.z) <= a.clip ? s[i].z : 0.f;
-            d.w += fabsf(wv.w) <= a.clip ? s[i].w : 0.f;
+            const float4 wv = *reinterpret_cast<const float4*>(a.w + idx[u]);
+            d.x += fabsf(wv.x) <= a.clip ? t.x : 0.f;
+            d.y += fabsf(wv.y) <= a.clip ? t.y : 0.f;
+            d.z += fabsf(wv.z) <= a.clip ? t.z : 0.f;
+            d.w += fabsf(wv.w) <= a.clip ? t.w : 0.f;
           } else {
-            d.x += s[i].x;
-            d.y += s[i].y;
-            d.z += s[i].z;
-            d.w += s[i].w;
+            d.x += t.x;
+            d.y += t.y;
+            d.z += t.z;
+            d.w += t.w;
           }
-          *reinterpret_cast<float4*>(dst + idx[i]) = d;
+          *reinterpret_cast<float4*>(dst + idx[u]) = d;
         } else {
-          *reinterpret_cast<float4*>(dst + idx[i]) = s[i];
+          float* o = dst + idx[u];
+          __hip_atomic_store(o + 0, t.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(o + 1, t.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(o + 2, t.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(o + 3, t.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     }
   }
+  lab_end();
 }
 
 int g_wr_lab = 0;  // zk_wgrad_rows_lab
@@ -478,18 +726,19 @@ bool wr_plan(int B, int H, int W, int Cin, int Cout, int target_blocks, WrPlan& 
   return true;
 }
 
-template <int W, bool SIGN, int LAB = 0, int FD = 6>
+template <int W, int OP, bool SPLIT = true, int LAB = 0, int FD = 0>
 hipError_t wr_launch(const WrArgs& a, unsigned grid, hipStream_t st) {
+  constexpr int lds = WrGeo<W, OP>::LDS;
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)wgrad_rows_kernel<W, SIGN, LAB, FD>,
+    const hipError_t e = hipFuncSetAttribute((const void*)wgrad_rows_kernel<W, OP, SPLIT, LAB, FD>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             WrGeo<W>::LDS);
+                                             lds);
     if (e != hipSuccess) return e;
     attr = true;
   }
   (void)hipGetLastError();
-  hipLaunchKernelGGL((wgrad_rows_kernel<W, SIGN, LAB, FD>), dim3(grid), dim3(WR_NT), WrGeo<W>::LDS,
+  hipLaunchKernelGGL((wgrad_rows_kernel<W, OP, SPLIT, LAB, FD>), dim3(grid), dim3(WR_NT), lds,
                      st, a);
   return hipGetLastError();
 }
@@ -499,7 +748,8 @@ hipError_t wr_launch(const WrArgs& a, unsigned grid, hipStream_t st) {
 // Ablation switch of the lab (tools/wgrad_lab.py): 0 normal, 1 loads only,
 // 2 compute only, 3 compute only without the MFMAs (LDS reads only), 4
 // compute only without the S fragment reads (results are garbage in 1-4),
-// 5 / 6 lookahead 3 / 7, 7 cycle accounting into dbg ([blocks][4 waves][4]).
+// 5 the 32 x 32 wave tiles (no SPLIT), 6 lookahead 4, 7 cycle accounting
+// into dbg ([blocks][4 waves][8]), 8 the step's DMA issued in one burst.
 ZK_EXPORT int zk_wgrad_rows_lab(int mode, void* dbg) {
   g_wr_lab = mode;
   g_wr_dbg = (long long*)dbg;
@@ -519,20 +769,25 @@ ZK_EXPORT int zk_wgrad_rows_plan(int B, int H, int W, int Cin, int Cout, int tar
 }
 
 // dw [Cout][3][3][Cin] fp32 += mask(|w| <= clip) * (3x3 stride-1 'same'
-// weight gradient of dy [B][H][W][Cout] against sx [B][H][W][Cin]).
-//   sign_act = 0: sx is the bf16 +-1 image; padding reads +1 (pad_ones) or 0;
-//   sign_act = 1: sx is the bf16 activation, sign taken in registers; needs
-//                 pad_ones (the padding, a zero, becomes +1).
+// weight gradient of dy [B][H][W][Cout] against the operand sx), by operand
+// mode op:
+//   0: sx is a bf16 image (the +-1 sign image, or a float activation);
+//      padding reads +1 (pad_ones) or 0;
+//   1: sx is the bf16 activation, sign taken in registers; needs pad_ones
+//      (the padding, a zero, becomes +1);
+//   2: sx is the e2m1 (FP4) +-1 sign image [B][H][W][Cin/2 bytes] (channel
+//      2j in the low nibble of byte j, zk_sign_pack's layout); padding +1
+//      (pad_ones) or 0.
 // w null: no kernel STE mask.  slab / cnt: zk_wgrad_rows_plan's bytes;
 // cnt must be zero before the first launch and is left zero by every launch
 // (one counter buffer per stream: launches on one stream never overlap).
 ZK_EXPORT int zk_wgrad_rows(const void* dy, const void* sx, const void* w, void* dw, void* slab,
                             long long slab_bytes, void* cnt, long long cnt_bytes, int B, int H,
-                            int W, int Cin, int Cout, int pad_ones, int sign_act, float clip,
+                            int W, int Cin, int Cout, int pad_ones, int op, float clip,
                             int target_blocks, hipStream_t st) {
   WrPlan p;
   if (!wr_plan(B, H, W, Cin, Cout, target_blocks, p)) return (int)hipErrorInvalidValue;
-  if (sign_act && !pad_ones) return (int)hipErrorInvalidValue;
+  if (op < OP_IMG || op > OP_FP4 || (op == OP_SIGN && !pad_ones)) return (int)hipErrorInvalidValue;
   if (p.levels > 0 && (!slab || !cnt || slab_bytes < p.slab_floats * 4 ||
                        cnt_bytes < p.cnt_ints * 4))
     return (int)hipErrorInvalidValue;
@@ -564,18 +819,29 @@ ZK_EXPORT int zk_wgrad_rows(const void* dy, const void* sx, const void* w, void*
   }
   const unsigned grid = (unsigned)(p.tiles * p.splits);
   a.dbg = g_wr_dbg;
-  if (g_wr_lab && W == 56 && sign_act) {  // lab ablations (tools/wgrad_lab.py)
+  if (g_wr_lab && W == 56 && op == OP_SIGN) {  // lab ablations (tools/wgrad_lab.py)
     switch (g_wr_lab) {
-      case 1: return (int)wr_launch<56, true, 1>(a, grid, st);
-      case 2: return (int)wr_launch<56, true, 2>(a, grid, st);
-      case 3: return (int)wr_launch<56, true, 3>(a, grid, st);
-      case 4: return (int)wr_launch<56, true, 4>(a, grid, st);
-      case 5: return (int)wr_launch<56, true, 0, 3>(a, grid, st);
-      case 6: return (int)wr_launch<56, true, 0, 7>(a, grid, st);
-      case 7: return (int)wr_launch<56, true, 7>(a, grid, st);
+      case 1: return (int)wr_launch<56, OP_SIGN, true, 1>(a, grid, st);
+      case 2: return (int)wr_launch<56, OP_SIGN, true, 2>(a, grid, st);
+      case 3: return (int)wr_launch<56, OP_SIGN, true, 3>(a, grid, st);
+      case 4: return (int)wr_launch<56, OP_SIGN, true, 4>(a, grid, st);
+      case 5: return (int)wr_launch<56, OP_SIGN, false>(a, grid, st);
+      case 6: return (int)wr_launch<56, OP_SIGN, true, 0, 4>(a, grid, st);
+      case 7: return (int)wr_launch<56, OP_SIGN, true, 7>(a, grid, st);
+      case 8: return (int)wr_launch<56, OP_SIGN, true, 8>(a, grid, st);
       default: return (int)hipErrorInvalidValue;
     }
   }
-  if (W == 56) return (int)(sign_act ? wr_launch<56, true>(a, grid, st) : wr_launch<56, false>(a, grid, st));
-  return (int)(sign_act ? wr_launch<28, true>(a, grid, st) : wr_launch<28, false>(a, grid, st));
+  if (g_wr_lab == 7 && W == 56) {
+    if (op == OP_IMG) return (int)wr_launch<56, OP_IMG, true, 7>(a, grid, st);
+    return (int)wr_launch<56, OP_FP4, true, 7>(a, grid, st);
+  }
+  switch (op * 2 + (W == 56)) {
+    case OP_IMG * 2 + 1: return (int)wr_launch<56, OP_IMG>(a, grid, st);
+    case OP_SIGN * 2 + 1: return (int)wr_launch<56, OP_SIGN>(a, grid, st);
+    case OP_FP4 * 2 + 1: return (int)wr_launch<56, OP_FP4>(a, grid, st);
+    case OP_IMG * 2: return (int)wr_launch<28, OP_IMG>(a, grid, st);
+    case OP_SIGN * 2: return (int)wr_launch<28, OP_SIGN>(a, grid, st);
+    default: return (int)wr_launch<28, OP_FP4>(a, grid, st);
+  }
 }

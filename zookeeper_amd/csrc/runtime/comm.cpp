@@ -39,6 +39,7 @@ typedef Result (*AllReduceFn)(const void*, void*, size_t, int, int, Comm, void*)
 typedef Result (*BroadcastFn)(const void*, void*, size_t, int, int, Comm, void*);
 typedef Result (*GroupFn)();
 typedef const char* (*ErrStrFn)(Result);
+typedef Result (*AsyncErrFn)(Comm, Result*);
 
 struct Api {
   void* lib = nullptr;
@@ -52,6 +53,7 @@ struct Api {
   GroupFn group_start = nullptr;
   GroupFn group_end = nullptr;
   ErrStrFn err_str = nullptr;
+  AsyncErrFn async_error = nullptr;  // optional (ncclCommGetAsyncError)
 };
 
 Api g_api;
@@ -85,6 +87,7 @@ ZK_EXPORT int zk_comm_load(const char* path) {
             resolve(lib, "ncclGroupEnd", a.group_end) &&
             resolve(lib, "ncclGetErrorString", a.err_str);
   if (!ok) return 2;
+  resolve(lib, "ncclCommGetAsyncError", a.async_error);  // optional
   g_api = a;
   return 0;
 }
@@ -140,6 +143,18 @@ ZK_EXPORT int zk_comm_broadcast(void* comm, const void* send, void* recv, int64_
 // Several collectives fused into one launch group (ncclGroupStart/End).
 ZK_EXPORT int zk_comm_group_start() { return g_api.lib ? g_api.group_start() : -1; }
 ZK_EXPORT int zk_comm_group_end() { return g_api.lib ? g_api.group_end() : -1; }
+
+// Asynchronous error state of a communicator (ncclCommGetAsyncError): *err
+// receives the RCCL result of the failed background operation, 0 if none.
+// Returns -1 if RCCL is not loaded, -2 if this RCCL lacks the entry point.
+ZK_EXPORT int zk_comm_async_error(void* comm, int* err) {
+  if (!g_api.lib || !comm || !err) return -1;
+  if (!g_api.async_error) return -2;
+  Result e = 0;
+  const Result r = g_api.async_error(comm, &e);
+  *err = e;
+  return r;
+}
 
 // abort = 1: ncclCommAbort (a peer failed; do not wait for it).
 ZK_EXPORT int zk_comm_destroy(void* comm, int abort) {

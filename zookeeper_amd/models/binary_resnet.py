@@ -67,6 +67,9 @@ class BinaryResBlock(nn.Module):
         self.conv = QuantConv2d(cin, cout, 3, stride, "same", "ste_sign", "ste_sign",
                                 "weight_clip", pad_values=pad_value)
         self.bn = BatchNorm(cout, momentum=momentum, eps=eps)
+        # the next block's conv: reads this block's output sign images (set
+        # by the model; decides whether the bf16 one is needed)
+        self.sign_consumer = None
         self.downsample = None
         if cin != cout:
             self.downsample = nn.Sequential(
@@ -94,7 +97,8 @@ class BinaryResBlock(nn.Module):
                     residual = self.downsample(x)
             else:
                 residual = x
-            return ops.binary_block(x, residual, self.conv, self.bn, dx_handoff=handoff)
+            return ops.binary_block(x, residual, self.conv, self.bn, dx_handoff=handoff,
+                                    sign_consumer=self.sign_consumer)
         residual = self.downsample(x) if self.downsample is not None else x
         return self.bn(self.conv(x)) + residual
 
@@ -129,6 +133,10 @@ class BinaryResNetE(nn.Module):
                 stride = 1 if stage == 0 or i != 0 else 2
                 body.append(BinaryResBlock(cin, f, stride, backend=backend))
                 cin = f
+        # (plain attributes, not submodules: no duplicate parameters / state keys)
+        for blk, nxt in zip(body, body[1:]):
+            object.__setattr__(blk, "sign_consumer", nxt.conv)
+        object.__setattr__(self.stem, "sign_consumer", body[0].conv)
         self.body = nn.Sequential(*body)
         self.pool = GlobalAvgPool()
         self.fc = nn.Linear(cin, num_classes)

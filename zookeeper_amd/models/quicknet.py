@@ -53,13 +53,17 @@ class QuickNetBlock(nn.Module):
         self.conv = _Clip125Conv(channels)
         self.bn = BatchNorm(channels, momentum=0.9, eps=1e-5)
         self.backend = backend
+        # the next block's conv when it reads this output's sign images
+        # (set by the model; ops.binary.bf16_sign_needed)
+        self.sign_consumer = None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.backend == "hip" and x.is_cuda:
             from zookeeper_amd import ops
 
             return ops.binary_block(x, x, self.conv, self.bn, act="relu",
-                                    clip_value=1.25, pad_value=1.0)
+                                    clip_value=1.25, pad_value=1.0,
+                                    sign_consumer=self.sign_consumer)
         return self.bn(F.relu(self.conv(x))) + x
 
 
@@ -123,6 +127,10 @@ class QuickNetModule(nn.Module):
                     body.append(Transition(cin, f))
                     cin = f
                 body.append(QuickNetBlock(cin, backend))
+        # consumer links (plain attributes, not submodules)
+        for blk, nxt in zip(body, body[1:]):
+            if isinstance(blk, QuickNetBlock) and isinstance(nxt, QuickNetBlock):
+                object.__setattr__(blk, "sign_consumer", nxt.conv)
         self.body = nn.Sequential(*body)
         self.pool = GlobalAvgPool()
         self.fc = nn.Linear(cin, num_classes)

@@ -470,6 +470,8 @@ class ImageStem(nn.Sequential):
     """
 
     sign_clip: Optional[float] = None
+    # ... and that block's conv (decides whether a bf16 sign image is needed)
+    sign_consumer = None
 
     def _fusable(self, x: torch.Tensor) -> bool:
         if not _use_native(x) or len(self) not in (3, 4):
@@ -498,5 +500,5 @@ class ImageStem(nn.Sequential):
             pool = self[2]
             return fused_stem(x, self[0], self[1], _pair(pool.pool_size)[0],
                               _pair(pool.stride)[0], self[3] if len(self) == 4 else None,
-                              sign_clip=self.sign_clip)
+                              sign_clip=self.sign_clip, sign_consumer=self.sign_consumer)
         return super().forward(x)

@@ -199,9 +199,12 @@ def wgrad_rows_ok(geom) -> bool:
     return lib().zk_wgrad_rows_plan(B, H, W, Cin, Cout, 0, None, None) == 0
 
 
+_WGRAD_OPERANDS = {"image": 0, "sign": 1, "fp4": 2}
+
+
 def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Tensor,
                 geom, pad_ones: int, clip: float, stream: int, what: str = "zk_igemm_wgrad",
-                variant: int = -1, sign_act: bool = False) -> None:
+                variant: int = -1, operand: str = "image") -> None:
     """Implicit-GEMM weight gradient ``dw += mask(|w| <= clip) * dyᵀ ⊛ x``.
 
     * 3x3 stride-1 layers the row-streaming kernel takes (``wgrad_rows_ok``):
@@ -210,12 +213,18 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Te
     * otherwise ``zk_igemm_wgrad``: per-split slabs (plain stores) summed in a
       fixed order by ``wgrad_reduce_kernel``.
 
-    Both are bit-reproducible.  ``sign_act``: ``x`` is the bf16 activation
-    and the kernel takes its sign (``zk_wgrad_rows`` only; needs pad_ones).
+    Both are bit-reproducible.  ``operand``: ``"image"`` (``x`` is a bf16
+    image: the +-1 sign image or a float activation), ``"sign"`` (``x`` is
+    the bf16 activation and the kernel takes its sign; needs pad_ones) or
+    ``"fp4"`` (``x`` is the e2m1 sign image [B][H][W][Cin/2]); the last two
+    only on ``zk_wgrad_rows``.
     ``geom`` = (B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl)."""
     L = lib()
     B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl = geom
-    if variant < 0 and wgrad_rows_ok(geom) and (pad_ones or not sign_act):
+    op = _WGRAD_OPERANDS.get(operand)
+    if op is None:
+        raise ValueError(f"{what}: unknown operand {operand!r}")
+    if variant < 0 and wgrad_rows_ok(geom) and (pad_ones or op != 1):
         sb, cb = ctypes.c_int64(0), ctypes.c_int64(0)
         check(L.zk_wgrad_rows_plan(B, H, W, Cin, Cout, 0, ctypes.byref(sb), ctypes.byref(cb)),
               what + " (plan)")
@@ -225,11 +234,11 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Te
         check(L.zk_wgrad_rows(dy.data_ptr(), x.data_ptr(), w.data_ptr() if w is not None else None,
                               dw.data_ptr(), slab.data_ptr() if slab is not None else None,
                               sb.value, cnt.data_ptr() if cnt is not None else None, cb.value,
-                              B, H, W, Cin, Cout, int(pad_ones), int(sign_act), float(clip), 0,
+                              B, H, W, Cin, Cout, int(pad_ones), op, float(clip), 0,
                               stream), what)
         return
-    if sign_act:
-        raise ValueError(f"{what}: the sign-of-activation operand needs zk_wgrad_rows")
+    if op:
+        raise ValueError(f"{what}: the {operand!r} operand needs zk_wgrad_rows")
     ws, ws_bytes = None, 0
     ws_bytes = max(int(L.zk_igemm_wgrad_ws_bytes(B, Cin, H, W, Ho, Wo, Cout, kh, kw, s, pt,
                                                  pl, 0, variant)), 0)

@@ -31,6 +31,7 @@ SIGNATURES = {
     "zk_comm_group_start": (I32, []),
     "zk_comm_group_end": (I32, []),
     "zk_comm_destroy": (I32, [P, I32]),
+    "zk_comm_async_error": (I32, [P, IP]),
     # preprocessing
     "zk_normalize_flip_c3": (I32, [P, P, I32, I32, I32, FP, FP, I32, U64, P]),
     # binary convolution

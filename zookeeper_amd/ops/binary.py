@@ -24,8 +24,10 @@ the input STE mask and the identity-residual gradient fused into its
 epilogue) and ``zk_igemm_wgrad`` (dyᵀ ⊛ sx, kernel STE mask in the
 epilogue, split-K fp32 atomics straight into the flat gradient buffer).
 
-Saved for backward: the STE mask bits, the sign image, the int16 conv
-output and per-channel vectors — no bf16 copy of the real-valued input.
+Saved for backward: the STE mask bits, the sign image (the e2m1 one when
+the weight gradient reads it: ``wgrad_reads_fp4``, then no bf16 sign image is
+written at all), the int16 conv output and per-channel vectors — no bf16
+copy of the real-valued input.
 """
 
 from __future__ import annotations
@@ -38,7 +40,7 @@ from zookeeper_amd.nn.layers import same_padding
 from zookeeper_amd.ops import streams
 from zookeeper_amd.ops.options import OPTS
 from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, igemm_wgrad, lib,
-                                        stream_ptr, zeroed_scratch)
+                                        stream_ptr, wgrad_rows_ok, zeroed_scratch)
 
 
 # Copies of the forward BN statistics the conv blocks add into (block b into
@@ -68,10 +70,39 @@ def _fp4() -> bool:
     return OPTS.bconv_fp4
 
 
-def bf16_sign_needed() -> bool:
-    """Whether producers of a binary block's input (BN epilogues, the stem)
-    must also write the bf16 +-1 sign image (the weight gradients' operand)."""
-    return True
+def _geom(B, H, W, Cin, Cout, kh, kw, stride):
+    """(B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl) of a 'same' conv."""
+    pt, pb = same_padding(H, kh, stride)
+    pl, pr = same_padding(W, kw, stride)
+    Ho, Wo = (H + pt + pb - kh) // stride + 1, (W + pl + pr - kw) // stride + 1
+    return (B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl)
+
+
+def wgrad_reads_fp4(geom) -> bool:
+    """Whether a binary conv's weight gradient reads the e2m1 sign image the
+    MX-FP4 forward already has (``zk_wgrad_rows`` operand 2, expanded to bf16
+    in LDS) instead of a bf16 +-1 image: FP4 forward, ``runtime.wgrad_fp4``
+    and a layer the row kernel takes (3x3 stride 1, 64 / 128-channel stages)."""
+    B, H, W, Cin, Ho, Wo, Cout = geom[:7]
+    return (OPTS.bconv_fp4 and OPTS.wgrad_fp4 and Cin % 64 == 0 and Cout % 64 == 0
+            and wgrad_rows_ok(geom))
+
+
+def bf16_sign_needed(consumer=None, shape=None) -> bool:
+    """Whether the producer of a binary block's input (a BN epilogue, the
+    stem) must also write the bf16 +-1 sign image, the weight gradient's
+    operand.  ``consumer``: the binary ``QuantConv2d`` that reads the tensor
+    (unknown: needed); ``shape``: the tensor's NHWC shape.  Not needed when
+    that conv's weight gradient reads the e2m1 image (:func:`wgrad_reads_fp4`);
+    a consumer that needs it after all re-quantises its input (correct, one
+    extra pass)."""
+    if consumer is None or shape is None:
+        return True
+    B, H, W, C = shape
+    kh, kw = consumer.kernel_size
+    geom = _geom(B, H, W, C, consumer.weight.shape[0], kh, kw, consumer.stride[0])
+    return not (consumer.padding == "same" and consumer.stride[0] == consumer.stride[1]
+                and wgrad_reads_fp4(geom))
 
 
 class _BnSum:
@@ -128,11 +159,14 @@ class _BinaryBlockFn(torch.autograd.Function):
                 and kh * kw * Cin <= 32767)
         FP4 = _fp4()
         fp4 = mfma and FP4
+        # weight gradient on the e2m1 image (no bf16 sign image at all)
+        wfp4 = fp4 and will_backward and wgrad_reads_fp4(
+            (B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl))
         # The previous block may already have quantised this input in its BN
         # epilogue (zk_bn_apply_sign): reuse its sign images and STE mask.
         cached = getattr(x, "_zk_sign", None)
         sx4 = None
-        need_sx = mfma  # bf16 sign image (wgrad / bf16 fwd)
+        need_sx = mfma and not wfp4  # bf16 sign image (wgrad / bf16 fwd)
         if (mfma and cached is not None and cached[0] == clip
                 and tuple(cached[2].shape) == (B * H * W * Cin // 32,)
                 and (not need_sx or cached[1] is not None)
@@ -214,7 +248,8 @@ class _BinaryBlockFn(torch.autograd.Function):
         out = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=dev)
         if next_sign is not None and Cout % 64 == 0:
             # also quantise the output for the next binary block (same clip)
-            sx_next = torch.empty_like(out) if bf16_sign_needed() else None
+            sx_next = (torch.empty_like(out)
+                       if bf16_sign_needed(side.get("sign_consumer"), (B, Ho, Wo, Cout)) else None)
             mask_next = torch.empty(P * Cout // 32, dtype=torch.int32, device=dev)
             sx4_next = (torch.empty((B, Ho, Wo, Cout // 2), dtype=torch.uint8, device=dev)
                         if FP4 else None)
@@ -253,6 +288,7 @@ class _BinaryBlockFn(torch.autograd.Function):
         ctx.save_for_backward(bits, mask, wt, y, mean, rstd, gamma, w_ohwi, sx, sx4)
         ctx.params = (weight, gamma, beta)
         ctx.geom = (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo)
+        ctx.wfp4 = wfp4
         ctx.meta = meta
         ctx.bn = bn
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
@@ -319,7 +355,8 @@ class _BinaryBlockFn(torch.autograd.Function):
             # then overlaps this block's dgrad and the next block's backward
             w_direct = direct_grad(weight_p, channels_last=True)
             dweight = None
-            sxw = sx  # weight-gradient sign operand
+            # weight-gradient sign operand: the bf16 image, or the e2m1 one
+            sxw, operand = (sx4, "fp4") if ctx.wfp4 else (sx, "image")
             side = streams.active() and w_direct is not None and sxw is not None
             if side:
                 sstream = streams.side_stream(dev)
@@ -328,7 +365,7 @@ class _BinaryBlockFn(torch.autograd.Function):
                 sstream.wait_event(ready)
                 with torch.cuda.stream(sstream):
                     _wgrad(L, dy, sxw, w_ohwi, w_direct.permute(0, 2, 3, 1), ctx,
-                           sstream.cuda_stream)
+                           sstream.cuda_stream, operand)
                     done = torch.cuda.Event()
                     done.record(sstream)
                 streams.keep(dy, sxw, w_ohwi)  # released once the compute stream joins
@@ -336,7 +373,7 @@ class _BinaryBlockFn(torch.autograd.Function):
                 dw = (w_direct.permute(0, 2, 3, 1) if w_direct is not None  # OHWI view
                       else torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev))
                 if sxw is not None:
-                    _wgrad(L, dy, sxw, w_ohwi, dw, ctx, st)
+                    _wgrad(L, dy, sxw, w_ohwi, dw, ctx, st, operand)
                 else:
                     check(L.zk_bconv_wgrad(dy.data_ptr(), bits.data_ptr(), w_ohwi.data_ptr(),
                                            dw.data_ptr(), B, H, W, Cin, Ho, Wo, Cout, kh, kw,
@@ -387,14 +424,15 @@ class _BinaryBlockFn(torch.autograd.Function):
         return dx, dres_out, dweight, dgamma, dbeta, None, None
 
 
-def _wgrad(L, dy, sx, w_ohwi, dw, ctx, st) -> None:
+def _wgrad(L, dy, sx, w_ohwi, dw, ctx, st, operand: str = "image") -> None:
     """Binary-conv weight gradient (dyᵀ ⊛ sign(x), kernel STE mask) added
     into ``dw`` (OHWI fp32) on stream ``st`` (split-K reduction:
-    ``_native.igemm_wgrad``)."""
+    ``_native.igemm_wgrad``); ``sx`` the bf16 sign image, or the e2m1 one
+    with ``operand="fp4"``."""
     (B, Cin, H, W, Cout, kh, kw, stride, pt, pb, pl, pr, Ho, Wo) = ctx.geom
     (_, _, clip, pad_ones) = ctx.meta[:4]
     igemm_wgrad(dy, sx, w_ohwi, dw, (B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl),
-                int(pad_ones), clip, st)
+                int(pad_ones), clip, st, operand=operand)
 
 
 def _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx):
@@ -440,7 +478,7 @@ def _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx):
 def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
                  act: Optional[str] = None, clip_value: float = 1.0,
                  pad_value: float = 0.0, quantize_output: bool = True,
-                 dx_handoff=None) -> torch.Tensor:
+                 dx_handoff=None, sign_consumer=None) -> torch.Tensor:
     """Run ``bn(act(conv(x))) + residual`` with the fused HIP kernels.
 
     ``conv`` must be a binary ``QuantConv2d`` (ste_sign input and kernel,
@@ -453,6 +491,10 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
     (attached to the returned tensor as ``_zk_sign`` = (clip, sx, mask, sx4);
     a block with the same clip value reuses them instead of re-reading its
     input).
+
+    ``sign_consumer``: the binary conv that reads the output's sign images
+    (the next block's); the bf16 sign image is skipped when its weight
+    gradient reads the e2m1 one (:func:`bf16_sign_needed`).
 
     ``dx_handoff`` (an ``ops.norm_pool.ResidualHandoff``): x's gradient is left
     there instead of returned, for x's other consumer whose backward runs
@@ -478,7 +520,8 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
     will_backward = torch.is_grad_enabled() and (
         x.requires_grad or conv.weight.requires_grad or bn.training)
     holder: list = [] if quantize_output else None
-    side = {"pred": getattr(x, "_zk_bnsum", None), "dx_handoff": dx_handoff}
+    side = {"pred": getattr(x, "_zk_bnsum", None), "dx_handoff": dx_handoff,
+            "sign_consumer": sign_consumer}
     meta = (conv.stride[0], act == "relu", float(clip_value), pad_value == 1.0, identity,
             will_backward, holder, side)
     out = _BinaryBlockFn.apply(x, None if identity else residual, conv.weight, bn.weight,

@@ -59,6 +59,10 @@ class KernelOptions:
     # (wgrad_rows.hip: every dY / S row loaded once per block, split-K summed
     # inside the launch by a fixed-order tree; 64 / 128-channel stages).
     wgrad_rows: bool = True
+    # ... reading the e2m1 (FP4) sign image the binary forward already has
+    # (expanded to bf16 in LDS): producers then skip the bf16 sign image of
+    # tensors whose consumer takes this path (bconv_fp4 forward only).
+    wgrad_fp4: bool = True
     # Phased data-gradient kernel (deep_gemm.hip) for the stride-1 3x3
     # binary convs with >= 128 input channels.
     dgrad_deep: bool = True

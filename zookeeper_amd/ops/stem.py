@@ -107,7 +107,7 @@ FUSED_BN2_SUMS = [0]
 class _StemFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, g1, b1, g2, b2, bn1, bn2, pool):
-        pk, ps, sign_clip, holder, bnsum_holder = pool
+        pk, ps, sign_clip, holder, bnsum_holder, sign_consumer = pool
         B, Cin, H, W = x.shape
         Cout, _, KH, KW = weight.shape
         s = 2
@@ -224,7 +224,8 @@ class _StemFn(torch.autograd.Function):
                 # also quantise the output for the first binary block
                 from zookeeper_amd.ops.binary import _fp4, bf16_sign_needed
 
-                sx = torch.empty_like(p) if bf16_sign_needed() else None
+                sx = (torch.empty_like(p)
+                      if bf16_sign_needed(sign_consumer, (B, H2, W2, Cout)) else None)
                 mask = torch.empty(P2 * Cout // 32, dtype=torch.int32, device=dev)
                 sx4 = (torch.empty((B, H2, W2, Cout // 2), dtype=torch.uint8, device=dev)
                        if _fp4() else None)
@@ -367,12 +368,14 @@ class _StemFn(torch.autograd.Function):
 
 
 def fused_stem(x: torch.Tensor, conv, bn1, pool_k: int = 3, pool_s: int = 2, bn2=None,
-               sign_clip: Optional[float] = None):
+               sign_clip: Optional[float] = None, sign_consumer=None):
     """``bn2(maxpool(relu(bn1(conv(x)))))`` with the fused stem kernels.
 
     With ``sign_clip`` (and ``bn2``) the final BN pass also writes the sign
     image and STE mask (|y| <= sign_clip) of the output, attached as
-    ``_zk_sign`` for the first binary block (see ``ops.binary_block``)."""
+    ``_zk_sign`` for the first binary block (see ``ops.binary_block``;
+    ``sign_consumer``: that block's conv, which decides whether the bf16 sign
+    image is needed: ``ops.binary.bf16_sign_needed``)."""
     holder = [] if (sign_clip is not None and bn2 is not None) else None
     # consumer: a binary block; only when a backward will run (grad mode is
     # off inside the autograd function's forward)
@@ -380,7 +383,7 @@ def fused_stem(x: torch.Tensor, conv, bn1, pool_k: int = 3, pool_s: int = 2, bn2
     out = _StemFn.apply(x, conv.weight, bn1.weight, bn1.bias,
                         bn2.weight if bn2 is not None else None,
                         bn2.bias if bn2 is not None else None, bn1, bn2,
-                        (pool_k, pool_s, float(sign_clip or 0.0), holder, bnsum))
+                        (pool_k, pool_s, float(sign_clip or 0.0), holder, bnsum, sign_consumer))
     if holder:
         out._zk_sign = tuple(holder)
     if bnsum:

@@ -59,6 +59,11 @@ from zookeeper_amd.ops import streams as side_streams
 from zookeeper_amd.parallel.flat import FlatParams
 
 
+# buckets smaller than this are folded into the next one (bench JSON: no
+# sub-0.1 MB bucket)
+MIN_BUCKET_BYTES = 256 * 1024
+
+
 class GradBucketer:
     def __init__(self, flat: FlatParams, world: int, bucket_mb: float = 10.0,
                  first_bucket_mb: float = 1.0, group=None, grad_dtype: Optional[torch.dtype] = None,
@@ -91,6 +96,27 @@ class GradBucketer:
             cur_elems += s.numel
         if cur:
             buckets.append(cur)
+        # fold buckets below MIN_BUCKET_BYTES (at most a quarter of the cap)
+        # into their successor: a 4 KB classifier-bias bucket (the head
+        # weight alone exceeds the first-bucket cap) would otherwise cost a
+        # whole collective's latency
+        fold_bytes = min(MIN_BUCKET_BYTES, limit)
+        merged: List[List[int]] = []
+        carry: List[int] = []
+        for bi, b in enumerate(buckets):
+            b = carry + b
+            if (sum(flat.slots[i].numel for i in b) * 4 < fold_bytes
+                    and bi != len(buckets) - 1):
+                carry = b
+                continue
+            carry = []
+            merged.append(b)
+        if carry:
+            if merged:
+                merged[-1] = merged[-1] + carry
+            else:
+                merged.append(carry)
+        buckets = merged
         self.buckets = buckets
         self.ranges = []
         for b in buckets:
@@ -248,6 +274,16 @@ class GradBucketer:
             return (dist.all_reduce(tmp, group=self.group, async_op=True), tmp)
         return (dist.all_reduce(view, group=self.group, async_op=True), None)
 
+    def watch_replay(self) -> None:
+        """After a graph replay that contains the collectives (native
+        communicator): the watchdog follows them through an event on the
+        current stream."""
+        if self.native is not None:
+            self.native.check()
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(self.flat.grad.device))
+            self.native.watch(done, "captured gradient all-reduce (graph replay)")
+
     def launch_all(self) -> None:
         """Issue every bucket not yet launched (after a graph replay, or for
         parameters whose hooks never fired)."""
@@ -262,6 +298,8 @@ class GradBucketer:
         the compute stream wait for every collective."""
         if not self.enabled:
             return
+        if self.native is not None:
+            self.native.check()  # the watchdog found an earlier step's collectives hung
         if self.timing:
             self._events()["bwd_end"].record(torch.cuda.current_stream(self.flat.grad.device))
         self.launch_all()
@@ -281,6 +319,11 @@ class GradBucketer:
                         ev["end"][b] = ev["mk"]()
                         ev["end"][b].record(self.comm_stream)
             torch.cuda.current_stream(self.flat.grad.device).wait_stream(self.comm_stream)
+            if self.native is not None and not torch.cuda.is_current_stream_capturing():
+                # watchdog: this step's collectives must complete within the timeout
+                done = torch.cuda.Event()
+                done.record(self.comm_stream)
+                self.native.watch(done, "bucketed gradient all-reduce")
             if self._sync_finish:
                 torch.cuda.synchronize(self.flat.grad.device)
         if self.timing and self._step_events is not None:
@@ -288,7 +331,7 @@ class GradBucketer:
             self._step_events = None
         self.last_order = list(self._order)
         self._order.clear()
-        if self.check_order:
+        if self.check_order and not (self.cuda and torch.cuda.is_current_stream_capturing()):
             self._compare_order(self.last_order)
         self._works.clear()
         self._pending = [len(b) for b in self.buckets]

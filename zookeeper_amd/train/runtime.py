@@ -43,6 +43,7 @@ class Runtime:
     bn_stats_epilogue: bool = Field(True)
     wgrad_slab_mb: int = Field(32)
     wgrad_rows: bool = Field(True)
+    wgrad_fp4: bool = Field(True)
     dgrad_deep: bool = Field(True)
     wgrad_deep: bool = Field(True)
     weight_images: bool = Field(True)

@@ -66,13 +66,6 @@ class Trainer:
 
             self.flat.images = WeightImages(self.flat)
             self.flat.images.attach()
-        if self.info.world > 1:
-            # One broadcast of the flat parameter buffer + the BN buffers.
-            zdist.broadcast_(self.flat.data)
-            for b in self.model.buffers():
-                zdist.broadcast_(b)
-            if getattr(self.flat, "images", None) is not None:
-                self.flat.images.invalidate()
         # force_dp: the bucketed all-reduce stays on with one rank (a 1-rank
         # RCCL group), so one GPU runs the exact data-parallel code path
         comm = self.info.comm
@@ -82,6 +75,18 @@ class Trainer:
             from zookeeper_amd.parallel.rccl import NativeComm
 
             native = NativeComm(self.info.rank, self.info.world)
+        self.native_comm = native
+        if self.info.world > 1:
+            # One broadcast of the flat parameter buffer + the BN buffers
+            # (through the native communicator when it is the transport: then
+            # the rank holds one RCCL communicator for its collectives)
+            for t in [self.flat.data] + list(self.model.buffers()):
+                if native is not None and t.is_cuda and t.is_contiguous():
+                    native.broadcast_(t, 0)
+                else:
+                    zdist.broadcast_(t)
+            if getattr(self.flat, "images", None) is not None:
+                self.flat.images.invalidate()
         self.bucketer = GradBucketer(self.flat, self.info.world, bucket_mb, first_bucket_mb,
                                      grad_dtype=grad_dtype, timing=comm_timing, force=force_dp,
                                      high_priority=comm.high_priority,
@@ -192,7 +197,9 @@ class Trainer:
             self._static_in[0].copy_(x)
             self._static_in[1].copy_(y)
         self._graph.replay()
-        if not capture_comm:
+        if capture_comm:
+            self.bucketer.watch_replay()  # watchdog over the captured collectives
+        else:
             self.bucketer.finish()  # DP: all buckets all-reduced after the replay
         self.optimizer.step()
         return self._static_out
