@@ -52,6 +52,40 @@ def test_batchnorm_train(C, relu, affine):
         torch.testing.assert_close(bn.bias.grad, ref.bias.grad, atol=5e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("C,relu", [(256, True), (64, False), (2048, True)])
+def test_batchnorm_residual_relu(C, relu):
+    """relu(bn(x) + r) (a bottleneck tail, norm_pool.batch_norm): output and
+    the gradients of x, r and the affine parameters against the fp32 oracle.
+    The backward masks with the 1-bit ReLU mask the forward stored (not the
+    bf16 output)."""
+    from zookeeper_amd.ops import norm_pool
+
+    torch.manual_seed(3)
+    bn = BatchNorm(C, momentum=0.9, eps=1e-5).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    x = _cl(torch.randn(4, C, 6, 5, device="cuda") * 2 + 0.5).to(torch.bfloat16)
+    r = _cl(torch.randn(4, C, 6, 5, device="cuda")).to(torch.bfloat16)
+    g = _cl(torch.randn(4, C, 6, 5, device="cuda")).to(torch.bfloat16)
+    ref = copy.deepcopy(bn).float()
+    xh, rh = x.clone().requires_grad_(True), r.clone().requires_grad_(True)
+    yh = norm_pool.batch_norm(xh, bn, relu=relu, residual=rh)
+    yh.backward(g)
+    xr, rr = x.float().clone().requires_grad_(True), r.float().clone().requires_grad_(True)
+    yr = ref(xr) + rr
+    yr = torch.relu(yr) if relu else yr
+    yr.backward(g.float())
+    torch.testing.assert_close(yh.float(), yr, atol=3e-2, rtol=2e-2)
+    # the mask decides exactly where the bf16 output is positive: compare the
+    # residual gradient where the oracle's output is clearly nonzero
+    live = (yr.abs() > 0.05) | (not relu)
+    torch.testing.assert_close(rh.grad.float()[live], rr.grad[live], atol=1e-2, rtol=1e-2)
+    torch.testing.assert_close(xh.grad.float(), xr.grad, atol=5e-2, rtol=5e-2)
+    torch.testing.assert_close(bn.weight.grad, ref.weight.grad, atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(bn.bias.grad, ref.bias.grad, atol=5e-2, rtol=2e-2)
+
+
 def test_batchnorm_eval_uses_running_stats():
     bn = BatchNorm(32, momentum=0.9, eps=1e-5).cuda()
     with torch.no_grad():

@@ -26,8 +26,8 @@ DGRAD: Dict[int, Tuple[int, int, bool]] = {
     32: (64, 64, True), 33: (128, 32, True), 34: (128, 32, True),
     # row-window kernel (conv3rw.hip): 64 -> 64 only, stride 1
     50: (64, 64, True),
-    # phased 256x256 / 256x128 kernel (deep_gemm.hip): stride 1, Cin % 128 == 0
-    60: (128, 128, True),
+    # phased 256x256 kernel (deep_gemm.hip): Cin % 256 == 0
+    60: (256, 128, True),
     # LDS-staged (coalesced) epilogue variants
     40: (128, 128, False), 41: (128, 64, False), 42: (64, 128, False), 43: (64, 64, False),
     44: (128, 128, False), 45: (256, 128, False), 46: (128, 64, False), 47: (256, 64, False),
@@ -77,7 +77,7 @@ def dgrad_ok(v: int, cin: int, cout: int, stride: int) -> bool:
     if v == 50:
         return stride == 1 and cin == 64 and cout == 64
     if v == 60:
-        return stride <= 2 and cin % 128 == 0 and cout % 64 == 0
+        return stride <= 2 and cin % 256 == 0 and cout % 64 == 0
     if c3 and not conv3_ok(stride):
         return False
     return (2 * cout) % cb == 0 and cin % bn == 0 and stride <= 2

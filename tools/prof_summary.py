@@ -21,6 +21,7 @@ import csv
 FAMILY_RULES = [
     ("stem_", "stem (fused 7x7 conv / BN / pool)"),
     ("wgrad_rows_kernel", "weight gradient (MFMA)"),
+    ("wr_pad_init_kernel", "weight gradient (MFMA)"),
     ("wgrad_deep_kernel", "weight gradient (MFMA)"),
     ("igemm_wgrad", "weight gradient (MFMA)"),
     ("wgrad_reduce", "weight gradient (MFMA)"),

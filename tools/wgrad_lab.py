@@ -182,7 +182,6 @@ def main():
         fns["rows_compute_only"] = lambda: ablate(2)
         fns["rows_lds_reads_only"] = lambda: ablate(3)
         fns["rows_mfma_no_s_reads"] = lambda: ablate(4)
-        fns["rows_nosplit_sign"] = lambda: ablate(5)
         fns["rows_fd4_sign"] = lambda: ablate(6)
         fns["rows_burst_issue_sign"] = lambda: ablate(8)
         times = {n: [] for n in fns}

@@ -63,7 +63,7 @@ struct DeepDgradArgs {
   int m_tiles;           // 256-pixel tiles of the largest stride-parity class
 };
 
-// BNC: input channels per block (256, or 128 for the 128-channel stage):
+// BNC: input channels per block (256; the launcher instantiates only that):
 // the weight pieces hold BNC rows, a wave's A rows are BNC / 2 in two phase
 // halves of FA = BNC / 64 fragments.
 template <int BNC>
@@ -468,7 +468,6 @@ __global__ __launch_bounds__(DP_NT, 1) void wgrad_deep_kernel(DeepWgradArgs a) {
 }
 
 bool g_dp_attr = false;
-bool g_dp_attr128 = false;
 bool g_wp_attr = false;
 
 }  // namespace
@@ -527,12 +526,14 @@ int zk_wgrad_deep_impl(const void* dy, const void* sx, const void* w, void* dw, 
 
 // Entry used by igemm.hip's dgrad dispatch (variant 60): data gradient of a
 // conv with kh, kw <= 3, stride 1 or 2 (one grid row per stride-parity class
-// of the input pixels), Cin % 128 == 0 (256-channel blocks when Cin % 256 ==
-// 0), Cout % 64 == 0; mask / dres optional.  dry: validate only.
+// of the input pixels), Cin % 256 == 0 (the dispatch's rule: the 128-channel
+// block form lost to conv3rw / igemm there and was removed,
+// profiles/r4/removed_variants.md), Cout % 64 == 0; mask / dres optional.
+// dry: validate only.
 int zk_dgrad_deep_impl(const void* dy, const void* wt, const void* mask, const void* dres, void* dx,
                        int B, int H, int W, int Cin, int Cout, int Ho, int Wo, int kh, int kw,
                        int s, int pt, int pl, bool dry, hipStream_t st) {
-  if (Cin % 128 || Cout % 64 || Cout < 64 || B < 1 || H < 1 || W < 1 || Ho < 1 || Wo < 1)
+  if (Cin % 256 || Cout % 64 || Cout < 64 || B < 1 || H < 1 || W < 1 || Ho < 1 || Wo < 1)
     return (int)hipErrorInvalidValue;
   if (kh < 1 || kh > 3 || kw < 1 || kw > 3 || s < 1 || s > 2 || pt < 0 || pl < 0 || pt >= kh ||
       pl >= kw)
@@ -540,7 +541,7 @@ int zk_dgrad_deep_impl(const void* dy, const void* wt, const void* mask, const v
   const long long P = (long long)B * H * W;
   if (P * Cin >= (1LL << 40) || (long long)B * Ho * Wo * Cout >= (1LL << 40))
     return (int)hipErrorInvalidValue;
-  const int bnc = Cin % 256 == 0 ? 256 : 128;
+  constexpr int bnc = 256;
   // the largest parity class: ceil(H / s) x ceil(W / s) pixels per image
   const long long Pc = (long long)B * ((H + s - 1) / s) * ((W + s - 1) / s);
   const long long m_tiles = (Pc + 255) / 256;
@@ -552,24 +553,13 @@ int zk_dgrad_deep_impl(const void* dy, const void* wt, const void* mask, const v
                   s, pt, pl, (int)m_tiles};
   const dim3 grid((unsigned)blocks, (unsigned)(s * s));
   (void)hipGetLastError();
-  if (bnc == 256) {
-    constexpr int lds = 2 * (2 * 256 * 64 + 2 * DP_PIECE);
-    if (!g_dp_attr) {
-      const hipError_t e = hipFuncSetAttribute((const void*)dgrad_deep_kernel<256>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      if (e != hipSuccess) return (int)e;
-      g_dp_attr = true;
-    }
-    hipLaunchKernelGGL(dgrad_deep_kernel<256>, grid, dim3(DP_NT), lds, st, a);
-  } else {
-    constexpr int lds = 2 * (2 * 128 * 64 + 2 * DP_PIECE);
-    if (!g_dp_attr128) {
-      const hipError_t e = hipFuncSetAttribute((const void*)dgrad_deep_kernel<128>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      if (e != hipSuccess) return (int)e;
-      g_dp_attr128 = true;
-    }
-    hipLaunchKernelGGL(dgrad_deep_kernel<128>, grid, dim3(DP_NT), lds, st, a);
+  constexpr int lds = 2 * (2 * 256 * 64 + 2 * DP_PIECE);
+  if (!g_dp_attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)dgrad_deep_kernel<256>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return (int)e;
+    g_dp_attr = true;
   }
+  hipLaunchKernelGGL(dgrad_deep_kernel<256>, grid, dim3(DP_NT), lds, st, a);
   return (int)hipGetLastError();
 }

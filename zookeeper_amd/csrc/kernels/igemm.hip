@@ -80,6 +80,17 @@ struct ConvArgs {
   // the next BatchNorm's statistics of the stored bf16 outputs,
   // fstats[stripe][0][c] += sum y, [1][c] += sum y^2 (fp64, stripe = block % stripes)
   double* fstats;
+  // float dgrad through the LDS epilogue (optional): the backward sums of the
+  // BatchNorm whose output gradient is exactly the dx stored here (float BN,
+  // bf16 input bxb [P][Cin], coefficients bcoef [4][Cin] = scale, shift,
+  // mean, rstd): bsums[0][c][stripe] += sum g', [1][c][stripe] += sum g' *
+  // xhat, g' = dx * relu mask (brelu 0: none, 1: recomputed from bxb, 2: the
+  // bits bmask [P][Cin/8]) -- the channel-major copies zk_bn_bwd_coef reads.
+  const uint16_t* bxb;
+  const float* bcoef;
+  const uint8_t* bmask;
+  int brelu;
+  float* bsums;
 };
 
 // Host-side kernel options, set from Python (ops/options.py -> zk_set_option;
@@ -241,12 +252,26 @@ __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeo
   }
   uint16_t* dx = reinterpret_cast<uint16_t*>(args.out);
   const uint16_t* dres = args.dres;
-  // args.fstats: this thread's 8 channels are fixed (NT is a multiple of BN/8)
+  // args.fstats / args.bsums: this thread's 8 channels are fixed (NT is a
+  // multiple of BN/8)
   static_assert(NT % (BN / 8) == 0, "LDS epilogue: fixed channel chunk per thread");
   const bool fst = args.fstats != nullptr;
+  const bool bsm = args.bsums != nullptr;
   float fs1[8], fs2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) fs1[k] = fs2[k] = 0.f;
+  // bsums: the BN coefficients of this thread's 8 channels
+  float bsc[8], bsh[8], bmu[8], brs[8];
+  if (bsm) {
+    const int c0 = n0 + 8 * (tid % (BN / 8));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bsc[k] = args.bcoef[c0 + k];
+      bsh[k] = args.bcoef[g.Cin + c0 + k];
+      bmu[k] = args.bcoef[2 * g.Cin + c0 + k];
+      brs[k] = args.bcoef[3 * g.Cin + c0 + k];
+    }
+  }
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     __syncthreads();  // the ring (p = 0) / the previous half's tile is free
@@ -295,6 +320,27 @@ __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeo
       const uint4 o = make_uint4(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
                                  zk::pack_bf16x2(v[4], v[5]), zk::pack_bf16x2(v[6], v[7]));
       *reinterpret_cast<uint4*>(dx + off) = o;
+      if (bsm) {
+        // the BN-backward sums over the stored gradient (zk_bn_bwd_reduce of
+        // the BN whose output this dx is the whole gradient of)
+        const uint4 xq = *reinterpret_cast<const uint4*>(args.bxb + off);
+        const uint32_t xw[4] = {xq.x, xq.y, xq.z, xq.w};
+        const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+        const uint32_t mb = args.brelu == 2 ? args.bmask[off >> 3] : 0xFFu;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float xk = zk::bf16_to_f32((uint16_t)(xw[k >> 1] >> (16 * (k & 1))));
+          float gk = zk::bf16_to_f32((uint16_t)(ow[k >> 1] >> (16 * (k & 1))));  // as stored
+          // ReLU mask as the forward stored it: bf16(scale * x + shift) > 0
+          // (norm_pool.hip bn_pre / relu_live), or the stored bits
+          const bool live = args.brelu == 1
+                                ? (int16_t)zk::f32_to_bf16(bsc[k] * xk + bsh[k] + 0.f) > 0
+                                : ((mb >> k) & 1u) != 0;
+          gk = live ? gk : 0.f;
+          fs1[k] += gk;
+          fs2[k] += gk * (xk - bmu[k]) * brs[k];
+        }
+      }
       if (fst) {
         const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
@@ -304,6 +350,27 @@ __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeo
           fs2[k] += r * r;
         }
       }
+    }
+  }
+  if (bsm) {
+    // as the statistics below, into the fp32 channel-major copies
+    constexpr int JC = BN / 8, RPT = NT / JC;
+    static_assert(NT * 16 * 4 <= BM * BN * 2, "LDS epilogue: sums exchange");
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();  // every thread is past its staged-tile reads
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[tid * 16 + k] = fs1[k];
+      red[tid * 16 + 8 + k] = fs2[k];
+    }
+    __syncthreads();
+    const int stripe = args.stripes > 1 ? (int)(blockIdx.x % args.stripes) : 0;
+    for (int c = tid; c < 2 * BN; c += NT) {
+      const int which = c / BN, nl = c % BN, j = nl >> 3, k = nl & 7;
+      float t = 0.f;
+#pragma unroll 4
+      for (int r = 0; r < RPT; ++r) t += red[(r * JC + j) * 16 + which * 8 + k];
+      atomicAdd(args.bsums + ((long long)which * g.Cin + n0 + nl) * args.stripes + stripe, t);
     }
   }
   if (fst) {
@@ -1053,13 +1120,19 @@ struct BnSum {
   int stripes;
   void* fstats = nullptr;  // LE variants only: ConvArgs::fstats (float forward statistics)
   int ypred_bf16 = 0;      // ypred bf16 (the stem's pooled BN-2 input): variant 50 only
+  // LE variants only: ConvArgs::bxb / bcoef / bmask / brelu / bsums (float BN backward sums)
+  const void* bxb = nullptr;
+  const void* bcoef = nullptr;
+  const void* bmask = nullptr;
+  int brelu = 0;
+  void* bsums = nullptr;
 };
 
 template <int BM, int BN, int WM, int WN, int NS, int CB = 128, bool LE = false>
 int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const void* dres,
                        void* dx, const IGeom& g, const BnSum& bs, hipStream_t stream) {
   if (LE && bs.sums) return (int)hipErrorInvalidValue;  // fused BN sums: register epilogue
-  if (!LE && bs.fstats) return (int)hipErrorInvalidValue;  // forward statistics: LDS epilogue
+  if (!LE && (bs.fstats || bs.bsums)) return (int)hipErrorInvalidValue;  // LDS epilogue only
   if ((g.Cout * 2) % CB || g.Cin % BN || g.s > 2 || g.kh > 4 || g.kw > 4)
     return (int)hipErrorInvalidValue;
   if (g_dry_run) return 0;
@@ -1082,6 +1155,11 @@ int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const v
                 (const int16_t*)bs.ypred, (const float*)bs.mean, (const float*)bs.rstd,
                 (float*)bs.sums};
   args.fstats = (double*)bs.fstats;
+  args.bxb = (const uint16_t*)bs.bxb;
+  args.bcoef = (const float*)bs.bcoef;
+  args.bmask = (const uint8_t*)bs.bmask;
+  args.brelu = bs.brelu;
+  args.bsums = (float*)bs.bsums;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, g.s * g.s), dim3(WM * WN * 64), LDS, stream,
                      args, g, m_tiles);
   return 0;
@@ -1241,7 +1319,8 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
                         const void* dres, void* dx, const IGeom& g, const BnSum& bs,
                         hipStream_t st) {
 #define ZK_IGD(...) return launch_igemm_dgrad<__VA_ARGS__>(dy, wt, mask, dres, dx, g, bs, st)
-  if (bs.fstats && (v < 40 || v > 48)) return (int)hipErrorInvalidValue;  // LE variants only
+  if ((bs.fstats || bs.bsums) && (v < 40 || v > 48))
+    return (int)hipErrorInvalidValue;  // LE variants only
   switch (v) {
     case 0: ZK_IGD(128, 128, 2, 2, 2);        // 64 KB: 2 WG/CU
     case 1: ZK_IGD(128, 128, 2, 2, 4, 64);    // 64 KB, 3 K-steps of 32 in flight
@@ -1903,7 +1982,7 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     // 14x14 N1024 K256 144 -> 127 us, 28x28 N128 K512 139 -> 120 us).
     const int Cin = g.Cin, stride = g.s;
     const bool c3 = conv3_ok(g, 0);
-    const bool le = bs.sums == nullptr;
+    const bool le = bs.sums == nullptr;  // (bs.bsums: LE variants, checked at the launch)
     const int v256 = le ? 45 : 14;
     if (g_opt_dgrad_deep && le && !bs.fstats && c3 && Cin % 256 == 0 && g.Cout % 64 == 0)
       // phased 256x256 schedule (deep_gemm.hip).  Measured at batch 1536 it
@@ -1932,12 +2011,12 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
       variant = 7;
   }
   if (variant == 60) {  // deep_gemm.hip (explicit, or the default above)
-    if (bs.fstats || bs.sums) return (int)hipErrorInvalidValue;
+    if (bs.fstats || bs.sums || bs.bsums) return (int)hipErrorInvalidValue;
     return zk_dgrad_deep_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Cout, g.Ho, g.Wo,
                               g.kh, g.kw, g.s, g.pt, g.pl, g_dry_run, stream);
   }
   if (variant == 50) {  // conv3rw.hip (explicit, or the default above)
-    if (bs.fstats) return (int)hipErrorInvalidValue;
+    if (bs.fstats || bs.bsums) return (int)hipErrorInvalidValue;
     if (g.s != 1 || g.kh != 3 || g.kw != 3 || g.pt != 1 || g.pl != 1 || g.Ho != g.H ||
         g.Wo != g.W)
       return (int)hipErrorInvalidValue;
@@ -2000,6 +2079,32 @@ ZK_EXPORT int zk_igemm_dgrad_fstats(const void* dy, const void* wt, void* dx, vo
                           BnSum{nullptr, nullptr, nullptr, nullptr, stripes < 1 ? 1 : stripes,
                                 fstats},
                           variant, stream);
+}
+
+// zk_igemm_dgrad + the backward sums of the float BatchNorm whose output
+// gradient dx is (its whole gradient): sums [2][Cin][stripes] fp32
+// channel-major (atomics into copy block % stripes; zk_bn_bwd_coef reads and
+// re-zeroes them) += (sum g', sum g' * (xb - mean) * rstd) with g' = the
+// stored dx times the BN's ReLU mask (relu 0: none, 1: recomputed from xb
+// and the forward scale / shift, 2: bits mask [P][Cin/8]); xb bf16
+// [B][H][W][Cin] is the BN input, coef [4][Cin] = scale, shift, mean, rstd.
+// Only the LDS-epilogue variants carry the sums: any other choice returns
+// hipErrorInvalidValue and the caller keeps the separate reduction.
+ZK_EXPORT int zk_igemm_dgrad_bsums(const void* dy, const void* wt, const void* dres, void* dx,
+                                   const void* xb, const void* coef, const void* mask, int relu,
+                                   void* sums, int stripes, int B, int H, int W, int Cin, int Ho,
+                                   int Wo, int Cout, int kh, int kw, int stride, int pt, int pl,
+                                   int variant, hipStream_t stream) {
+  IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
+  if (!xb || !coef || !sums || Cin % 8 || relu < 0 || relu > 2 || (relu == 2 && !mask))
+    return (int)hipErrorInvalidValue;
+  BnSum bs{nullptr, nullptr, nullptr, nullptr, stripes < 1 ? 1 : stripes};
+  bs.bxb = xb;
+  bs.bcoef = coef;
+  bs.bmask = mask;
+  bs.brelu = relu;
+  bs.bsums = sums;
+  return igemm_dgrad_impl(dy, wt, nullptr, dres, dx, g, bs, variant, stream);
 }
 
 namespace {

@@ -148,7 +148,8 @@ __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __re
                                                             uint8_t* __restrict__ smask = nullptr,
                                                             float clip = 1.f,
                                                             uint32_t* __restrict__ sx4 = nullptr,
-                                                            const uint16_t* __restrict__ res = nullptr) {
+                                                            const uint16_t* __restrict__ res = nullptr,
+                                                            uint8_t* __restrict__ omask = nullptr) {
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;
   const int cg = threadIdx.x % CG;
@@ -172,6 +173,17 @@ __global__ __launch_bounds__(256) void bn_apply_bf16_kernel(const uint16_t* __re
     const uint32_t ow[4] = {zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
                             zk::pack_bf16x2(v[4], v[5]), zk::pack_bf16x2(v[6], v[7])};
     *reinterpret_cast<uint4*>(y + r * C + cg * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    if (omask) {
+      // the ReLU mask of the stored output (bit k: y[8 cg + k] > 0), the
+      // backward's instead of re-reading y: 1 bit per element, not 16
+      uint32_t mk = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        mk |= (uint32_t)((int16_t)(ow[k] & 0xffff) > 0) << (2 * k);
+        mk |= (uint32_t)((int16_t)(ow[k] >> 16) > 0) << (2 * k + 1);
+      }
+      omask[r * CG + cg] = (uint8_t)mk;
+    }
     if (sx || sx4) {
       // next binary layer's input quantisation from the stored bf16 values
       // (same layout as batchnorm.hip's bn_apply_kernel / zk_sign_pack)
@@ -201,10 +213,12 @@ constexpr int kBnBwdParts = 512;  // copy capacity of the PARTS reduce (red_grid
 // 512: run-to-run deterministic) instead of fp32 atomics into one [2][C] row.
 // RC: BN + ReLU without a stored output: the ReLU mask is recomputed from x
 // and the forward coefficients (relu_live(bn_pre(...))), saving a read of y.
+// m (otherwise): the ReLU mask bits of the output (bn_apply's omask: a
+// residual was added before the ReLU, so x alone does not give it), or null.
 template <int CG, bool PARTS = false, bool RC = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
     const uint16_t* __restrict__ g, const uint16_t* __restrict__ x,
-    const uint16_t* __restrict__ y, const float* __restrict__ coef, float* __restrict__ sums,
+    const uint8_t* __restrict__ m, const float* __restrict__ coef, float* __restrict__ sums,
     long long P) {
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;
@@ -221,7 +235,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
   constexpr int UR = 4;  // rows in flight per thread (loads first, then math)
   const long long rstep = (long long)gridDim.x * RB;
   for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P; r += UR * rstep) {
-    uint4 gq[UR], xq[UR], yq[UR];
+    uint4 gq[UR], xq[UR];
+    uint32_t mq[UR];
 #pragma unroll
     for (int u = 0; u < UR; ++u) {
       const long long ru = r + u * rstep;
@@ -230,15 +245,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
       gq[u] = in ? *reinterpret_cast<const uint4*>(g + off) : make_uint4(0, 0, 0, 0);
       xq[u] = in ? *reinterpret_cast<const uint4*>(x + off) : make_uint4(0, 0, 0, 0);
       // fused ReLU: gradient only where the output was positive
-      yq[u] = (!RC && in && y)
-                  ? *reinterpret_cast<const uint4*>(y + off)
-                  : make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+      mq[u] = (!RC && in && m) ? m[ru * CG + cg] : 0xFFu;
     }
 #pragma unroll
     for (int u = 0; u < UR; ++u) {
       const uint32_t g4[4] = {gq[u].x, gq[u].y, gq[u].z, gq[u].w};
       const uint32_t x4[4] = {xq[u].x, xq[u].y, xq[u].z, xq[u].w};
-      const uint32_t y4[4] = {yq[u].x, yq[u].y, yq[u].z, yq[u].w};
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int sh = 16 * (k & 1);
@@ -246,7 +258,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
         const float xk = zk::bf16_to_f32((uint16_t)(x4[k >> 1] >> sh));
         if (RC) {
           if (!relu_live(bn_pre(fa[k], xk, fs[k], 0.f))) gk = 0.f;
-        } else if (!(zk::bf16_to_f32((uint16_t)(y4[k >> 1] >> sh)) > 0.f)) {
+        } else if (!((mq[u] >> k) & 1u)) {
           gk = 0.f;
         }
         sg[k] += gk;
@@ -280,10 +292,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_bf16_kernel(
 // bcoef: [k1, k0, k3] x C with dx = k1*g' + k0 - k3*x
 // fcoef (forward coefficients, scale / shift rows): BN + ReLU with the mask
 // recomputed from x instead of read from y (see bn_bwd_reduce_bf16_kernel).
+// m: the output's ReLU mask bits (see bn_bwd_reduce_bf16_kernel), or null.
 template <int CG>
 __global__ __launch_bounds__(256) void bn_bwd_dx_bf16_kernel(
     const uint16_t* __restrict__ g, const uint16_t* __restrict__ x,
-    const uint16_t* __restrict__ y, const float* __restrict__ bcoef, uint16_t* __restrict__ dx,
+    const uint8_t* __restrict__ m, const float* __restrict__ bcoef, uint16_t* __restrict__ dx,
     long long P, uint16_t* __restrict__ dres = nullptr, const float* __restrict__ fcoef = nullptr) {
   constexpr int C = CG * 8;
   constexpr int RB = 256 / CG;
@@ -302,11 +315,10 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_bf16_kernel(
     float gv[8], xv[8], o[8];
     load8_bf16(g + r * C + cg * 8, gv);
     load8_bf16(x + r * C + cg * 8, xv);
-    if (y) {
-      float yv[8];
-      load8_bf16(y + r * C + cg * 8, yv);
+    if (m) {
+      const uint32_t b = m[r * CG + cg];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+      for (int k = 0; k < 8; ++k) gv[k] = (b >> k) & 1u ? gv[k] : 0.f;
     } else if (fcoef) {
 #pragma unroll
       for (int k = 0; k < 8; ++k)
@@ -630,14 +642,15 @@ ZK_EXPORT int zk_bn_apply_bf16_sign(const void* x, const void* coef, void* y, vo
   return 0;
 }
 
-ZK_EXPORT int zk_bn_bwd_reduce_bf16(const void* g, const void* x, const void* y,
+// m: the output's ReLU mask bits (zk_bn_apply_res_bf16's omask), or null.
+ZK_EXPORT int zk_bn_bwd_reduce_bf16(const void* g, const void* x, const void* m,
                                     const void* coef, void* sums, long long P, int C,
                                     hipStream_t st) {
   if (C % 8) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                              \
   case cg:                                                                                    \
     hipLaunchKernelGGL(bn_bwd_reduce_bf16_kernel<cg>, dim3(red_grid(P, C)), dim3(256), 0, st, \
-                       (const uint16_t*)g, (const uint16_t*)x, (const uint16_t*)y,            \
+                       (const uint16_t*)g, (const uint16_t*)x, (const uint8_t*)m,             \
                        (const float*)coef, (float*)sums, P);                                  \
     break;
   ZK_CG_CASES(C, CASE)
@@ -651,7 +664,7 @@ ZK_EXPORT int zk_bn_bwd_reduce_bf16(const void* g, const void* x, const void* y,
 // zk_bn_bwd_parts_max() as sums / stripes / stride to zk_bn_bwd_coef.
 ZK_EXPORT int zk_bn_bwd_parts_max() { return kBnBwdParts; }
 
-ZK_EXPORT int zk_bn_bwd_reduce_bf16_parts(const void* g, const void* x, const void* y,
+ZK_EXPORT int zk_bn_bwd_reduce_bf16_parts(const void* g, const void* x, const void* m,
                                           const void* coef, void* parts, long long P, int C,
                                           int* nparts, hipStream_t st) {
   if (C % 8) return (int)hipErrorInvalidValue;
@@ -660,7 +673,7 @@ ZK_EXPORT int zk_bn_bwd_reduce_bf16_parts(const void* g, const void* x, const vo
 #define CASE(cg)                                                                           \
   case cg:                                                                                 \
     hipLaunchKernelGGL((bn_bwd_reduce_bf16_kernel<cg, true>), dim3(grid), dim3(256), 0, st, \
-                       (const uint16_t*)g, (const uint16_t*)x, (const uint16_t*)y,         \
+                       (const uint16_t*)g, (const uint16_t*)x, (const uint8_t*)m,          \
                        (const float*)coef, (float*)parts, P);                              \
     break;
   ZK_CG_CASES(C, CASE)
@@ -669,13 +682,13 @@ ZK_EXPORT int zk_bn_bwd_reduce_bf16_parts(const void* g, const void* x, const vo
   return 0;
 }
 
-ZK_EXPORT int zk_bn_bwd_dx_bf16(const void* g, const void* x, const void* y, const void* bcoef,
+ZK_EXPORT int zk_bn_bwd_dx_bf16(const void* g, const void* x, const void* m, const void* bcoef,
                                 void* dx, long long P, int C, hipStream_t st) {
   if (C % 8) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                             \
   case cg:                                                                                   \
     hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,   \
-                       (const uint16_t*)g, (const uint16_t*)x, (const uint16_t*)y,           \
+                       (const uint16_t*)g, (const uint16_t*)x, (const uint8_t*)m,            \
                        (const float*)bcoef, (uint16_t*)dx, P);                               \
     break;
   ZK_CG_CASES(C, CASE)
@@ -719,14 +732,16 @@ ZK_EXPORT int zk_bn_bwd_dx_relu_bf16(const void* g, const void* x, const void* c
 
 // y = act(scale * x + shift + res): BN apply with a residual added before
 // the optional ReLU (a ResNet bottleneck's tail: relu(bn3(conv3) + shortcut)).
+// omask (optional): the ReLU mask bits of y, [P][C/8] bytes, for the backward.
 ZK_EXPORT int zk_bn_apply_res_bf16(const void* x, const void* coef, const void* res, void* y,
-                                   long long P, int C, int relu, hipStream_t st) {
+                                   void* omask, long long P, int C, int relu, hipStream_t st) {
   if (C % 8) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                           \
   case cg:                                                                                 \
     hipLaunchKernelGGL(bn_apply_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,  \
                        (const uint16_t*)x, (const float*)coef, (uint16_t*)y, P, relu,      \
-                       nullptr, nullptr, 1.f, nullptr, (const uint16_t*)res);              \
+                       nullptr, nullptr, 1.f, nullptr, (const uint16_t*)res,               \
+                       (uint8_t*)omask);                                                   \
     break;
   ZK_CG_CASES(C, CASE)
 #undef CASE
@@ -735,15 +750,15 @@ ZK_EXPORT int zk_bn_apply_res_bf16(const void* x, const void* coef, const void* 
 }
 
 // zk_bn_bwd_dx_bf16 + the residual's gradient (the ReLU-masked output
-// gradient) written to dres in the same pass.
-ZK_EXPORT int zk_bn_bwd_dx_res_bf16(const void* g, const void* x, const void* y,
+// gradient) written to dres in the same pass; m: the ReLU mask bits or null.
+ZK_EXPORT int zk_bn_bwd_dx_res_bf16(const void* g, const void* x, const void* m,
                                     const void* bcoef, void* dx, void* dres, long long P, int C,
                                     hipStream_t st) {
   if (C % 8) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                             \
   case cg:                                                                                   \
     hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,   \
-                       (const uint16_t*)g, (const uint16_t*)x, (const uint16_t*)y,           \
+                       (const uint16_t*)g, (const uint16_t*)x, (const uint8_t*)m,            \
                        (const float*)bcoef, (uint16_t*)dx, P, (uint16_t*)dres);              \
     break;
   ZK_CG_CASES(C, CASE)

@@ -45,6 +45,8 @@
 //
 // Reference: the QuantConv2D stack whose weight gradients these are
 // (/root/reference/examples/larq_experiment.py:62-99).
+#include <climits>
+
 #include "mfma_common.h"
 
 namespace {
@@ -66,29 +68,59 @@ constexpr int WR_SC1 = 16;     // buffer-op cache policy: sc1 (agent-coherent)
 // sign image for these layers.
 enum { OP_IMG = 0, OP_SIGN = 1, OP_FP4 = 2 };
 
+// Window rows are padded to whole KB in LDS (RB, R4B) so that every 1-KB
+// LDS-DMA piece lies in one window row: a piece's source row, and whether it
+// is a padding row above / below the image, are wave-uniform (scalar
+// selects); per lane only the static halo / row-padding lanes differ (one
+// select): ~3 VALU per DMA piece instead of ~15.
 template <int W, int OP>
 struct WrGeo {
   static constexpr int R = WR_RW / W;           // image rows per step
-  static constexpr int PW = W + 2;              // S window row pitch (pixels)
-  static constexpr int RB = PW * 64;            // S window row bytes in one plane
+  static constexpr int PW = W + 2;              // S window row (pixels, with the halo)
+  static constexpr int RB = (PW * 64 + 1023) / 1024 * 1024;  // bf16 row pitch, one plane
   static constexpr int SPLANE = (R + 2) * RB;   // window rows h0-1 .. h0+R
   static constexpr int SBYTES = 2 * SPLANE;     // bf16 window, 2 planes of 32 channels
-  static constexpr int S4BYTES = (R + 2) * PW * 32;  // e2m1 window, 32 B per pixel
+  static constexpr int R4B = (PW * 32 + 1023) / 1024 * 1024;  // e2m1 row pitch (32 B / pixel)
+  static constexpr int S4BYTES = (R + 2) * R4B;
   static constexpr int DPLANE = WR_RW * 64;
-  static constexpr int DBYTES = 2 * DPLANE;     // 14 KB
-  static constexpr int DINS = DBYTES / 1024;
-  // staged per step: dY + the S window (bf16, or e2m1 for OP_FP4)
-  static constexpr int STAGED = OP == OP_FP4 ? S4BYTES : SBYTES;
-  static constexpr int TOT = (DINS + (STAGED + 1023) / 1024 + 3) / 4 * 4;  // DMA pieces
+  static constexpr int DBYTES = 2 * DPLANE;     // 14 KB of dY ...
+  static constexpr int SOFF = 16 * 1024;        // ... in a 16-KB region: the S window at 16 KB
+  // staged per step: dY + the S window (bf16, or e2m1 for OP_FP4), in 4-KB
+  // units: a slot is 4 KB x NI, and DMA instruction k of every wave covers
+  // bytes [4k, 4k + 4) KB (1 KB per wave): k < KD dY, then KS window units
+  static constexpr int STAGED = ((OP == OP_FP4 ? S4BYTES : SBYTES) + 4095) / 4096 * 4096;
+  static constexpr int SROW = OP == OP_FP4 ? R4B : RB;  // staged row pitch
+  static constexpr int RBK = SROW / 1024;       // DMA pieces per staged row (1, 2, 4)
+  static constexpr int KD = SOFF / 4096, KS = STAGED / 4096;
+  static constexpr int TOT = 4 * (KD + KS);     // DMA pieces (1 KB)
   static constexpr int NI = TOT / 4;            // DMA pieces per wave per step
   static constexpr int SLOT = TOT * 1024;
   // OP_FP4: two expanded bf16 windows after the slots (step j's, step j+1's)
   static constexpr int SBF = WR_NSLOT * SLOT;
   static constexpr int FLAG = SBF + (OP == OP_FP4 ? 2 * SBYTES : 0);  // arrival word
   static constexpr int LDS = FLAG + 16;
-  static constexpr int CHUNKS = SBYTES / 16;    // OP_FP4 expansion: 16-B bf16 chunks
-  static_assert(WR_RW % W == 0 && LDS <= 160 * 1024, "row-stream geometry");
+  // OP_FP4 expansion: 16-B bf16 chunks of the real window pixels
+  static constexpr int CPR = PW * 4;            // chunks per row of one plane
+  static constexpr int CHUNKS = 2 * (R + 2) * CPR;
+  static_assert(WR_RW % W == 0 && LDS <= 160 * 1024 && DBYTES <= SOFF && 4 % RBK == 0,
+                "row-stream geometry");
 };
+
+// Rows above / below the image: DMA'd from these (zero, bf16 +1, e2m1 +1
+// pairs), one image row of up to WR_MAXCIN channels long.  Filled once by
+// wr_pad_init_kernel.
+constexpr int WR_MAXCIN = 256;
+constexpr int WR_PADROW = 56 * WR_MAXCIN * 2;
+__device__ __attribute__((aligned(1024))) uint32_t g_wr_pad[3][WR_PADROW / 4];
+
+__global__ void wr_pad_init_kernel() {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < WR_PADROW / 4) {
+    g_wr_pad[0][i] = 0u;
+    g_wr_pad[1][i] = 0x3F803F80u;
+    g_wr_pad[2][i] = 0x22222222u;
+  }
+}
 
 struct WrArgs {
   const uint16_t* dy;  // [B][H][W][Cout] bf16
@@ -115,6 +147,11 @@ __device__ __forceinline__ __attribute__((address_space(3))) s16x4* lds_s16x4(
       const __attribute__((address_space(3))) void*)(smem + off);
 }
 
+// global_load_lds_dwordx4 into LDS byte address lds (wave-uniform: M0)
+__device__ __forceinline__ void glds16_at(const void* src, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "m0");
+}
+
 // 8 k-values of one column from two per-lane LDS addresses (rows q and q + 4
 // of the lane's 4-row group, as tr_frag_swz)
 __device__ __forceinline__ uint4 tr_read2(const unsigned char* smem, int o0, int o1) {
@@ -131,20 +168,17 @@ __device__ __forceinline__ uint32_t sign_bf16x2(uint32_t v, uint32_t ones) {
   return (v & 0x80008000u) | (ones & 0x7FFF7FFFu);
 }
 
-// Unit schedules of the main loop (a unit = one S fragment: K-step kk, tap t).
-// M 0 / 1: the SPLIT pair members (taps 0-3 / 5-8 of every K-step, tap 4 of
-// K-steps 0-3 / 4-6: 32 / 31 units); M 2: all 63 units in (kk, t) order.
-__host__ __device__ constexpr int wr_units(int m) { return m == 2 ? 63 : (m == 0 ? 32 : 31); }
+// Unit schedules of the main loop (a unit = one S fragment: K-step kk, tap t)
+// of the two pair members M 0 / 1: taps 0-3 / 5-8 of every K-step, tap 4 of
+// K-steps 0-3 / 4-6: 32 / 31 units.
+__host__ __device__ constexpr int wr_units(int m) { return m == 0 ? 32 : 31; }
 // (closed forms, so unrolled loops fold them to constants: M 0 has 5 units
 // per K-step below kk 4 and 4 above, M 1 the reverse)
 __host__ __device__ constexpr int wr_unit_kk(int m, int n) {
-  return m == 2 ? n / 9
-       : m == 0 ? (n < 20 ? n / 5 : 4 + (n - 20) / 4)
-                : (n < 16 ? n / 4 : 4 + (n - 16) / 5);
+  return m == 0 ? (n < 20 ? n / 5 : 4 + (n - 20) / 4) : (n < 16 ? n / 4 : 4 + (n - 16) / 5);
 }
 __host__ __device__ constexpr int wr_unit_tap(int m, int n) {
-  return m == 2 ? n % 9
-       : m == 0 ? (n < 20 ? n % 5 : (n - 20) % 4)
+  return m == 0 ? (n < 20 ? n % 5 : (n - 20) % 4)
                 : (n < 16 ? 5 + n % 4 : ((n - 16) % 5 == 4 ? 4 : 5 + (n - 16) % 5));
 }
 // accumulator slot of tap t, and back (M 1 keeps tap 4 in slot 0)
@@ -164,21 +198,22 @@ static_assert(wr_unit_kk(0, 31) == 6 && wr_unit_tap(0, 31) == 3 && wr_unit_tap(0
 // fragment reads; results are garbage in 1-4)
 // FD: how many MFMAs ahead each S fragment is read (one wave per SIMD: only
 // this lookahead hides the LDS latency)
-// SPLIT: wave tile 64(co) x 32(ci) x 9 taps, the two waves of a ci half
-// splitting the step's 63 (K-step, tap) units 32 / 31 (each S fragment feeds
-// both co halves: half the LDS fragment reads per MFMA); partial tiles of the
-// pair combined through LDS after the loop.  Otherwise 32 x 32 x 9 per wave.
-template <int W, int OP, bool SPLIT, int LAB = 0, int FD0 = 0>
+// A wave's tile is 64 (co) x 32 (ci); the two waves of a ci half split the
+// step's 63 (K-step, tap) units by taps (wr_unit_*), so each S fragment read
+// feeds both co halves; their tap-4 partials are combined through LDS.
+// (Measured against 32 x 32 x 9-tap wave tiles: stage 1 sign operand 417 vs
+// 491 us; profiles/r5/removed_variants.md.)
+template <int W, int OP, int LAB = 0, int FD0 = 0>
 __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
-  // lookahead: 5 units (SPLIT: 10 S + up to 4 dY reads in flight, under the
-  // 15 lgkmcnt can count) or 6 MFMAs
-  constexpr int FD = FD0 > 0 ? FD0 : (SPLIT ? 5 : 6);
+  // lookahead: 5 units (10 S + up to 4 dY reads in flight, under the 15
+  // lgkmcnt can count)
+  constexpr int FD = FD0 > 0 ? FD0 : 5;
   using G = WrGeo<W, OP>;
   constexpr int R = G::R, PW = G::PW, RB = G::RB, NI = G::NI;
   constexpr bool FP4 = OP == OP_FP4, SIGN = OP == OP_SIGN;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wn = wave & 1;
   const int tiles = a.co_tiles * a.ci_tiles;
   const int L = xcd_linear(blockIdx.x, gridDim.x);
   const int split = L / tiles, tile = L % tiles;
@@ -189,84 +224,95 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
 
   const unsigned char* dyb = reinterpret_cast<const unsigned char*>(a.dy);
   const unsigned char* sxb = reinterpret_cast<const unsigned char*>(a.sx);
-  const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
-  const unsigned char* pp =
-      !a.pad_ones || SIGN ? zp
-      : FP4 ? reinterpret_cast<const unsigned char*>(g_ones_page_fp4)
-            : reinterpret_cast<const unsigned char*>(g_ones_page_bf16);
+  // padding rows (and pixel) source: zeros, or +1 (bf16 / e2m1) with pad_ones
+  // (OP_SIGN: zeros, whose sign is +1)
+  const int padk = !a.pad_ones || SIGN ? 0 : (FP4 ? 2 : 1);
+  const unsigned char* padp = reinterpret_cast<const unsigned char*>(g_wr_pad[padk]);
   constexpr bool do_load = LAB < 2 || LAB > 4, do_mma = LAB != 1;
   // the next step's LDS-DMA pieces spread over the MFMA units (LAB 8: all
   // issued at the top of the step, before the first MFMA)
   constexpr bool spread = LAB != 8;
   constexpr bool lab_reads = LAB != 4, lab_mfma = LAB != 3;
 
-  // per-lane LDS-DMA sources of a slot's NI pieces per wave (piece t = k*4 +
-  // wave covers slot bytes [t KB, t KB + 1 KB)): a byte offset (multiple of
-  // 16) from the step's first dY / S pixel, with a code in its low 4 bits:
-  // 0 = dY, 1 + wr = S window row wr, 14 = padding page (halo column),
-  // 15 = slot tail (zeros)
-  int src[NI];
+  // LDS-DMA pieces: piece t = k * 4 + wave covers slot bytes [t KB, t KB +
+  // 1 KB).  k < KD: dY; then window units: staged window row r(k, wave) =
+  // (k - KD) * 4 / RBK + wave / RBK -- compile-time but for a wave-uniform
+  // term.  Per lane, loff[k] = its source offset from the step's first dY
+  // pixel / first S row (the row offset folded in), or WR_HALO for a lane
+  // that reads the pad page (halo pixel, row padding).
+  constexpr int WR_HALO = INT_MIN;
+  int loff[NI];
+  const long long srow = (long long)W * a.Cin * (FP4 ? 1 : 4) / 2;  // image row bytes
 #pragma unroll
   for (int k = 0; k < NI; ++k) {
     const int b = (k * 4 + wave) * 1024 + lane * 16;
-    if (b < G::DBYTES) {
-      const int plane = b / G::DPLANE, rem = b % G::DPLANE;
-      const int p = rem >> 6, ch = (rem & 63) >> 4;
-      src[k] = (p * a.Cout + co0 + plane * 32 + ch * 8) * 2;
-    } else if (b - G::DBYTES < G::STAGED) {
-      const int bs = b - G::DBYTES;
-      int wr, col, off;
-      if constexpr (FP4) {  // [window pixel][32 B]: the tile's 64 channels as nibbles
-        const int pix = bs >> 5, half = (bs & 31) >> 4;
-        wr = pix / PW;
-        col = pix % PW;
-        off = ((wr - 1) * W + col - 1) * (a.Cin / 2) + ci0 / 2 + half * 16;
-      } else {  // [plane][window pixel][32 channels]
+    loff[k] = WR_HALO;
+    if (k < G::KD) {
+      if (b < G::DBYTES) {
+        const int plane = b / G::DPLANE, rem = b % G::DPLANE;
+        const int p = rem >> 6, ch = (rem & 63) >> 4;
+        loff[k] = (p * a.Cout + co0 + plane * 32 + ch * 8) * 2;
+      } else {
+        loff[k] = 0;  // the unused dY tail: any valid bytes
+      }
+    } else {
+      const int bs = b - G::SOFF;
+      int wr, col, choff;
+      if constexpr (FP4) {  // [window row][pixel][32 B]: the tile's 64 channels as nibbles
+        wr = bs / G::R4B;
+        col = (bs % G::R4B) >> 5;
+        choff = ci0 / 2 + ((bs & 31) >> 4) * 16;
+      } else {  // [plane][window row][pixel][32 channels]
         const int plane = bs / G::SPLANE, rem = bs % G::SPLANE;
-        const int ch = (rem & 63) >> 4;
         wr = rem / RB;
         col = (rem % RB) >> 6;
-        off = (((wr - 1) * W + col - 1) * a.Cin + ci0 + plane * 32 + ch * 8) * 2;
+        choff = (ci0 + plane * 32 + ((rem & 63) >> 4) * 8) * 2;
       }
-      src[k] = (col >= 1 && col <= W) ? (off | (1 + wr)) : 14;
-    } else {
-      src[k] = 15;
+      if (col >= 1 && col <= W && wr <= R + 1)
+        loff[k] = (int)((wr - 1) * srow) + (col - 1) * (a.Cin * (FP4 ? 1 : 4) / 2) + choff;
     }
   }
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const long long dy_step = (long long)WR_RW * a.Cout * 2;
   const long long sx_step = (long long)WR_RW * a.Cin * (FP4 ? 1 : 4) / 2;
   // stage dY of step jd and the S window of step js into `slot` (OP_FP4
-  // stages the window one step ahead: js = jd + 1); out-of-range steps read
-  // zeros / padding
-  // (steps past the end stage zeros / padding: the loop issues two steps
-  // ahead unconditionally, branch-free)
+  // stages the window one step ahead: js = jd + 1).  The loop issues two
+  // steps ahead unconditionally: steps out of range are clamped to real ones
+  // (valid addresses; what they stage is never used).
   struct Stage {
-    uint64_t dyu, sxu;
-    int top, bot;
-    bool dok, sok;
-    unsigned char* dst;
+    const unsigned char* dyp;  // the step's first dY pixel
+    const unsigned char* sxp;  // the step's first S row
+    bool top, bot;             // window row 0 / R + 1 is outside the image
+    int dst;                   // LDS byte offset of this wave's piece 0
   };
   auto prep = [&](int jd, int js, int slot) -> Stage {
     Stage t;
-    t.dok = jd >= 0 && jd < a.nsteps;
-    t.sok = js >= 0 && js < a.nsteps;
-    t.dyu = (uint64_t)(uintptr_t)(dyb + (long long)(t.dok ? jd : 0) * dy_step);
-    t.sxu = (uint64_t)(uintptr_t)(sxb + (long long)(t.sok ? js : 0) * sx_step);
-    const int h0 = t.sok ? (int)(((long long)js * R) % H) : 0;
-    t.top = h0 == 0 ? 1 : -100;          // window row 0 is above the image
-    t.bot = h0 + R == H ? R + 2 : -100;  // window row R + 1 is below it
-    t.dst = smem + slot * G::SLOT + wave * 1024;
+    jd = min(max(jd, 0), a.nsteps - 1);
+    js = min(max(js, 0), a.nsteps - 1);
+    t.dyp = dyb + (long long)jd * dy_step;
+    t.sxp = sxb + (long long)js * sx_step;
+    const int h0 = (int)(((long long)js * R) % H);
+    t.top = h0 == 0;
+    t.bot = h0 + R == H;
+    t.dst = slot * G::SLOT + wave_u * 1024;
     return t;
   };
-  const uint64_t ppu = (uint64_t)(uintptr_t)pp, zpu = (uint64_t)(uintptr_t)zp;
+  const unsigned lds0 = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)smem;
   auto piece = [&](const Stage& t, int k) {
     if constexpr (!do_load) return;
-    // branch-free source selection (selects, no divergent branches)
-    const int kd = src[k] & 15, off = src[k] & ~15;
-    const bool pad = kd >= 14 || kd == t.top || kd == t.bot || (kd == 0 ? !t.dok : !t.sok);
-    const uint64_t real = (kd == 0 ? t.dyu : t.sxu) + (uint64_t)(int64_t)off;
-    const uint64_t fill = kd == 15 || kd == 0 || !t.sok ? zpu : ppu;
-    ZK_GLDS16((const void*)(uintptr_t)(pad ? fill : real), t.dst + k * 4096);
+    const unsigned char* base;
+    if (k < G::KD) {
+      base = t.dyp;
+    } else {
+      // staged row of this piece (wave-uniform) and its window row
+      const int r = (k - G::KD) * (4 / G::RBK) + wave_u / G::RBK;
+      const int wr = FP4 ? r : r % (R + 2);
+      // a padding row: the pad page, offset back by the row offset folded in loff
+      const bool pad = (wr == 0 && t.top) || (wr == R + 1 && t.bot);
+      base = pad ? padp - (wr - 1) * srow : t.sxp;
+    }
+    const unsigned char* src = loff[k] == WR_HALO ? padp : base + loff[k];
+    glds16_at(src, lds0 + t.dst + k * 4096);
   };
   auto issue = [&](int jd, int js, int slot) {
     const Stage t = prep(jd, js, slot);
@@ -275,48 +321,51 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
   };
 
   // OP_FP4: expand the e2m1 window staged in `slot` into bf16 window buffer
-  // `buf` (chunks c0, c0 + 256, ... of this thread; `part` of the NPART parts
-  // this is split into so it can interleave with the MFMAs)
+  // `buf`, chunk c (of CPT) of this thread: 4 B of nibbles -> 16 B of bf16
+  // (8 channels of one pixel); chunks cover the real window pixels only
   constexpr int CPT = (G::CHUNKS + WR_NT - 1) / WR_NT;  // chunks per thread
-  constexpr int CPP = (R + 2) * PW * 4;                  // chunks per plane
+  constexpr int CPP = (R + 2) * G::CPR;                  // chunks per plane
   auto expand_read = [&](int slot, int c) -> uint32_t {
     const int o = min(c * WR_NT + tid, G::CHUNKS - 1);
     const int plane = o / CPP, rem = o % CPP;
-    const int pix = rem >> 2, q = rem & 3;
-    return *reinterpret_cast<const uint32_t*>(smem + slot * G::SLOT + G::DBYTES + pix * 32 +
-                                              plane * 16 + q * 4);
+    const int row = rem / G::CPR, q = rem % G::CPR;
+    return *reinterpret_cast<const uint32_t*>(smem + slot * G::SLOT + G::SOFF + row * G::R4B +
+                                              (q >> 2) * 32 + plane * 16 + (q & 3) * 4);
   };
   // (lanes past the last chunk redo the last one: same bytes, no branch)
   auto expand_write = [&](int buf, int c, uint32_t v) {
     const int o = min(c * WR_NT + tid, G::CHUNKS - 1);
+    const int plane = o / CPP, rem = o % CPP;
+    const int row = rem / G::CPR, q = rem % G::CPR;
     typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
     uint4 out;
     out.x = __builtin_bit_cast(uint32_t, (bf2)__builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(v, 1.0f, 0));
     out.y = __builtin_bit_cast(uint32_t, (bf2)__builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(v, 1.0f, 1));
     out.z = __builtin_bit_cast(uint32_t, (bf2)__builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(v, 1.0f, 2));
     out.w = __builtin_bit_cast(uint32_t, (bf2)__builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(v, 1.0f, 3));
-    *reinterpret_cast<uint4*>(smem + G::SBF + buf * G::SBYTES + o * 16) = out;
+    *reinterpret_cast<uint4*>(smem + G::SBF + buf * G::SBYTES + plane * G::SPLANE + row * RB +
+                              (q >> 2) * 64 + (q & 3) * 16) = out;
   };
 
   // fragment offsets: lane group gq = lane >> 4 reads pixels p = kk*16 +
   // 8*(gq>>1) + q (and + 4) of the step, 4 channels at (gq&1)*16 + 4p of its
-  // 32-channel plane.  dY: offD + kk KB.  S: the pixel's window position
-  // (r*PW + w) * 64 = (p + 2r) * 64 with r = p / W: a compile-time offset
-  // from offS0 except where the lanes of one K-step straddle an image row
-  // (then r differs by one across lanes: offS0 + 128 for those lanes, xS).
+  // 32-channel plane.  dY: offDp + hh*DPLANE + kk KB.  S: the pixel's window position
+  // r*RB + (w + 1)*64 - 64 = p*64 + r*(RB - W*64) with r = p / W: a
+  // compile-time offset from offS0 except where the lanes of one K-step
+  // straddle an image row (then r differs by one across lanes: offS0 +
+  // RB - W*64 for those lanes, xS).
   const int gq = lane >> 4, qi = lane & 15, qq = qi >> 2, pq = qi & 3;
   const int colb = (gq & 1) * 32 + pq * 8;
   const int p0 = 8 * (gq >> 1) + qq;  // 0 .. 11
-  const int offDp = p0 * 64 + colb;  // SPLIT: both co halves (+ h * DPLANE)
-  const int offD = wm * G::DPLANE + offDp;
+  const int offDp = p0 * 64 + colb;  // co half hh: + hh * DPLANE
   const int offS0 = wn * G::SPLANE + p0 * 64 + colb;  // from the S window base
-  int xS[WR_NK][2];  // per (kk, hf): offS0 + 128 * (r - r_min) (used where lanes straddle)
+  int xS[WR_NK][2];  // per (kk, hf): offS0 + (RB - W*64) * (r - r_min) (where lanes straddle)
 #pragma unroll
   for (int kk = 0; kk < WR_NK; ++kk)
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       const int q0 = kk * 16 + 4 * hf;
-      xS[kk][hf] = offS0 + 128 * ((q0 + p0) / W - q0 / W);
+      xS[kk][hf] = offS0 + (RB - W * 64) * ((q0 + p0) / W - q0 / W);
     }
 
   uint32_t ones;
@@ -332,20 +381,18 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
   const long long DWN = (long long)a.Cout * NT9;
   const int ci = ci0 + wn * 32 + r32;
 
-  // The main loop and the partial-tile stores, per member M of the wave's
-  // schedule (a wave-uniform branch around all of it, so each path keeps its
-  // own accumulators in registers: no copies at the join):
-  //   SPLIT: M = 0 (waves 0, 1) / 1 (waves 2, 3) of the ci half wn; a wave
-  //     covers both co halves (64 x 32) on taps 0-3 (M 0) or 5-8 (M 1) of
-  //     every K-step and tap 4 of K-steps 0-3 (M 0) or 4-6 (M 1): 32 / 31
-  //     (K-step, tap) units of two MFMAs that share one S fragment; the two
-  //     tap-4 partials are combined through LDS in a fixed order.
-  //   else:  M = 2, the 32 x 32 tile (wm, wn) on all 9 taps.
-  // Returns false if the block is done (no tree work).
+  // The main loop and the partial-tile stores, per pair member M (waves 0,
+  // 1: M 0; waves 2, 3: M 1) of the ci half wn, in a wave-uniform branch
+  // around all of it, so each path keeps its own accumulators in registers
+  // (no copies at the join).  A wave covers both co halves (64 x 32) on taps
+  // 0-3 (M 0) or 5-8 (M 1) of every K-step and tap 4 of K-steps 0-3 (M 0) or
+  // 4-6 (M 1): 32 / 31 (K-step, tap) units of two MFMAs that share one S
+  // fragment; the two tap-4 partials are combined through LDS in a fixed
+  // order.  Returns false if the block is done (no tree work).
   auto body = [&](auto mc) -> bool {
     constexpr int M = decltype(mc)::value;
-    constexpr int NH = M < 2 ? 2 : 1;      // co halves per wave
-    constexpr int NT = M < 2 ? 5 : 9;      // taps held
+    constexpr int NH = 2;                  // co halves per wave
+    constexpr int NT = 5;                  // taps held
     constexpr int NU = wr_units(M);        // units per step
     f32x16 acc[NH][NT];
 #pragma unroll
@@ -403,7 +450,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
       }
       if constexpr (!do_mma) continue;
       const int base = slot * G::SLOT;
-      const int sbase = FP4 ? G::SBF + (j & 1) * G::SBYTES : base + G::DBYTES;
+      const int sbase = FP4 ? G::SBF + (j & 1) * G::SBYTES : base + G::SOFF;
       // OP_FP4: the window of step j + 1 is expanded for the next iteration
       // (unconditionally: after the last step it fills a buffer nobody reads).
       // Each S fragment is read FD units ahead into a small rotating buffer
@@ -424,7 +471,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
           const int q0 = kk * 16 + 4 * hf;
           // lanes p0 = 0 .. 11 of this K-step in one image row: a constant offset
           const bool one_row = q0 / W == (q0 + 11) / W;
-          o[hf] = (one_row ? sbase + offS0 : sbase + xS[kk][hf]) + (q0 + 2 * (q0 / W)) * 64 +
+          o[hf] = (one_row ? sbase + offS0 : sbase + xS[kk][hf]) + q0 * 64 + (q0 / W) * (RB - W * 64) +
                   kh * RB + kw * 64;
         }
         fb[n % NB] = tr_read2(smem, o[0], o[1]);
@@ -432,7 +479,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
       auto read_a = [&](int kk) {
 #pragma unroll
         for (int hh = 0; hh < NH; ++hh) {
-          const int aD = base + (M < 2 ? hh * G::DPLANE + offDp : offD) + kk * 1024;
+          const int aD = base + hh * G::DPLANE + offDp + kk * 1024;
           fa[kk % 3][hh] = tr_read2(smem, aD, aD + 256);
         }
       };
@@ -449,10 +496,10 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
 #pragma unroll
       for (int n = 0; n < NU; ++n) {
         if constexpr (spread && do_mma) {
-          // DMA piece k at unit k * NU / NI
-#pragma unroll
-          for (int k = 0; k < NI; ++k)
-            if (n == k * NU / NI) piece(nx, k);
+          // DMA piece k at unit k * DS
+          constexpr int DS = NU / NI;
+          static_assert(DS >= 1, "DMA spread");
+          if (n % DS == 0 && n / DS < NI) piece(nx, n / DS);
         }
         if (n + FD < NU) {
           if (first_of_kk(n + FD)) read_a(wr_unit_kk(M, n + FD));
@@ -501,7 +548,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
         dbg[6] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID
       }
     }
-    if constexpr (M < 2) {
+    {
       // tap 4: member 1 hands its partial to member 0 through LDS (fixed
       // order: member 0's + member 1's); 8 KB per wave
       float4* cb = reinterpret_cast<float4*>(smem);
@@ -530,7 +577,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
       }
     }
     // ---- this wave's final partial taps: D[co][ci] of tap t: co = co0 + 32*cw
-    // + (e&3) + 8*(e>>2) + 4*(lane>>5) with cw = hh (SPLIT) or wm, ci = ci0 +
+    // + (e&3) + 8*(e>>2) + 4*(lane>>5) with cw = hh, ci = ci0 +
     // wn*32 + (lane&31).  Member 1's tap 4 went to member 0.
     constexpr int TLO = M == 1 ? 1 : 0;
     if (a.levels == 0) {  // one split: straight into dW
@@ -541,7 +588,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int t = wr_slot_tap(M, ti);
-            const int co = co0 + (M < 2 ? hh : wm) * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int co = co0 + hh * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
             const long long idx = (long long)co * NT9 + (long long)t * a.Cin + ci;
             if (!a.w || fabsf(a.w[idx]) <= a.clip) a.dw[idx] += acc[hh][ti][e];
           }
@@ -562,21 +609,14 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_rows_kernel(WrArgs a) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int t = wr_slot_tap(M, ti);
-          const int co = co0 + (M < 2 ? hh : wm) * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const int co = co0 + hh * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
           __hip_atomic_store(sl + (long long)co * NT9 + (long long)t * a.Cin + ci, acc[hh][ti][e],
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     return true;
   };
-  bool more;
-  if constexpr (SPLIT) {
-    if (wave < 2)
-      more = body(std::integral_constant<int, 0>{});
-    else
-      more = body(std::integral_constant<int, 1>{});
-  } else {
-    more = body(std::integral_constant<int, 2>{});
-  }
+  const bool more = wave < 2 ? body(std::integral_constant<int, 0>{})
+                             : body(std::integral_constant<int, 1>{});
   if (!more) {
     lab_end();
     return;
@@ -685,9 +725,10 @@ struct WrPlan {
 };
 
 // Supported: W in {56, 28} (a step = 112 pixels = R whole image rows), H % R
-// == 0 (steps never straddle images), channels in multiples of 64.
+// == 0 (steps never straddle images), channels in multiples of 64, Cin <=
+// WR_MAXCIN (the pad-row pages; the 64 / 128-channel stages this serves).
 bool wr_plan(int B, int H, int W, int Cin, int Cout, int target_blocks, WrPlan& p) {
-  if (B < 1 || H < 1 || Cin % 64 || Cout % 64 || Cin > 1024 || Cout > 1024) return false;
+  if (B < 1 || H < 1 || Cin % 64 || Cout % 64 || Cin > WR_MAXCIN || Cout > 1024) return false;
   if (W != 56 && W != 28) return false;
   const int R = WR_RW / W;
   if (H % R) return false;
@@ -726,19 +767,37 @@ bool wr_plan(int B, int H, int W, int Cin, int Cout, int target_blocks, WrPlan& 
   return true;
 }
 
-template <int W, int OP, bool SPLIT = true, int LAB = 0, int FD = 0>
+// the pad-row pages, once per device (before the first launch on it)
+hipError_t wr_pad_ready(hipStream_t st) {
+  static bool done[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  if (!done[dev]) {
+    hipLaunchKernelGGL(wr_pad_init_kernel, dim3((WR_PADROW / 4 + 255) / 256), dim3(256), 0, st);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    done[dev] = true;
+  }
+  return hipSuccess;
+}
+
+template <int W, int OP, int LAB = 0, int FD = 0>
 hipError_t wr_launch(const WrArgs& a, unsigned grid, hipStream_t st) {
   constexpr int lds = WrGeo<W, OP>::LDS;
+  {
+    const hipError_t e = wr_pad_ready(st);
+    if (e != hipSuccess) return e;
+  }
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)wgrad_rows_kernel<W, OP, SPLIT, LAB, FD>,
+    const hipError_t e = hipFuncSetAttribute((const void*)wgrad_rows_kernel<W, OP, LAB, FD>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
                                              lds);
     if (e != hipSuccess) return e;
     attr = true;
   }
   (void)hipGetLastError();
-  hipLaunchKernelGGL((wgrad_rows_kernel<W, OP, SPLIT, LAB, FD>), dim3(grid), dim3(WR_NT), lds,
+  hipLaunchKernelGGL((wgrad_rows_kernel<W, OP, LAB, FD>), dim3(grid), dim3(WR_NT), lds,
                      st, a);
   return hipGetLastError();
 }
@@ -748,7 +807,7 @@ hipError_t wr_launch(const WrArgs& a, unsigned grid, hipStream_t st) {
 // Ablation switch of the lab (tools/wgrad_lab.py): 0 normal, 1 loads only,
 // 2 compute only, 3 compute only without the MFMAs (LDS reads only), 4
 // compute only without the S fragment reads (results are garbage in 1-4),
-// 5 the 32 x 32 wave tiles (no SPLIT), 6 lookahead 4, 7 cycle accounting
+// 6 lookahead 4, 7 cycle accounting
 // into dbg ([blocks][4 waves][8]), 8 the step's DMA issued in one burst.
 ZK_EXPORT int zk_wgrad_rows_lab(int mode, void* dbg) {
   g_wr_lab = mode;
@@ -821,20 +880,19 @@ ZK_EXPORT int zk_wgrad_rows(const void* dy, const void* sx, const void* w, void*
   a.dbg = g_wr_dbg;
   if (g_wr_lab && W == 56 && op == OP_SIGN) {  // lab ablations (tools/wgrad_lab.py)
     switch (g_wr_lab) {
-      case 1: return (int)wr_launch<56, OP_SIGN, true, 1>(a, grid, st);
-      case 2: return (int)wr_launch<56, OP_SIGN, true, 2>(a, grid, st);
-      case 3: return (int)wr_launch<56, OP_SIGN, true, 3>(a, grid, st);
-      case 4: return (int)wr_launch<56, OP_SIGN, true, 4>(a, grid, st);
-      case 5: return (int)wr_launch<56, OP_SIGN, false>(a, grid, st);
-      case 6: return (int)wr_launch<56, OP_SIGN, true, 0, 4>(a, grid, st);
-      case 7: return (int)wr_launch<56, OP_SIGN, true, 7>(a, grid, st);
-      case 8: return (int)wr_launch<56, OP_SIGN, true, 8>(a, grid, st);
+      case 1: return (int)wr_launch<56, OP_SIGN, 1>(a, grid, st);
+      case 2: return (int)wr_launch<56, OP_SIGN, 2>(a, grid, st);
+      case 3: return (int)wr_launch<56, OP_SIGN, 3>(a, grid, st);
+      case 4: return (int)wr_launch<56, OP_SIGN, 4>(a, grid, st);
+      case 6: return (int)wr_launch<56, OP_SIGN, 0, 4>(a, grid, st);
+      case 7: return (int)wr_launch<56, OP_SIGN, 7>(a, grid, st);
+      case 8: return (int)wr_launch<56, OP_SIGN, 8>(a, grid, st);
       default: return (int)hipErrorInvalidValue;
     }
   }
   if (g_wr_lab == 7 && W == 56) {
-    if (op == OP_IMG) return (int)wr_launch<56, OP_IMG, true, 7>(a, grid, st);
-    return (int)wr_launch<56, OP_FP4, true, 7>(a, grid, st);
+    if (op == OP_IMG) return (int)wr_launch<56, OP_IMG, 7>(a, grid, st);
+    return (int)wr_launch<56, OP_FP4, 7>(a, grid, st);
   }
   switch (op * 2 + (W == 56)) {
     case OP_IMG * 2 + 1: return (int)wr_launch<56, OP_IMG>(a, grid, st);

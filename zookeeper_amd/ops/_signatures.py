@@ -43,6 +43,7 @@ SIGNATURES = {
     "zk_igemm_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
     "zk_igemm_dgrad_bnsum": (I32, [P] * 9 + [I32] * 15 + [P]),
     "zk_igemm_dgrad_fstats": (I32, [P] * 4 + [I32] * 14 + [P]),
+    "zk_igemm_dgrad_bsums": (I32, [P] * 7 + [I32, P] + [I32] * 14 + [P]),
     "zk_igemm_fwd": (I32, [P, P, P, P] + [I32] * 16 + [P]),
     "zk_igemm_fwd_fp4": (I32, [P, P, P, P] + [I32] * 16 + [P]),
     "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),
@@ -64,7 +65,7 @@ SIGNATURES = {
     "zk_igemm_fwd_bf16_supported": (I32, [I32] * 13),
     "zk_igemm_fwd_supported": (I32, [I32] * 15),
     "zk_bconv_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P]),
-    "zk_bn_apply_res_bf16": (I32, [P, P, P, P, I64, I32, I32, P]),
+    "zk_bn_apply_res_bf16": (I32, [P, P, P, P, P, I64, I32, I32, P]),
     "zk_bn_bwd_dx_res_bf16": (I32, [P, P, P, P, P, P, I64, I32, P]),
     # small-K convolutions (smallconv.hip)
     "zk_smallk_conv_fwd": (I32, [P, P, P] + [I32] * 12 + [P]),

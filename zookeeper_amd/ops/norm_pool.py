@@ -33,9 +33,40 @@ def supported(x: torch.Tensor) -> bool:
             and x.shape[1] % 8 == 0 and 1 <= cg <= 256 and cg & (cg - 1) == 0)
 
 
+class FloatBnSum:
+    """Hand-off of a float BatchNorm's backward reduction to the data gradient
+    of the layer that consumes its output (``pointwise.conv1x1``): that
+    kernel's LDS epilogue adds (sum g', sum g' * xhat) over the gradient it
+    stores into ``sums`` (the channel-major copies ``zk_bn_bwd_coef`` reads
+    and re-zeroes), with g' masked by the BN's ReLU (``relu``: 0 none, 1
+    recomputed from the input ``xn`` and ``coef``, 2 the stored ``mask`` bits).
+    The BN backward uses them only if they were taken over exactly the
+    gradient it receives (:meth:`reduced`: same storage, not modified since);
+    otherwise it re-zeroes ``sums`` and runs its own reduction."""
+
+    __slots__ = ("xn", "coef", "mask", "relu", "sums", "dx", "dx_version")
+
+    def __init__(self, xn, coef, mask, relu: int, sums):
+        self.xn, self.coef, self.mask, self.relu, self.sums = xn, coef, mask, relu, sums
+        self.dx = self.dx_version = None
+
+    def take(self, dx) -> None:
+        """Consumer side: the sums were added over ``dx`` (its final value)."""
+        self.dx, self.dx_version = dx, dx._version
+
+    def reduced(self, dout: torch.Tensor) -> bool:
+        ok = (self.dx is not None and dout.data_ptr() == self.dx.data_ptr()
+              and dout._version == self.dx_version)
+        used = self.dx is not None
+        self.dx = None
+        if used and not ok:
+            self.sums.zero_()  # added over another gradient: not this BN's
+        return ok
+
+
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, bn, relu, handoff=None):
+    def forward(ctx, x, gamma, beta, residual, bn, relu, handoff=None, holder=None):
         dim = x.dim()
         C = x.shape[1]
         xn = _nhwc(x)
@@ -88,10 +119,17 @@ class _BatchNormFn(torch.autograd.Function):
             coef[2] = bn.running_mean
             coef[3] = rstd
         y = torch.empty_like(xn)
+        omask = None
         if residual is not None:
             rn = _nhwc(residual.to(torch.bfloat16))
+            # BN + residual + ReLU: the backward needs the output's ReLU mask,
+            # which x alone does not give: 1 bit per element, not the output
+            omask = (torch.empty((P, C // 8), dtype=torch.uint8, device=dev)
+                     if relu and any(ctx.needs_input_grad) else None)
             check(L.zk_bn_apply_res_bf16(xn.data_ptr(), coef.data_ptr(), rn.data_ptr(),
-                                         y.data_ptr(), P, C, int(relu), st), "zk_bn_apply_res_bf16")
+                                         y.data_ptr(),
+                                         omask.data_ptr() if omask is not None else None, P, C,
+                                         int(relu), st), "zk_bn_apply_res_bf16")
         else:
             check(L.zk_bn_apply_bf16(xn.data_ptr(), coef.data_ptr(), y.data_ptr(), P, C, int(relu),
                                      st), "zk_bn_apply_bf16")
@@ -100,7 +138,17 @@ class _BatchNormFn(torch.autograd.Function):
         # BN + ReLU without a residual keeps no output: the backward kernels
         # recompute the ReLU mask from x (one read less in each of them)
         ctx.relu_rc = relu and residual is None
-        ctx.save_for_backward(xn, y if (relu and residual is not None) else None, coef, gamma)
+        ctx.save_for_backward(xn, omask, coef, gamma)
+        # backward reduction handed to the consumer's data-gradient epilogue
+        ctx.fsum = None
+        if (holder is not None and bn.training and not OPTS.deterministic and OPTS.bn_bwd_fuse
+                and any(ctx.needs_input_grad)):
+            mode = 2 if omask is not None else (1 if relu else 0)
+            if not (relu and residual is not None and omask is None):
+                sums = zeroed_scratch(bn, "bwd_sums_fused", (2, C, L.zk_bn_bwd_parts_max()),
+                                      torch.float32, dev)
+                ctx.fsum = FloatBnSum(xn, coef, omask, mode, sums)
+                holder.append(ctx.fsum)
         ctx.params = (gamma, beta)
         ctx.dim, ctx.P, ctx.C = dim, P, C
         ctx.bn = bn
@@ -109,7 +157,7 @@ class _BatchNormFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        xn, y, coef, gamma = ctx.saved_tensors
+        xn, m, coef, gamma = ctx.saved_tensors
         P, C = ctx.P, ctx.C
         dev = dy.device
         st = stream_ptr(dev)
@@ -122,14 +170,19 @@ class _BatchNormFn(torch.autograd.Function):
         # channel-major copies [2][C][parts_max]
         sums = torch.empty((2, C, L.zk_bn_bwd_parts_max()), dtype=torch.float32, device=dev)
         n = ctypes.c_int(0)
-        if ctx.relu_rc:
+        fused = ctx.fsum is not None and ctx.fsum.reduced(g)
+        if fused:
+            # the consumer's data-gradient epilogue reduced exactly this g
+            sums = ctx.fsum.sums
+            n.value = sums.shape[2]
+        elif ctx.relu_rc:
             check(L.zk_bn_bwd_reduce_relu_bf16_parts(g.data_ptr(), xn.data_ptr(),
                                                      coef.data_ptr(), sums.data_ptr(), P, C,
                                                      ctypes.byref(n), st),
                   "zk_bn_bwd_reduce_relu_bf16_parts")
         else:
             check(L.zk_bn_bwd_reduce_bf16_parts(g.data_ptr(), xn.data_ptr(),
-                                                y.data_ptr() if y is not None else None,
+                                                m.data_ptr() if m is not None else None,
                                                 coef.data_ptr(), sums.data_ptr(), P, C,
                                                 ctypes.byref(n), st),
                   "zk_bn_bwd_reduce_bf16_parts")
@@ -159,7 +212,7 @@ class _BatchNormFn(torch.autograd.Function):
         if ctx.has_res and ctx.needs_input_grad[3]:
             dres = torch.empty_like(g)
             check(L.zk_bn_bwd_dx_res_bf16(g.data_ptr(), xn.data_ptr(),
-                                          y.data_ptr() if y is not None else None,
+                                          m.data_ptr() if m is not None else None,
                                           bcoef.data_ptr(), dx.data_ptr(), dres.data_ptr(), P, C,
                                           st), "zk_bn_bwd_dx_res_bf16")
             if ctx.handoff is not None and ctx.handoff.give(dres):
@@ -174,9 +227,9 @@ class _BatchNormFn(torch.autograd.Function):
                   "zk_bn_bwd_dx_relu_bf16")
         else:
             check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), xn.data_ptr(),
-                                      y.data_ptr() if y is not None else None, bcoef.data_ptr(),
+                                      m.data_ptr() if m is not None else None, bcoef.data_ptr(),
                                       dx.data_ptr(), P, C, st), "zk_bn_bwd_dx_bf16")
-        return _back(dx, ctx.dim), dgamma, dbeta, dres, None, None, None
+        return _back(dx, ctx.dim), dgamma, dbeta, dres, None, None, None, None
 
 
 class ResidualHandoff:
@@ -221,8 +274,14 @@ def batch_norm(x: torch.Tensor, bn, relu: bool = False,
                residual: torch.Tensor = None, handoff: ResidualHandoff = None) -> torch.Tensor:
     """``act(bn(x) [+ residual])`` in one pass (forward) / one pass (the
     data gradient, plus the residual's gradient when given — or left in
-    ``handoff`` for the residual's other consumer)."""
-    return _BatchNormFn.apply(x, bn.weight, bn.bias, residual, bn, relu, handoff)
+    ``handoff`` for the residual's other consumer).  In training the output
+    carries ``_zk_fbnsum`` (:class:`FloatBnSum`): a consumer that computes
+    its whole gradient may reduce the backward sums in its epilogue."""
+    holder: list = []
+    y = _BatchNormFn.apply(x, bn.weight, bn.bias, residual, bn, relu, handoff, holder)
+    if holder:
+        y._zk_fbnsum = holder[0]
+    return y
 
 
 class _MaxPoolFn(torch.autograd.Function):

@@ -69,6 +69,11 @@ class KernelOptions:
     # ... and weight-gradient kernel for the stride-1 3x3 convs with >= 256
     # input and output channels.
     wgrad_deep: bool = True
+    # Float BatchNorm backward sums (sum g, sum g*xhat) added up in the data-
+    # gradient epilogue of the 1x1 conv that consumes the BN output (when that
+    # epilogue writes the BN output's whole gradient) instead of a separate
+    # reduction pass over g and x (outside the deterministic mode).
+    bn_bwd_fuse: bool = True
     # Float conv weights as persistent bf16 GEMM-layout images written by the
     # fused optimizer (ops/weight_images.py) instead of a cast / transpose
     # per conv and pass.

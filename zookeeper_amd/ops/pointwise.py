@@ -108,6 +108,11 @@ class _Conv1x1Fn(torch.autograd.Function):
                                    B, H, W, Cout, H, W, Cin, 1, 1, 1, 0, 0, -1, st),
                   "zk_igemm_dgrad(1x1 fwd)")
         ctx.save_for_backward(x2, w2)
+        # the producing BatchNorm's backward sums, reduced in our dgrad
+        # epilogue when it writes x's whole gradient (norm_pool.FloatBnSum)
+        fsum = getattr(x, "_zk_fbnsum", None)
+        ctx.fsum = (fsum if fsum is not None and give is None
+                    and tuple(fsum.xn.shape) == (B, H, W, Cin) else None)
         ctx.wt = wt
         ctx.weight = weight
         ctx.handoff, ctx.give = handoff, give
@@ -132,10 +137,23 @@ class _Conv1x1Fn(torch.autograd.Function):
             if dres is not None and tuple(dres.shape) != (B, H, W, Cin):
                 raise RuntimeError(f"residual gradient {tuple(dres.shape)} does not match the "
                                    f"1x1 conv input {(B, H, W, Cin)}")
-            check(L.zk_igemm_dgrad(g2.data_ptr(), wt.data_ptr(), None,
-                                   dres.data_ptr() if dres is not None else None, dx2.data_ptr(),
-                                   B, H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0, -1, st),
-                  "zk_igemm_dgrad(1x1)")
+            fs = ctx.fsum
+            rc = _HIP_INVALID_VALUE
+            if fs is not None:
+                rc = L.zk_igemm_dgrad_bsums(
+                    g2.data_ptr(), wt.data_ptr(), dres.data_ptr() if dres is not None else None,
+                    dx2.data_ptr(), fs.xn.data_ptr(), fs.coef.data_ptr(),
+                    fs.mask.data_ptr() if fs.mask is not None else None, fs.relu,
+                    fs.sums.data_ptr(), fs.sums.shape[2], B, H, W, Cin, H, W, Cout, 1, 1, 1, 0,
+                    0, -1, st)
+                if rc != _HIP_INVALID_VALUE:
+                    check(rc, "zk_igemm_dgrad_bsums(1x1)")
+                    fs.take(dx2)
+            if rc == _HIP_INVALID_VALUE:  # no LDS-epilogue tile: the plain GEMM
+                check(L.zk_igemm_dgrad(g2.data_ptr(), wt.data_ptr(), None,
+                                       dres.data_ptr() if dres is not None else None,
+                                       dx2.data_ptr(), B, H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0,
+                                       -1, st), "zk_igemm_dgrad(1x1)")
             if ctx.give is not None and ctx.give.give(dx2.view(B, H, W, Cin)):
                 dx = None  # x's other consumer adds it (a downsampling shortcut conv)
             else:

@@ -47,6 +47,7 @@ class Runtime:
     dgrad_deep: bool = Field(True)
     wgrad_deep: bool = Field(True)
     weight_images: bool = Field(True)
+    bn_bwd_fuse: bool = Field(True)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
     deterministic: bool = Field(False)
