@@ -83,14 +83,20 @@ struct ConvArgs {
   // float dgrad through the LDS epilogue (optional): the backward sums of the
   // BatchNorm whose output gradient is exactly the dx stored here (float BN,
   // bf16 input bxb [P][Cin], coefficients bcoef [4][Cin] = scale, shift,
-  // mean, rstd): bsums[0][c][stripe] += sum g', [1][c][stripe] += sum g' *
-  // xhat, g' = dx * relu mask (brelu 0: none, 1: recomputed from bxb, 2: the
-  // bits bmask [P][Cin/8]) -- the channel-major copies zk_bn_bwd_coef reads.
+  // mean, rstd): bsums[mtile][0][c] = sum g', [mtile][1][c] = sum g' * xhat
+  // over the block's pixels (plain stores, one row per M tile: stripes >=
+  // m_tiles), g' = dx * relu mask (brelu 0: none, 1: recomputed from bxb, 2:
+  // the bits bmask [P][Cin/8]); zk_bn_bwd_tiles_reduce folds the rows in a
+  // fixed order into the channel-major copies zk_bn_bwd_coef reads.
   const uint16_t* bxb;
   const float* bcoef;
   const uint8_t* bmask;
   int brelu;
   float* bsums;
+  // LDS epilogue (optional): dres is masked by these bits [P][Cin/8] before
+  // it is added (a ResNet tail's residual gradient g * relu mask, handed over
+  // as g and the mask instead of a materialised tensor)
+  const uint8_t* dmask;
 };
 
 // Host-side kernel options, set from Python (ops/options.py -> zk_set_option;
@@ -120,6 +126,9 @@ int g_opt_dgrad_deep = 1;
 // wgrad_deep (key 7): the same for stride-1 3x3 weight gradients with
 // Cin % 256 == 0 and Cout % 256 == 0 (variant 60 of the wgrad dispatch).
 int g_opt_wgrad_deep = 1;
+// epilogue_prefetch (key 8): the LDS-epilogue dgrad prefetches its residual /
+// BN-input loads in groups of 4 chunks before they are needed.
+int g_opt_epilogue_prefetch = 1;
 
 // splits limited by the slab cap (plan_wgrad / plan_wgrad3)
 inline long long cap_splits(long long splits, long long dw_bytes) {
@@ -228,7 +237,7 @@ __device__ __forceinline__ void dgrad_store_block(const ConvArgs& args, const IG
 // register epilogue (masked fp32 + residual, one rounding).  pix(m) maps a
 // tile row to its pixel.  The ring is free once every wave is past its last
 // fragment read (first barrier).
-template <int BM, int BN, int WM, int NT, int TM, int TN, typename PixFn>
+template <int BM, int BN, int WM, int NT, int TM, int TN, bool EPF, typename PixFn>
 __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeom& g,
                                                 const f32x16 (&acc)[TM][TN], unsigned char* smem,
                                                 long long m0, long long M, int n0, int wm,
@@ -272,8 +281,39 @@ __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeo
       brs[k] = args.bcoef[3 * g.Cin + c0 + k];
     }
   }
+  // the store pass of a half tile: ITER 16-B chunks per thread; their
+  // residual-gradient / BN-input loads are issued before the half is staged
+  // (latency hidden behind the staging and the barrier instead of exposed
+  // once per chunk)
+  constexpr int ITER = (BM / 2) * (BN / 8) / NT;
+  static_assert((BM / 2) * (BN / 8) % NT == 0, "LDS epilogue: chunks per thread");
+  // chunks whose loads are in flight together (EPF off: one, as loaded at use)
+  constexpr int PF = !EPF ? 1 : ITER > 4 ? 4 : ITER;
+  static_assert(ITER % PF == 0, "LDS epilogue: prefetch groups");
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
+    long long offs[PF];
+    uint4 dq[PF], xq[PF];
+    uint32_t mq[PF], dm[PF];
+    // loads of chunks it0 .. it0 + PF - 1
+    auto prefetch = [&](int it0) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int i = tid + (it0 + u) * NT;
+        const int lr = i / (BN / 8), j = i % (BN / 8);
+        const int row = (lr / (WTM / 2)) * WTM + (p * HT + (lr % (WTM / 2)) / 32) * 32 + lr % 32;
+        const long long m = m0 + row;
+        offs[u] = m < M ? pix(m) * g.Cin + n0 + 8 * j : -1;
+        const long long o = offs[u] < 0 ? 0 : offs[u];
+        dq[u] = (dres && offs[u] >= 0) ? *reinterpret_cast<const uint4*>(dres + o)
+                                       : make_uint4(0u, 0u, 0u, 0u);
+        xq[u] = (bsm && offs[u] >= 0) ? *reinterpret_cast<const uint4*>(args.bxb + o)
+                                      : make_uint4(0u, 0u, 0u, 0u);
+        mq[u] = (bsm && args.brelu == 2 && offs[u] >= 0) ? args.bmask[o >> 3] : 0xFFu;
+        dm[u] = (args.dmask && offs[u] >= 0) ? args.dmask[o >> 3] : 0xFFu;
+      }
+    };
+    prefetch(0);
     __syncthreads();  // the ring (p = 0) / the previous half's tile is free
 #pragma unroll
     for (int aa = 0; aa < HT; ++aa) {
@@ -297,24 +337,28 @@ __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeo
       }
     }
     __syncthreads();
-    for (int i = tid; i < (BM / 2) * (BN / 8); i += NT) {
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int u = it % PF;
+      if (u == 0 && it > 0) prefetch(it);
+      const int i = tid + it * NT;
       const int lr = i / (BN / 8), j = i % (BN / 8);
-      const int row = (lr / (WTM / 2)) * WTM + (p * HT + (lr % (WTM / 2)) / 32) * 32 + lr % 32;
-      const long long m = m0 + row;
-      if (m >= M) continue;
+      const long long off = offs[u];
+      if (off < 0) continue;
       const unsigned char* rb = smem + lr * (BN * 4);
       const int sw = lr & (NCH - 1);
       const float4 f0 = *reinterpret_cast<const float4*>(rb + (((2 * j) ^ sw) << 4));
       const float4 f1 = *reinterpret_cast<const float4*>(rb + (((2 * j + 1) ^ sw) << 4));
       float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-      const long long off = pix(m) * g.Cin + n0 + 8 * j;
       if (dres) {
-        const uint4 d = *reinterpret_cast<const uint4*>(dres + off);
+        const uint4 d = dq[u];
         const uint32_t dd[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          v[2 * k] += zk::bf16_to_f32((uint16_t)(dd[k] & 0xffff));
-          v[2 * k + 1] += zk::bf16_to_f32((uint16_t)(dd[k] >> 16));
+          const float lo = zk::bf16_to_f32((uint16_t)(dd[k] & 0xffff));
+          const float hi = zk::bf16_to_f32((uint16_t)(dd[k] >> 16));
+          v[2 * k] += (dm[u] >> (2 * k)) & 1u ? lo : 0.f;
+          v[2 * k + 1] += (dm[u] >> (2 * k + 1)) & 1u ? hi : 0.f;
         }
       }
       const uint4 o = make_uint4(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
@@ -323,10 +367,9 @@ __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeo
       if (bsm) {
         // the BN-backward sums over the stored gradient (zk_bn_bwd_reduce of
         // the BN whose output this dx is the whole gradient of)
-        const uint4 xq = *reinterpret_cast<const uint4*>(args.bxb + off);
-        const uint32_t xw[4] = {xq.x, xq.y, xq.z, xq.w};
+        const uint32_t xw[4] = {xq[u].x, xq[u].y, xq[u].z, xq[u].w};
         const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
-        const uint32_t mb = args.brelu == 2 ? args.bmask[off >> 3] : 0xFFu;
+        const uint32_t mb = mq[u];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float xk = zk::bf16_to_f32((uint16_t)(xw[k >> 1] >> (16 * (k & 1))));
@@ -353,7 +396,7 @@ __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeo
     }
   }
   if (bsm) {
-    // as the statistics below, into the fp32 channel-major copies
+    // as the statistics below, into this M tile's fp32 channel-major copy
     constexpr int JC = BN / 8, RPT = NT / JC;
     static_assert(NT * 16 * 4 <= BM * BN * 2, "LDS epilogue: sums exchange");
     float* red = reinterpret_cast<float*>(smem);
@@ -364,13 +407,13 @@ __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeo
       red[tid * 16 + 8 + k] = fs2[k];
     }
     __syncthreads();
-    const int stripe = args.stripes > 1 ? (int)(blockIdx.x % args.stripes) : 0;
+    const long long copy = m0 / BM;  // this block's M tile (stride 1: one parity class)
     for (int c = tid; c < 2 * BN; c += NT) {
       const int which = c / BN, nl = c % BN, j = nl >> 3, k = nl & 7;
       float t = 0.f;
 #pragma unroll 4
       for (int r = 0; r < RPT; ++r) t += red[(r * JC + j) * 16 + which * 8 + k];
-      atomicAdd(args.bsums + ((long long)which * g.Cin + n0 + nl) * args.stripes + stripe, t);
+      args.bsums[(copy * 2 + which) * g.Cin + n0 + nl] = t;
     }
   }
   if (fst) {
@@ -404,7 +447,7 @@ __device__ __forceinline__ void dgrad_store_lds(const ConvArgs& args, const IGeo
 }
 
 template <bool FWD, int BM, int BN, int WM, int WN, int NS, int CB, bool F4 = false,
-          bool OB = false, bool LE = false>
+          bool OB = false, bool LE = false, bool EPF = true>
 __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs args, IGeom g,
                                                                      int m_tiles) {
   constexpr int NWAVES = WM * WN;
@@ -719,7 +762,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
     } else if constexpr (LE) {
       static_assert(BM * BN * 2 <= NS * STAGE, "LDS epilogue: the ring holds half the tile");
       const int W = g.W, H = g.H;
-      dgrad_store_lds<BM, BN, WM, NWAVES * 64, TM, TN>(
+      dgrad_store_lds<BM, BN, WM, NWAVES * 64, TM, TN, EPF>(
           args, g, acc, smem, m0, M, n0, wm, wn * WTN, h, r32, tid,
           [=](long long mc) -> long long {
             if (s == 1) return mc;
@@ -1126,30 +1169,37 @@ struct BnSum {
   const void* bmask = nullptr;
   int brelu = 0;
   void* bsums = nullptr;
+  const void* dmask = nullptr;  // LE variants only: ConvArgs::dmask
 };
 
 template <int BM, int BN, int WM, int WN, int NS, int CB = 128, bool LE = false>
 int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const void* dres,
                        void* dx, const IGeom& g, const BnSum& bs, hipStream_t stream) {
   if (LE && bs.sums) return (int)hipErrorInvalidValue;  // fused BN sums: register epilogue
-  if (!LE && (bs.fstats || bs.bsums)) return (int)hipErrorInvalidValue;  // LDS epilogue only
+  if (!LE && (bs.fstats || bs.bsums || bs.dmask))
+    return (int)hipErrorInvalidValue;  // LDS epilogue only
   if ((g.Cout * 2) % CB || g.Cin % BN || g.s > 2 || g.kh > 4 || g.kw > 4)
     return (int)hipErrorInvalidValue;
   if (g_dry_run) return 0;
   constexpr int LDS = NS * (BM + BN) * CB;
   static_assert(LDS <= 160 * 1024, "LDS");
-  auto kern = igemm_conv_kernel<false, BM, BN, WM, WN, NS, CB, false, false, LE>;
-  static bool attr = false;
-  if (!attr) {
+  // LE: the epilogue's residual / BN-input loads prefetched in groups
+  // (runtime.epilogue_prefetch) or issued at each chunk
+  auto kern = !LE || g_opt_epilogue_prefetch
+                  ? igemm_conv_kernel<false, BM, BN, WM, WN, NS, CB, false, false, LE, true>
+                  : igemm_conv_kernel<false, BM, BN, WM, WN, NS, CB, false, false, LE, false>;
+  static bool attr[2] = {false, false};
+  if (!attr[g_opt_epilogue_prefetch ? 1 : 0]) {
     hipError_t e = hipFuncSetAttribute((const void*)kern,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     if (e != hipSuccess) return (int)e;
-    attr = true;
+    attr[g_opt_epilogue_prefetch ? 1 : 0] = true;
   }
   const int Hc = (g.H + g.s - 1) / g.s, Wc = (g.W + g.s - 1) / g.s;
   const long long Mc = (long long)g.B * Hc * Wc;
   const int m_tiles = (int)((Mc + BM - 1) / BM);
   const long long blocks = (long long)m_tiles * (g.Cin / BN);
+  if (bs.bsums && (g.s != 1 || m_tiles > bs.stripes)) return (int)hipErrorInvalidValue;
   ConvArgs args{(const uint16_t*)dy, (const uint16_t*)wt, (const uint32_t*)mask,
                 (const uint16_t*)dres, dx, nullptr, 0, 0, bs.stripes,
                 (const int16_t*)bs.ypred, (const float*)bs.mean, (const float*)bs.rstd,
@@ -1160,6 +1210,7 @@ int launch_igemm_dgrad(const void* dy, const void* wt, const void* mask, const v
   args.bmask = (const uint8_t*)bs.bmask;
   args.brelu = bs.brelu;
   args.bsums = (float*)bs.bsums;
+  args.dmask = (const uint8_t*)bs.dmask;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks, g.s * g.s), dim3(WM * WN * 64), LDS, stream,
                      args, g, m_tiles);
   return 0;
@@ -1319,7 +1370,7 @@ int igemm_dgrad_variant(int v, const void* dy, const void* wt, const void* mask,
                         const void* dres, void* dx, const IGeom& g, const BnSum& bs,
                         hipStream_t st) {
 #define ZK_IGD(...) return launch_igemm_dgrad<__VA_ARGS__>(dy, wt, mask, dres, dx, g, bs, st)
-  if ((bs.fstats || bs.bsums) && (v < 40 || v > 48))
+  if ((bs.fstats || bs.bsums || bs.dmask) && (v < 40 || v > 48))
     return (int)hipErrorInvalidValue;  // LE variants only
   switch (v) {
     case 0: ZK_IGD(128, 128, 2, 2, 2);        // 64 KB: 2 WG/CU
@@ -1984,12 +2035,16 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     const bool c3 = conv3_ok(g, 0);
     const bool le = bs.sums == nullptr;  // (bs.bsums: LE variants, checked at the launch)
     const int v256 = le ? 45 : 14;
-    if (g_opt_dgrad_deep && le && !bs.fstats && c3 && Cin % 256 == 0 && g.Cout % 64 == 0)
+    if (g_opt_dgrad_deep && le && !bs.fstats && !bs.bsums && !bs.dmask && c3 &&
+        Cin % 256 == 0 && g.Cout % 64 == 0 && !mask)
       // phased 256x256 schedule (deep_gemm.hip).  Measured at batch 1536 it
       // ties the 256x256 implicit GEMM (14x14x256: 428-484 vs 495 us; 7x7x512
       // 432-462 vs 406 us) and loses for 128 channels (769 vs 594 us) and the
       // stride-2 transitions, so only the stride-1 >= 256-channel layers take it
-      // by default (profiles/r4/b_deep_gemm.md)
+      // by default (profiles/r4/b_deep_gemm.md).  In the step (round 5,
+      // interleaved A/B): the float convs keep it (ResNet-50 without the deep
+      // kernels 10.71k vs 10.91k img/s); the binary ones (STE mask epilogue)
+      // do not (E18 with it off 51.6k vs 51.3k)
       variant = 60;
     else if (le && g.kh == 1 && g.kw == 1 && stride == 1 && Cin % 64 == 0)
       variant = Cin % 256 == 0 ? 45 : Cin % 128 == 0 ? 41 : 43;
@@ -2011,12 +2066,12 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
       variant = 7;
   }
   if (variant == 60) {  // deep_gemm.hip (explicit, or the default above)
-    if (bs.fstats || bs.sums || bs.bsums) return (int)hipErrorInvalidValue;
+    if (bs.fstats || bs.sums || bs.bsums || bs.dmask) return (int)hipErrorInvalidValue;
     return zk_dgrad_deep_impl(dy, wt, mask, dres, dx, g.B, g.H, g.W, g.Cin, g.Cout, g.Ho, g.Wo,
                               g.kh, g.kw, g.s, g.pt, g.pl, g_dry_run, stream);
   }
   if (variant == 50) {  // conv3rw.hip (explicit, or the default above)
-    if (bs.fstats || bs.bsums) return (int)hipErrorInvalidValue;
+    if (bs.fstats || bs.bsums || bs.dmask) return (int)hipErrorInvalidValue;
     if (g.s != 1 || g.kh != 3 || g.kw != 3 || g.pt != 1 || g.pl != 1 || g.Ho != g.H ||
         g.Wo != g.W)
       return (int)hipErrorInvalidValue;
@@ -2081,29 +2136,38 @@ ZK_EXPORT int zk_igemm_dgrad_fstats(const void* dy, const void* wt, void* dx, vo
                           variant, stream);
 }
 
-// zk_igemm_dgrad + the backward sums of the float BatchNorm whose output
-// gradient dx is (its whole gradient): sums [2][Cin][stripes] fp32
-// channel-major (atomics into copy block % stripes; zk_bn_bwd_coef reads and
-// re-zeroes them) += (sum g', sum g' * (xb - mean) * rstd) with g' = the
+// zk_igemm_dgrad with the LDS-epilogue extras (a tile with the LDS epilogue
+// only: any other choice returns hipErrorInvalidValue and the caller keeps
+// the separate passes):
+//  * dres_mask (optional): bits [P][Cin/8] masking dres before it is added;
+//  * sums (optional): the backward sums of the float BatchNorm whose output
+// gradient dx is (its whole gradient): sums [stripes][2][Cin] fp32, row m =
+// the M tile m's (sum g', sum g' * (xb - mean) * rstd) (plain stores: stripes
+// >= the tiles of any LDS-epilogue variant, BM >= 128, so >= ceil(B*H*W /
+// 128); the rows of unused tiles must be zero: zk_bn_bwd_tiles_reduce folds
+// all stripes rows in a fixed order and re-zeroes them) with g' = the
 // stored dx times the BN's ReLU mask (relu 0: none, 1: recomputed from xb
 // and the forward scale / shift, 2: bits mask [P][Cin/8]); xb bf16
 // [B][H][W][Cin] is the BN input, coef [4][Cin] = scale, shift, mean, rstd.
-// Only the LDS-epilogue variants carry the sums: any other choice returns
-// hipErrorInvalidValue and the caller keeps the separate reduction.
-ZK_EXPORT int zk_igemm_dgrad_bsums(const void* dy, const void* wt, const void* dres, void* dx,
-                                   const void* xb, const void* coef, const void* mask, int relu,
-                                   void* sums, int stripes, int B, int H, int W, int Cin, int Ho,
-                                   int Wo, int Cout, int kh, int kw, int stride, int pt, int pl,
-                                   int variant, hipStream_t stream) {
+ZK_EXPORT int zk_igemm_dgrad_ex(const void* dy, const void* wt, const void* dres,
+                                const void* dres_mask, void* dx, const void* xb,
+                                const void* coef, const void* mask, int relu, void* sums,
+                                int stripes, int B, int H, int W, int Cin, int Ho, int Wo,
+                                int Cout, int kh, int kw, int stride, int pt, int pl, int variant,
+                                hipStream_t stream) {
   IGeom g{B, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pt, pl};
-  if (!xb || !coef || !sums || Cin % 8 || relu < 0 || relu > 2 || (relu == 2 && !mask))
+  if (Cin % 8 || (dres_mask && !dres) || (!sums && !dres_mask)) return (int)hipErrorInvalidValue;
+  if (sums && (!xb || !coef || relu < 0 || relu > 2 || (relu == 2 && !mask) || stride != 1))
     return (int)hipErrorInvalidValue;
   BnSum bs{nullptr, nullptr, nullptr, nullptr, stripes < 1 ? 1 : stripes};
-  bs.bxb = xb;
-  bs.bcoef = coef;
-  bs.bmask = mask;
-  bs.brelu = relu;
-  bs.bsums = sums;
+  if (sums) {
+    bs.bxb = xb;
+    bs.bcoef = coef;
+    bs.bmask = mask;
+    bs.brelu = relu;
+    bs.bsums = sums;
+  }
+  bs.dmask = dres_mask;
   return igemm_dgrad_impl(dy, wt, nullptr, dres, dx, g, bs, variant, stream);
 }
 
@@ -2359,6 +2423,7 @@ ZK_EXPORT int zk_set_option(int key, int value) {
     case 5: g_opt_wgrad_slab_mb = value; return 0;
     case 6: g_opt_dgrad_deep = value; return 0;
     case 7: g_opt_wgrad_deep = value; return 0;
+    case 8: g_opt_epilogue_prefetch = value; return 0;
     default: return -1;
   }
 }
@@ -2371,6 +2436,7 @@ ZK_EXPORT int zk_get_option(int key) {
     case 5: return g_opt_wgrad_slab_mb;
     case 6: return g_opt_dgrad_deep;
     case 7: return g_opt_wgrad_deep;
+    case 8: return g_opt_epilogue_prefetch;
     default: return -1;
   }
 }

@@ -485,6 +485,25 @@ __global__ __launch_bounds__(256) void avgpool2_bwd_kernel(const uint16_t* __res
   }
 }
 
+// Per-tile BN-backward partials [tiles][2][C] (a GEMM epilogue's rows,
+// zk_igemm_dgrad_bsums) -> the channel-major copies [2][C][kBnBwdParts] that
+// zk_bn_bwd_coef sums: copy b = rows b, b + kBnBwdParts, ... in that order
+// (fixed: bit-reproducible), each row read once by one block and re-zeroed.
+__global__ __launch_bounds__(256) void bn_bwd_tiles_reduce_kernel(float* __restrict__ rows,
+                                                                  int tiles, int C,
+                                                                  float* __restrict__ out) {
+  const int b = blockIdx.x;
+  for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
+    float t = 0.f;
+    for (int r = b; r < tiles; r += kBnBwdParts) {
+      float* p = rows + (long long)r * 2 * C + c;
+      t += *p;
+      *p = 0.f;
+    }
+    out[(long long)c * kBnBwdParts + b] = t;
+  }
+}
+
 int rows_grid(long long P, int C) {
   const long long rb = 256 / (C / 8);
   long long b = (P + rb - 1) / rb;
@@ -663,6 +682,17 @@ ZK_EXPORT int zk_bn_bwd_reduce_bf16(const void* g, const void* x, const void* m,
 // receives one copy per block (*nparts of them); pass parts, *nparts and
 // zk_bn_bwd_parts_max() as sums / stripes / stride to zk_bn_bwd_coef.
 ZK_EXPORT int zk_bn_bwd_parts_max() { return kBnBwdParts; }
+
+// rows [tiles][2][C] (re-zeroed) -> parts [2][C][zk_bn_bwd_parts_max()]: every
+// copy written; pass parts, zk_bn_bwd_parts_max() (stripes and stride) to
+// zk_bn_bwd_coef.
+ZK_EXPORT int zk_bn_bwd_tiles_reduce(void* rows, int tiles, int C, void* parts, hipStream_t st) {
+  if (tiles < 1 || C < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_tiles_reduce_kernel, dim3(kBnBwdParts), dim3(256), 0, st,
+                     (float*)rows, tiles, C, (float*)parts);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
 
 ZK_EXPORT int zk_bn_bwd_reduce_bf16_parts(const void* g, const void* x, const void* m,
                                           const void* coef, void* parts, long long P, int C,

@@ -43,7 +43,8 @@ SIGNATURES = {
     "zk_igemm_dgrad": (I32, [P, P, P, P, P] + [I32] * 13 + [P]),
     "zk_igemm_dgrad_bnsum": (I32, [P] * 9 + [I32] * 15 + [P]),
     "zk_igemm_dgrad_fstats": (I32, [P] * 4 + [I32] * 14 + [P]),
-    "zk_igemm_dgrad_bsums": (I32, [P] * 7 + [I32, P] + [I32] * 14 + [P]),
+    "zk_igemm_dgrad_ex": (I32, [P] * 8 + [I32, P] + [I32] * 14 + [P]),
+    "zk_bn_bwd_tiles_reduce": (I32, [P, I32, I32, P, P]),
     "zk_igemm_fwd": (I32, [P, P, P, P] + [I32] * 16 + [P]),
     "zk_igemm_fwd_fp4": (I32, [P, P, P, P] + [I32] * 16 + [P]),
     "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),

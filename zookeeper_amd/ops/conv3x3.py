@@ -75,6 +75,10 @@ class _Conv3x3Fn(torch.autograd.Function):
                                        H, W, Cout, H, W, Cin, 3, 3, 1, 1, 1, -1, st),
                   "zk_igemm_dgrad(3x3 fwd)")
         ctx.save_for_backward(xn)
+        # (the producing BatchNorm's backward sums are not taken here: the 3x3
+        # data gradients with an LDS epilogue are the 256-channel ones, whose
+        # default is the phased deep kernel -- faster than v45 carrying the
+        # fused sums, profiles/r5/c_resnet50_bn_fusion.md)
         ctx.weight = weight
         ctx.shape = (B, Cin, H, W, Cout)
         return y.permute(0, 3, 1, 2)

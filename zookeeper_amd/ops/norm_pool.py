@@ -35,11 +35,14 @@ def supported(x: torch.Tensor) -> bool:
 
 class FloatBnSum:
     """Hand-off of a float BatchNorm's backward reduction to the data gradient
-    of the layer that consumes its output (``pointwise.conv1x1``): that
-    kernel's LDS epilogue adds (sum g', sum g' * xhat) over the gradient it
-    stores into ``sums`` (the channel-major copies ``zk_bn_bwd_coef`` reads
-    and re-zeroes), with g' masked by the BN's ReLU (``relu``: 0 none, 1
-    recomputed from the input ``xn`` and ``coef``, 2 the stored ``mask`` bits).
+    of the layer that consumes its output (``pointwise.conv1x1``,
+    ``conv3x3``): that kernel's LDS epilogue writes (sum g', sum g' * xhat)
+    over each of its M tiles of the gradient it stores into ``sums``
+    [tiles][2][C] (plain stores, one row per tile; ``zk_bn_bwd_tiles_reduce``
+    folds the rows in a fixed order -- bit-reproducible -- into the copies
+    ``zk_bn_bwd_coef`` reads, and re-zeroes them), with
+    g' masked by the BN's ReLU (``relu``: 0 none, 1 recomputed from the input
+    ``xn`` and ``coef``, 2 the stored ``mask`` bits).
     The BN backward uses them only if they were taken over exactly the
     gradient it receives (:meth:`reduced`: same storage, not modified since);
     otherwise it re-zeroes ``sums`` and runs its own reduction."""
@@ -145,8 +148,9 @@ class _BatchNormFn(torch.autograd.Function):
                 and any(ctx.needs_input_grad)):
             mode = 2 if omask is not None else (1 if relu else 0)
             if not (relu and residual is not None and omask is None):
-                sums = zeroed_scratch(bn, "bwd_sums_fused", (2, C, L.zk_bn_bwd_parts_max()),
-                                      torch.float32, dev)
+                # one row per M tile of the consumer's LDS-epilogue GEMM (>= 128 pixels)
+                tiles = (P + 127) // 128
+                sums = zeroed_scratch(bn, "bwd_sums_fused", (tiles, 2, C), torch.float32, dev)
                 ctx.fsum = FloatBnSum(xn, coef, omask, mode, sums)
                 holder.append(ctx.fsum)
         ctx.params = (gamma, beta)
@@ -173,7 +177,9 @@ class _BatchNormFn(torch.autograd.Function):
         fused = ctx.fsum is not None and ctx.fsum.reduced(g)
         if fused:
             # the consumer's data-gradient epilogue reduced exactly this g
-            sums = ctx.fsum.sums
+            rows = ctx.fsum.sums
+            check(L.zk_bn_bwd_tiles_reduce(rows.data_ptr(), rows.shape[0], C, sums.data_ptr(), st),
+                  "zk_bn_bwd_tiles_reduce")
             n.value = sums.shape[2]
         elif ctx.relu_rc:
             check(L.zk_bn_bwd_reduce_relu_bf16_parts(g.data_ptr(), xn.data_ptr(),
@@ -209,7 +215,16 @@ class _BatchNormFn(torch.autograd.Function):
             dbeta = None
         dx = torch.empty_like(g)
         dres = None
-        if ctx.has_res and ctx.needs_input_grad[3]:
+        h = ctx.handoff
+        if (ctx.has_res and ctx.needs_input_grad[3] and h is not None and h.masked_ok
+                and OPTS.bn_masked_handoff and m is not None and not h.closed):
+            # the residual's consumer masks g itself (its epilogue reads g and
+            # the mask bits): no residual-gradient tensor is written
+            check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), xn.data_ptr(), m.data_ptr(),
+                                      bcoef.data_ptr(), dx.data_ptr(), P, C, st),
+                  "zk_bn_bwd_dx_bf16")
+            h.give((g, m))
+        elif ctx.has_res and ctx.needs_input_grad[3]:
             dres = torch.empty_like(g)
             check(L.zk_bn_bwd_dx_res_bf16(g.data_ptr(), xn.data_ptr(),
                                           m.data_ptr() if m is not None else None,
@@ -250,11 +265,15 @@ class ResidualHandoff:
     (``give`` returns False) returns its gradient to autograd instead, so an
     unexpected order costs the fused add, never a gradient."""
 
-    __slots__ = ("dres", "closed")
+    __slots__ = ("dres", "closed", "masked_ok")
 
     def __init__(self):
         self.dres = None
         self.closed = False
+        # set by a consumer whose epilogue can take the gradient as (g, ReLU
+        # mask bits) and mask it itself (pointwise.conv1x1): the BN tail then
+        # hands over its incoming gradient and mask instead of writing g*mask
+        self.masked_ok = False
 
     def give(self, d) -> bool:
         """Producer side: leave ``d`` for the consumer; False if it already ran."""

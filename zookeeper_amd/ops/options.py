@@ -74,6 +74,12 @@ class KernelOptions:
     # epilogue writes the BN output's whole gradient) instead of a separate
     # reduction pass over g and x (outside the deterministic mode).
     bn_bwd_fuse: bool = True
+    # The BN tail hands (g, ReLU mask bits) to a 1x1 conv whose epilogue masks
+    # and adds them, instead of writing the residual gradient g * mask.
+    bn_masked_handoff: bool = True
+    # The LDS-epilogue data gradient prefetches its residual / BN-input loads
+    # in groups (igemm.hip dgrad_store_lds) instead of loading at each chunk.
+    epilogue_prefetch: bool = True
     # Float conv weights as persistent bf16 GEMM-layout images written by the
     # fused optimizer (ops/weight_images.py) instead of a cast / transpose
     # per conv and pass.
@@ -84,7 +90,7 @@ OPTS = KernelOptions()
 
 # keys the native library reads (zk_set_option); values are ints
 _NATIVE_KEYS = {"tile_huge": 0, "deterministic": 2, "dgrad_rw": 3, "wgrad_slab_mb": 5,
-                "dgrad_deep": 6, "wgrad_deep": 7}
+                "dgrad_deep": 6, "wgrad_deep": 7, "epilogue_prefetch": 8}
 
 
 def _push_native() -> None:

@@ -116,6 +116,8 @@ class _Conv1x1Fn(torch.autograd.Function):
         ctx.wt = wt
         ctx.weight = weight
         ctx.handoff, ctx.give = handoff, give
+        if handoff is not None:
+            handoff.masked_ok = True  # our epilogue masks a (g, mask) hand-off itself
         ctx.shape = (B, Cin, H, W, Cout)
         return y2.view(B, H, W, Cout).permute(0, 3, 1, 2)
 
@@ -129,27 +131,39 @@ class _Conv1x1Fn(torch.autograd.Function):
         L = lib()
         st = stream_ptr(dev)
         dx = dweight = None
-        # + the identity shortcut's gradient of x (norm_pool.ResidualHandoff)
+        # + the identity shortcut's gradient of x (norm_pool.ResidualHandoff):
+        # a tensor, or (g, ReLU mask bits) that the epilogue masks itself
         dres = ctx.handoff.take() if ctx.handoff is not None else None
+        dmask = None
+        if isinstance(dres, tuple):
+            dres, dmask = dres
         if ctx.needs_input_grad[0]:
             dx2 = torch.empty((g2.shape[0], Cin), dtype=torch.bfloat16, device=dev)
             wt = ctx.wt if ctx.wt is not None else w2.t().contiguous()  # [Cin][Cout]
-            if dres is not None and tuple(dres.shape) != (B, H, W, Cin):
+            if dres is not None and dres.numel() != B * H * W * Cin:
                 raise RuntimeError(f"residual gradient {tuple(dres.shape)} does not match the "
                                    f"1x1 conv input {(B, H, W, Cin)}")
             fs = ctx.fsum
             rc = _HIP_INVALID_VALUE
-            if fs is not None:
-                rc = L.zk_igemm_dgrad_bsums(
+            if fs is not None or dmask is not None:
+                rc = L.zk_igemm_dgrad_ex(
                     g2.data_ptr(), wt.data_ptr(), dres.data_ptr() if dres is not None else None,
-                    dx2.data_ptr(), fs.xn.data_ptr(), fs.coef.data_ptr(),
-                    fs.mask.data_ptr() if fs.mask is not None else None, fs.relu,
-                    fs.sums.data_ptr(), fs.sums.shape[2], B, H, W, Cin, H, W, Cout, 1, 1, 1, 0,
-                    0, -1, st)
+                    dmask.data_ptr() if dmask is not None else None, dx2.data_ptr(),
+                    fs.xn.data_ptr() if fs is not None else None,
+                    fs.coef.data_ptr() if fs is not None else None,
+                    fs.mask.data_ptr() if fs is not None and fs.mask is not None else None,
+                    fs.relu if fs is not None else 0,
+                    fs.sums.data_ptr() if fs is not None else None,
+                    fs.sums.shape[0] if fs is not None else 1, B, H, W, Cin, H, W, Cout, 1, 1, 1,
+                    0, 0, -1, st)
                 if rc != _HIP_INVALID_VALUE:
-                    check(rc, "zk_igemm_dgrad_bsums(1x1)")
-                    fs.take(dx2)
+                    check(rc, "zk_igemm_dgrad_ex(1x1)")
+                    if fs is not None:
+                        fs.take(dx2)
             if rc == _HIP_INVALID_VALUE:  # no LDS-epilogue tile: the plain GEMM
+                if dmask is not None:  # materialise g * mask
+                    bits = (dmask.unsqueeze(-1) >> torch.arange(8, device=dev, dtype=torch.uint8)) & 1
+                    dres = dres.reshape(-1) * bits.reshape(-1).to(dres.dtype)
                 check(L.zk_igemm_dgrad(g2.data_ptr(), wt.data_ptr(), None,
                                        dres.data_ptr() if dres is not None else None,
                                        dx2.data_ptr(), B, H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0,

@@ -48,6 +48,8 @@ class Runtime:
     wgrad_deep: bool = Field(True)
     weight_images: bool = Field(True)
     bn_bwd_fuse: bool = Field(True)
+    bn_masked_handoff: bool = Field(True)
+    epilogue_prefetch: bool = Field(True)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
     deterministic: bool = Field(False)
