@@ -49,7 +49,9 @@ from __future__ import annotations
 import contextlib
 import os
 import queue
+import sys
 import threading
+import time
 from typing import Dict, List, Optional
 
 import torch
@@ -62,6 +64,10 @@ from zookeeper_amd.parallel.flat import FlatParams
 # buckets smaller than this are folded into the next one (bench JSON: no
 # sub-0.1 MB bucket)
 MIN_BUCKET_BYTES = 256 * 1024
+
+# ZK_COMM_DEBUG_EVENTS=1: log, per bucket launch and per staged copy, whether
+# the side-stream events it depends on report complete (ordering diagnostics)
+_DEBUG_EVENTS = os.environ.get("ZK_COMM_DEBUG_EVENTS", "0") == "1"
 
 
 class GradBucketer:
@@ -238,13 +244,18 @@ class GradBucketer:
         # weight gradients still running on the side stream (ops/streams.py)
         for ev in side_streams.unwaited_events():
             self.comm_stream.wait_event(ev)
+        if _DEBUG_EVENTS:
+            print(f"[bucketer] launch {b}: side events "
+                  f"{[(id(e) % 10007, e.query()) for e in side_streams.unwaited_events()]}",
+                  file=sys.stderr, flush=True)
         with torch.cuda.stream(self.comm_stream):
             if self.timing:
                 ev = self._events()
                 ev["start"][b] = ev["mk"]()
                 ev["start"][b].record(self.comm_stream)
             if self._stager is not None:
-                self._works.append((self._stager.submit(b, lo, hi, view, self.comm_stream),
+                self._works.append((self._stager.submit(b, lo, hi, view, self.comm_stream,
+                                                        list(side_streams.unwaited_events())),
                                     view, b))
             else:
                 work, tmp = self._issue(view)
@@ -440,11 +451,15 @@ class _HostStager:
             item = self.q.get()
             if item is None:
                 return
-            lo, hi, view, ready, done, box = item
+            lo, hi, view, ready, done, box, deps = item
             try:
                 if self.copy_stream is None:
                     self.copy_stream = torch.cuda.Stream(view.device)
                 self.copy_stream.wait_event(ready)
+                if _DEBUG_EVENTS:
+                    print(f"[stager] {time.perf_counter():.6f} copy [{lo}:{hi}] ready="
+                          f"{ready.query()} side={[(id(e) % 10007, e.query()) for e in deps]}",
+                          file=sys.stderr, flush=True)
                 with torch.cuda.stream(self.copy_stream):
                     self.host[lo:hi].copy_(view, non_blocking=False)
                 dist.all_reduce(self.host[lo:hi], group=self.group)
@@ -452,12 +467,12 @@ class _HostStager:
                 box.append(e)
             done.set()
 
-    def submit(self, b: int, lo: int, hi: int, view: torch.Tensor, stream) -> tuple:
+    def submit(self, b: int, lo: int, hi: int, view: torch.Tensor, stream, deps=()) -> tuple:
         host = self.host[lo:hi]
         ready = torch.cuda.Event()
         ready.record(stream)  # after the bucket's readiness waits
         done, box = threading.Event(), []
-        self.q.put((lo, hi, view, ready, done, box))
+        self.q.put((lo, hi, view, ready, done, box, deps))
         return _StagedWork(done, box), host
 
 

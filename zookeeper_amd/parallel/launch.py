@@ -101,7 +101,9 @@ def spawn(argv: Sequence[str], nproc: int, env: Optional[Dict[str, str]] = None,
                 p.kill()
     finally:
         for s, h in old.items():
-            signal.signal(s, h)
+            # None: the previous handler was installed outside Python (e.g. by
+            # a profiler's preloaded library) and cannot be reinstated from here
+            signal.signal(s, h if h is not None else signal.SIG_DFL)
         for f in files:
             f.close()
     return code
