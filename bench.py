@@ -184,7 +184,9 @@ def main() -> int:
     if args.data == "stream":
         src, _ = cfg.dataset.train()
         loader = DeviceLoader(src, args.batch, info.device, shuffle=True, seed=0,
-                              rank=info.rank, world=info.world, slots=4)
+                              rank=info.rank, world=info.world, slots=4,
+                              transform=(prep.device_transform(training=True)
+                                         if runtime.loader_preprocess else None))
         it = iter(loader)
         next_batch = lambda i: next(it)  # noqa: E731
     else:

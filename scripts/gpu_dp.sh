@@ -1,6 +1,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
-# world-1 vs world-2 (side stream, deterministic, 2 steps) with the bucketer's
-# event-readiness log
-ZK_COMM_DEBUG_EVENTS=1 ZK_TEST_STEPS=2 DIAG_REPS=2 timeout -k 10 300 python -u scripts/diag_dp.py /tmp/dpd5 1 > gpurun_out/dp_diag5.log 2>&1
+# data-parallel GPU tests after the readiness fix, the loader tests, then 3
+# more world-1 vs world-2 comparisons
+timeout -k 10 900 python -u -m pytest tests/gpu/test_dp_gpu.py tests/gpu/test_loader_gpu.py -v --timeout 300 --timeout-method thread > gpurun_out/dp_tests3.log 2>&1 &&
+ZK_TEST_STEPS=4 DIAG_REPS=3 DIAG_BRIEF=1 timeout -k 10 300 python -u scripts/diag_dp.py /tmp/dpd8 1 > gpurun_out/dp_diag8.log 2>&1

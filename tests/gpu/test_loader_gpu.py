@@ -108,3 +108,38 @@ def test_device_slots_reused_under_slow_consumer():
     assert len(ptrs) <= 4  # ahead + 2 device slots, round-robin
     # (the sum results are the only allocations; the caching allocator reuses them)
     assert allocs1 == allocs0
+
+
+@pytest.mark.timeout(120)
+def test_preprocessing_on_the_loader_stream_matches_the_consumer_path():
+    """``Preprocessing.device_transform`` (runtime.loader_preprocess): the fused
+    normalise kernel runs on the copy stream into a per-slot buffer; under a
+    slow consumer every batch's model input must equal ``input()`` of the same
+    uint8 batch on the compute stream (no flip: seed-independent), and the
+    buffers must be reused (one per device slot)."""
+    from zookeeper_amd.core import configure
+    from zookeeper_amd.data import ImageNetPreprocessing
+    from zookeeper_amd.data.dataset import ArraySource
+    from zookeeper_amd.data.loader import DeviceLoader
+
+    arr = np.random.default_rng(6).integers(0, 255, (256, 32, 32, 3), dtype=np.uint8)
+    src = ArraySource(arr, np.arange(256) % 7)
+    prep = ImageNetPreprocessing()
+    configure(prep, {"input_shape": (32, 32, 3)})
+    tf = prep.device_transform(training=False)
+    assert tf is not None
+    loader = DeviceLoader(src, 32, torch.device("cuda", 0), shuffle=True, seed=3, slots=4,
+                          transform=tf)
+    it = iter(loader)
+    ptrs = set()
+    for _ in range(20):
+        batch = next(it)
+        torch.cuda._sleep(2_000_000)
+        x, y = prep(batch, training=False)
+        want = prep.input({"image": batch["image"].clone()}, training=False)
+        assert x.shape == want.shape and x.dtype == torch.bfloat16
+        assert torch.equal(x, want)
+        assert torch.equal(y, batch["label"])
+        ptrs.add(x.data_ptr())
+    loader.close()
+    assert len(ptrs) <= 4

@@ -82,6 +82,72 @@ def test_bucketer_layout():
 
 
 @pytest.mark.timeout(120)
+def test_bucketer_waits_for_a_deferred_direct_gradient():
+    """A kernel that writes a gradient straight into the flat buffer returns
+    None to autograd, whose post-accumulate hook still fires; the bucket must
+    launch at the writer's own readiness signal (``_zk_grad_ready``: for a
+    side-stream weight gradient that comes a block later, once its event
+    exists), not at autograd's call.  Launching at autograd's call all-reduced
+    side-stream weight gradients before they were computed
+    (``tests/gpu/test_dp_gpu.py`` two-rank mismatch, profiles/r5/dp_hook_race.md)."""
+    import socket
+
+    import torch.distributed as dist
+    import torch.nn as nn
+
+    from zookeeper_amd.ops._native import direct_grad, grad_ready
+    from zookeeper_amd.parallel.ddp import GradBucketer
+    from zookeeper_amd.parallel.flat import FlatParams
+
+    deferred = []
+
+    class DirectScale(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, w):
+            ctx.save_for_backward(x)
+            ctx.w = w
+            return x * w
+
+        @staticmethod
+        def backward(ctx, g):
+            (x,) = ctx.saved_tensors
+            gw = direct_grad(ctx.w)
+            assert gw is not None
+            gw.add_((g * x).sum(0))
+            deferred.append(ctx.w)  # readiness signalled later, like ops/streams.py
+            return g * ctx.w, None
+
+    class M(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = nn.Parameter(torch.ones(8))
+
+        def forward(self, x):
+            return DirectScale.apply(x, self.w)
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1)
+    try:
+        m = M()
+        flat = FlatParams(m)
+        b = GradBucketer(flat, world=1, force=True)
+        flat.zero_grad()
+        m(torch.randn(4, 8, requires_grad=True)).sum().backward()
+        assert b._order == []  # autograd's hook call did not launch the bucket
+        for p in deferred:
+            grad_ready(p)
+        assert b._order == [0]
+        b.finish()
+        assert b.last_order == [0]
+        b.remove()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
 def test_bn_buffers_all_reduced(tmp_path):
     assert _launch("bnsync", tmp_path) == 0
     r = [torch.load(tmp_path / f"bn{i}.pt", weights_only=True) for i in range(2)]

@@ -80,7 +80,8 @@ def test_runtime_is_part_of_the_experiment_config():
     assert "runtime.deterministic" in flat
 
 
-_DEBUG_ONLY = {"ZK_NATIVE", "ZK_DEBUG_SYNC", "ZK_DEBUG_SYNC_LOG", "ZK_DEBUG_STEM"}
+_DEBUG_ONLY = {"ZK_NATIVE", "ZK_DEBUG_SYNC", "ZK_DEBUG_SYNC_LOG", "ZK_DEBUG_STEM",
+               "ZK_COMM_DEBUG_EVENTS"}
 
 
 def test_ops_and_kernels_read_no_runtime_environment():

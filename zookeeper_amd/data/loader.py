@@ -88,17 +88,24 @@ class DeviceLoader:
     slots: pinned ring depth (≥2 for overlap).
     device_pool: if >0, materialise that many batches on the device once and
         cycle them forever (synthetic benchmarking).
+    transform: optional ``f(batch)`` run on the copy stream right after each
+        batch's H2D copy (streaming path), e.g.
+        :meth:`~zookeeper_amd.data.preprocessing.Preprocessing.device_transform`:
+        it may add keys to the batch (reusing the buffers the device slot held
+        for its previous batch); the compute stream's wait on the copy event
+        then covers them too.
     """
 
     def __init__(self, source: Source, batch_size: int, device: torch.device,
                  shuffle: bool = True, seed: int = 0, rank: int = 0, world: int = 1,
                  slots: int = 4, device_pool: int = 0, start_step: int = 0,
-                 gather_threads: int = 8):
+                 gather_threads: int = 8, transform=None):
         self.source, self.batch_size, self.device = source, batch_size, torch.device(device)
         self.sampler = IndexSampler(len(source), batch_size, shuffle, seed, rank, world)
         self.steps_per_epoch = self.sampler.steps_per_epoch
         self.slots, self.device_pool = max(3, slots), device_pool
         self.gather_threads = gather_threads
+        self.transform = transform
         self._start_step = start_step
         self._pool = None
         self._thread: Optional[threading.Thread] = None
@@ -212,6 +219,8 @@ class DeviceLoader:
                                 copy_stream.wait_event(consumed[d])
                             for k, v in pinned[slot].items():
                                 dev_slots[d][k].copy_(v, non_blocking=True)
+                            if self.transform is not None:
+                                self.transform(dev_slots[d])
                             copied[d].record(copy_stream)
                         used[d] = True
                         in_flight.append((slot, d, copied[d]))

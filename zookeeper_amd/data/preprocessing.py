@@ -19,7 +19,7 @@ from __future__ import annotations
 
 import functools
 import inspect
-from typing import Any, Dict, Optional, Sequence, Tuple
+from typing import Any, Callable, Dict, Optional, Sequence, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -49,9 +49,21 @@ class Preprocessing:
     def output(self, data: TensorDict, training: bool) -> torch.Tensor:
         raise NotImplementedError("Must be implemented in subclasses.")
 
+    def device_transform(self, training: bool) -> Optional[Callable[[TensorDict], None]]:
+        """Optional: a function the :class:`~zookeeper_amd.data.loader.DeviceLoader`
+        runs on its copy stream right after a batch's H2D copy.  It stores the
+        model input under ``data["input"]`` (reusing that buffer from the
+        slot's previous batch), so the input pipeline's kernels overlap the
+        previous step instead of opening the next one on the compute stream;
+        :meth:`__call__` then passes ``data["input"]`` through.  ``None`` (the
+        default): preprocess in :meth:`input` on the consumer's stream."""
+        return None
+
     def __call__(self, data: TensorDict, training: bool = False):
-        input_fn = pass_training_kwarg(self.input, training=training)
         output_fn = pass_training_kwarg(self.output, training=training)
+        if "input" in data:  # already preprocessed by the loader (device_transform)
+            return data["input"], output_fn(data)
+        input_fn = pass_training_kwarg(self.input, training=training)
         return input_fn(data), output_fn(data)
 
 
@@ -153,3 +165,27 @@ class ImageNetPreprocessing(Preprocessing):
 
     def output(self, data: TensorDict) -> torch.Tensor:
         return data["label"]
+
+    def device_transform(self, training: bool) -> Optional[Callable[[TensorDict], None]]:
+        """The fused normalise + flip kernel on the loader's copy stream, into a
+        per-slot bf16 buffer (0.2 ms per E18 step at batch 1536 off the compute
+        stream).  Only when no resize is needed and the kernel is available."""
+        from zookeeper_amd import ops
+
+        if not ops.available() or self.dtype != "bfloat16":
+            return None
+        h, w = self.input_shape[:2]
+        flip = training and self.flip
+
+        def transform(data: TensorDict) -> None:
+            image = data["image"]
+            if not image.is_cuda or image.shape[1:3] != (h, w) or image.shape[3] != 3:
+                return  # left to input() on the consumer's stream
+            buf = data.get("input")
+            base = buf.permute(0, 2, 3, 1) if buf is not None else None
+            if base is not None and (base.shape != image.shape or not base.is_contiguous()):
+                base = None
+            data["input"] = nhwc_to_model(
+                ops.normalize_flip(image, self.mean, self.std, flip, out=base))
+
+        return transform

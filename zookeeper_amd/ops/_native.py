@@ -147,6 +147,10 @@ def direct_grad(p, channels_last: bool = False):
         return None
     if not channels_last and not g.is_contiguous():
         return None
+    # claimed for this step: the data-parallel bucketer then ignores autograd's
+    # post-accumulate call for p (it runs even though the op returns None) and
+    # waits for the kernel's own grad_ready
+    p._zk_direct_claim = True
     return g
 
 

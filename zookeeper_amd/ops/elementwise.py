@@ -14,9 +14,10 @@ _flip_seed = itertools.count(1)
 
 
 def normalize_flip(image: torch.Tensor, mean: Sequence[float], std: Sequence[float],
-                   flip: bool, seed: int = None) -> torch.Tensor:
+                   flip: bool, seed: int = None, out: torch.Tensor = None) -> torch.Tensor:
     """uint8 ``[B,H,W,3]`` → bf16 ``[B,H,W,3]`` normalised, optionally with a
-    per-image random horizontal flip (one kernel)."""
+    per-image random horizontal flip (one kernel).  ``out``: a contiguous bf16
+    ``[B,H,W,3]`` tensor to write (the loader's per-slot buffer)."""
     if image.dtype != torch.uint8 or image.dim() != 4 or image.shape[3] != 3:
         raise ValueError("normalize_flip expects uint8 [B,H,W,3]")
     if not image.is_contiguous():
@@ -24,7 +25,12 @@ def normalize_flip(image: torch.Tensor, mean: Sequence[float], std: Sequence[flo
     B, H, W, _ = image.shape
     if W % 4:
         raise ValueError("normalize_flip needs W % 4 == 0")
-    out = torch.empty((B, H, W, 3), dtype=torch.bfloat16, device=image.device)
+    if out is None:
+        out = torch.empty((B, H, W, 3), dtype=torch.bfloat16, device=image.device)
+    elif (out.shape != (B, H, W, 3) or out.dtype != torch.bfloat16 or not out.is_contiguous()
+          or out.device != image.device):
+        raise ValueError("normalize_flip: out must be a contiguous bf16 [B,H,W,3] tensor "
+                         "on the image's device")
     m = (ctypes.c_float * 3)(*[float(v) for v in mean])
     s = (ctypes.c_float * 3)(*[float(v) for v in std])
     seed = next(_flip_seed) if seed is None else seed

@@ -31,6 +31,8 @@ semantics.  ``runtime.wgrad_side_stream=False`` disables it.
 from __future__ import annotations
 
 import contextlib
+import os
+import sys
 from typing import Dict, List, Tuple
 
 import torch
@@ -75,8 +77,15 @@ def keep(*tensors: torch.Tensor) -> None:
     _keep.extend(tensors)
 
 
+# ZK_COMM_DEBUG_EVENTS=1: log deferrals and flushes (ordering diagnostics)
+_DEBUG = os.environ.get("ZK_COMM_DEBUG_EVENTS", "0") == "1"
+
+
 def defer_ready(event: torch.cuda.Event, param) -> None:
     """``param``'s gradient is complete once ``event`` (side stream) fires."""
+    if _DEBUG:
+        print(f"[streams {os.getpid()}] defer {tuple(param.shape)} event {id(event) % 10007}",
+              file=sys.stderr, flush=True)
     _pending.append((event, param))
 
 
@@ -95,6 +104,9 @@ def flush(wait: bool = True) -> None:
     cur = torch.cuda.current_stream()
     items = list(_pending)
     _pending.clear()
+    if _DEBUG:
+        print(f"[streams {os.getpid()}] flush wait={wait}: {[id(ev) % 10007 for ev, _ in items]}",
+              file=sys.stderr, flush=True)
     if wait:
         for ev in _unwaited:
             cur.wait_event(ev)

@@ -209,10 +209,28 @@ class GradBucketer:
             self._suspended = old
             self._seen = [False] * len(self.flat.slots)
             self._pending = [len(b) for b in self.buckets]
+            self._clear_claims()
+
+    def _clear_claims(self) -> None:
+        for s in self.flat.slots:
+            if getattr(s.param, "_zk_direct_claim", False):
+                s.param._zk_direct_claim = False
 
     def _make_hook(self, slot_index: int):
         def hook(_param):
+            if _DEBUG_EVENTS:
+                print(f"[bucketer {os.getpid()}] ready {self.flat.slots[slot_index].name} "
+                      f"(bucket {self.slot_bucket[slot_index]}, seen {self._seen[slot_index]}, "
+                      f"{'autograd' if _param is not None else 'direct'})",
+                      file=sys.stderr, flush=True)
             if self._suspended or self._seen[slot_index]:
+                return
+            if _param is not None and getattr(_param, "_zk_direct_claim", False):
+                # autograd's post-accumulate call for a gradient a kernel writes
+                # straight into the flat buffer: the op returned None for it,
+                # yet the hook still runs, possibly before the write is even
+                # ordered (a side-stream weight gradient is deferred).  Its
+                # writer signals readiness itself (``_zk_grad_ready``).
                 return
             self._seen[slot_index] = True
             b = self.slot_bucket[slot_index]
@@ -245,7 +263,7 @@ class GradBucketer:
         for ev in side_streams.unwaited_events():
             self.comm_stream.wait_event(ev)
         if _DEBUG_EVENTS:
-            print(f"[bucketer] launch {b}: side events "
+            print(f"[bucketer {os.getpid()}] launch {b}: side events "
                   f"{[(id(e) % 10007, e.query()) for e in side_streams.unwaited_events()]}",
                   file=sys.stderr, flush=True)
         with torch.cuda.stream(self.comm_stream):
@@ -348,6 +366,7 @@ class GradBucketer:
         self._pending = [len(b) for b in self.buckets]
         self._launched = [False] * len(self.buckets)
         self._seen = [False] * len(self.flat.slots)
+        self._clear_claims()
 
     def _compare_order(self, order: List[int]) -> None:
         h = order_hash(order)
@@ -457,7 +476,7 @@ class _HostStager:
                     self.copy_stream = torch.cuda.Stream(view.device)
                 self.copy_stream.wait_event(ready)
                 if _DEBUG_EVENTS:
-                    print(f"[stager] {time.perf_counter():.6f} copy [{lo}:{hi}] ready="
+                    print(f"[stager {os.getpid()}] {time.perf_counter():.6f} copy [{lo}:{hi}] ready="
                           f"{ready.query()} side={[(id(e) % 10007, e.query()) for e in deps]}",
                           file=sys.stderr, flush=True)
                 with torch.cuda.stream(self.copy_stream):

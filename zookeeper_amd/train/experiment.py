@@ -132,7 +132,9 @@ class TrainingExperiment(Experiment):
 
         loader = DeviceLoader(train_src, self.batch_size, info.device, shuffle=True,
                               seed=self.seed, rank=info.rank, world=info.world,
-                              device_pool=self.device_pool, start_step=start_step)
+                              device_pool=self.device_pool, start_step=start_step,
+                              transform=(self.preprocessing.device_transform(training=True)
+                                         if rt.loader_preprocess else None))
         metrics = MetricsLogger(info.device,
                                 os.path.join(run_dir, "metrics.jsonl") if run_dir else None,
                                 info.rank, info.world, metrics=self.metrics)

@@ -64,12 +64,17 @@ class Runtime:
     force_dp: bool = Field(False)
     # Time every bucket's collective (comm_ms / exposed_ms in metrics.jsonl).
     comm_timing: bool = Field(True)
+    # Run the preprocessing's device kernels (normalise + flip) on the
+    # loader's copy stream after each H2D copy (Preprocessing.device_transform)
+    # instead of at the head of the step on the compute stream.
+    loader_preprocess: bool = Field(True)
 
     # --- data-parallel communicator (parallel/dist.py CommConfig documents each)
     # RCCL streams and the comm stream at high HIP priority.  Off by default:
-    # with it on, the two-rank gloo GPU test exposed a stale-gradient race in
-    # the (since fixed) host stager (profiles/r4/d_dp_stager_race.md), and the
-    # high-priority RCCL ordering has no multi-rank GPU verification yet.
+    # no multi-GPU measurement shows it helps.  (The stale-gradient race once
+    # blamed on it, profiles/r4/d_dp_stager_race.md, was the bucketer counting
+    # autograd's hook call for directly written gradients:
+    # profiles/r5/dp_hook_race.md; the two-rank GPU tests run at high priority.)
     comm_high_priority: bool = Field(False)
     # NCCL_MIN_NCHANNELS / NCCL_MAX_NCHANNELS (0: RCCL's default).
     rccl_min_channels: int = Field(0)
@@ -122,6 +127,7 @@ class Runtime:
     def as_dict(self) -> Dict[str, Any]:
         d = self.kernel_options()
         d.update(graph=self.graph, force_dp=self.force_dp, comm_timing=self.comm_timing,
+                 loader_preprocess=self.loader_preprocess,
                  comm_high_priority=self.comm_high_priority,
                  rccl_min_channels=self.rccl_min_channels,
                  rccl_max_channels=self.rccl_max_channels, cpu_affinity=self.cpu_affinity,
