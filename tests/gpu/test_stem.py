@@ -235,3 +235,40 @@ def test_bn2_sums_from_the_first_binary_block(monkeypatch):
     assert used == 1 and used0 == 0
     torch.testing.assert_close(gw, gw0, rtol=1e-4, atol=1e-4 * gw0.abs().max().item())
     torch.testing.assert_close(gb, gb0, rtol=1e-4, atol=1e-4 * gb0.abs().max().item())
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_loader_packed_input_is_bit_identical(flip):
+    """runtime.loader_preprocess: the loader's fused normalise + pack kernel
+    writes the stem's padded input next to the image (PACK_SPECS, published by
+    the first stem forward); the stem then takes it (no pack kernel) and every
+    output and gradient must equal the self-packing run bit for bit."""
+    from zookeeper_amd import ops
+    from zookeeper_amd.ops import stem as stem_ops
+
+    torch.manual_seed(3)
+    mean, std = (123.7, 116.3, 103.5), (58.4, 57.1, 57.4)
+    img = torch.randint(0, 256, (4, 64, 64, 3), dtype=torch.uint8, device="cuda")
+    a = _stem(True).cuda().to(memory_format=torch.channels_last)
+    b = copy.deepcopy(a)
+    x_ref = ops.normalize_flip(img, mean, std, flip, seed=77).permute(0, 3, 1, 2)
+    y_a = a(x_ref)  # publishes the padded-input spec of this shape
+    spec = stem_ops.PACK_SPECS[(64, 64, 3)]
+    out, xp = ops.normalize_flip_pack(img, mean, std, flip, spec, seed=77)
+    assert torch.equal(out, x_ref.permute(0, 2, 3, 1))
+    x = out.permute(0, 3, 1, 2)
+    x._zk_stem_xp = (xp, spec, x._version)
+    n0 = stem_ops.PREPACKED[0]
+    y_b = b(x)
+    assert stem_ops.PREPACKED[0] == n0 + 1  # the stem took the loader's xp
+    assert torch.equal(y_a, y_b)
+    g = torch.randn_like(y_a)
+    y_a.backward(g)
+    y_b.backward(g)
+    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        assert torch.equal(p.grad, q.grad), n
+    # a modified input is not paired with a stale padded copy
+    x.add_(0)
+    n1 = stem_ops.PREPACKED[0]
+    b(x)
+    assert stem_ops.PREPACKED[0] == n1

@@ -177,6 +177,8 @@ class ImageNetPreprocessing(Preprocessing):
         h, w = self.input_shape[:2]
         flip = training and self.flip
 
+        from zookeeper_amd.ops.stem import PACK_SPECS
+
         def transform(data: TensorDict) -> None:
             image = data["image"]
             if not image.is_cuda or image.shape[1:3] != (h, w) or image.shape[3] != 3:
@@ -185,7 +187,20 @@ class ImageNetPreprocessing(Preprocessing):
             base = buf.permute(0, 2, 3, 1) if buf is not None else None
             if base is not None and (base.shape != image.shape or not base.is_contiguous()):
                 base = None
-            data["input"] = nhwc_to_model(
-                ops.normalize_flip(image, self.mean, self.std, flip, out=base))
+            spec = PACK_SPECS.get((h, w, 3))
+            if spec is None:
+                data["input"] = nhwc_to_model(
+                    ops.normalize_flip(image, self.mean, self.std, flip, out=base))
+                return
+            # a fused stem ran on this shape: also write its padded input, in
+            # the same pass (the stem then skips its pack kernel)
+            xp = data.get("input_xp")
+            if xp is not None and xp.shape != (image.shape[0], spec[0], spec[1], 4):
+                xp = None
+            out, xp = ops.normalize_flip_pack(image, self.mean, self.std, flip, spec,
+                                              out=base, xp=xp)
+            x = nhwc_to_model(out)
+            x._zk_stem_xp = (xp, spec, x._version)
+            data["input"], data["input_xp"] = x, xp
 
         return transform

@@ -34,6 +34,7 @@ SIGNATURES = {
     "zk_comm_async_error": (I32, [P, IP]),
     # preprocessing
     "zk_normalize_flip_c3": (I32, [P, P, I32, I32, I32, FP, FP, I32, U64, P]),
+    "zk_normalize_flip_pack_c3": (I32, [P, P, P] + [I32] * 7 + [FP, FP, I32, U64, P]),
     # binary convolution
     "zk_sign_pack": (I32, [P, P, P, P, P, I64, F32, P]),
     "zk_weight_pack": (I32, [P, P, P, P, P, P, I32, I32, I32, P]),

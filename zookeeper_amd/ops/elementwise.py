@@ -40,6 +40,38 @@ def normalize_flip(image: torch.Tensor, mean: Sequence[float], std: Sequence[flo
     return out
 
 
+def normalize_flip_pack(image: torch.Tensor, mean: Sequence[float], std: Sequence[float],
+                        flip: bool, spec, out: torch.Tensor = None, xp: torch.Tensor = None,
+                        seed: int = None):
+    """:func:`normalize_flip` that also writes the fused stem's padded input
+    ``xp`` bf16 ``[B, Hp, Wp, 4]`` in the same pass (``spec = (Hp, Wp, pt,
+    pl)``, published by ``ops.stem``).  Returns ``(out, xp)``; both
+    bit-identical to ``normalize_flip`` followed by the stem's own pack."""
+    if image.dtype != torch.uint8 or image.dim() != 4 or image.shape[3] != 3:
+        raise ValueError("normalize_flip_pack expects uint8 [B,H,W,3]")
+    if not image.is_contiguous():
+        image = image.contiguous()
+    B, H, W, _ = image.shape
+    Hp, Wp, pt, pl = spec
+    dev = image.device
+    if out is None:
+        out = torch.empty((B, H, W, 3), dtype=torch.bfloat16, device=dev)
+    if xp is None:
+        xp = torch.empty((B, Hp, Wp, 4), dtype=torch.bfloat16, device=dev)
+    for t, shape in ((out, (B, H, W, 3)), (xp, (B, Hp, Wp, 4))):
+        if t.shape != shape or t.dtype != torch.bfloat16 or not t.is_contiguous() \
+                or t.device != dev:
+            raise ValueError(f"normalize_flip_pack: output must be a contiguous bf16 {shape} "
+                             "tensor on the image's device")
+    m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    s = (ctypes.c_float * 3)(*[float(v) for v in std])
+    seed = next(_flip_seed) if seed is None else seed
+    check(lib().zk_normalize_flip_pack_c3(image.data_ptr(), out.data_ptr(), xp.data_ptr(), B, H,
+                                          W, Hp, Wp, pt, pl, m, s, int(bool(flip)), seed,
+                                          stream_ptr(dev)), "zk_normalize_flip_pack_c3")
+    return out, xp
+
+
 CHUNK = 16384
 
 

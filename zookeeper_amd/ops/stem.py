@@ -22,7 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Optional
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -103,6 +103,26 @@ def _bn_bwd_coef(L, st, sums, coef, gamma_p, beta_p, P, C, dev, stripes: int = 1
 # (backward passes; tests / diagnostics)
 FUSED_BN2_SUMS = [0]
 
+# Padded-input layouts of the stems that ran: (H, W, Cin) -> (Hp, Wp, pt, pl).
+# The loader's preprocessing (data/preprocessing.py device_transform) writes
+# that layout itself on its copy stream, next to the normalised image, and
+# hands it over as ``x._zk_stem_xp = (xp, spec, x._version)``; the stem then
+# skips its pack kernel (PREPACKED counts those forwards).
+PACK_SPECS: Dict[Tuple[int, int, int], Tuple[int, int, int, int]] = {}
+PREPACKED = [0]
+
+
+def prepacked_input(x: torch.Tensor, spec) -> Optional[torch.Tensor]:
+    """The loader-written padded input of ``x`` if it matches ``spec`` and x
+    was not modified since."""
+    h = getattr(x, "_zk_stem_xp", None)
+    if h is None:
+        return None
+    xp, hspec, version = h
+    if tuple(hspec) != tuple(spec) or version != x._version or xp.device != x.device:
+        return None
+    return xp
+
 
 class _StemFn(torch.autograd.Function):
     @staticmethod
@@ -122,9 +142,15 @@ class _StemFn(torch.autograd.Function):
         L = lib()
 
         xn = x.permute(0, 2, 3, 1).contiguous()
-        xp = torch.empty((B, Hp, Wp, 4), dtype=torch.bfloat16, device=dev)
-        check(L.zk_stem_pack_input(xn.data_ptr(), xp.data_ptr(), B, H, W, Cin, Hp, Wp, pt, pl,
-                                   st), "zk_stem_pack_input")
+        spec = (Hp, Wp, pt, pl)
+        PACK_SPECS[(H, W, Cin)] = spec
+        xp = prepacked_input(x, spec) if Cin == 3 else None
+        if xp is not None:
+            PREPACKED[0] += 1
+        else:
+            xp = torch.empty((B, Hp, Wp, 4), dtype=torch.bfloat16, device=dev)
+            check(L.zk_stem_pack_input(xn.data_ptr(), xp.data_ptr(), B, H, W, Cin, Hp, Wp, pt,
+                                       pl, st), "zk_stem_pack_input")
         w_ohwi = weight.detach().permute(0, 2, 3, 1).contiguous()
         ws = torch.empty((KH, Cout, 32), dtype=torch.bfloat16, device=dev)
         if os.environ.get("ZK_DEBUG_STEM"):
