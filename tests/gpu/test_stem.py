@@ -272,34 +272,3 @@ def test_loader_packed_input_is_bit_identical(flip):
     n1 = stem_ops.PREPACKED[0]
     b(x)
     assert stem_ops.PREPACKED[0] == n1
-
-
-@pytest.mark.parametrize("hw,B", [(64, 5), (224, 3)])
-def test_pipelined_pool_kernel_is_bit_identical(hw, B):
-    """runtime.stem_pool_pp: the software-pipelined F2 kernel (conv of tile T
-    with the pool of tile T-1, two y1 buffers) must write exactly what the
-    sequential kernel writes: pooled output, BN-2 statistics and every
-    gradient downstream of the argmax routing."""
-    from zookeeper_amd.ops.options import OPTS, set_options
-
-    torch.manual_seed(5)
-    a = _stem(True).cuda().to(memory_format=torch.channels_last)
-    b = copy.deepcopy(a)
-    x = torch.randn(B, 3, hw, hw, device="cuda").to(torch.bfloat16)
-    x = x.contiguous(memory_format=torch.channels_last)
-    old = OPTS.stem_pool_pp
-    try:
-        set_options(stem_pool_pp=True)
-        y_a = a(x)
-        set_options(stem_pool_pp=False)
-        y_b = b(x)
-    finally:
-        set_options(stem_pool_pp=old)
-    assert torch.equal(y_a, y_b)
-    for (n, u), (_, v) in zip(a.named_buffers(), b.named_buffers()):
-        assert torch.equal(u, v), n
-    g = torch.randn_like(y_a)
-    y_a.backward(g)
-    y_b.backward(g)
-    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
-        assert torch.equal(p.grad, q.grad), n

@@ -2413,9 +2413,6 @@ ZK_EXPORT int zk_igemm_fwd_supported(int B, int H, int W, int Cin, int Cout, int
                       pl, Ho, Wo, pad_ones, 0, variant, 1, nullptr) == 0;
 }
 
-// stem_fused.hip: the software-pipelined F2 kernel (key 9)
-extern int g_opt_stem_pool_pp;
-
 // Host-side kernel options (see g_opt_* above; ops/options.py).  Returns 0,
 // or -1 for an unknown key.
 ZK_EXPORT int zk_set_option(int key, int value) {
@@ -2427,7 +2424,6 @@ ZK_EXPORT int zk_set_option(int key, int value) {
     case 6: g_opt_dgrad_deep = value; return 0;
     case 7: g_opt_wgrad_deep = value; return 0;
     case 8: g_opt_epilogue_prefetch = value; return 0;
-    case 9: g_opt_stem_pool_pp = value; return 0;
     default: return -1;
   }
 }
@@ -2441,7 +2437,6 @@ ZK_EXPORT int zk_get_option(int key) {
     case 6: return g_opt_dgrad_deep;
     case 7: return g_opt_wgrad_deep;
     case 8: return g_opt_epilogue_prefetch;
-    case 9: return g_opt_stem_pool_pp;
     default: return -1;
   }
 }

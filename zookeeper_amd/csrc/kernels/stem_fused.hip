@@ -521,202 +521,6 @@ __global__ __launch_bounds__(F2_NT, 1) void stem_fwd_pool_kernel(
   }
 }
 
-// F2, software-pipelined: the conv of tile T and the pool of tile T - 1 run
-// in the same iteration (y1 staged in two LDS buffers), and waves 0-3 do the
-// conv first while waves 4-7 pool first, so the two waves that share a SIMD
-// are in different phases (MFMA on one, VALU / LDS on the other) instead of
-// both waiting at the barrier with the same unit busy.
-constexpr int F2P_LDS = W_BYTES + 2 * F2_LB + 2 * F2_YT;
-static_assert(F2P_LDS <= 160 * 1024, "F2 pipelined LDS");
-
-__global__ __launch_bounds__(F2_NT, 1) void stem_fwd_pool_pp_kernel(
-    const unsigned char* __restrict__ xp, const unsigned char* __restrict__ ws,
-    const float* __restrict__ coef1, uint16_t* __restrict__ p, uint8_t* __restrict__ arg,
-    uint16_t* __restrict__ ya, float* __restrict__ part, FGeom g, int tiles_w, int tiles_img,
-    int ntiles) {
-  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
-  unsigned char* wl = smem;
-  unsigned char* lb0 = smem + W_BYTES;
-  unsigned char* yt0 = smem + W_BYTES + 2 * F2_LB;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int r32 = lane & 31, h = lane >> 5;
-  const int blk = xcd_linear(blockIdx.x, gridDim.x), nblk = gridDim.x;
-  const int cg = tid & 7;  // channel group of this thread in the pool phase
-  const int po = tid >> 3;
-  const int pi = po / F2_PC, pj = po - (po / F2_PC) * F2_PC;
-  const bool pitem = po < F2_PR * F2_PC;
-  float a1[8], s1[8], sg[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    a1[k] = coef1[cg * 8 + k];
-    s1[k] = coef1[SC + cg * 8 + k];
-    sg[k] = a1[k] < 0.f ? -1.f : 1.f;
-  }
-  uint4 flip;  // bf16 sign bits of the channels with a < 0
-  {
-    uint32_t f[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      f[q] = (a1[2 * q] < 0.f ? 0x8000u : 0u) | (a1[2 * q + 1] < 0.f ? 0x80000000u : 0u);
-    flip = make_uint4(f[0], f[1], f[2], f[3]);
-  }
-  auto tile_pos = [&](int T, int& b, int& oh0, int& ow0) {
-    b = T / tiles_img;
-    const int rem = T - b * tiles_img;
-    const int th = rem / tiles_w;
-    oh0 = th * F2_PR;
-    ow0 = (rem - th * tiles_w) * F2_PC;
-  };
-  float bs1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bs2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-
-  // conv of the tile whose line buffer is lbc -> y1 (bf16) in ytb[m][co]
-  auto conv = [&](const unsigned char* lbc, unsigned char* ytb) {
-    f32x16 acc[2][1];
-    conv_tile<F2_TR, F2_TC, 1>(wl, lbc, 32 * wave, lane, acc);
-    const int m = 32 * wave + r32;
-    const int swz = (m >> 1) & 7;
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int chunk = 4 * a + q;
-        const uint2 v = make_uint2(zk::pack_bf16x2(acc[a][0][4 * q], acc[a][0][4 * q + 1]),
-                                   zk::pack_bf16x2(acc[a][0][4 * q + 2], acc[a][0][4 * q + 3]));
-        *reinterpret_cast<uint2*>(ytb + m * 128 + ((chunk ^ swz) << 4) + 8 * h) = v;
-      }
-  };
-  // relu(BN-1) -> 3x3/2 max pool of tile Tp from its y1 in ytb: one (pool
-  // output, channel group) per thread, exactly three stores per thread
-  auto pool = [&](int Tp, const unsigned char* ytb) {
-    int b, oh0, ow0;
-    tile_pos(Tp, b, oh0, ow0);
-    const int hr0 = 2 * oh0 - g.pt2, wc0 = 2 * ow0 - g.pl2;  // conv coords of region (0, 0)
-    const int i = pitem ? pi : 0, j = pitem ? pj : 0;
-    const int oh = oh0 + i, ow = ow0 + j;
-    const bool live = pitem && oh < g.H2 && ow < g.W2;
-    // first maximum of relu(a y + s) = first maximum of y ^ sign(a) (see
-    // stem_fwd_pool_kernel); out-of-image taps read -inf
-    uint4 tv[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int m = (2 * i + t / 3) * F2_TC + 2 * j + t % 3;
-      tv[t] = *reinterpret_cast<const uint4*>(ytb + m * 128 + ((cg ^ ((m >> 1) & 7)) << 4));
-    }
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      tv[t].x ^= flip.x;
-      tv[t].y ^= flip.y;
-      tv[t].z ^= flip.z;
-      tv[t].w ^= flip.w;
-    }
-    const bool interior = hr0 + 2 * i >= 0 && hr0 + 2 * i + 2 < g.Ho && wc0 + 2 * j >= 0 &&
-                          wc0 + 2 * j + 2 < g.Wo;
-    if (!interior) {
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int hc = hr0 + 2 * i + t / 3, wc = wc0 + 2 * j + t % 3;
-        if (!(hc >= 0 && hc < g.Ho && wc >= 0 && wc < g.Wo))
-          tv[t] = make_uint4(0xFF80FF80u, 0xFF80FF80u, 0xFF80FF80u, 0xFF80FF80u);  // -inf
-      }
-    }
-    float best[8], yb[8];
-    uint32_t bi[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) bi[k] = 0;
-    unpack8(tv[0], best);
-#pragma unroll
-    for (int t = 1; t < 9; ++t) {
-      float v[8];
-      unpack8(tv[t], v);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const bool gt = v[k] > best[k];
-        best[k] = gt ? v[k] : best[k];
-        bi[k] = gt ? (uint32_t)t : bi[k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      yb[k] = best[k] * sg[k];
-      best[k] = fmaxf(fmaf(a1[k], yb[k], s1[k]), 0.f);
-    }
-    const uint4 pk = pack8f(best);
-    const long long off = (((long long)b * g.H2 + oh) * g.W2 + ow) * SC + cg * 8;
-    uint4* dp_ = live ? reinterpret_cast<uint4*>(p + off) : &g_pool_sink[0];
-    uint4* dy_ = live ? reinterpret_cast<uint4*>(ya + off) : &g_pool_sink[1];
-    uint2* da_ = live ? reinterpret_cast<uint2*>(arg + off)
-                      : reinterpret_cast<uint2*>(&g_pool_sink[0]);
-    *dp_ = pk;
-    *dy_ = pack8f(yb);
-    *da_ = make_uint2(bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
-                      bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
-    float st[8];
-    unpack8(pk, st);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float v = live ? st[k] : 0.f;
-      bs1[k] += v;
-      bs2[k] += v * v;
-    }
-  };
-
-  load_weights<F2_NT>(wl, ws, tid);
-  if (blk < ntiles) {
-    int b, oh0, ow0;
-    tile_pos(blk, b, oh0, ow0);
-    issue_lbuf<F2_TR, F2_TC, F2_NT>(lb0, xp, g, b, 2 * oh0 - g.pt2, 2 * ow0 - g.pl2, tid);
-  }
-  const bool conv_first = wave < F2_NT / 128;  // waves 0-3 (4-7 share their SIMDs)
-  int it = 0;
-  for (int T = blk; T < ntiles; T += nblk, ++it) {
-    // the line buffer of T retired (issued in the previous iteration, before
-    // that iteration's three pool stores, which may stay in flight); the
-    // barrier also publishes the previous conv's y1 and ends every read of
-    // the buffers this iteration overwrites
-    if (it <= 1)
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (T + nblk < ntiles) {
-      int bn, on, wn;
-      tile_pos(T + nblk, bn, on, wn);
-      issue_lbuf<F2_TR, F2_TC, F2_NT>(lb0 + ((it + 1) & 1) * F2_LB, xp, g, bn, 2 * on - g.pt2,
-                                      2 * wn - g.pl2, tid);
-    }
-    const unsigned char* lbc = lb0 + (it & 1) * F2_LB;
-    unsigned char* ytc = yt0 + (it & 1) * F2_YT;
-    const unsigned char* ytp = yt0 + ((it & 1) ^ 1) * F2_YT;
-    if (conv_first) {
-      conv(lbc, ytc);
-      if (it > 0) pool(T - nblk, ytp);
-    } else {
-      if (it > 0) pool(T - nblk, ytp);
-      conv(lbc, ytc);
-    }
-  }
-  if (it > 0) {  // the last tile's pool
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    pool(blk + (it - 1) * nblk, yt0 + ((it - 1) & 1) * F2_YT);
-  }
-  if (!part) return;
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);  // [512][2][8]
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    red[(tid * 2 + 0) * 8 + k] = bs1[k];
-    red[(tid * 2 + 1) * 8 + k] = bs2[k];
-  }
-  __syncthreads();
-  if (tid < 2 * SC) {
-    const int which = tid / SC, c = tid % SC, g8 = c >> 3, k = c & 7;
-    float t = 0.f;
-    for (int r = g8; r < F2_NT; r += 8) t += red[(r * 2 + which) * 8 + k];
-    part[((long long)blockIdx.x * 2 + which) * SC + c] = t;
-  }
-}
-
 // ===========================================================================
 // B2: conv (recomputed) -> dy1 -> weight gradient.  Tile 8 x 16 conv outputs
 // (4 x 8 pool stride cells).  Per tile:
@@ -1136,9 +940,6 @@ ZK_EXPORT int zk_stem_fwd_stats(const void* xp, const void* ws, void* part, int 
   return 0;
 }
 
-// stem_pool_pp (option key 9): the software-pipelined F2 kernel.
-int g_opt_stem_pool_pp = 1;
-
 ZK_EXPORT int zk_stem_fwd_pool(const void* xp, const void* ws, const void* coef1, void* p,
                                void* arg, void* ya, void* part, int B, int Cin, int KW, int Ho,
                                int Wo, int Hp, int Wp, int H2, int W2, int pt2, int pl2,
@@ -1150,19 +951,11 @@ ZK_EXPORT int zk_stem_fwd_pool(const void* xp, const void* ws, const void* coef1
   if (nt >= (1LL << 31)) return (int)hipErrorInvalidValue;
   const int grid = grid_for(nt, 1);
   if (nparts) *nparts = grid;
-  if (g_opt_stem_pool_pp) {
-    if (int e = set_lds_once(stem_fwd_pool_pp_kernel, F2P_LDS)) return e;
-    hipLaunchKernelGGL(stem_fwd_pool_pp_kernel, dim3(grid), dim3(F2_NT), F2P_LDS, st,
-                       (const unsigned char*)xp, (const unsigned char*)ws, (const float*)coef1,
-                       (uint16_t*)p, (uint8_t*)arg, (uint16_t*)ya, (float*)part, g, tw, th * tw,
-                       (int)nt);
-  } else {
-    if (int e = set_lds_once(stem_fwd_pool_kernel, F2_LDS)) return e;
-    hipLaunchKernelGGL(stem_fwd_pool_kernel, dim3(grid), dim3(F2_NT), F2_LDS, st,
-                       (const unsigned char*)xp, (const unsigned char*)ws, (const float*)coef1,
-                       (uint16_t*)p, (uint8_t*)arg, (uint16_t*)ya, (float*)part, g, tw, th * tw,
-                       (int)nt);
-  }
+  if (int e = set_lds_once(stem_fwd_pool_kernel, F2_LDS)) return e;
+  hipLaunchKernelGGL(stem_fwd_pool_kernel, dim3(grid), dim3(F2_NT), F2_LDS, st,
+                     (const unsigned char*)xp, (const unsigned char*)ws, (const float*)coef1,
+                     (uint16_t*)p, (uint8_t*)arg, (uint16_t*)ya, (float*)part, g, tw, th * tw,
+                     (int)nt);
   ZK_CHECK_LAUNCH();
   return 0;
 }

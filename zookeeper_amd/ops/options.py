@@ -67,15 +67,8 @@ class KernelOptions:
     # binary convs with >= 128 input channels.
     dgrad_deep: bool = True
     # ... and weight-gradient kernel for the stride-1 3x3 convs with >= 256
-    # input and output channels.  Exempt from wgrad_slab_mb: its 256x256 dW
-    # tiles leave (Cout/256)(Cin/256)*9 tiles per split, so the cap would cut
-    # a 14x14x256 layer from 57 splits (513 blocks) to 13 (117 blocks, under
-    # half the CUs).  Peak slab at batch 1536: ~134 MB (14x14x256, 57 x
-    # 2.36 MB) and ~141 MB (7x7x512, 15 x 9.4 MB), freed after the layer.
+    # input and output channels.
     wgrad_deep: bool = True
-    # Fused stem F2 (conv -> BN-1 + ReLU -> max pool) software-pipelined:
-    # conv of tile T with the pool of tile T-1, half the waves in each phase.
-    stem_pool_pp: bool = True
     # Float BatchNorm backward sums (sum g, sum g*xhat) added up in the data-
     # gradient epilogue of the 1x1 conv that consumes the BN output (when that
     # epilogue writes the BN output's whole gradient) instead of a separate
@@ -97,7 +90,7 @@ OPTS = KernelOptions()
 
 # keys the native library reads (zk_set_option); values are ints
 _NATIVE_KEYS = {"tile_huge": 0, "deterministic": 2, "dgrad_rw": 3, "wgrad_slab_mb": 5,
-                "dgrad_deep": 6, "wgrad_deep": 7, "epilogue_prefetch": 8, "stem_pool_pp": 9}
+                "dgrad_deep": 6, "wgrad_deep": 7, "epilogue_prefetch": 8}
 
 
 def _push_native() -> None:

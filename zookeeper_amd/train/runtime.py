@@ -50,7 +50,6 @@ class Runtime:
     bn_bwd_fuse: bool = Field(True)
     bn_masked_handoff: bool = Field(True)
     epilogue_prefetch: bool = Field(True)
-    stem_pool_pp: bool = Field(True)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
     deterministic: bool = Field(False)
