@@ -67,7 +67,11 @@ class KernelOptions:
     # binary convs with >= 128 input channels.
     dgrad_deep: bool = True
     # ... and weight-gradient kernel for the stride-1 3x3 convs with >= 256
-    # input and output channels.
+    # input and output channels.  Exempt from wgrad_slab_mb: its 256x256 dW
+    # tiles leave (Cout/256)(Cin/256)*9 tiles per split, so the cap would cut
+    # a 14x14x256 layer from 57 splits (513 blocks) to 13 (117 blocks, under
+    # half the CUs).  Peak slab at batch 1536: ~134 MB (14x14x256, 57 x
+    # 2.36 MB) and ~141 MB (7x7x512, 15 x 9.4 MB), freed after the layer.
     wgrad_deep: bool = True
     # Float BatchNorm backward sums (sum g, sum g*xhat) added up in the data-
     # gradient epilogue of the 1x1 conv that consumes the BN output (when that
