@@ -335,24 +335,3 @@ def test_default_mode_gradients_bit_identical(model):
     assert diff.numel() == 0, f"{diff.shape[0]} gradient elements differ, first at {diff[:5]}"
     for a, b in zip(b0, b1):
         assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("hold_hw", [1, 16 * 16])
-def test_held_back_side_stream_weight_gradients_are_identical(hold_hw):
-    """runtime.wgrad_hold_hw: side-stream weight gradients of the layers with
-    >= hold_hw input pixels launch at the head of the stem's backward instead
-    of right after their dy; the gradients are bit-identical to launching
-    them at once (every one of them, 1: all binary convs held)."""
-    from zookeeper_amd.ops import options, streams
-
-    x = _batch(seed=21)
-    try:
-        options.set_options(wgrad_hold_hw=0)
-        base = _e18_grads(x)
-        options.set_options(wgrad_hold_hw=hold_hw)
-        held = _e18_grads(x)
-        assert not streams._held  # every held launch was released
-    finally:
-        options.reset()
-    assert torch.equal(base[0], held[0])
-    assert torch.equal(base[1], held[1])

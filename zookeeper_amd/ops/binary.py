@@ -358,28 +358,16 @@ class _BinaryBlockFn(torch.autograd.Function):
             # weight-gradient sign operand: the bf16 image, or the e2m1 one
             sxw, operand = (sx4, "fp4") if ctx.wfp4 else (sx, "image")
             side = streams.active() and w_direct is not None and sxw is not None
-            held = side and 0 < OPTS.wgrad_hold_hw <= H * W
             if side:
                 sstream = streams.side_stream(dev)
                 ready = torch.cuda.Event()
                 ready.record()  # dy written (compute stream)
-
-                def launch(ready=ready, sstream=sstream, dy=dy, sxw=sxw, w_ohwi=w_ohwi,
-                           dw=w_direct.permute(0, 2, 3, 1), operand=operand):
-                    sstream.wait_event(ready)
-                    with torch.cuda.stream(sstream):
-                        _wgrad(L, dy, sxw, w_ohwi, dw, ctx, sstream.cuda_stream, operand)
-                        done = torch.cuda.Event()
-                        done.record(sstream)
-                    return done
-
-                if held:
-                    # runtime.wgrad_hold_hw: launched when the stem's backward
-                    # starts (readiness signalled from there)
-                    streams.hold(lambda launch=launch, p=weight_p:
-                                 streams.defer_ready(launch(), p))
-                else:
-                    done = launch()
+                sstream.wait_event(ready)
+                with torch.cuda.stream(sstream):
+                    _wgrad(L, dy, sxw, w_ohwi, w_direct.permute(0, 2, 3, 1), ctx,
+                           sstream.cuda_stream, operand)
+                    done = torch.cuda.Event()
+                    done.record(sstream)
                 streams.keep(dy, sxw, w_ohwi)  # released once the compute stream joins
             else:
                 dw = (w_direct.permute(0, 2, 3, 1) if w_direct is not None  # OHWI view
@@ -427,8 +415,7 @@ class _BinaryBlockFn(torch.autograd.Function):
                 # (the bucketer's comm stream waits for their events; the
                 # compute stream only at the end of the backward)
                 streams.flush(wait=False)
-                if not held:
-                    streams.defer_ready(done, weight_p)
+                streams.defer_ready(done, weight_p)
             elif w_direct is not None:
                 grad_ready(weight_p)
         else:

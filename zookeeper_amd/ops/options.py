@@ -29,10 +29,6 @@ class KernelOptions:
     bconv_fp4: bool = True
     # Binary-conv weight gradients on a side HIP stream (44.9k vs 41.7k off).
     wgrad_side_stream: bool = True
-    # Side-stream weight gradients of binary convs whose input has >= this
-    # many pixels (H*W) are held back until the stem's backward starts
-    # (streams.hold); 0 = launch every one as soon as its dy exists.
-    wgrad_hold_hw: int = 0
     # Recompute-fused ImageNet stem (False: the materialising kernels).
     stem_fused: bool = True
     # Float convolutions on the MFMA implicit-GEMM kernels (False: library).

@@ -27,7 +27,6 @@ from typing import Dict, Optional, Tuple
 import torch
 
 from zookeeper_amd.nn.layers import same_padding
-from zookeeper_amd.ops import streams
 from zookeeper_amd.ops.options import OPTS
 from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, slab_reduce,
                                         stream_ptr, zeroed, zeroed_scratch)
@@ -290,9 +289,6 @@ class _StemFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        # held-back side-stream weight gradients (runtime.wgrad_hold_hw) now
-        # overlap the stem's backward
-        streams.release_held()
         xp, ws, y1, arg, p, coef1, coef2, g1, g2 = ctx.saved_tensors  # fused: y1 = ya
         weight, g1p, b1p, g2p, b2p = ctx.params
         (B, Cin, Cout, KH, KW, s, Ho, Wo, Hp, Wp, H2, W2, pk, ps, pt2, pl2) = ctx.geom

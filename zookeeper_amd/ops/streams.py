@@ -33,7 +33,7 @@ from __future__ import annotations
 import contextlib
 import os
 import sys
-from typing import Callable, Dict, List, Tuple
+from typing import Dict, List, Tuple
 
 import torch
 
@@ -53,10 +53,6 @@ _unwaited: List[torch.cuda.Event] = []
 # which runs a step ahead of the GPU: ~2.5 fresh device allocations per E18
 # step, memory growth and multi-second hipMalloc stalls.)
 _keep: List[torch.Tensor] = []
-# side-stream weight-gradient launches held back (hold / release_held): run
-# when the stem's backward starts, where the compute stream has no other
-# work for the side stream to contend with
-_held: List[Callable[[], None]] = []
 
 
 def active() -> bool:
@@ -91,21 +87,6 @@ def defer_ready(event: torch.cuda.Event, param) -> None:
         print(f"[streams {os.getpid()}] defer {tuple(param.shape)} event {id(event) % 10007}",
               file=sys.stderr, flush=True)
     _pending.append((event, param))
-
-
-def hold(launch: Callable[[], None]) -> None:
-    """Queue a side-stream launch until :func:`release_held` (its inputs must
-    be kept alive with :func:`keep`)."""
-    _held.append(launch)
-
-
-def release_held() -> None:
-    """Launch every held weight gradient now (called at the head of the stem's
-    backward, and at session exit for models without one)."""
-    items = list(_held)
-    _held.clear()
-    for launch in items:
-        launch()
 
 
 def unwaited_events() -> List[torch.cuda.Event]:
@@ -150,12 +131,10 @@ def session(device: torch.device):
     _pending.clear()
     _unwaited.clear()
     _keep.clear()
-    _held.clear()
     _active = use
     try:
         yield
     finally:
         _active = False
         if use:
-            release_held()
             flush()

@@ -34,7 +34,6 @@ class Runtime:
     # --- kernel variants (ops/options.py documents each and its measurement)
     bconv_fp4: bool = Field(True)
     wgrad_side_stream: bool = Field(True)
-    wgrad_hold_hw: int = Field(0)
     stem_fused: bool = Field(True)
     conv_mfma: bool = Field(True)
     conv3_mfma: bool = Field(True)
