@@ -242,7 +242,8 @@ def main() -> int:
         worst = max(range(len(step_ms)), key=lambda i: step_ms[i])
         hw = max(range(len(host_t)), key=lambda i: host_t[i])
         print(f"[bench] slowest step {worst}: GPU {step_ms[worst]:.2f} ms; slowest host step "
-              f"{hw}: {1e3 * host_t[hw]:.2f} ms; allocator in timed region {alloc_delta}",
+              f"{hw}: {1e3 * host_t[hw]:.2f} ms; allocator in timed region {alloc_delta}; "
+              f"peak allocated {torch.cuda.max_memory_allocated(info.device) / 2**30:.1f} GiB",
               file=sys.stderr, flush=True)
     comm = trainer.bucketer.pop_timings()
     if loader is not None:

@@ -335,3 +335,23 @@ def test_default_mode_gradients_bit_identical(model):
     assert diff.numel() == 0, f"{diff.shape[0]} gradient elements differ, first at {diff[:5]}"
     for a, b in zip(b0, b1):
         assert torch.equal(a, b)
+
+
+def test_float_wgrad_side_stream_gradients_identical():
+    """runtime.float_wgrad_side_stream: the ResNet's 1x1 / 3x3 weight
+    gradients run on the side stream (ops.streams.side_wgrad, inputs released
+    SIDE_LAG launches later); the gradients must be bit-identical to the
+    compute-stream order, and every lagged hold is released at the join."""
+    from zookeeper_amd.ops import options, streams
+
+    batch = _batch(seed=17)
+    try:
+        options.set_options(float_wgrad_side_stream=False)
+        base = _resnet_grads(batch)
+        options.set_options(float_wgrad_side_stream=True)
+        side = _resnet_grads(batch)
+    finally:
+        options.reset()
+    assert not streams._lagged and not streams._keep
+    assert torch.equal(base[0], side[0])
+    assert torch.equal(base[1], side[1])

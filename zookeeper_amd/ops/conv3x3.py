@@ -27,7 +27,7 @@ from typing import Optional
 import torch
 
 from zookeeper_amd.ops import pointwise
-from zookeeper_amd.ops import weight_images
+from zookeeper_amd.ops import streams, weight_images
 from zookeeper_amd.ops._native import check, direct_grad, grad_ready, igemm_wgrad, lib, stream_ptr
 from zookeeper_amd.ops.options import OPTS
 
@@ -93,6 +93,19 @@ class _Conv3x3Fn(torch.autograd.Function):
         L = lib()
         st = stream_ptr(dev)
         dx = dweight = None
+        side = False
+        if ctx.needs_input_grad[1]:
+            # weight gradient first, on the side stream when one is active
+            target = direct_grad(weight, channels_last=True)
+            if target is not None:
+                dw_t = target.permute(0, 2, 3, 1)
+                wf_t = weight.detach().permute(0, 2, 3, 1)
+                if wf_t.dtype == torch.float32 and wf_t.is_contiguous():
+                    side = streams.side_wgrad(
+                        dev, lambda sp: igemm_wgrad(g, xn, wf_t, dw_t,
+                                                    (B, H, W, Cin, H, W, Cout, 3, 3, 1, 1, 1),
+                                                    0, _INF, sp, "zk_igemm_wgrad(3x3)"),
+                        weight, (g, xn))
         if ctx.needs_input_grad[0]:
             wt = ctx.wt
             if wt is None:
@@ -103,7 +116,7 @@ class _Conv3x3Fn(torch.autograd.Function):
                                    W, Cin, H, W, Cout, 3, 3, 1, 1, 1, -1, st),
                   "zk_igemm_dgrad(3x3)")
             dx = dxn.permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and not side:
             target = direct_grad(weight, channels_last=True)
             dw = (target.permute(0, 2, 3, 1) if target is not None
                   else torch.zeros((Cout, 3, 3, Cin), dtype=torch.float32, device=dev))

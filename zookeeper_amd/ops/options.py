@@ -29,6 +29,9 @@ class KernelOptions:
     bconv_fp4: bool = True
     # Binary-conv weight gradients on a side HIP stream (44.9k vs 41.7k off).
     wgrad_side_stream: bool = True
+    # ... and the float 1x1 / 3x3 convs' (ResNet): MFMA-bound weight
+    # gradients next to the memory-bound BN passes (ops.streams.side_wgrad).
+    float_wgrad_side_stream: bool = True
     # Recompute-fused ImageNet stem (False: the materialising kernels).
     stem_fused: bool = True
     # Float convolutions on the MFMA implicit-GEMM kernels (False: library).

@@ -28,7 +28,7 @@ from typing import Optional
 
 import torch
 
-from zookeeper_amd.ops import weight_images
+from zookeeper_amd.ops import streams, weight_images
 from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, igemm_wgrad, lib,
                                         stream_ptr, zeroed_scratch)
 from zookeeper_amd.ops.options import OPTS
@@ -131,6 +131,20 @@ class _Conv1x1Fn(torch.autograd.Function):
         L = lib()
         st = stream_ptr(dev)
         dx = dweight = None
+        side = False
+        if ctx.needs_input_grad[1]:
+            # weight gradient first, on the side stream when one is active: it
+            # then overlaps this data gradient and the BN passes that follow
+            target = direct_grad(weight)
+            if target is not None:
+                dw_t = target.view(Cout, Cin)
+                wf_t = weight.detach().reshape(Cout, Cin)
+                if wf_t.dtype == torch.float32 and wf_t.is_contiguous():
+                    side = streams.side_wgrad(
+                        dev, lambda sp: igemm_wgrad(g2, x2, wf_t, dw_t,
+                                                    (B, H, W, Cin, H, W, Cout, 1, 1, 1, 0, 0),
+                                                    0, _INF, sp, "zk_igemm_wgrad(1x1)"),
+                        weight, (g2, x2))
         # + the identity shortcut's gradient of x (norm_pool.ResidualHandoff):
         # a tensor, or (g, ReLU mask bits) that the epilogue masks itself
         dres = ctx.handoff.take() if ctx.handoff is not None else None
@@ -172,7 +186,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 dx = None  # x's other consumer adds it (a downsampling shortcut conv)
             else:
                 dx = dx2.view(B, H, W, Cin).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and not side:
             target = direct_grad(weight)
             dw = target.view(Cout, Cin) if target is not None else torch.zeros(
                 (Cout, Cin), dtype=torch.float32, device=dev)

@@ -33,7 +33,7 @@ from __future__ import annotations
 import contextlib
 import os
 import sys
-from typing import Dict, List, Tuple
+from typing import Callable, Dict, List, Tuple
 
 import torch
 
@@ -81,6 +81,41 @@ def keep(*tensors: torch.Tensor) -> None:
 _DEBUG = os.environ.get("ZK_COMM_DEBUG_EVENTS", "0") == "1"
 
 
+# side_wgrad: the compute stream joins a float-conv weight gradient this many
+# launches later and releases its inputs then (bounds the memory kept alive
+# and the side stream's backlog)
+SIDE_LAG = 4
+_lagged: List[Tuple[torch.cuda.Event, tuple]] = []
+
+
+def side_wgrad(device: torch.device, launch: Callable[[int], None], param,
+               keep_alive: tuple = ()) -> bool:
+    """Float-conv weight gradient on the side stream: ``launch(stream)``
+    enqueues it (``stream`` = the raw ``hipStream_t``) after everything the
+    compute stream has queued so far; ``param``'s readiness is signalled at
+    the next :func:`flush`.  ``keep_alive``: compute-stream tensors the launch
+    reads, released once the compute stream has joined it (``SIDE_LAG``
+    launches later).  Returns False (nothing launched) when the side stream
+    is off (outside a :func:`session` or ``runtime.float_wgrad_side_stream``)."""
+    if not (_active and OPTS.float_wgrad_side_stream):
+        return False
+    s = side_stream(device)
+    ready = torch.cuda.Event()
+    ready.record()
+    s.wait_event(ready)
+    with torch.cuda.stream(s):
+        launch(s.cuda_stream)
+        done = torch.cuda.Event()
+        done.record(s)
+    _lagged.append((done, keep_alive))
+    if len(_lagged) > SIDE_LAG:
+        ev, _ = _lagged.pop(0)
+        torch.cuda.current_stream(device).wait_event(ev)
+    flush(wait=False)
+    defer_ready(done, param)
+    return True
+
+
 def defer_ready(event: torch.cuda.Event, param) -> None:
     """``param``'s gradient is complete once ``event`` (side stream) fires."""
     if _DEBUG:
@@ -116,6 +151,7 @@ def flush(wait: bool = True) -> None:
         # every side-stream reader of these is now ordered before the compute
         # stream's next use of their memory
         _keep.clear()
+        _lagged.clear()
     else:
         _unwaited.extend(ev for ev, _ in items)
     for _, p in items:
@@ -131,6 +167,7 @@ def session(device: torch.device):
     _pending.clear()
     _unwaited.clear()
     _keep.clear()
+    _lagged.clear()
     _active = use
     try:
         yield

@@ -34,6 +34,7 @@ class Runtime:
     # --- kernel variants (ops/options.py documents each and its measurement)
     bconv_fp4: bool = Field(True)
     wgrad_side_stream: bool = Field(True)
+    float_wgrad_side_stream: bool = Field(True)
     stem_fused: bool = Field(True)
     conv_mfma: bool = Field(True)
     conv3_mfma: bool = Field(True)
