@@ -25,7 +25,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from zookeeper_amd.ops import weight_images
+from zookeeper_amd.ops import streams, weight_images
 from zookeeper_amd.ops._native import check, direct_grad, grad_ready, igemm_wgrad, lib, stream_ptr
 from zookeeper_amd.ops.options import OPTS
 
@@ -98,6 +98,19 @@ class _ConvFn(torch.autograd.Function):
         L = lib()
         st = stream_ptr(dev)
         dx = dweight = None
+        side = False
+        if ctx.needs_input_grad[1]:
+            # weight gradient first, on the side stream when one is active
+            target = direct_grad(weight, channels_last=True)
+            if target is not None:
+                dw_t = target.permute(0, 2, 3, 1)
+                wf_t = weight.detach().permute(0, 2, 3, 1)
+                if wf_t.dtype == torch.float32 and wf_t.is_contiguous():
+                    geo = (B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl)
+                    side = streams.side_wgrad(
+                        dev, lambda sp: igemm_wgrad(g, xn, wf_t, dw_t, geo, 0, _INF, sp,
+                                                    "zk_igemm_wgrad(conv)"),
+                        weight, (g, xn))
         # + x's other gradient, left by a consumer that ran first (ResidualHandoff)
         dres = ctx.handoff.take() if ctx.handoff is not None else None
         if ctx.needs_input_grad[0]:
@@ -115,7 +128,7 @@ class _ConvFn(torch.autograd.Function):
                                    B, H, W, Cin, Ho, Wo, Cout, kh, kw, s, pt, pl, -1, st),
                   "zk_igemm_dgrad(conv)")
             dx = dxn.permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and not side:
             target = direct_grad(weight, channels_last=True)
             dw = (target.permute(0, 2, 3, 1) if target is not None
                   else torch.zeros((Cout, kh, kw, Cin), dtype=torch.float32, device=dev))
