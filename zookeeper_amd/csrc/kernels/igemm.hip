@@ -121,7 +121,8 @@ int g_opt_dgrad_rw = 1;
 // Default 32 MB (ops/options.py has the measurements).
 int g_opt_wgrad_slab_mb = 32;
 // dgrad_deep (key 6): the phased kernel (deep_gemm.hip, variant 60) for
-// stride-1 3x3 data gradients with Cin % 256 == 0 (igemm_dgrad_impl).
+// stride-1 3x3 data gradients with Cin % 256 == 0 (igemm_dgrad_impl): 1 for
+// the float convs, 2 also for the binary (STE-mask) ones, 0 never.
 int g_opt_dgrad_deep = 1;
 // wgrad_deep (key 7): the same for stride-1 3x3 weight gradients with
 // Cin % 256 == 0 and Cout % 256 == 0 (variant 60 of the wgrad dispatch).
@@ -2036,7 +2037,7 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     const bool le = bs.sums == nullptr;  // (bs.bsums: LE variants, checked at the launch)
     const int v256 = le ? 45 : 14;
     if (g_opt_dgrad_deep && le && !bs.fstats && !bs.bsums && !bs.dmask && c3 &&
-        Cin % 256 == 0 && g.Cout % 64 == 0 && !mask)
+        Cin % 256 == 0 && g.Cout % 64 == 0 && (!mask || g_opt_dgrad_deep >= 2))
       // phased 256x256 schedule (deep_gemm.hip).  Measured at batch 1536 it
       // ties the 256x256 implicit GEMM (14x14x256: 428-484 vs 495 us; 7x7x512
       // 432-462 vs 406 us) and loses for 128 channels (769 vs 594 us) and the

@@ -67,8 +67,9 @@ class KernelOptions:
     # tensors whose consumer takes this path (bconv_fp4 forward only).
     wgrad_fp4: bool = True
     # Phased data-gradient kernel (deep_gemm.hip) for the stride-1 3x3
-    # binary convs with >= 128 input channels.
-    dgrad_deep: bool = True
+    # convs with >= 256 input channels: 1 = float convs only, 2 = the binary
+    # (STE-mask) ones too, 0 = never.
+    dgrad_deep: int = 1
     # ... and weight-gradient kernel for the stride-1 3x3 convs with >= 256
     # input and output channels.  Exempt from wgrad_slab_mb: its 256x256 dW
     # tiles leave (Cout/256)(Cin/256)*9 tiles per split, so the cap would cut
