@@ -68,7 +68,9 @@ class KernelOptions:
     wgrad_fp4: bool = True
     # Phased data-gradient kernel (deep_gemm.hip) for the stride-1 3x3
     # convs with >= 256 input channels: 1 = float convs only, 2 = the binary
-    # (STE-mask) ones too, 0 = never.
+    # (STE-mask) ones too, 0 = never.  Same box, 2 rounds: QuickNet-Large
+    # b1024 28.19k / 28.15k (1) vs 28.01k / 27.96k (2); E18 b1536 50.67k /
+    # 50.77k (1) vs 50.82k / 50.87k (2).
     dgrad_deep: int = 1
     # ... and weight-gradient kernel for the stride-1 3x3 convs with >= 256
     # input and output channels.  Exempt from wgrad_slab_mb: its 256x256 dW
