@@ -229,11 +229,8 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Te
     if op is None:
         raise ValueError(f"{what}: unknown operand {operand!r}")
     if variant < 0 and wgrad_rows_ok(geom) and (pad_ones or op != 1):
-        from zookeeper_amd.ops.options import OPTS
-
-        tb = int(OPTS.wgrad_rows_blocks)
         sb, cb = ctypes.c_int64(0), ctypes.c_int64(0)
-        check(L.zk_wgrad_rows_plan(B, H, W, Cin, Cout, tb, ctypes.byref(sb), ctypes.byref(cb)),
+        check(L.zk_wgrad_rows_plan(B, H, W, Cin, Cout, 0, ctypes.byref(sb), ctypes.byref(cb)),
               what + " (plan)")
         slab = (torch.empty(sb.value // 4, dtype=torch.float32, device=dy.device)
                 if sb.value > 0 else None)
@@ -241,7 +238,7 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, dw: torch.Te
         check(L.zk_wgrad_rows(dy.data_ptr(), x.data_ptr(), w.data_ptr() if w is not None else None,
                               dw.data_ptr(), slab.data_ptr() if slab is not None else None,
                               sb.value, cnt.data_ptr() if cnt is not None else None, cb.value,
-                              B, H, W, Cin, Cout, int(pad_ones), op, float(clip), tb,
+                              B, H, W, Cin, Cout, int(pad_ones), op, float(clip), 0,
                               stream), what)
         return
     if op:

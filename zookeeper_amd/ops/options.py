@@ -66,8 +66,6 @@ class KernelOptions:
     # (expanded to bf16 in LDS): producers then skip the bf16 sign image of
     # tensors whose consumer takes this path (bconv_fp4 forward only).
     wgrad_fp4: bool = True
-    # Grid of the row-streaming weight gradient (blocks; 0 = 256, one per CU).
-    wgrad_rows_blocks: int = 0
     # Phased data-gradient kernel (deep_gemm.hip) for the stride-1 3x3
     # convs with >= 256 input channels: 1 = float convs only, 2 = the binary
     # (STE-mask) ones too, 0 = never.  Same box, 2 rounds: QuickNet-Large

@@ -45,7 +45,6 @@ class Runtime:
     wgrad_slab_mb: int = Field(32)
     wgrad_rows: bool = Field(True)
     wgrad_fp4: bool = Field(True)
-    wgrad_rows_blocks: int = Field(0)
     dgrad_deep: int = Field(1)
     wgrad_deep: bool = Field(True)
     weight_images: bool = Field(True)
