@@ -105,7 +105,8 @@ struct ConvArgs {
 //     1: 28x28x128 wgrad on conv3 64x64, 2: 256-input-channel wgrad 256x256 x 3
 //     stages, 4: 64 -> 128 transition wgrad at 1024 blocks, 8: 7x7x512 wgrad on
 //     128x128, 16: 28x28x128 dgrad variant 27,
-//     32: 3x3 256x256 dgrads with the register epilogue (14, not 45).  Default 16: each wgrad rule wins
+//     32: 3x3 256x256 dgrads with the register epilogue (14, not 45).
+//     Default 48 (16 | 32; bit 32 since round 5): each wgrad rule wins
 //     alone (tools/tune_bconv.py --batch 1024) but costs 0.4-0.9 % of the E18
 //     step, where those kernels overlap the data-gradient chain on the side
 //     stream (bench A/B, 40 steps each: none 43.7k, 1 43.5k, 2 43.5k, 4 43.6k,
@@ -114,7 +115,7 @@ struct ConvArgs {
 //     a fixed order (no float atomics).
 //   dgrad_rw (key 3): the row-window kernel (conv3rw.hip, variant 50) for the
 //     64 -> 64 stride-1 3x3 data gradient by default.
-int g_opt_tile_huge = 16;
+int g_opt_tile_huge = 48;
 int g_opt_deterministic = 0;
 int g_opt_dgrad_rw = 1;
 // wgrad_slab_mb (key 5): cap on the split-K slab bytes of one weight gradient
@@ -2036,10 +2037,13 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
     const int Cin = g.Cin, stride = g.s;
     const bool c3 = conv3_ok(g, 0);
     const bool le = bs.sums == nullptr;  // (bs.bsums: LE variants, checked at the launch)
-    // 3x3 256x256 tiles: the register epilogue (14) when tile_huge bit 32 is
-    // set (batch 1536 standalone, tools/tune_bconv.py: 14x14x256 383 vs 414 us,
-    // 7x7x512 398 vs 418 us, 14x14 256->512 stride 2 215 vs 269 us)
-    const int v256 = (le && !(g.kh == 3 && huge_tiles_env(32))) ? 45 : 14;
+    // 3x3 256x256 tiles at batch >= 1024: the register epilogue (14) when
+    // tile_huge bit 32 is set (batch 1536 standalone, tools/tune_bconv.py:
+    // 14x14x256 383 vs 414 us, 7x7x512 398 vs 418 us, 14x14 256->512 stride 2
+    // 215 vs 269 us; in-step QuickNet-Large b1024 27.63k / 27.64k vs 27.16k /
+    // 27.12k img/s, E18 b1536 49.69k / 49.96k vs 50.15k / 49.80k)
+    const int v256 =
+        (le && !(g.kh == 3 && g.B >= 1024 && huge_tiles_env(32))) ? 45 : 14;
     if (g_opt_dgrad_deep && le && !bs.fstats && !bs.bsums && !bs.dmask && c3 &&
         Cin % 256 == 0 && g.Cout % 64 == 0 && (!mask || g_opt_dgrad_deep >= 2))
       // phased 256x256 schedule (deep_gemm.hip).  Measured at batch 1536 it

@@ -40,7 +40,7 @@ class KernelOptions:
     # 1x1 float convolutions as MFMA GEMMs.
     pw_gemm: bool = True
     # Batch >= 1024 tile-rule bitmask (igemm.hip, see tile_rule comments).
-    tile_huge: int = 16
+    tile_huge: int = 48
     # Bit-reproducible gradients: split-K weight gradients reduced from slabs
     # in a fixed order, BN / bias sums without float atomics.
     deterministic: bool = False

@@ -39,7 +39,7 @@ class Runtime:
     conv_mfma: bool = Field(True)
     conv3_mfma: bool = Field(True)
     pw_gemm: bool = Field(True)
-    tile_huge: int = Field(16)
+    tile_huge: int = Field(48)
     dgrad_rw: bool = Field(True)
     bn_stats_epilogue: bool = Field(True)
     wgrad_slab_mb: int = Field(32)
