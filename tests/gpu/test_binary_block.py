@@ -254,3 +254,34 @@ def test_fp4_weight_gradient_skips_bf16_sign_image(monkeypatch, hw):
     assert ((dx1 - dx2).norm() / dx2.norm()).item() < 1e-3
     for a, b in zip(w1, w2):
         assert torch.equal(a, b)
+
+
+@pytest.mark.timeout(120)
+def test_shortcut_pool_from_the_bn_epilogue_is_bit_identical():
+    """ops.binary_block(pool_out=True): a stage's last block writes the next
+    block's 2x2/2 average-pooled shortcut input in its BN-apply pass
+    (zk_bn_apply_sign_pool) and avg_pool2 takes it; the E18 forward, loss and
+    every gradient must equal the separate pooling pass bit for bit."""
+    import copy
+
+    from zookeeper_amd.models.binary_resnet import BinaryResNetE
+    from zookeeper_amd.train.trainer import prepare_model
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    a = prepare_model(BinaryResNetE((64, 64, 3), 10, 18, backend="hip"), dev).train()
+    assert sum(blk.pool_out for blk in a.body) == 3  # one per stage transition
+    b = copy.deepcopy(a)
+    for blk in b.body:
+        blk.pool_out = False
+    x = torch.randn(6, 3, 64, 64, device=dev).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    ya, yb = a(x), b(x)
+    assert torch.equal(ya, yb)
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        assert torch.equal(p.grad, q.grad), n
+    for (n, u), (_, v) in zip(a.named_buffers(), b.named_buffers()):
+        assert torch.equal(u, v), n

@@ -61,6 +61,57 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
   }
 }
 
+// One 8-channel chunk i (= row * C / 8 + cg) of the BN apply: out bf16 =
+// scale*y + shift (+ residual), and the next binary layer's input
+// quantisation from the stored bf16 values (bf16 sign image, STE mask bits,
+// e2m1 sign image; each optional).  Returns the stored chunk.
+__device__ __forceinline__ uint4 bn_apply_chunk(long long i, const int16_t* __restrict__ y,
+                                                const float (&sc)[8], const float (&sh)[8],
+                                                const uint16_t* __restrict__ res,
+                                                uint16_t* __restrict__ out,
+                                                uint16_t* __restrict__ sx,
+                                                uint8_t* __restrict__ smask, float clip,
+                                                uint32_t* __restrict__ sx4) {
+  const uint4 yv = reinterpret_cast<const uint4*>(y)[i];
+  const int16_t* yy = reinterpret_cast<const int16_t*>(&yv);
+  float o[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = sc[k] * (float)yy[k] + sh[k];
+  if (res) {
+    const uint4 rv = reinterpret_cast<const uint4*>(res)[i];
+    const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[2 * k] += zk::bf16_to_f32((uint16_t)(rr[k] & 0xffff));
+      o[2 * k + 1] += zk::bf16_to_f32((uint16_t)(rr[k] >> 16));
+    }
+  }
+  const uint4 ov = make_uint4(zk::pack_bf16x2(o[0], o[1]), zk::pack_bf16x2(o[2], o[3]),
+                              zk::pack_bf16x2(o[4], o[5]), zk::pack_bf16x2(o[6], o[7]));
+  reinterpret_cast<uint4*>(out)[i] = ov;
+  if (sx || sx4) {
+    // the NEXT binary block's input quantisation, from the stored bf16
+    // values: sign image (bf16 +-1 for the weight gradient, e2m1 nibbles
+    // for the MX-FP4 forward) and STE mask bits (|x| <= clip)
+    const uint32_t ow[4] = {ov.x, ov.y, ov.z, ov.w};
+    uint32_t sw[4];
+    uint32_t mk = 0, n4 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float lo = zk::bf16_to_f32((uint16_t)(ow[k] & 0xffff));
+      const float hi = zk::bf16_to_f32((uint16_t)(ow[k] >> 16));
+      sw[k] = (lo >= 0.f ? 0x3F80u : 0xBF80u) | ((hi >= 0.f ? 0x3F80u : 0xBF80u) << 16);
+      mk |= (uint32_t)(fabsf(lo) <= clip) << (2 * k);
+      mk |= (uint32_t)(fabsf(hi) <= clip) << (2 * k + 1);
+      n4 |= (zk::fp4_sign(lo) | (zk::fp4_sign(hi) << 4)) << (8 * k);
+    }
+    if (sx) reinterpret_cast<uint4*>(sx)[i] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+    if (smask) smask[i] = (uint8_t)mk;  // byte i = channels 8i..8i+7 of the packed mask words
+    if (sx4) sx4[i] = n4;               // 8 channels = 4 bytes of the [P][C/2] e2m1 image
+  }
+  return ov;
+}
+
 // y int16 [P][C] -> out bf16 = scale*y + shift (+ residual bf16).
 // Each thread owns one group of 8 channels (coefficients in registers) and
 // walks rows; CG = C/8 threads cover a row.
@@ -85,45 +136,55 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const int16_t* __restrict
     sh[k] = shift[cg * 8 + k];
   }
   for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
-       r += (long long)gridDim.x * RB) {
-    const long long i = (r * C) / 8 + cg;
-    const uint4 yv = reinterpret_cast<const uint4*>(y)[i];
-    const int16_t* yy = reinterpret_cast<const int16_t*>(&yv);
-    float o[8];
+       r += (long long)gridDim.x * RB)
+    bn_apply_chunk((r * C) / 8 + cg, y, sc, sh, res, out, sx, smask, clip, sx4);
+}
+
+// bn_apply_kernel over 2x2 pixel quads of an even [B][H][W] image, plus the
+// 2x2/2 average pool of the stored output (a downsampling shortcut's input):
+// pooled [B][H/2][W/2][C] bf16, summed in avgpool2_fwd_kernel's order
+// ((h, w), (h, w+1), (h+1, w), (h+1, w+1)) from the stored bf16 values, so it
+// equals that kernel's result bit for bit.
+template <int CG>
+__global__ __launch_bounds__(256) void bn_apply_pool_kernel(
+    const int16_t* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const uint16_t* __restrict__ res,
+    uint16_t* __restrict__ out, int B, int H, int W, uint16_t* __restrict__ sx,
+    uint8_t* __restrict__ smask, float clip, uint32_t* __restrict__ sx4,
+    uint16_t* __restrict__ pooled) {
+  constexpr int QB = 256 / CG;  // quads per block iteration
+  const int cg = threadIdx.x % CG;
+  const int Ho = H / 2, Wo = W / 2;
+  float sc[8], sh[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = sc[k] * (float)yy[k] + sh[k];
-    if (res) {
-      const uint4 rv = reinterpret_cast<const uint4*>(res)[i];
-      const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = scale[cg * 8 + k];
+    sh[k] = shift[cg * 8 + k];
+  }
+  const long long nq = (long long)B * Ho * Wo;
+  for (long long q = (long long)blockIdx.x * QB + threadIdx.x / CG; q < nq;
+       q += (long long)gridDim.x * QB) {
+    const int wo = (int)(q % Wo);
+    const long long t = q / Wo;
+    const int ho = (int)(t % Ho);
+    const int b = (int)(t / Ho);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        o[2 * k] += zk::bf16_to_f32((uint16_t)(rr[k] & 0xffff));
-        o[2 * k + 1] += zk::bf16_to_f32((uint16_t)(rr[k] >> 16));
-      }
-    }
-    const uint4 ov = make_uint4(zk::pack_bf16x2(o[0], o[1]), zk::pack_bf16x2(o[2], o[3]),
-                                zk::pack_bf16x2(o[4], o[5]), zk::pack_bf16x2(o[6], o[7]));
-    reinterpret_cast<uint4*>(out)[i] = ov;
-    if (sx || sx4) {
-      // the NEXT binary block's input quantisation, from the stored bf16
-      // values: sign image (bf16 +-1 for the weight gradient, e2m1 nibbles
-      // for the MX-FP4 forward) and STE mask bits (|x| <= clip)
+    for (int d = 0; d < 4; ++d) {
+      const long long r = ((long long)b * H + 2 * ho + (d >> 1)) * W + 2 * wo + (d & 1);
+      const uint4 ov = bn_apply_chunk(r * CG + cg, y, sc, sh, res, out, sx, smask, clip, sx4);
       const uint32_t ow[4] = {ov.x, ov.y, ov.z, ov.w};
-      uint32_t sw[4];
-      uint32_t mk = 0, n4 = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float lo = zk::bf16_to_f32((uint16_t)(ow[k] & 0xffff));
-        const float hi = zk::bf16_to_f32((uint16_t)(ow[k] >> 16));
-        sw[k] = (lo >= 0.f ? 0x3F80u : 0xBF80u) | ((hi >= 0.f ? 0x3F80u : 0xBF80u) << 16);
-        mk |= (uint32_t)(fabsf(lo) <= clip) << (2 * k);
-        mk |= (uint32_t)(fabsf(hi) <= clip) << (2 * k + 1);
-        n4 |= (zk::fp4_sign(lo) | (zk::fp4_sign(hi) << 4)) << (8 * k);
+        acc[2 * k] += zk::bf16_to_f32((uint16_t)(ow[k] & 0xffff));
+        acc[2 * k + 1] += zk::bf16_to_f32((uint16_t)(ow[k] >> 16));
       }
-      if (sx) reinterpret_cast<uint4*>(sx)[i] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
-      if (smask) smask[i] = (uint8_t)mk;  // byte i = channels 8i..8i+7 of the packed mask words
-      if (sx4) sx4[i] = n4;               // 8 channels = 4 bytes of the [P][C/2] e2m1 image
     }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] *= 0.25f;
+    reinterpret_cast<uint4*>(pooled)[q * CG + cg] =
+        make_uint4(zk::pack_bf16x2(acc[0], acc[1]), zk::pack_bf16x2(acc[2], acc[3]),
+                   zk::pack_bf16x2(acc[4], acc[5]), zk::pack_bf16x2(acc[6], acc[7]));
   }
 }
 
@@ -409,6 +470,31 @@ ZK_EXPORT int zk_bn_apply_sign(const void* y, const void* scale, const void* shi
     break;
   ZK_CG_SWITCH(C, ZK_APPLY_CASE)
 #undef ZK_APPLY_CASE
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// zk_bn_apply_sign over an even [B][H][W] image, plus pooled = the 2x2/2
+// average pool of out (bit-identical to zk_avgpool2 of it): the stage
+// transition's shortcut input without a pass over out.
+ZK_EXPORT int zk_bn_apply_sign_pool(const void* y, const void* scale, const void* shift,
+                                    const void* res, void* out, void* sx, void* mask, void* sx4,
+                                    float clip, void* pooled, int B, int H, int W, int C,
+                                    hipStream_t stream) {
+  if (C % 32 || H % 2 || W % 2 || !pooled || B < 1) return (int)hipErrorInvalidValue;
+  const long long nq = (long long)B * (H / 2) * (W / 2);
+#define ZK_APPLY_POOL_CASE(cg)                                                              \
+  case cg: {                                                                                \
+    long long blocks = (nq + 256 / cg - 1) / (256 / cg);                                    \
+    if (blocks > 4096) blocks = 4096;                                                       \
+    hipLaunchKernelGGL(bn_apply_pool_kernel<cg>, dim3((int)blocks), dim3(256), 0, stream,   \
+                       (const int16_t*)y, (const float*)scale, (const float*)shift,         \
+                       (const uint16_t*)res, (uint16_t*)out, B, H, W, (uint16_t*)sx,        \
+                       (uint8_t*)mask, clip, (uint32_t*)sx4, (uint16_t*)pooled);            \
+    break;                                                                                  \
+  }
+  ZK_CG_SWITCH(C, ZK_APPLY_POOL_CASE)
+#undef ZK_APPLY_POOL_CASE
   ZK_CHECK_LAUNCH();
   return 0;
 }

@@ -70,6 +70,9 @@ class BinaryResBlock(nn.Module):
         # the next block's conv: reads this block's output sign images (set
         # by the model; decides whether the bf16 one is needed)
         self.sign_consumer = None
+        # the next block pools this block's output (its downsampling
+        # shortcut): the BN epilogue writes the pooled image too (set by the model)
+        self.pool_out = False
         self.downsample = None
         if cin != cout:
             self.downsample = nn.Sequential(
@@ -98,7 +101,7 @@ class BinaryResBlock(nn.Module):
             else:
                 residual = x
             return ops.binary_block(x, residual, self.conv, self.bn, dx_handoff=handoff,
-                                    sign_consumer=self.sign_consumer)
+                                    sign_consumer=self.sign_consumer, pool_out=self.pool_out)
         residual = self.downsample(x) if self.downsample is not None else x
         return self.bn(self.conv(x)) + residual
 
@@ -136,6 +139,9 @@ class BinaryResNetE(nn.Module):
         # (plain attributes, not submodules: no duplicate parameters / state keys)
         for blk, nxt in zip(body, body[1:]):
             object.__setattr__(blk, "sign_consumer", nxt.conv)
+            ds = nxt.downsample
+            blk.pool_out = (ds is not None and isinstance(ds[0], AvgPool2d)
+                            and ds[0].pool_size == (2, 2) and ds[0].stride == (2, 2))
         object.__setattr__(self.stem, "sign_consumer", body[0].conv)
         self.body = nn.Sequential(*body)
         self.pool = GlobalAvgPool()

@@ -82,6 +82,7 @@ SIGNATURES = {
     "zk_bn_finalize": (I32, [P, I32, I32, C.c_double, P, P, F32, F32, P, P, P, P, P, P, P]),
     "zk_bn_apply": (I32, [P, P, P, P, P, I64, I32, P]),
     "zk_bn_apply_sign": (I32, [P, P, P, P, P, P, P, P, F32, I64, I32, P]),
+    "zk_bn_apply_sign_pool": (I32, [P, P, P, P, P, P, P, P, F32, P, I32, I32, I32, I32, P]),
     "zk_bn_bwd_reduce": (I32, [P, P, P, P, P, I64, I32, I32, P]),
     "zk_bn_bwd_dx": (I32, [P, P, P, P, I64, I32, I32, P]),
     "zk_ste_combine": (I32, [P, P, P, P, I64, P]),

@@ -253,13 +253,26 @@ class _BinaryBlockFn(torch.autograd.Function):
             mask_next = torch.empty(P * Cout // 32, dtype=torch.int32, device=dev)
             sx4_next = (torch.empty((B, Ho, Wo, Cout // 2), dtype=torch.uint8, device=dev)
                         if FP4 else None)
-            check(L.zk_bn_apply_sign(y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
-                                     res.data_ptr() if res is not None else None,
-                                     out.data_ptr(),
-                                     sx_next.data_ptr() if sx_next is not None else None,
-                                     mask_next.data_ptr(),
-                                     sx4_next.data_ptr() if sx4_next is not None else None,
-                                     clip, P, Cout, st), "zk_bn_apply_sign")
+            pool_box = side.get("pool_out")
+            if pool_box is not None and Ho % 2 == 0 and Wo % 2 == 0:
+                # the next block's shortcut pools this output 2x2/2: in this pass
+                pooled = torch.empty((B, Ho // 2, Wo // 2, Cout), dtype=torch.bfloat16,
+                                     device=dev)
+                check(L.zk_bn_apply_sign_pool(
+                    y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                    res.data_ptr() if res is not None else None, out.data_ptr(),
+                    sx_next.data_ptr() if sx_next is not None else None, mask_next.data_ptr(),
+                    sx4_next.data_ptr() if sx4_next is not None else None, clip,
+                    pooled.data_ptr(), B, Ho, Wo, Cout, st), "zk_bn_apply_sign_pool")
+                pool_box.append(pooled)
+            else:
+                check(L.zk_bn_apply_sign(y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                                         res.data_ptr() if res is not None else None,
+                                         out.data_ptr(),
+                                         sx_next.data_ptr() if sx_next is not None else None,
+                                         mask_next.data_ptr(),
+                                         sx4_next.data_ptr() if sx4_next is not None else None,
+                                         clip, P, Cout, st), "zk_bn_apply_sign")
             next_sign[:] = [clip, sx_next, mask_next, sx4_next]
         else:
             check(L.zk_bn_apply(y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
@@ -478,7 +491,7 @@ def _library_conv_backward(ctx, dy, g, bits, mask, wt, w_ohwi, need_dx):
 def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
                  act: Optional[str] = None, clip_value: float = 1.0,
                  pad_value: float = 0.0, quantize_output: bool = True,
-                 dx_handoff=None, sign_consumer=None) -> torch.Tensor:
+                 dx_handoff=None, sign_consumer=None, pool_out: bool = False) -> torch.Tensor:
     """Run ``bn(act(conv(x))) + residual`` with the fused HIP kernels.
 
     ``conv`` must be a binary ``QuantConv2d`` (ste_sign input and kernel,
@@ -495,6 +508,10 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
     ``sign_consumer``: the binary conv that reads the output's sign images
     (the next block's); the bf16 sign image is skipped when its weight
     gradient reads the e2m1 one (:func:`bf16_sign_needed`).
+
+    ``pool_out``: the output's consumer also 2x2/2-average-pools it (the next
+    block's downsampling shortcut): the BN epilogue writes that pooled image
+    in the same pass, attached as ``_zk_pooled`` for ``ops.norm_pool.avg_pool2``.
 
     ``dx_handoff`` (an ``ops.norm_pool.ResidualHandoff``): x's gradient is left
     there instead of returned, for x's other consumer whose backward runs
@@ -521,7 +538,8 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
         x.requires_grad or conv.weight.requires_grad or bn.training)
     holder: list = [] if quantize_output else None
     side = {"pred": getattr(x, "_zk_bnsum", None), "dx_handoff": dx_handoff,
-            "sign_consumer": sign_consumer}
+            "sign_consumer": sign_consumer,
+            "pool_out": [] if (pool_out and OPTS.bn_pool_fuse) else None}
     meta = (conv.stride[0], act == "relu", float(clip_value), pad_value == 1.0, identity,
             will_backward, holder, side)
     out = _BinaryBlockFn.apply(x, None if identity else residual, conv.weight, bn.weight,
@@ -531,4 +549,6 @@ def binary_block(x: torch.Tensor, residual: Optional[torch.Tensor], conv, bn,
         out._zk_sign = tuple(holder)
     if side.get("bnsum") is not None:
         out._zk_bnsum = side["bnsum"]
+    if side["pool_out"]:
+        out._zk_pooled = (side["pool_out"][0], out._version)
     return out

@@ -346,10 +346,17 @@ class _AvgPool2Fn(torch.autograd.Function):
     def forward(ctx, x, handoff=None):
         B, C, H, W = x.shape
         Ho, Wo = H // 2, W // 2
-        xn = _nhwc(x)
-        y = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=x.device)
-        check(lib().zk_avgpool2_fwd(xn.data_ptr(), y.data_ptr(), B, H, W, C, Ho, Wo,
-                                    stream_ptr(x.device)), "zk_avgpool2_fwd")
+        pre = getattr(x, "_zk_pooled", None)
+        if (pre is not None and pre[1] == x._version and tuple(pre[0].shape) == (B, Ho, Wo, C)
+                and pre[0].dtype == x.dtype and H % 2 == 0 and W % 2 == 0):
+            # written by the producer's BN epilogue (ops.binary_block pool_out),
+            # bit-identical to this kernel's output
+            y = pre[0]
+        else:
+            xn = _nhwc(x)
+            y = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=x.device)
+            check(lib().zk_avgpool2_fwd(xn.data_ptr(), y.data_ptr(), B, H, W, C, Ho, Wo,
+                                        stream_ptr(x.device)), "zk_avgpool2_fwd")
         ctx.geom = (B, H, W, C, Ho, Wo)
         ctx.handoff = handoff
         return y.permute(0, 3, 1, 2)

@@ -87,6 +87,10 @@ class KernelOptions:
     # The BN tail hands (g, ReLU mask bits) to a 1x1 conv whose epilogue masks
     # and adds them, instead of writing the residual gradient g * mask.
     bn_masked_handoff: bool = True
+    # A binary block whose output the next block's shortcut average-pools
+    # writes the pooled image in its BN-apply pass (ops.binary_block pool_out)
+    # instead of a separate pooling pass over the output.
+    bn_pool_fuse: bool = True
     # The LDS-epilogue data gradient prefetches its residual / BN-input loads
     # in groups (igemm.hip dgrad_store_lds) instead of loading at each chunk.
     epilogue_prefetch: bool = True

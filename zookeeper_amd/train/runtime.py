@@ -50,6 +50,7 @@ class Runtime:
     weight_images: bool = Field(True)
     bn_bwd_fuse: bool = Field(True)
     bn_masked_handoff: bool = Field(True)
+    bn_pool_fuse: bool = Field(True)
     epilogue_prefetch: bool = Field(True)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
