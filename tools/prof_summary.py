@@ -56,6 +56,9 @@ FAMILY_RULES = [
     ("sgd", "optimizer"),
     ("xent", "softmax cross-entropy"),
     ("normalize_flip", "input preprocessing"),
+    # HIP runtime blit kernels: copies to / from pinned host memory and
+    # memsets (hipMemcpyAsync / hipMemsetAsync)
+    ("__amd_rocclr_", "HIP runtime copy / fill"),
 ]
 
 
