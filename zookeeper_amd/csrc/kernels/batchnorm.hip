@@ -61,24 +61,15 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
   }
 }
 
-// One 8-channel chunk i (= row * C / 8 + cg) of the BN apply: out bf16 =
-// scale*y + shift (+ residual), and the next binary layer's input
-// quantisation from the stored bf16 values (bf16 sign image, STE mask bits,
-// e2m1 sign image; each optional).  Returns the stored chunk.
-__device__ __forceinline__ uint4 bn_apply_chunk(long long i, const int16_t* __restrict__ y,
-                                                const float (&sc)[8], const float (&sh)[8],
-                                                const uint16_t* __restrict__ res,
-                                                uint16_t* __restrict__ out,
-                                                uint16_t* __restrict__ sx,
-                                                uint8_t* __restrict__ smask, float clip,
-                                                uint32_t* __restrict__ sx4) {
-  const uint4 yv = reinterpret_cast<const uint4*>(y)[i];
+// The BN apply of one 8-channel chunk: scale*y + shift (+ the residual
+// chunk rv when has_res), packed as stored (bf16).
+__device__ __forceinline__ uint4 bn_apply_values(const uint4& yv, const uint4& rv, bool has_res,
+                                                 const float (&sc)[8], const float (&sh)[8]) {
   const int16_t* yy = reinterpret_cast<const int16_t*>(&yv);
   float o[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) o[k] = sc[k] * (float)yy[k] + sh[k];
-  if (res) {
-    const uint4 rv = reinterpret_cast<const uint4*>(res)[i];
+  if (has_res) {
     const uint32_t rr[4] = {rv.x, rv.y, rv.z, rv.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -86,8 +77,18 @@ __device__ __forceinline__ uint4 bn_apply_chunk(long long i, const int16_t* __re
       o[2 * k + 1] += zk::bf16_to_f32((uint16_t)(rr[k] >> 16));
     }
   }
-  const uint4 ov = make_uint4(zk::pack_bf16x2(o[0], o[1]), zk::pack_bf16x2(o[2], o[3]),
-                              zk::pack_bf16x2(o[4], o[5]), zk::pack_bf16x2(o[6], o[7]));
+  return make_uint4(zk::pack_bf16x2(o[0], o[1]), zk::pack_bf16x2(o[2], o[3]),
+                    zk::pack_bf16x2(o[4], o[5]), zk::pack_bf16x2(o[6], o[7]));
+}
+
+// Store chunk i of the BN output and the next binary layer's input
+// quantisation from the stored bf16 values (bf16 sign image, STE mask bits,
+// e2m1 sign image; each optional).
+__device__ __forceinline__ void bn_apply_store(long long i, const uint4& ov,
+                                               uint16_t* __restrict__ out,
+                                               uint16_t* __restrict__ sx,
+                                               uint8_t* __restrict__ smask, float clip,
+                                               uint32_t* __restrict__ sx4) {
   reinterpret_cast<uint4*>(out)[i] = ov;
   if (sx || sx4) {
     // the NEXT binary block's input quantisation, from the stored bf16
@@ -109,7 +110,6 @@ __device__ __forceinline__ uint4 bn_apply_chunk(long long i, const int16_t* __re
     if (smask) smask[i] = (uint8_t)mk;  // byte i = channels 8i..8i+7 of the packed mask words
     if (sx4) sx4[i] = n4;               // 8 channels = 4 bytes of the [P][C/2] e2m1 image
   }
-  return ov;
 }
 
 // y int16 [P][C] -> out bf16 = scale*y + shift (+ residual bf16).
@@ -136,8 +136,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const int16_t* __restrict
     sh[k] = shift[cg * 8 + k];
   }
   for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
-       r += (long long)gridDim.x * RB)
-    bn_apply_chunk((r * C) / 8 + cg, y, sc, sh, res, out, sx, smask, clip, sx4);
+       r += (long long)gridDim.x * RB) {
+    const long long i = (r * C) / 8 + cg;
+    const uint4 yv = reinterpret_cast<const uint4*>(y)[i];
+    const uint4 rv = res ? reinterpret_cast<const uint4*>(res)[i] : make_uint4(0, 0, 0, 0);
+    bn_apply_store(i, bn_apply_values(yv, rv, res != nullptr, sc, sh), out, sx, smask, clip,
+                   sx4);
+  }
 }
 
 // bn_apply_kernel over 2x2 pixel quads of an even [B][H][W] image, plus the
@@ -168,11 +173,22 @@ __global__ __launch_bounds__(256) void bn_apply_pool_kernel(
     const long long t = q / Wo;
     const int ho = (int)(t % Ho);
     const int b = (int)(t / Ho);
+    // the quad's loads all issued before the first store
+    long long ci[4];
+    uint4 yv[4], rv[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      ci[d] = (((long long)b * H + 2 * ho + (d >> 1)) * W + 2 * wo + (d & 1)) * CG + cg;
+      yv[d] = reinterpret_cast<const uint4*>(y)[ci[d]];
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      rv[d] = res ? reinterpret_cast<const uint4*>(res)[ci[d]] : make_uint4(0, 0, 0, 0);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      const long long r = ((long long)b * H + 2 * ho + (d >> 1)) * W + 2 * wo + (d & 1);
-      const uint4 ov = bn_apply_chunk(r * CG + cg, y, sc, sh, res, out, sx, smask, clip, sx4);
+      const uint4 ov = bn_apply_values(yv[d], rv[d], res != nullptr, sc, sh);
+      bn_apply_store(ci[d], ov, out, sx, smask, clip, sx4);
       const uint32_t ow[4] = {ov.x, ov.y, ov.z, ov.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
