@@ -285,35 +285,3 @@ def test_shortcut_pool_from_the_bn_epilogue_is_bit_identical():
         assert torch.equal(p.grad, q.grad), n
     for (n, u), (_, v) in zip(a.named_buffers(), b.named_buffers()):
         assert torch.equal(u, v), n
-
-
-@pytest.mark.timeout(120)
-def test_unrolled_bn_apply_is_bit_identical():
-    """runtime.bn_apply_unroll=2 (two rows per thread, both rows' loads
-    before the first store): the same outputs, sign images and gradients."""
-    import copy
-
-    from zookeeper_amd.models.binary_resnet import BinaryResNetE
-    from zookeeper_amd.ops.options import set_options
-    from zookeeper_amd.train.trainer import prepare_model
-
-    torch.manual_seed(2)
-    dev = torch.device("cuda", 0)
-    a = prepare_model(BinaryResNetE((64, 64, 3), 10, 18, backend="hip"), dev).train()
-    b = copy.deepcopy(a)
-    x = torch.randn(5, 3, 64, 64, device=dev).to(torch.bfloat16)
-    x = x.contiguous(memory_format=torch.channels_last)
-    old = OPTS.bn_apply_unroll
-    try:
-        set_options(bn_apply_unroll=2)
-        ya = a(x)
-        set_options(bn_apply_unroll=1)
-        yb = b(x)
-    finally:
-        set_options(bn_apply_unroll=old)
-    assert torch.equal(ya, yb)
-    g = torch.randn_like(ya)
-    ya.backward(g)
-    yb.backward(g)
-    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
-        assert torch.equal(p.grad, q.grad), n

@@ -115,7 +115,7 @@ __device__ __forceinline__ void bn_apply_store(long long i, const uint4& ov,
 // y int16 [P][C] -> out bf16 = scale*y + shift (+ residual bf16).
 // Each thread owns one group of 8 channels (coefficients in registers) and
 // walks rows; CG = C/8 threads cover a row.
-template <int CG, int UR = 1>
+template <int CG>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const int16_t* __restrict__ y,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
@@ -135,26 +135,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const int16_t* __restrict
     sc[k] = scale[cg * 8 + k];
     sh[k] = shift[cg * 8 + k];
   }
-  // UR rows per thread and iteration, every row's loads issued before the
-  // first store
-  for (long long r = (long long)blockIdx.x * RB * UR + threadIdx.x / CG; r < P;
-       r += (long long)gridDim.x * RB * UR) {
-    long long ci[UR];
-    uint4 yv[UR], rv[UR];
-#pragma unroll
-    for (int u = 0; u < UR; ++u) {
-      ci[u] = ((r + (long long)u * RB) * C) / 8 + cg;
-      if (r + u * RB < P) yv[u] = reinterpret_cast<const uint4*>(y)[ci[u]];
-    }
-#pragma unroll
-    for (int u = 0; u < UR; ++u)
-      rv[u] = (res && r + u * RB < P) ? reinterpret_cast<const uint4*>(res)[ci[u]]
-                                      : make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int u = 0; u < UR; ++u)
-      if (r + u * RB < P)
-        bn_apply_store(ci[u], bn_apply_values(yv[u], rv[u], res != nullptr, sc, sh), out, sx,
-                       smask, clip, sx4);
+  for (long long r = (long long)blockIdx.x * RB + threadIdx.x / CG; r < P;
+       r += (long long)gridDim.x * RB) {
+    const long long i = (r * C) / 8 + cg;
+    const uint4 yv = reinterpret_cast<const uint4*>(y)[i];
+    const uint4 rv = res ? reinterpret_cast<const uint4*>(res)[i] : make_uint4(0, 0, 0, 0);
+    bn_apply_store(i, bn_apply_values(yv, rv, res != nullptr, sc, sh), out, sx, smask, clip,
+                   sx4);
   }
 }
 
@@ -486,26 +473,16 @@ ZK_EXPORT int zk_bn_apply(const void* y, const void* scale, const void* shift, c
 // zk_bn_apply + the next binary layer's input quantisation (sign image sx
 // bf16 +-1, STE mask bits |out| <= clip and the e2m1 sign image sx4, packed
 // like zk_sign_pack's; each optional).
-// bn_apply_unroll (option key 10): rows per thread and iteration of the
-// binary blocks' BN apply (1 or 2).
-int g_opt_bn_apply_unroll = 1;
-
 ZK_EXPORT int zk_bn_apply_sign(const void* y, const void* scale, const void* shift,
                                const void* res, void* out, void* sx, void* mask, void* sx4,
                                float clip, long long P, int C, hipStream_t stream) {
   if (C % 32) return (int)hipErrorInvalidValue;
 #define ZK_APPLY_CASE(cg)                                                                   \
   case cg:                                                                                  \
-    if (g_opt_bn_apply_unroll == 2)                                                         \
-      hipLaunchKernelGGL((bn_apply_kernel<cg, 2>), dim3(rows_grid(P, C)), dim3(256), 0,      \
-                         stream, (const int16_t*)y, (const float*)scale,                    \
-                         (const float*)shift, (const uint16_t*)res, (uint16_t*)out, P,      \
-                         (uint16_t*)sx, (uint8_t*)mask, clip, (uint32_t*)sx4);              \
-    else                                                                                    \
-      hipLaunchKernelGGL(bn_apply_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, stream,  \
-                         (const int16_t*)y, (const float*)scale, (const float*)shift,       \
-                         (const uint16_t*)res, (uint16_t*)out, P, (uint16_t*)sx,            \
-                         (uint8_t*)mask, clip, (uint32_t*)sx4);                             \
+    hipLaunchKernelGGL(bn_apply_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, stream,    \
+                       (const int16_t*)y, (const float*)scale, (const float*)shift,         \
+                       (const uint16_t*)res, (uint16_t*)out, P, (uint16_t*)sx,              \
+                       (uint8_t*)mask, clip, (uint32_t*)sx4);                               \
     break;
   ZK_CG_SWITCH(C, ZK_APPLY_CASE)
 #undef ZK_APPLY_CASE

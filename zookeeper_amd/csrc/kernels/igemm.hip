@@ -2422,9 +2422,6 @@ ZK_EXPORT int zk_igemm_fwd_supported(int B, int H, int W, int Cin, int Cout, int
                       pl, Ho, Wo, pad_ones, 0, variant, 1, nullptr) == 0;
 }
 
-// batchnorm.hip: rows per thread of the binary blocks' BN apply (key 10)
-extern int g_opt_bn_apply_unroll;
-
 // Host-side kernel options (see g_opt_* above; ops/options.py).  Returns 0,
 // or -1 for an unknown key.
 ZK_EXPORT int zk_set_option(int key, int value) {
@@ -2436,7 +2433,6 @@ ZK_EXPORT int zk_set_option(int key, int value) {
     case 6: g_opt_dgrad_deep = value; return 0;
     case 7: g_opt_wgrad_deep = value; return 0;
     case 8: g_opt_epilogue_prefetch = value; return 0;
-    case 10: g_opt_bn_apply_unroll = value; return 0;
     default: return -1;
   }
 }
@@ -2450,7 +2446,6 @@ ZK_EXPORT int zk_get_option(int key) {
     case 6: return g_opt_dgrad_deep;
     case 7: return g_opt_wgrad_deep;
     case 8: return g_opt_epilogue_prefetch;
-    case 10: return g_opt_bn_apply_unroll;
     default: return -1;
   }
 }

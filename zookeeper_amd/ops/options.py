@@ -91,9 +91,6 @@ class KernelOptions:
     # writes the pooled image in its BN-apply pass (ops.binary_block pool_out)
     # instead of a separate pooling pass over the output.
     bn_pool_fuse: bool = True
-    # Rows per thread and iteration of the binary blocks' BN apply (1 or 2;
-    # 2 issues both rows' loads before the first store).
-    bn_apply_unroll: int = 1
     # The LDS-epilogue data gradient prefetches its residual / BN-input loads
     # in groups (igemm.hip dgrad_store_lds) instead of loading at each chunk.
     epilogue_prefetch: bool = True
@@ -107,8 +104,7 @@ OPTS = KernelOptions()
 
 # keys the native library reads (zk_set_option); values are ints
 _NATIVE_KEYS = {"tile_huge": 0, "deterministic": 2, "dgrad_rw": 3, "wgrad_slab_mb": 5,
-                "dgrad_deep": 6, "wgrad_deep": 7, "epilogue_prefetch": 8,
-                "bn_apply_unroll": 10}
+                "dgrad_deep": 6, "wgrad_deep": 7, "epilogue_prefetch": 8}
 
 
 def _push_native() -> None:

@@ -51,7 +51,6 @@ class Runtime:
     bn_bwd_fuse: bool = Field(True)
     bn_masked_handoff: bool = Field(True)
     bn_pool_fuse: bool = Field(True)
-    bn_apply_unroll: int = Field(1)
     epilogue_prefetch: bool = Field(True)
     # Bit-reproducible gradients (fixed-order reductions, no float atomics on
     # the gradient path); slower.
