@@ -23,6 +23,11 @@ Ordering is explicit with HIP events:
   per E18 step of compute-stream stalls behind the stage-4 weight gradients
   when every block waited).
 
+The float 1x1 / 3x3 / strided convs (ResNet-50) put their weight gradients
+on the same stream through :func:`side_wgrad` (``runtime.float_wgrad_side_stream``):
+the compute stream joins each one ``SIDE_LAG`` launches later, which releases
+its inputs and bounds the backlog.
+
 Only active inside :func:`session` (the trainer opens one per step and
 flushes at its end), so direct callers of the ops keep single-stream
 semantics.  ``runtime.wgrad_side_stream=False`` disables it.
