@@ -85,9 +85,12 @@ class Runtime:
     cpu_affinity: bool = Field(True)
     # Debug: compare the launched bucket order across ranks every step.
     check_bucket_order: bool = Field(False)
-    # Gradient all-reduce transport: "torch" (ProcessGroupNCCL) or "native"
-    # (parallel/rccl.py: the in-tree RCCL communicator; graph-capturable).
-    comm_backend: str = Field("torch")
+    # Gradient all-reduce transport: "torch" (ProcessGroupNCCL), "native"
+    # (parallel/rccl.py: the in-tree RCCL communicator; graph-capturable) or
+    # "auto": native, falling back to torch on every rank if its set-up fails
+    # on any.  Forced 1-rank RCCL, E18 b1536 (scripts/gpu_call23.sh): torch
+    # 34.56 ms/step vs native 30.06 vs 29.93 without data parallelism.
+    comm_backend: str = Field("auto")
 
     def __post_configure__(self) -> None:
         if self.graph not in ("off", "on", "auto"):
@@ -96,14 +99,15 @@ class Runtime:
             raise ValueError("runtime.rccl_min_channels / rccl_max_channels must be >= 0")
         if 0 < self.rccl_max_channels < self.rccl_min_channels:
             raise ValueError("runtime.rccl_min_channels > rccl_max_channels")
-        if self.comm_backend not in ("torch", "native"):
-            raise ValueError(f"runtime.comm_backend must be 'torch' or 'native', "
+        if self.comm_backend not in ("torch", "native", "auto"):
+            raise ValueError(f"runtime.comm_backend must be 'torch', 'native' or 'auto', "
                              f"got {self.comm_backend!r}")
-        if self.check_bucket_order and self.comm_backend == "native" and self.graph != "off":
+        if (self.check_bucket_order and self.comm_backend in ("native", "auto")
+                and self.graph != "off"):
             # the order check all-reduces and reads a hash on the host inside
             # bucketer.finish(), which the native backend captures into the graph
             raise ValueError("runtime.check_bucket_order needs runtime.graph='off' with "
-                             "runtime.comm_backend='native'")
+                             "runtime.comm_backend='native' / 'auto'")
 
     def kernel_options(self) -> Dict[str, Any]:
         return {k: getattr(self, k) for k in _KERNEL_FIELDS}

@@ -11,6 +11,7 @@ the device until the metrics logger flushes.
 from __future__ import annotations
 
 import dataclasses
+import sys
 import time
 from typing import Callable, Optional, Tuple, Union
 
@@ -70,11 +71,9 @@ class Trainer:
         # RCCL group), so one GPU runs the exact data-parallel code path
         comm = self.info.comm
         native = None
-        if (comm.backend == "native" and self.device.type == "cuda"
-                and (self.info.world > 1 or force_dp)):
-            from zookeeper_amd.parallel.rccl import NativeComm
-
-            native = NativeComm(self.info.rank, self.info.world)
+        if (comm.backend in ("native", "auto") and self.device.type == "cuda"
+                and self.info.backend == "nccl" and (self.info.world > 1 or force_dp)):
+            native = self._native_comm(comm.backend == "auto")
         self.native_comm = native
         if self.info.world > 1:
             # One broadcast of the flat parameter buffer + the BN buffers
@@ -116,6 +115,33 @@ class Trainer:
         self._graph = None
         self._static_in = None
         self._static_out = None
+
+    def _native_comm(self, fallback: bool):
+        """The in-tree RCCL communicator for the gradient all-reduce.  With
+        ``fallback`` (``runtime.comm_backend="auto"``) a failed set-up on any
+        rank makes every rank use ProcessGroupNCCL instead (the ranks agree
+        through a MIN all-reduce over the process group, so none is left
+        waiting in a collective the others never issue)."""
+        from zookeeper_amd.parallel.rccl import NativeComm
+
+        if not fallback:
+            return NativeComm(self.info.rank, self.info.world)
+        native, err = None, None
+        try:
+            native = NativeComm(self.info.rank, self.info.world)
+        except Exception as e:  # noqa: BLE001 -- any set-up failure selects the fallback
+            err = e
+        # MIN over the ranks (as -MAX of the negation)
+        ok = -zdist.all_reduce_max_values([-1.0 if native is not None else 0.0], self.device)[0]
+        if ok < 1.0:
+            if self.info.is_main:
+                print(f"[trainer] native RCCL communicator unavailable on some rank "
+                      f"({err!r} here); gradient all-reduce through ProcessGroupNCCL",
+                      file=sys.stderr, flush=True)
+            if native is not None:
+                native.close()
+            return None
+        return native
 
     def _forward_backward(self, x: torch.Tensor, y: torch.Tensor):
         self.flat.zero_grad()
