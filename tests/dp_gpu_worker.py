@@ -54,8 +54,8 @@ def run(mode: str, out: str) -> None:
     # ZK_TEST_CHECK_ORDER=1: every step compares the launched bucket order
     # across ranks (runtime.check_bucket_order)
     comm = zdist.CommConfig(check_bucket_order=os.environ.get("ZK_TEST_CHECK_ORDER", "0") == "1",
-                            backend=os.environ.get("ZK_TEST_COMM", "torch"),
-                            high_priority=os.environ.get("ZK_TEST_COMM_PRIO", "1") == "1",
+                            backend=os.environ.get("ZK_TEST_COMM", "auto"),
+                            high_priority=os.environ.get("ZK_TEST_COMM_PRIO", "0") == "1",
                             cpu_affinity=os.environ.get("ZK_TEST_AFFINITY", "1") == "1")
     if world > 1 or force:
         info = zdist.init(backend, single_group=force, comm=comm)
@@ -81,13 +81,43 @@ def run(mode: str, out: str) -> None:
     # the same tensors for every world size (at most 2 ranks)
     xs = torch.randn(steps, 2 * per, 3, 64, 64, generator=g)
     ys = torch.randint(0, 10, (steps, 2 * per), generator=g)
+    # ZK_TEST_ABORT_AFTER=k: after step k, mark the native communicator as
+    # failed (what the watchdog does on a hung collective); the next step must
+    # raise before replaying a graph that holds the aborted communicator's
+    # collectives
+    abort_after = int(os.environ.get("ZK_TEST_ABORT_AFTER", "-1"))
+    replays = [0]
+    abort = {}
     for s in range(steps):
         lo = 0 if mode == "same" else info.rank * per
         x = xs[s, lo:lo + per].to(info.device, torch.bfloat16).contiguous(
             memory_format=torch.channels_last)
         y = ys[s, lo:lo + per].to(info.device)
+        if s == abort_after + 1 and abort_after >= 0:
+            torch.cuda.synchronize()
+            native = tr.bucketer.native
+            assert native is not None and tr._graph is not None
+            real = tr._graph.replay
+
+            def counted():
+                replays[0] += 1
+                real()
+
+            tr._graph.replay = counted
+            native._failed = "injected failure"
+            try:
+                tr.train_step(x, y)
+                abort = {"raised": False}
+            except RuntimeError as e:
+                abort = {"raised": "injected failure" in str(e)}
+            abort["replays"] = replays[0]
+            break
         loss, _ = tr.train_step(x, y)
     torch.cuda.synchronize()
+    if abort:
+        torch.save(abort, os.path.join(out, "abort.pt"))
+        zdist.shutdown()
+        return
     timings = tr.bucketer.pop_timings()
     torch.save({"params": tr.flat.data.cpu(), "init": init, "loss": float(loss),
                 "buckets": tr.bucketer.num_buckets, "graph": tr.graph,

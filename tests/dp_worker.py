@@ -107,7 +107,7 @@ if __name__ == "__main__":
         tr = train(rank, world, bucket_mb=0.001, check_order=True)
         ok_checks = tr.bucketer.order_checks
         try:
-            tr.bucketer._compare_order([0, 1] if rank == 0 else [1, 0])
+            tr.bucketer.compare_order([0, 1] if rank == 0 else [1, 0])
             flagged = False
         except RuntimeError:
             flagged = True

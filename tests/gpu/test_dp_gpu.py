@@ -25,10 +25,13 @@ WORKER = os.path.join(os.path.dirname(HERE), "dp_gpu_worker.py")
 
 
 def _run(mode, out, nproc, side="1", graph="0", force="0", backend="gloo", rt="",
-         check_order="0", comm="torch"):
+         check_order="0", comm="auto", prio="0", extra=None):
+    """The worker in the shipped communicator settings by default
+    (``runtime.comm_backend="auto"``, ``comm_high_priority=False``)."""
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4", ZK_TEST_SIDE=side,
                ZK_TEST_GRAPH=graph, ZK_TEST_FORCE_DP=force, ZK_TEST_BACKEND=backend,
-               ZK_TEST_RT=rt, ZK_TEST_CHECK_ORDER=check_order, ZK_TEST_COMM=comm)
+               ZK_TEST_RT=rt, ZK_TEST_CHECK_ORDER=check_order, ZK_TEST_COMM=comm,
+               ZK_TEST_COMM_PRIO=prio, **(extra or {}))
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     if nproc == 1:
@@ -106,46 +109,69 @@ def test_two_ranks_disjoint_data_stay_identical(tmp_path):
 @pytest.mark.parametrize("side,graph", [("1", "0"), ("0", "0"), ("1", "1")],
                          ids=["side-stream", "single-stream", "graph"])
 def test_rccl_single_rank_forced_dp_matches_plain_run(tmp_path, side, graph, mode):
-    """Deterministic mode (``runtime.deterministic``: no float atomics on the
-    gradient path): the forced 1-rank RCCL run must equal the plain run BIT
-    FOR BIT, and so must the default mode since round 4 (round 3's default
-    mode used fp32 atomics in the BN-backward sums, whose noise the binary
-    blocks amplified into O(1) differences between any two runs after two
-    steps: profiles/r3/g_dp_forced_diag.md; those sums, the split-K weight
-    gradients and the loss sum are fixed-order now)."""
-    exact = True
+    """The shipped transport (``runtime.comm_backend="auto"``: the in-tree
+    RCCL communicator after its agreed set-up and canary) with a 1-rank
+    ``nccl`` group and the bucketer forced on: the forced run must equal the
+    plain run BIT FOR BIT in the deterministic AND the default mode (every
+    gradient sum is fixed-order since round 4; round 3's default mode used
+    fp32 atomics whose noise the binary blocks amplified:
+    profiles/r3/g_dp_forced_diag.md).  Under graph replay the collectives are
+    captured with the backward."""
     rt = "deterministic=1" if mode == "deterministic" else ""
     assert _run("same", tmp_path, 1, side, graph, rt=rt) == 0
     assert _run("same", tmp_path, 1, side, graph, force="1", backend="nccl", rt=rt) == 0
     ref = torch.load(tmp_path / "same_w1_r0.pt", weights_only=True)
     dp = torch.load(tmp_path / "same_w1dp_r0.pt", weights_only=True)
     assert dp["backend"] == "nccl" and dp["bucketer"] and not ref["bucketer"]
+    assert dp["native"]  # "auto" selected the native communicator
     assert dp["buckets"] > 1
     assert dp["graph"] == (graph == "1")
-    # pop_timings: one record per step, with real (non-negative) spans
-    assert dp["comm_steps"] == 2, dp["timings"]
-    for t in dp["timings"]:
-        assert t["comm_ms"] >= 0 and t["bucket_sum_ms"] >= 0 and t["exposed_ms"] >= 0
+    if graph == "0":
+        # pop_timings: one record per step, with real (non-negative) spans
+        assert dp["comm_steps"] == 2, dp["timings"]
+        for t in dp["timings"]:
+            assert t["comm_ms"] >= 0 and t["bucket_sum_ms"] >= 0 and t["exposed_ms"] >= 0
     torch.testing.assert_close(dp["init"], ref["init"], atol=0, rtol=0)
     assert (ref["params"] - ref["init"]).norm().item() > 0
     # a 1-rank all-reduce is the identity and nothing else differs
-    _close(dp["params"], ref["params"], exact)
+    torch.testing.assert_close(dp["params"], ref["params"], atol=0, rtol=0)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("side,graph", [("1", "0"), ("1", "1")], ids=["side-stream", "graph"])
+def test_process_group_transport_forced_dp_matches_plain_run(tmp_path, side, graph):
+    """``runtime.comm_backend="torch"`` (ProcessGroupNCCL work objects, the
+    fallback of "auto"), default mode: bit-equal to the plain run."""
+    assert _run("same", tmp_path, 1, side, graph) == 0
+    assert _run("same", tmp_path, 1, side, graph, force="1", backend="nccl", comm="torch") == 0
+    ref = torch.load(tmp_path / "same_w1_r0.pt", weights_only=True)
+    dp = torch.load(tmp_path / "same_w1dp_r0.pt", weights_only=True)
+    assert dp["bucketer"] and not dp["native"]
+    assert dp["comm_steps"] == 2, dp["timings"]
+    torch.testing.assert_close(dp["params"], ref["params"], atol=0, rtol=0)
 
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("graph", ["0", "1"], ids=["eager", "graph"])
 def test_native_rccl_communicator_forced_dp_matches_plain_run(tmp_path, graph):
-    """runtime.comm_backend="native": the bucketed all-reduce through the
-    in-tree RCCL communicator (parallel/rccl.py, runtime/comm.cpp), issued
-    straight onto the comm stream; with graph replay the collectives are
-    captured INTO the graph with the backward.  One rank (a 1-rank RCCL
-    communicator), deterministic mode: bit-equal to the plain run."""
-    rt = "deterministic=1"
-    assert _run("same", tmp_path, 1, "1", graph, rt=rt) == 0
-    assert _run("same", tmp_path, 1, "1", graph, force="1", backend="nccl", rt=rt,
-                comm="native") == 0
+    """runtime.comm_backend="native" (no fallback), default mode, high-priority
+    comm stream: bit-equal to the plain run."""
+    assert _run("same", tmp_path, 1, "1", graph) == 0
+    assert _run("same", tmp_path, 1, "1", graph, force="1", backend="nccl",
+                comm="native", prio="1") == 0
     ref = torch.load(tmp_path / "same_w1_r0.pt", weights_only=True)
     dp = torch.load(tmp_path / "same_w1dp_r0.pt", weights_only=True)
     assert dp["native"] and dp["bucketer"]
     assert dp["graph"] == (graph == "1")
     torch.testing.assert_close(dp["params"], ref["params"], atol=0, rtol=0)
+
+
+@pytest.mark.timeout(300)
+def test_aborted_communicator_is_not_replayed(tmp_path):
+    """after the watchdog marks the native communicator failed,
+    the next graph step raises BEFORE replaying the captured collectives
+    (their RCCL resources are freed by the abort)."""
+    assert _run("same", tmp_path, 1, "1", "1", force="1", backend="nccl",
+                extra={"ZK_TEST_ABORT_AFTER": "2", "ZK_TEST_STEPS": "4"}) == 0
+    res = torch.load(tmp_path / "abort.pt", weights_only=True)
+    assert res["raised"] is True and res["replays"] == 0, res

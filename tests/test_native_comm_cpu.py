@@ -92,3 +92,112 @@ def test_small_buckets_are_folded():
     assert all(s >= MIN_BUCKET_BYTES for s in sizes), sizes  # (cap 10 MB: full threshold)
     covered = sorted(i for bucket in b.buckets for i in bucket)
     assert covered == list(range(len(flat.slots)))
+
+
+# --- connect(): the agreed set-up of the "auto" transport (VERDICT r5 item 3,
+# ADVICE r5).  Two processes over a TCPStore, RCCL replaced by stubs; one rank
+# fails in a given phase and BOTH ranks must return None promptly.
+
+def _connect_main(rank, world, port, fail, out):
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    from zookeeper_amd.parallel import rccl
+
+    store = dist.TCPStore("127.0.0.1", port, world, rank == 0, timedelta(seconds=60))
+    bad = rank == 1
+
+    def load():
+        if bad and fail == "load":
+            raise RuntimeError("stub: no librccl")
+
+    def init(uid, w, r):
+        if bad and fail == "init":
+            raise RuntimeError("stub: ncclCommInitRank failed")
+        if bad and fail == "init_hang":
+            time.sleep(600)
+        return 100 + r
+
+    def canary(comm):
+        if bad and fail == "canary":
+            raise RuntimeError("stub: canary sum mismatch")
+
+    t0 = time.monotonic()
+    comm = rccl.connect(rank, world, store=store, fallback=True, timeout_s=60,
+                        init_timeout_s=3, tag=f"zk_conn_{fail}", log=lambda m: None,
+                        _load=load, _make_uid=lambda: os.urandom(128), _init=init,
+                        _canary=canary)
+    out.put((rank, None if comm is None else comm.handle, time.monotonic() - t0))
+    time.sleep(1.0)  # keep rank 0's store alive until the peer has voted/read
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("fail", ["none", "load", "init", "init_hang", "canary"])
+def test_connect_agrees_on_fallback_when_one_rank_fails(fail):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_connect_main, args=(r, 2, port, fail, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in ps:
+        r, handle, dt = q.get(timeout=90)
+        res[r] = (handle, dt)
+    for p in ps:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    if fail == "none":
+        assert res[0][0] == 100 and res[1][0] == 101
+    else:
+        # every rank falls back together, none waits out the 60 s rendezvous
+        assert res[0][0] is None and res[1][0] is None, res
+    for r in (0, 1):
+        assert res[r][1] < 30, res
+
+
+def test_connect_without_fallback_raises():
+    from zookeeper_amd.parallel import rccl
+
+    def load():
+        raise RuntimeError("stub: no librccl")
+
+    with pytest.raises(RuntimeError, match="RCCL load"):
+        rccl.connect(0, 1, fallback=False, tag="zk_conn_strict", log=lambda m: None,
+                     _load=load, _make_uid=lambda: b"x" * 128, _init=lambda u, w, r: 1,
+                     _canary=lambda c: None)
+
+
+def test_init_deadline_and_locked_abort():
+    """A stub init that never returns raises TimeoutError at the deadline;
+    the watchdog's failure path (_fail) takes the handle mutex, so a holder
+    (an enqueue in progress) delays it, and check() cancels the hard exit."""
+    import threading
+
+    from zookeeper_amd.parallel.rccl import NativeComm
+
+    t0 = time.monotonic()
+    with pytest.raises(TimeoutError, match="did not return"):
+        NativeComm(0, 1, tag="zk_hang", init_timeout_s=1, _make_uid=lambda: b"u" * 128,
+                   _init=lambda u, w, r: time.sleep(60))
+    assert time.monotonic() - t0 < 10
+
+    c = NativeComm(0, 1, tag="zk_lock", _make_uid=lambda: b"u" * 128, _init=lambda u, w, r: 7)
+    c._mu.acquire()  # this thread is "inside an enqueue"; the watchdog is another
+    held = []
+    th = threading.Thread(target=lambda: held.append(c._fail("stub expiry", grace_s=0.2)))
+    th.start()
+    th.join(10)
+    assert held == [False]  # mutex held: no abort of a handle in use
+    assert c._failed is None and c.handle == 7
+    c._mu.release()
+    done = []
+    th = threading.Thread(target=lambda: done.append(c._fail("stub expiry", grace_s=5)))
+    th.start()
+    th.join(10)
+    assert done == [True] and c.handle == 0
+    assert not c._stop.is_set()
+    with pytest.raises(RuntimeError, match="stub expiry"):
+        c.check()
+    assert c._stop.is_set()  # the training thread handles it: no hard exit

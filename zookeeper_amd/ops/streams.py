@@ -51,6 +51,9 @@ _pending: List[Tuple[torch.cuda.Event, object]] = []
 # side-stream events whose gradients were signalled ready without the
 # compute stream waiting for them (flush(wait=False)); joined at session exit
 _unwaited: List[torch.cuda.Event] = []
+# the same events by parameter (id): a bucket's all-reduce waits only for the
+# weight gradients inside its own range
+_unwaited_by_param: Dict[int, torch.cuda.Event] = {}
 # compute-stream tensors the side stream reads: held until the compute stream
 # has waited for the side stream (flush(wait=True)), then released on their
 # own stream.  (record_stream instead made the caching allocator treat their
@@ -136,6 +139,17 @@ def unwaited_events() -> List[torch.cuda.Event]:
     return _unwaited
 
 
+def unwaited_events_for(param_ids) -> List[torch.cuda.Event]:
+    """The unwaited events of the parameters ``param_ids`` (``id(param)``):
+    what a consumer of just those gradients must wait for."""
+    out = []
+    for pid in param_ids:
+        ev = _unwaited_by_param.get(pid)
+        if ev is not None:
+            out.append(ev)
+    return out
+
+
 def flush(wait: bool = True) -> None:
     """Signal the readiness of every deferred weight gradient (bucketed
     all-reduce).  ``wait``: order the compute stream after them (and after
@@ -151,6 +165,7 @@ def flush(wait: bool = True) -> None:
         for ev in _unwaited:
             cur.wait_event(ev)
         _unwaited.clear()
+        _unwaited_by_param.clear()
         for ev, _ in items:
             cur.wait_event(ev)
         # every side-stream reader of these is now ordered before the compute
@@ -159,6 +174,8 @@ def flush(wait: bool = True) -> None:
         _lagged.clear()
     else:
         _unwaited.extend(ev for ev, _ in items)
+        for ev, p in items:
+            _unwaited_by_param[id(p)] = ev
     for _, p in items:
         grad_ready(p)
 
@@ -171,6 +188,7 @@ def session(device: torch.device):
     use = OPTS.wgrad_side_stream and device.type == "cuda"
     _pending.clear()
     _unwaited.clear()
+    _unwaited_by_param.clear()
     _keep.clear()
     _lagged.clear()
     _active = use

@@ -134,6 +134,9 @@ class GradBucketer:
         for bi, b in enumerate(buckets):
             for i in b:
                 self.slot_bucket[i] = bi
+        # id() of each bucket's parameters: the side-stream weight gradients a
+        # bucket's collective must wait for
+        self._bucket_pids = [[id(flat.slots[i].param) for i in b] for b in buckets]
         self._pending = [len(b) for b in buckets]
         self._works: List = []
         self._launched = [False] * len(buckets)
@@ -259,8 +262,9 @@ class GradBucketer:
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(view.device))
         self.comm_stream.wait_event(ready)
-        # weight gradients still running on the side stream (ops/streams.py)
-        for ev in side_streams.unwaited_events():
+        # this bucket's weight gradients still running on the side stream
+        # (ops/streams.py); the other buckets' are not waited for
+        for ev in side_streams.unwaited_events_for(self._bucket_pids[b]):
             self.comm_stream.wait_event(ev)
         if _DEBUG_EVENTS:
             print(f"[bucketer {os.getpid()}] launch {b}: side events "
@@ -308,7 +312,6 @@ class GradBucketer:
         communicator): the watchdog follows them through an event on the
         current stream."""
         if self.native is not None:
-            self.native.check()
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.flat.grad.device))
             self.native.watch(done, "captured gradient all-reduce (graph replay)")
@@ -361,14 +364,14 @@ class GradBucketer:
         self.last_order = list(self._order)
         self._order.clear()
         if self.check_order and not (self.cuda and torch.cuda.is_current_stream_capturing()):
-            self._compare_order(self.last_order)
+            self.compare_order(self.last_order)
         self._works.clear()
         self._pending = [len(b) for b in self.buckets]
         self._launched = [False] * len(self.buckets)
         self._seen = [False] * len(self.flat.slots)
         self._clear_claims()
 
-    def _compare_order(self, order: List[int]) -> None:
+    def compare_order(self, order: List[int]) -> None:
         h = order_hash(order)
         dev = self.flat.grad.device if dist.get_backend(self.group) == "nccl" else "cpu"
         t = torch.tensor([h, -h], dtype=torch.int64, device=dev)

@@ -83,7 +83,9 @@ class Runtime:
     rccl_max_channels: int = Field(0)
     # Pin each rank to its share of its GPU's NUMA-local CPUs.
     cpu_affinity: bool = Field(True)
-    # Debug: compare the launched bucket order across ranks every step.
+    # Debug: compare the launched bucket order across ranks every step (with
+    # the native communicator under graph replay: eager steps, plus the
+    # captured order once after the capture -- every replay issues that).
     check_bucket_order: bool = Field(False)
     # Gradient all-reduce transport: "torch" (ProcessGroupNCCL), "native"
     # (parallel/rccl.py: the in-tree RCCL communicator; graph-capturable) or
@@ -102,12 +104,6 @@ class Runtime:
         if self.comm_backend not in ("torch", "native", "auto"):
             raise ValueError(f"runtime.comm_backend must be 'torch', 'native' or 'auto', "
                              f"got {self.comm_backend!r}")
-        if (self.check_bucket_order and self.comm_backend in ("native", "auto")
-                and self.graph != "off"):
-            # the order check all-reduces and reads a hash on the host inside
-            # bucketer.finish(), which the native backend captures into the graph
-            raise ValueError("runtime.check_bucket_order needs runtime.graph='off' with "
-                             "runtime.comm_backend='native' / 'auto'")
 
     def kernel_options(self) -> Dict[str, Any]:
         return {k: getattr(self, k) for k in _KERNEL_FIELDS}

@@ -117,31 +117,15 @@ class Trainer:
         self._static_out = None
 
     def _native_comm(self, fallback: bool):
-        """The in-tree RCCL communicator for the gradient all-reduce.  With
-        ``fallback`` (``runtime.comm_backend="auto"``) a failed set-up on any
-        rank makes every rank use ProcessGroupNCCL instead (the ranks agree
-        through a MIN all-reduce over the process group, so none is left
-        waiting in a collective the others never issue)."""
-        from zookeeper_amd.parallel.rccl import NativeComm
+        """The in-tree RCCL communicator for the gradient all-reduce
+        (:func:`~zookeeper_amd.parallel.rccl.connect`: load, rendezvous,
+        ``ncclCommInitRank`` under a deadline and a canary all-reduce, each
+        phase agreed through the store).  With ``fallback``
+        (``runtime.comm_backend="auto"``) a failure on any rank makes every
+        rank return ``None`` together: ProcessGroupNCCL carries the buckets."""
+        from zookeeper_amd.parallel.rccl import connect
 
-        if not fallback:
-            return NativeComm(self.info.rank, self.info.world)
-        native, err = None, None
-        try:
-            native = NativeComm(self.info.rank, self.info.world)
-        except Exception as e:  # noqa: BLE001 -- any set-up failure selects the fallback
-            err = e
-        # MIN over the ranks (as -MAX of the negation)
-        ok = -zdist.all_reduce_max_values([-1.0 if native is not None else 0.0], self.device)[0]
-        if ok < 1.0:
-            if self.info.is_main:
-                print(f"[trainer] native RCCL communicator unavailable on some rank "
-                      f"({err!r} here); gradient all-reduce through ProcessGroupNCCL",
-                      file=sys.stderr, flush=True)
-            if native is not None:
-                native.close()
-            return None
-        return native
+        return connect(self.info.rank, self.info.world, fallback=fallback)
 
     def _forward_backward(self, x: torch.Tensor, y: torch.Tensor):
         self.flat.zero_grad()
@@ -219,9 +203,17 @@ class Trainer:
                 with self.bucketer.suspended(), torch.cuda.graph(
                         self._graph, capture_error_mode="thread_local"):
                     self._static_out = self._forward_backward(*self._static_in)
+            if capture_comm and self.bucketer.check_order:
+                # the captured launch order is what every replay issues:
+                # compare it across ranks once, outside the capture
+                self.bucketer.compare_order(self.bucketer.last_order)
         else:
             self._static_in[0].copy_(x)
             self._static_in[1].copy_(y)
+        if capture_comm:
+            # a communicator the watchdog aborted must not be replayed: the
+            # captured RCCL kernels are bound to its (freed) resources
+            self.bucketer.native.check()
         self._graph.replay()
         if capture_comm:
             self.bucketer.watch_replay()  # watchdog over the captured collectives
