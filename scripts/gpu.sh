@@ -118,6 +118,12 @@ for spec in "$@"; do
           -d "$R/$OUT/pmcpy_${n}_${tag}" -o run --output-format csv -- python3 "$R/$script" $rest) || exit $?
       done
       ;;
+    profpy)
+      # kernel trace of python3 <a1 with commas as spaces>
+      script="${a1%%,*}"; rest=""; [ "$script" != "$a1" ] && rest="${a1#*,}"; rest="${rest//,/ }"
+      gpu_step 300 "$OUT/profpy_${n}.log" rocprofv3 --kernel-trace --stats \
+        -d "$OUT/profpy_$n" -o run --output-format csv -- python3 "$script" $rest || exit $?
+      ;;
     tune)
       targs="${a1//,/ }"  # '+' stands for a comma inside one argument (--igw 20+120)
       gpu_step 600 "$OUT/tune_${n}.log" python -u tools/tune_bconv.py ${targs//+/,} || exit $?

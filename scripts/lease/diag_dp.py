@@ -8,7 +8,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "tests", "gpu"))
 sys.path.insert(0, ROOT)
 
@@ -41,7 +41,7 @@ def main():
         os.makedirs(d, exist_ok=True)
         assert _run("same", d, 1, side, "0", rt=rt) == 0
         ref = torch.load(os.path.join(d, "same_w1_r0.pt"), weights_only=True)
-        burn = subprocess.Popen([sys.executable, os.path.join(ROOT, "scripts", "gpu_burn.py"),
+        burn = subprocess.Popen([sys.executable, os.path.join(ROOT, "scripts", "lease", "gpu_burn.py"),
                                  str(8 * reps + 20)])
         try:
             for i in range(reps):

@@ -458,7 +458,7 @@ class _HostStager:
     worker then all-reduced host data that did not yet hold the whole copy
     in ~1 of 3 two-rank runs (tests/gpu/test_dp_gpu.py, deterministic mode,
     side stream on: a partially stale weight gradient, identical on both
-    ranks); with the blocking copy: 0 of 12 (scripts/diag_dp.py)."""
+    ranks); with the blocking copy: 0 of 12 (scripts/lease/diag_dp.py)."""
 
     def __init__(self, total: int, group):
         self.host = torch.empty(total, dtype=torch.float32, pin_memory=True)

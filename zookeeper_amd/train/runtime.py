@@ -90,7 +90,7 @@ class Runtime:
     # Gradient all-reduce transport: "torch" (ProcessGroupNCCL), "native"
     # (parallel/rccl.py: the in-tree RCCL communicator; graph-capturable) or
     # "auto": native, falling back to torch on every rank if its set-up fails
-    # on any.  Forced 1-rank RCCL, E18 b1536 (scripts/gpu_call23.sh): torch
+    # on any.  Forced 1-rank RCCL, E18 b1536 (scripts/lease/gpu_call23.sh): torch
     # 34.56 ms/step vs native 30.06 vs 29.93 without data parallelism.
     comm_backend: str = Field("auto")
 
