@@ -3,36 +3,43 @@
 // output y1 (822 MB at batch 512) and a dense dy1 of the same size: written
 // once, read three times.  Here neither tensor exists; the conv is cheap
 // (K = 7 rows x 32) and is recomputed from the 4-channel padded image xp in
-// each of the three passes that need it:
+// each of the two passes that need it:
 //
-//   F1  zk_stem_fwd_stats   conv -> BN-1 partial sums (per block)
-//   F2  zk_stem_fwd_pool    conv -> BN-1 + ReLU -> 3x3/2 max pool: pooled p,
-//                           argmax tap, y1 at the argmax (ya), BN-2 partials
-//   B1  zk_stem_pool_bwd_sums_ya   BN-1 backward sums from (dp, ya)
+//   F   zk_stem_fwd_fused   conv -> BN-1 partial sums AND the 3x3/2 max pool
+//                           of y1 * sign(gamma1): argmax tap, y1 there (ya)
+//   P   zk_stem_pool_relu   p = relu(a1 ya + s1), BN-2 partial sums
+//   B0  zk_stem_bn2_bwd_sums       BN-2 backward dx (dp) + the BN-1 backward
+//                                  sums from (dp, ya), one pass
 //   B2  zk_stem_bwd_fused   conv -> dy1 = k1 relu'(u) route(dp) + k0 - k3 y1
 //                           -> weight gradient (MFMA), per-block slabs
 //
-// Every pass runs the same tile machinery: a persistent block walks spatial
-// tiles of conv outputs; a tile's input is a LINE BUFFER of xp rows (the
-// (pixel, kh) K-rows of all its pixels overlap: 8 x 16 outputs read 21 x 38
-// input pixels = 8 KB instead of the 56 KB im2col image), loaded by
-// global_load_lds one tile ahead.  The conv is D[co][px] = W[co][k] X[px][k]
-// on v_mfma_f32_32x32x16_bf16 with the 64 x 7 x 32 weights resident in LDS
-// (lane = pixel, 4 consecutive channels per register group).  Line-buffer
-// rows are padded so that the 16-B K-chunk of pixel m sits at 16 m + const
-// (mod 256): the B-operand reads of 32 consecutive pixels are bank-conflict
-// free, and so are the transposed reads of the weight gradient.
+// F and B2 are two-role software pipelines, one 512-thread block per CU:
+// four "matrix" waves run the MFMA work (conv, weight gradient) of one tile
+// while four VALU waves run the element work (pool / dy1 routing) of the
+// previous tile and issue the LDS-DMA rings, one barrier per tile.  Waves w
+// and w + 4 share a SIMD, so every SIMD pairs an MFMA stream with a VALU
+// stream; rounds 1-5 alternated the phases inside every wave (B2 1.93 ms, F1 +
+// F2 1.80 ms per E18 step at batch 1536).  A tile's input is a LINE BUFFER of
+// xp rows (the (pixel, kh) K-rows of all its pixels overlap: 8 x 16 outputs
+// read 21 x 38 input pixels = 8 KB instead of the 56 KB im2col image).  The
+// conv is D[co][px] = W[co][k] X[px][k] on v_mfma_f32_32x32x16_bf16 with each
+// matrix wave's 32 x 224 weights in VGPRs (lane = pixel, 4 consecutive
+// channels per register group).  Line-buffer rows are padded so that the
+// 16-B K-chunk of pixel m sits at 16 m + const (mod 256): the B-operand reads
+// of consecutive pixels are bank-conflict free, and so are the transposed
+// reads of the weight gradient.
 //
-// Numerics match stem.hip: y1 is rounded to bf16 before every use (the MFMA
-// chain per output is identical in all passes, so F1, F2 and B2 see the same
-// y1), the pool compares relu(a*y1 + b) in fp32 and keeps the first maximum.
+// Numerics: y1 is rounded to bf16 before every use (the MFMA chain per output
+// is identical in F and B2, so both see the same y1); the pool keeps the
+// first maximum of y1 * sign(gamma1), which is the first maximum of
+// relu(a1 y1 + s1) up to ties at relu's 0 (which route no gradient); the
+// BN-1 statistics are of the fp32 accumulators.
 #include "mfma_common.h"
 
 namespace {
 
 constexpr int SC = 64;                    // stem output channels
 constexpr int SKH = 7;                    // kernel rows (7x7 stems)
-constexpr int W_BYTES = SKH * SC * 64;    // [kh][co][32 bf16] = 28 KB
 
 struct FGeom {
   int B, Cin, KW, Ho, Wo, Hp, Wp;  // conv: stride 2, 7 x KW, xp [B][Hp][Wp][4]
@@ -56,10 +63,9 @@ struct LBuf {
 
 // Issue the line buffer of the tile whose first conv output is (b, r0, c0).
 // Rows / pixels outside xp (and the row padding) read the zero page.
-template <int TR, int TC, int NT>
-__device__ __forceinline__ void issue_lbuf(unsigned char* lb, const unsigned char* xp,
-                                           const FGeom& g, int b, int r0, int c0, int tid) {
-  using L = LBuf<TR, TC>;
+template <class L, int NT>
+__device__ __forceinline__ void issue_lines(unsigned char* lb, const unsigned char* xp,
+                                            const FGeom& g, int b, int r0, int c0, int tid) {
   const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
   const int wave = tid >> 6, lane = tid & 63;
   const long long rowb = (long long)g.Wp * 8;
@@ -79,107 +85,33 @@ __device__ __forceinline__ void issue_lbuf(unsigned char* lb, const unsigned cha
   }
 }
 
-// Weights ws [kh][co][32] bf16 -> LDS with the 16-B chunk of row co at slot
-// chunk ^ ((co >> 2) & 3) (the A-operand reads of 32 rows are conflict free).
-template <int NT>
-__device__ __forceinline__ void load_weights(unsigned char* wl, const unsigned char* ws,
-                                             int tid) {
-  for (int i = tid; i < W_BYTES / 16; i += NT) {
-    const int row = i >> 2, slot = i & 3, co = row & (SC - 1);
-    const uint4 v = *reinterpret_cast<const uint4*>(ws + row * 64 + ((slot ^ ((co >> 2) & 3)) << 4));
-    *reinterpret_cast<uint4*>(wl + i * 16) = v;
+// counted wait on this wave's own vector-memory operations (n <= 15, wave-uniform)
+__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
+  switch (n) {
+#define ZK_VMC(k) \
+  case k:         \
+    asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); \
+    break;
+    ZK_VMC(0) ZK_VMC(1) ZK_VMC(2) ZK_VMC(3) ZK_VMC(4) ZK_VMC(5) ZK_VMC(6) ZK_VMC(7)
+    ZK_VMC(8) ZK_VMC(9) ZK_VMC(10) ZK_VMC(11) ZK_VMC(12) ZK_VMC(13) ZK_VMC(14)
+#undef ZK_VMC
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
   }
 }
 
-// Conv of TN 32-pixel groups starting at tile pixel px0 (pixel m = r TC + c
-// of the tile; m >= TR*TC are dummies that read pixel 0):
-// acc[a][t][r] = y1[co = 32a + 8(r>>2) + 4h + (r&3)][px0 + 32t + lane%32].
-template <int TR, int TC, int TN>
-__device__ __forceinline__ void conv_tile(const unsigned char* wl, const unsigned char* lb,
-                                          int px0, int lane, f32x16 (&acc)[2][TN]) {
-  using L = LBuf<TR, TC>;
-  const int r32 = lane & 31, h = lane >> 5;
-  int segb[TN];
-#pragma unroll
-  for (int t = 0; t < TN; ++t) {
-    int px = px0 + 32 * t + r32;
-    if (px >= TR * TC) px = 0;
-    const int rr = px / TC, cc = px - rr * TC;
-    segb[t] = 2 * rr * L::RB + 16 * cc + 16 * h;
-  }
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int t = 0; t < TN; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][t][r] = 0.f;
-  int wrow[2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a) wrow[a] = (32 * a + r32) * 64;
-  const int wsw = (r32 >> 2) & 3;  // (co >> 2) & 3 for co = 32a + r32
-#pragma unroll
-  for (int kh = 0; kh < SKH; ++kh) {
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      const int chunk = 2 * sub + h;
-      uint4 af[2], bf[TN];
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-        af[a] = *reinterpret_cast<const uint4*>(wl + kh * SC * 64 + wrow[a] + ((chunk ^ wsw) << 4));
-#pragma unroll
-      for (int t = 0; t < TN; ++t)
-        bf[t] = *reinterpret_cast<const uint4*>(lb + segb[t] + kh * L::RB + 32 * sub);
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int t = 0; t < TN; ++t) acc[a][t] = mfma_bf16(af[a], bf[t], acc[a][t]);
-    }
-  }
+// LDS-DMA instructions issue_lines<L, NT> issues in wave `wave`
+template <class L, int NT>
+__device__ __forceinline__ int lines_count(int wave) {
+  int n = 0;
+  for (int j = 0; j < (L::CHUNKS + NT - 1) / NT; ++j) n += j * NT + wave * 64 < L::CHUNKS;
+  return n;
 }
 
-// Weight fragments of all 64 channels for every K-substep, in registers
-// (112 VGPRs): w[kh][sub][a] = chunk 2 sub + h of row 32a + lane%32 of kernel
-// row kh.
-__device__ __forceinline__ void load_wfrags(const unsigned char* ws, int lane,
-                                            uint4 (&w)[SKH][2][2]) {
-  const int r32 = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int kh = 0; kh < SKH; ++kh)
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-        w[kh][sub][a] = *reinterpret_cast<const uint4*>(
-            ws + (kh * SC + 32 * a + r32) * 64 + (2 * sub + h) * 16);
+template <int TR, int TC, int NT>
+__device__ __forceinline__ void issue_lbuf(unsigned char* lb, const unsigned char* xp,
+                                           const FGeom& g, int b, int r0, int c0, int tid) {
+  issue_lines<LBuf<TR, TC>, NT>(lb, xp, g, b, r0, c0, tid);
 }
-
-// conv_tile with the A operand (weights) from registers: one LDS read per
-// two MFMAs.
-template <int TR, int TC>
-__device__ __forceinline__ void conv_tile_wreg(const uint4 (&w)[SKH][2][2],
-                                               const unsigned char* lb, int px0, int lane,
-                                               f32x16 (&acc)[2]) {
-  using L = LBuf<TR, TC>;
-  const int r32 = lane & 31, h = lane >> 5;
-  int px = px0 + r32;
-  if (px >= TR * TC) px = 0;
-  const int rr = px / TC, cc = px - rr * TC;
-  const int segb = 2 * rr * L::RB + 16 * cc + 16 * h;
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
-#pragma unroll
-  for (int kh = 0; kh < SKH; ++kh)
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      const uint4 bf = *reinterpret_cast<const uint4*>(lb + segb + kh * L::RB + 32 * sub);
-#pragma unroll
-      for (int a = 0; a < 2; ++a) acc[a] = mfma_bf16(w[kh][sub][a], bf, acc[a]);
-    }
-}
-
-__device__ __forceinline__ float bf16r(float v) { return zk::bf16_to_f32(zk::f32_to_bf16(v)); }
 
 __device__ __forceinline__ void unpack8(const uint4& q, float (&v)[8]) {
   const uint32_t u[4] = {q.x, q.y, q.z, q.w};
@@ -193,18 +125,6 @@ __device__ __forceinline__ void unpack8(const uint4& q, float (&v)[8]) {
 __device__ __forceinline__ uint4 pack8f(const float (&v)[8]) {
   return make_uint4(zk::pack_bf16x2(v[0], v[1]), zk::pack_bf16x2(v[2], v[3]),
                     zk::pack_bf16x2(v[4], v[5]), zk::pack_bf16x2(v[6], v[7]));
-}
-
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-}
-
-// Top of a tile: this wave's line-buffer DMA (and any stores) retired, then
-// the barrier makes every wave's DMA visible.
-__device__ __forceinline__ void tile_barrier() {
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
 }
 
 // Reduce-scatter of 32 values over the 32 lanes of a wave half (lane r ends
@@ -229,295 +149,416 @@ __device__ __forceinline__ float rs32(float (&v)[32], int r32) {
 }
 
 // ===========================================================================
-// F1: BN-1 statistics of y1 (bf16-rounded) without storing it.
-// Tile 8 x 16 outputs, 4 waves x 32 pixels, line buffer double-buffered.
-// part[block][2][64] (sum, sum of squares).
+// F: conv -> BN-1 statistics AND the 3x3/2 max pool, in one pass.
+// The pool needs no BN-1 coefficients: relu(a y + s) is monotone in y in the
+// direction of a = gamma1 * rstd, i.e. of gamma1, which is known before the
+// batch statistics exist.  The first maximum of relu(a y + s) over a window
+// is the first maximum of y * sign(gamma1) (ties at relu's 0 route no
+// gradient), so this pass writes ya (y1 at that tap, bf16) and arg (the tap)
+// while it accumulates the statistics; p = relu(a ya + s) and BN-2's partial
+// sums follow in the elementwise zk_stem_pool_relu once BN-1 is finalised.
+// (Rounds 1-5 ran the conv twice: statistics, then BN-1 + pool.)
+//
+// Tile = 8 x 7 pool outputs <- a 17 x 15 conv region (255 pixels + 1
+// dummy = 8 groups of 32).  Pixels are numbered owned-first: m < 224 are the
+// 16 x 14 outputs the tile owns for the statistics; 224..254 the halo row and
+// column it shares with the next tile (group 7, counted only in the last tile
+// of a row / column); 255 a dummy.  4 waves, 2 blocks per CU: wave w computes
+// channel half a = w & 1 of pixel groups 4 (w >> 1) .. +3 with its 32 x 224
+// weights in VGPRs (one B read per MFMA).  y1 goes to LDS as int16 order keys
+// of y * sign(gamma1) (the two's complement of the bf16 sign-magnitude, so
+// -0 == +0); the pool takes one 32-bit max per tap over (key << 16 | 15 - tap):
+// keys are distinct, the max is the first maximum, and max is order-free.
 // ===========================================================================
-constexpr int F1_TR = 8, F1_TC = 16;
-constexpr int F1_LB = LBuf<F1_TR, F1_TC>::BYTES;
-constexpr int F1_LDS = 2 * F1_LB;
+constexpr int F_PR = 8, F_PC = 7;                        // pool outputs per tile
+constexpr int F_TR = 2 * F_PR + 1, F_TC = 2 * F_PC + 1;  // 17 x 15 conv region
+constexpr int F_OR = 2 * F_PR, F_OC = 2 * F_PC;          // 16 x 14 owned outputs
+constexpr int F_NOWN = F_OR * F_OC;                      // 224 = 7 pixel groups
+static_assert(F_TR * F_TC < 256 && F_NOWN == 7 * 32, "F region");
 
-__global__ __launch_bounds__(256, 2) void stem_fwd_stats_kernel(
-    const unsigned char* __restrict__ xp, const unsigned char* __restrict__ ws,
-    float* __restrict__ part, FGeom g, int tiles_w, int tiles_img, int ntiles) {
-  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
-  unsigned char* lbuf0 = smem;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int r32 = lane & 31, h = lane >> 5;
-  const int blk = xcd_linear(blockIdx.x, gridDim.x), nblk = gridDim.x;
+struct FLB {  // line buffer of the 17 x 15 region
+  static constexpr int ROWS = 2 * (F_TR - 1) + SKH;  // 39 xp rows
+  static constexpr int BASE = (2 * F_TC + 6) * 8;     // 36 pixels of 8 B
+  // 2 RB = 16 F_OC (mod 256): the K-chunk of owned pixel m sits at 16 m
+  // (mod 256), so the B reads of 16 consecutive pixels are conflict free
+  static constexpr int RB = BASE + ((((8 * F_OC) % 128 - BASE) % 128) + 128) % 128;
+  static constexpr int CHUNKS = ROWS * RB / 16;
+  static constexpr int BYTES = (CHUNKS + 63) / 64 * 64 * 16;
+  static_assert(RB % 16 == 0 && (2 * RB) % 256 == (16 * F_OC) % 256, "F line buffer");
+};
+constexpr int F_YT = 256 * 128;  // y1 keys [pixel][64 channels]
 
-  auto tile_pos = [&](int T, int& b, int& r0, int& c0) {
-    b = T / tiles_img;
-    const int rem = T - b * tiles_img;
-    const int th = rem / tiles_w;
-    r0 = th * F1_TR;
-    c0 = (rem - th * tiles_w) * F1_TC;
-  };
-  if (blk < ntiles) {
-    int b, r0, c0;
-    tile_pos(blk, b, r0, c0);
-    issue_lbuf<F1_TR, F1_TC, 256>(lbuf0, xp, g, b, r0, c0, tid);
-  }
-  uint4 wf[SKH][2][2];
-  load_wfrags(ws, lane, wf);
-
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
-  f32x2 cs[16], cq[16];  // value pairs (a = 0, 1) of register r: packed adds / FMAs
-#pragma unroll
-  for (int r = 0; r < 16; ++r) cs[r] = cq[r] = (f32x2){0.f, 0.f};
-
-  int it = 0;
-  for (int T = blk; T < ntiles; T += nblk, ++it) {
-    const int cur = it & 1;
-    tile_barrier();
-    int b, r0, c0;
-    tile_pos(T, b, r0, c0);
-    if (T + nblk < ntiles) {
-      int bn, rn, cn;
-      tile_pos(T + nblk, bn, rn, cn);
-      issue_lbuf<F1_TR, F1_TC, 256>(lbuf0 + (cur ^ 1) * F1_LB, xp, g, bn, rn, cn, tid);
-    }
-    f32x16 acc[2];
-    conv_tile_wreg<F1_TR, F1_TC>(wf, lbuf0 + cur * F1_LB, 32 * wave, lane, acc);
-    // statistics of the fp32 accumulators (the stored-bf16 rounding of
-    // stem.hip is below the statistics' own summation error)
-    if (r0 + F1_TR > g.Ho || c0 + F1_TC > g.Wo) {  // partial tile (uniform)
-      const int px = 32 * wave + r32;
-      const bool live = r0 + px / F1_TC < g.Ho && c0 + px % F1_TC < g.Wo;
-      if (!live) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[0][r] = acc[1][r] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const f32x2 v = {acc[0][r], acc[1][r]};
-      cs[r] += v;
-      cq[r] += v * v;
-    }
-  }
-
-  // channel co = 32a + 8(r>>2) + 4h + (r&3): reduce over the 32 pixel lanes
-  float v[32];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    v[r] = cs[r].x;
-    v[16 + r] = cs[r].y;
-  }
-  const float s_sum = rs32(v, r32);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    v[r] = cq[r].x;
-    v[16 + r] = cq[r].y;
-  }
-  const float s_sq = rs32(v, r32);
-  // lane r32 holds value index i = r32 = a*16 + r
-  const int a = r32 >> 4, r = r32 & 15;
-  const int co = 32 * a + 8 * (r >> 2) + 4 * h + (r & 3);
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);  // [4 waves][2][64]
-  red[(wave * 2 + 0) * SC + co] = s_sum;
-  red[(wave * 2 + 1) * SC + co] = s_sq;
-  __syncthreads();
-  if (tid < 2 * SC) {
-    float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) t += red[w * 2 * SC + tid];
-    part[(long long)blockIdx.x * 2 * SC + tid] = t;
-  }
+// LDS row of pixel m: rows 2k / 2k+1 swap when bit 1 of m is set, so the pool
+// reads of pixels m and m + 2 fall in opposite 128-B bank halves; 16-B slot
+// s ^ f_swz(m), a bijection of m mod 8 whose bit 2 ignores bit 2 of m: the
+// ds_write_b128 stores of 8 consecutive pixels and the pool reads of pixels
+// m and m + 4 (opposite channel halves) are conflict free.
+__device__ __forceinline__ int f_off(int m, int slot) {
+  const int row = m ^ ((m >> 1) & 1);
+  const int swz = ((m & 3) << 1) | ((m >> 2) & 1);
+  return row * 128 + ((slot ^ swz) << 4);
 }
 
-// ===========================================================================
-// F2: conv -> relu(BN-1) -> 3x3/2 max pool.  Tile = 8 x 7 pool outputs, whose
-// windows cover a 17 x 15 conv region (255 pixels + 1 dummy = 8 waves x 32).
-// Writes p (pooled), arg (tap of the first maximum), ya (y1 there) and
-// per-block BN-2 partial sums of p.  y1 of the region is staged in LDS
-// ([pixel][channel] bf16, chunk slot ^ ((m >> 1) & 7)).  One block per CU,
-// the line buffer double-buffered and issued a whole tile ahead; every wave
-// issues exactly three output stores per tile (pool outputs outside the
-// image store to a sink), so the next tile waits for its line buffer with
-// vmcnt(3) instead of draining the stores.
-// ===========================================================================
-constexpr int F2_PR = 8, F2_PC = 7;
-constexpr int F2_TR = 2 * F2_PR + 1, F2_TC = 2 * F2_PC + 1;
-constexpr int F2_LB = LBuf<F2_TR, F2_TC>::BYTES;
-constexpr int F2_YT = 256 * 128;
-constexpr int F2_NT = 512;
-constexpr int F2_LDS = W_BYTES + 2 * F2_LB + F2_YT;
-static_assert(F2_TR * F2_TC <= 256, "F2 region");
-static_assert(F2_PR * F2_PC * 8 <= F2_NT, "one pool item per thread");
-static_assert(F2_LDS <= 160 * 1024, "F2 LDS");
+// region coordinates of pixel m / pixel number of region (rr, cc)
+__device__ __forceinline__ void f_pix(int m, int& rr, int& cc) {
+  if (m < F_NOWN) {
+    rr = m / F_OC;
+    cc = m - rr * F_OC;
+  } else if (m < F_NOWN + F_TC) {
+    rr = F_OR;
+    cc = m - F_NOWN;
+  } else if (m < F_NOWN + F_TC + F_OR) {
+    rr = m - (F_NOWN + F_TC);
+    cc = F_OC;
+  } else {
+    rr = 0;  // dummy: reads pixel 0, never counted or pooled
+    cc = 0;
+  }
+}
+__device__ __forceinline__ int f_m(int rr, int cc) {
+  return rr < F_OR ? (cc < F_OC ? rr * F_OC + cc : F_NOWN + F_TC + rr) : F_NOWN + cc;
+}
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// bf16 pair -> int16 order keys: negative values get their magnitude bits
+// flipped (an involution).  -0 sorts below +0; the conv never produces -0
+// (its fp32 accumulators start at +0 and x + (-x) = +0).
+__device__ __forceinline__ uint32_t key16x2(uint32_t d) {
+  const s16x2 x = __builtin_bit_cast(s16x2, d);
+  const s16x2 s = x >> (s16x2){15, 15};
+  return d ^ (__builtin_bit_cast(uint32_t, s) & 0x7FFF7FFFu);
+}
 
 __device__ __attribute__((aligned(16))) uint4 g_pool_sink[2];
 
-__global__ __launch_bounds__(F2_NT, 1) void stem_fwd_pool_kernel(
+// F runs as a two-role software pipeline, one 512-thread block per CU:
+// waves 4-7 ("matrix" waves) compute the conv, the statistics and the y1 keys
+// of tile i while waves 0-3 ("pool" waves) pool tile i - 1, store its ya / arg
+// and issue the line-buffer DMA two tiles ahead.  Wave w and wave w + 4 share
+// a SIMD: the MFMA stream of one overlaps the VALU stream of the other.
+constexpr int F_NLB = 3, F_NYT = 2;
+constexpr int F_LDS = F_NLB * FLB::BYTES + F_NYT * F_YT;
+static_assert(F_LDS <= 160 * 1024, "F pipeline LDS");
+
+__global__ __launch_bounds__(512, 2) void stem_fwd_fused_kernel(
     const unsigned char* __restrict__ xp, const unsigned char* __restrict__ ws,
-    const float* __restrict__ coef1, uint16_t* __restrict__ p, uint8_t* __restrict__ arg,
-    uint16_t* __restrict__ ya, float* __restrict__ part, FGeom g, int tiles_w, int tiles_img,
-    int ntiles) {
+    const float* __restrict__ gamma1, uint16_t* __restrict__ ya, uint8_t* __restrict__ arg,
+    float* __restrict__ part, FGeom g, int tiles_w, int tiles_h, int ntiles) {
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
-  unsigned char* wl = smem;
-  unsigned char* lb0 = smem + W_BYTES;
-  unsigned char* yt = smem + W_BYTES + 2 * F2_LB;
+  unsigned char* lbr = smem;                          // [3][FLB::BYTES]
+  unsigned char* ytr = smem + F_NLB * FLB::BYTES;     // [2][F_YT]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r32 = lane & 31, h = lane >> 5;
   const int blk = xcd_linear(blockIdx.x, gridDim.x), nblk = gridDim.x;
-  const int cg = tid & 7;  // channel group of this thread in the pool phase
-  const int po = tid >> 3;
-  const int pi = po / F2_PC, pj = po - (po / F2_PC) * F2_PC;
-  const bool pitem = po < F2_PR * F2_PC;
-  float a1[8], s1[8], sg[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    a1[k] = coef1[cg * 8 + k];
-    s1[k] = coef1[SC + cg * 8 + k];
-    sg[k] = a1[k] < 0.f ? -1.f : 1.f;
-  }
-  uint4 flip;  // bf16 sign bits of the channels with a < 0
-  {
-    uint32_t f[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      f[q] = (a1[2 * q] < 0.f ? 0x8000u : 0u) | (a1[2 * q + 1] < 0.f ? 0x80000000u : 0u);
-    flip = make_uint4(f[0], f[1], f[2], f[3]);
-  }
-  auto tile_pos = [&](int T, int& b, int& oh0, int& ow0) {
+  const int n = blk < ntiles ? (ntiles - 1 - blk) / nblk + 1 : 0;  // this block's tiles
+  const int tiles_img = tiles_w * tiles_h;
+  const bool pooler = wave < 4;
+  const int mw = wave & 3, a = mw & 1, g0 = 4 * (mw >> 1);  // matrix waves: channel half, first group
+
+  auto tile_pos = [&](int j, int& b, int& th, int& tw) {
+    const int T = blk + j * nblk;
     b = T / tiles_img;
     const int rem = T - b * tiles_img;
-    const int th = rem / tiles_w;
-    oh0 = th * F2_PR;
-    ow0 = (rem - th * tiles_w) * F2_PC;
+    th = rem / tiles_w;
+    tw = rem - th * tiles_w;
   };
-  load_weights<F2_NT>(wl, ws, tid);
-  if (blk < ntiles) {
-    int b, oh0, ow0;
-    tile_pos(blk, b, oh0, ow0);
-    issue_lbuf<F2_TR, F2_TC, F2_NT>(lb0, xp, g, b, 2 * oh0 - g.pt2, 2 * ow0 - g.pl2, tid);
+  auto issue_lb = [&](int j) {
+    int b, th, tw;
+    tile_pos(j, b, th, tw);
+    issue_lines<FLB, 256>(lbr + (j % F_NLB) * FLB::BYTES, xp, g, b, 2 * F_PR * th - g.pt2,
+                          2 * F_PC * tw - g.pl2, tid);
+  };
+
+  float cs[16], cq[16];  // matrix waves: BN-1 sums / squares of this lane's 16 channels
+  if (pooler) {
+    // pool items it = tid + 256 k (k = 0, 1; k = 1 only in waves 0-2): pool
+    // output po = it >> 3 of the tile, channels 8 cg .. 8 cg + 7
+    const int cg = tid & 7;
+    uint32_t pflip[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int c = 8 * cg + 2 * d;
+      pflip[d] = gamma1 ? ((gamma1[c] < 0.f ? 0x8000u : 0u) | (gamma1[c + 1] < 0.f ? 0x80000000u : 0u))
+                        : 0u;
+    }
+    uint32_t toff[2][5];  // the 9 tap offsets of each item, two 16-bit halves per register
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int po = (tid >> 3) + 32 * k;
+      const int i = po / F_PC, j = po - (po / F_PC) * F_PC;
+#pragma unroll
+      for (int t = 0; t < 10; t += 2) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          if (t + e < 9 && po < F_PR * F_PC)
+            v |= (uint32_t)f_off(f_m(2 * i + (t + e) / 3, 2 * j + (t + e) % 3), cg) << (16 * e);
+        toff[k][t / 2] = v;
+      }
+    }
+    if (n > 0) issue_lb(0);
+    if (n > 1) issue_lb(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int n_lb = lines_count<FLB, 256>(wave);
+    const int nst = wave < 3 ? 4 : 2;  // ya / arg stores per tile
+    for (int ii = 0; ii <= n; ++ii) {
+      int issued = 0;
+      if (ii + 2 < n) {
+        issue_lb(ii + 2);
+        issued = n_lb;
+      }
+      if (ii >= 1) {
+        const unsigned char* yt = ytr + ((ii - 1) % F_NYT) * F_YT;
+        int b, th, tw;
+        tile_pos(ii - 1, b, th, tw);
+        const int hr0 = 2 * F_PR * th - g.pt2, wc0 = 2 * F_PC * tw - g.pl2;
+        // tile inside the image: every tap in the image, every pool output live
+        const bool tile_in = hr0 >= 0 && hr0 + F_TR <= g.Ho && wc0 >= 0 && wc0 + F_TC <= g.Wo &&
+                             F_PR * th + F_PR <= g.H2 && F_PC * tw + F_PC <= g.W2;
+        // ---- pool: one (pool output, 8 channels) item per thread and k
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          if (k == 1 && wave == 3) continue;  // 56 outputs x 8 = 448 items (uniform)
+          const int po = (tid >> 3) + 32 * k;
+          const int i = po / F_PC, j = po - (po / F_PC) * F_PC;
+          const int oh = F_PR * th + i, ow = F_PC * tw + j;
+          uint4 tv[9];
+#pragma unroll
+          for (int t = 0; t < 9; ++t)
+            tv[t] = *reinterpret_cast<const uint4*>(yt + ((toff[k][t >> 1] >> (16 * (t & 1))) & 0xFFFFu));
+          if (!tile_in) {  // a tile at the image border (uniform); then per item
+            const bool interior = hr0 + 2 * i >= 0 && hr0 + 2 * i + 2 < g.Ho && wc0 + 2 * j >= 0 &&
+                                  wc0 + 2 * j + 2 < g.Wo;
+            if (!interior) {
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+              const int hc = hr0 + 2 * i + t / 3, wc = wc0 + 2 * j + t % 3;
+              if (!(hc >= 0 && hc < g.Ho && wc >= 0 && wc < g.Wo))
+                tv[t] = make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);  // -inf
+            }
+            }
+          }
+          int best[8];
+#pragma unroll
+          for (int t = 0; t < 9; ++t) {
+            const uint32_t u[4] = {tv[t].x, tv[t].y, tv[t].z, tv[t].w};
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              const int lo = (int)((u[d] << 16) | (uint32_t)(15 - t));
+              const int hi = (int)((u[d] & 0xFFFF0000u) | (uint32_t)(15 - t));
+              best[2 * d] = t == 0 ? lo : max(best[2 * d], lo);
+              best[2 * d + 1] = t == 0 ? hi : max(best[2 * d + 1], hi);
+            }
+          }
+          // arg: 15 - (low byte); ya: the key halves, un-keyed and un-flipped
+          const uint32_t t01 = __builtin_amdgcn_perm((uint32_t)best[1], (uint32_t)best[0], 0x0c0c0400u);
+          const uint32_t t23 = __builtin_amdgcn_perm((uint32_t)best[3], (uint32_t)best[2], 0x0c0c0400u);
+          const uint32_t t45 = __builtin_amdgcn_perm((uint32_t)best[5], (uint32_t)best[4], 0x0c0c0400u);
+          const uint32_t t67 = __builtin_amdgcn_perm((uint32_t)best[7], (uint32_t)best[6], 0x0c0c0400u);
+          const uint2 av = make_uint2(__builtin_amdgcn_perm(t23, t01, 0x05040100u) ^ 0x0F0F0F0Fu,
+                                      __builtin_amdgcn_perm(t67, t45, 0x05040100u) ^ 0x0F0F0F0Fu);
+          uint32_t yv[4];
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+            yv[d] = key16x2(__builtin_amdgcn_perm((uint32_t)best[2 * d + 1], (uint32_t)best[2 * d],
+                                                  0x07060302u)) ^ pflip[d];
+          const bool live = tile_in || (oh < g.H2 && ow < g.W2);  // po < 56 always here
+          const long long off = (((long long)b * g.H2 + oh) * g.W2 + ow) * SC + cg * 8;
+          uint4* dy_ = live ? reinterpret_cast<uint4*>(ya + off) : &g_pool_sink[0];
+          uint2* da_ = live ? reinterpret_cast<uint2*>(arg + off) : reinterpret_cast<uint2*>(&g_pool_sink[1]);
+          *dy_ = make_uint4(yv[0], yv[1], yv[2], yv[3]);
+          *da_ = av;
+        }
+        issued += nst;
+      }
+      // everything issued before this interval (line buffer ii + 1, the
+      // previous tile's stores) landed
+      wait_vmcnt_dyn(issued);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    // weights of channel half a, w[kh][sub] = K-chunk 2 sub + h of row
+    // co = 32 a + r32, negated where gamma1[co] < 0 (exact in bf16): the MFMA
+    // then yields y1 * sign(gamma1) itself, and so do its statistics (the sums
+    // get the sign back at the end, the squares need none)
+    const uint32_t wneg = gamma1 && gamma1[32 * a + r32] < 0.f ? 0x80008000u : 0u;
+    uint4 w[SKH][2];
+#pragma unroll
+    for (int kh = 0; kh < SKH; ++kh)
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const uint4 v = *reinterpret_cast<const uint4*>(ws + (kh * SC + 32 * a + r32) * 64 +
+                                                        (2 * sub + h) * 16);
+        w[kh][sub] = make_uint4(v.x ^ wneg, v.y ^ wneg, v.z ^ wneg, v.w ^ wneg);
+      }
+    int segb[4];  // B-operand byte offsets of this lane's pixel in the 4 groups
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      int rr, cc;
+      f_pix(32 * (g0 + t) + r32, rr, cc);
+      segb[t] = 2 * rr * FLB::RB + 16 * cc + 16 * h;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cs[r] = cq[r] = 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ii = 0; ii <= n; ++ii) {
+      if (ii < n) {
+        int b, th, tw;
+        tile_pos(ii, b, th, tw);
+        const int hr0 = 2 * F_PR * th - g.pt2, wc0 = 2 * F_PC * tw - g.pl2;
+        const unsigned char* lbc = lbr + (ii % F_NLB) * FLB::BYTES;
+        unsigned char* yt = ytr + (ii % F_NYT) * F_YT;
+        const bool last_r = th == tiles_h - 1, last_c = tw == tiles_w - 1;
+        const bool fast = hr0 >= 0 && hr0 + F_OR <= g.Ho && wc0 >= 0 && wc0 + F_OC <= g.Wo &&
+                          !(last_r && hr0 + F_OR < g.Ho) && !(last_c && wc0 + F_OC < g.Wo);
+#pragma unroll
+        for (int hg = 0; hg < 2; ++hg) {
+          // ---- conv: 2 groups x 32 pixels x channel half a
+          f32x16 acc[2];
+#pragma unroll
+          for (int kh = 0; kh < SKH; ++kh)
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub) {
+              uint4 bf[2];
+#pragma unroll
+              for (int u = 0; u < 2; ++u)
+                bf[u] = *reinterpret_cast<const uint4*>(lbc + segb[2 * hg + u] + kh * FLB::RB +
+                                                        32 * sub);
+#pragma unroll
+              for (int u = 0; u < 2; ++u)  // the first step takes C = 0 (no register zeroing)
+                acc[u] = mfma_bf16(w[kh][sub], bf[u], kh + sub ? acc[u] : f32x16{});
+            }
+          // ---- BN-1 statistics of the fp32 accumulators, each conv output once
+          if (fast) {  // the 7 owned groups, no halo (uniform); packed fp32
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              if (g0 + 2 * hg + u < 7) {
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) {
+                  const f32x2 v = {acc[u][r], acc[u][r + 1]};
+                  f32x2 s2 = {cs[r], cs[r + 1]}, q2 = {cq[r], cq[r + 1]};
+                  s2 += v;
+                  q2 = __builtin_elementwise_fma(v, v, q2);
+                  cs[r] = s2.x;
+                  cs[r + 1] = s2.y;
+                  cq[r] = q2.x;
+                  cq[r + 1] = q2.y;
+                }
+              }
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int m = 32 * (g0 + 2 * hg + u) + r32;
+              int rr, cc;
+              f_pix(m, rr, cc);
+              const int hc = hr0 + rr, wc = wc0 + cc;
+              const bool counted = m < 255 && hc >= 0 && hc < g.Ho && wc >= 0 && wc < g.Wo &&
+                                   (rr < F_OR || last_r) && (cc < F_OC || last_c);
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                const float v = counted ? acc[u][r] : 0.f;
+                cs[r] += v;
+                cq[r] = fmaf(v, v, cq[r]);
+              }
+            }
+          }
+          // ---- y1 * sign(gamma1) -> LDS keys: per register pair (q, q+1) one
+          // permlane32 swap per dword gives each lane a whole 16-B slot
+          // (cdna_hip_programming.md T21)
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int m = 32 * (g0 + 2 * hg + u) + r32;
+#pragma unroll
+            for (int pq = 0; pq < 2; ++pq) {
+              uint32_t d[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int r = 4 * (2 * pq + (e >> 1)) + 2 * (e & 1);
+                d[e] = key16x2(zk::pack_bf16x2(acc[u][r], acc[u][r + 1]));
+              }
+              const auto s0 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+              const auto s1 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+              *reinterpret_cast<uint4*>(yt + f_off(m, 4 * a + 2 * pq + h)) =
+                  make_uint4(s0[0], s1[0], s0[1], s1[1]);
+            }
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // y1 keys stored
+      __builtin_amdgcn_s_barrier();
+    }
   }
 
-  float bs1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bs2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  int it = 0;
-  for (int T = blk; T < ntiles; T += nblk, ++it) {
-    const int cur = it & 1;
-    // line buffer of T retired (the previous tile's 3 stores may stay in
-    // flight); the barrier also ends the previous pool phase's reads of yt
-    if (it == 0)
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    int b, oh0, ow0;
-    tile_pos(T, b, oh0, ow0);
-    if (T + nblk < ntiles) {
-      int bn, on, wn;
-      tile_pos(T + nblk, bn, on, wn);
-      issue_lbuf<F2_TR, F2_TC, F2_NT>(lb0 + (cur ^ 1) * F2_LB, xp, g, bn, 2 * on - g.pt2,
-                                      2 * wn - g.pl2, tid);
+  // statistics: lane r32 of each half ends with the half's total of value r32
+  // (r32 < 16: sum of channel(r32), else sum of squares of channel(r32 - 16))
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // [pixel half of the matrix waves][2][64]
+  if (!pooler) {
+    float v[32];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      v[r] = cs[r];
+      v[16 + r] = cq[r];
     }
-    f32x16 acc[2][1];
-    conv_tile<F2_TR, F2_TC, 1>(wl, lb0 + cur * F2_LB, 32 * wave, lane, acc);
-    // y1 (bf16) -> yt[m][co]: 4 consecutive channels per 8-B store
-    {
-      const int m = 32 * wave + r32;
-      const int swz = (m >> 1) & 7;
+    const float tot = rs32(v, r32);
+    const int which = r32 >> 4, r = r32 & 15;
+    const int co = 32 * a + 8 * (r >> 2) + 4 * h + (r & 3);
+    const bool neg = which == 0 && gamma1 && gamma1[co] < 0.f;  // sums of y1 * sign(gamma1)
+    red[((mw >> 1) * 2 + which) * SC + co] = neg ? -tot : tot;
+  }
+  __syncthreads();
+  if (part && tid < 2 * SC) part[(long long)blockIdx.x * 2 * SC + tid] = red[tid] + red[2 * SC + tid];
+}
+
+// p = relu(a1 ya + s1) (bf16, as the pool's output) and BN-2 partial sums of
+// the rounded p: part[block][2][64].
+__global__ __launch_bounds__(256) void stem_pool_relu_kernel(const uint16_t* __restrict__ ya,
+                                                             const float* __restrict__ coef,
+                                                             uint16_t* __restrict__ p,
+                                                             float* __restrict__ part,
+                                                             long long P2) {
+  const int cg = threadIdx.x & 7;
+  float a[8], sh[8];
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+  for (int k = 0; k < 8; ++k) {
+    a[k] = coef[cg * 8 + k];
+    sh[k] = coef[SC + cg * 8 + k];
+  }
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (long long o = blockIdx.x * 32LL + (threadIdx.x >> 3); o < P2; o += gridDim.x * 32LL) {
+    const long long off = o * SC + cg * 8;
+    float yv[8], pv[8];
+    unpack8(*reinterpret_cast<const uint4*>(ya + off), yv);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int chunk = 4 * a + q;
-          const uint2 v = make_uint2(zk::pack_bf16x2(acc[a][0][4 * q], acc[a][0][4 * q + 1]),
-                                     zk::pack_bf16x2(acc[a][0][4 * q + 2], acc[a][0][4 * q + 3]));
-          *reinterpret_cast<uint2*>(yt + m * 128 + ((chunk ^ swz) << 4) + 8 * h) = v;
-        }
-    }
-    lds_barrier();
-    // pool: one (pool output, channel group) per thread, branch-free
-    {
-      const int hr0 = 2 * oh0 - g.pt2, wc0 = 2 * ow0 - g.pl2;  // conv coords of region (0, 0)
-      const int i = pitem ? pi : 0, j = pitem ? pj : 0;
-      const int oh = oh0 + i, ow = ow0 + j;
-      const bool live = pitem && oh < g.H2 && ow < g.W2;
-      // relu(a y + s) is monotone in y (increasing for a >= 0, else
-      // decreasing), so the first maximum of the window is the first maximum
-      // of y ^ sign(a) (a sign flip on the packed bf16); ties at relu's 0 do
-      // not matter (they route no gradient).  Out-of-image taps read -inf.
-      uint4 tv[9];
+    for (int k = 0; k < 8; ++k) pv[k] = fmaxf(fmaf(a[k], yv[k], sh[k]), 0.f);
+    const uint4 pk = pack8f(pv);
+    *reinterpret_cast<uint4*>(p + off) = pk;
+    float st[8];
+    unpack8(pk, st);
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int m = (2 * i + t / 3) * F2_TC + 2 * j + t % 3;
-        tv[t] = *reinterpret_cast<const uint4*>(yt + m * 128 + ((cg ^ ((m >> 1) & 7)) << 4));
-      }
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {  // y -> y * sign(a) on the packed bf16
-        tv[t].x ^= flip.x;
-        tv[t].y ^= flip.y;
-        tv[t].z ^= flip.z;
-        tv[t].w ^= flip.w;
-      }
-      const bool interior = hr0 + 2 * i >= 0 && hr0 + 2 * i + 2 < g.Ho && wc0 + 2 * j >= 0 &&
-                            wc0 + 2 * j + 2 < g.Wo;
-      if (!interior) {
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const int hc = hr0 + 2 * i + t / 3, wc = wc0 + 2 * j + t % 3;
-          if (!(hc >= 0 && hc < g.Ho && wc >= 0 && wc < g.Wo))
-            tv[t] = make_uint4(0xFF80FF80u, 0xFF80FF80u, 0xFF80FF80u, 0xFF80FF80u);  // -inf
-        }
-      }
-      float best[8], yb[8];
-      uint32_t bi[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) bi[k] = 0;
-      unpack8(tv[0], best);
-#pragma unroll
-      for (int t = 1; t < 9; ++t) {
-        float v[8];
-        unpack8(tv[t], v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const bool gt = v[k] > best[k];
-          best[k] = gt ? v[k] : best[k];
-          bi[k] = gt ? (uint32_t)t : bi[k];
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        yb[k] = best[k] * sg[k];
-        best[k] = fmaxf(fmaf(a1[k], yb[k], s1[k]), 0.f);
-      }
-      const uint4 pk = pack8f(best);
-      const long long off = (((long long)b * g.H2 + oh) * g.W2 + ow) * SC + cg * 8;
-      uint4* dp_ = live ? reinterpret_cast<uint4*>(p + off) : &g_pool_sink[0];
-      uint4* dy_ = live ? reinterpret_cast<uint4*>(ya + off) : &g_pool_sink[1];
-      uint2* da_ = live ? reinterpret_cast<uint2*>(arg + off) : reinterpret_cast<uint2*>(&g_pool_sink[0]);
-      *dp_ = pk;
-      *dy_ = pack8f(yb);
-      *da_ = make_uint2(bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
-                        bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
-      float st[8];
-      unpack8(pk, st);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float v = live ? st[k] : 0.f;
-        bs1[k] += v;
-        bs2[k] += v * v;
-      }
+    for (int k = 0; k < 8; ++k) {
+      s1[k] += st[k];
+      s2[k] = fmaf(st[k], st[k], s2[k]);
     }
   }
   if (!part) return;
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);  // [512][2][8]
+  __shared__ float red[2][256][9];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    red[(tid * 2 + 0) * 8 + k] = bs1[k];
-    red[(tid * 2 + 1) * 8 + k] = bs2[k];
+    red[0][threadIdx.x][k] = s1[k];
+    red[1][threadIdx.x][k] = s2[k];
   }
   __syncthreads();
-  if (tid < 2 * SC) {
-    const int which = tid / SC, c = tid % SC, g8 = c >> 3, k = c & 7;
+  if (threadIdx.x < 2 * SC) {
+    const int which = threadIdx.x / SC, ch = threadIdx.x % SC, gq = ch >> 3, k = ch & 7;
     float t = 0.f;
-    for (int r = g8; r < F2_NT; r += 8) t += red[(r * 2 + which) * 8 + k];
-    part[((long long)blockIdx.x * 2 + which) * SC + c] = t;
+    for (int r = gq; r < 256; r += 8) t += red[which][r][k];
+    part[((long long)blockIdx.x * 2 + which) * SC + ch] = t;
   }
 }
 
@@ -543,10 +584,34 @@ constexpr int RT_DP = RT_N * 128;                    // dp rows (64 bf16)
 constexpr int RT_CHUNKS = RT_N * (128 + 64) / 16;    // + arg rows (64 B)
 constexpr int B2_RT = (RT_CHUNKS + 63) / 64 * 64 * 16;
 constexpr int B2_YT = 128 * 128;
-constexpr int B2_CF = 5 * SC * 4;
-constexpr int B2_LDS = W_BYTES + 2 * B2_LB + 2 * B2_RT + B2_YT + B2_CF;
-static_assert(B2_LDS <= 80 * 1024, "two B2 blocks per CU");
 constexpr int B2_NSLAB = SC * SKH * 32;  // dW partial per block [co][kh*32 + j]
+
+// B2's y1 / dy1 image yt [128 pixels][64 channels]: 16-B slot s of row r at
+// s ^ b2_swz(r).  b2_swz is a bijection of r mod 8 (the ds_write_b128 stores
+// of 8 consecutive pixels are conflict free) whose bit 2 differs between rows
+// r and r + 2 for r = 0, 1 (mod 4) (the transposed reads of rows r .. r + 3
+// fall in disjoint slot blocks per 128-B bank half).
+__device__ __forceinline__ int b2_swz(int r) { return ((((r >> 1) ^ (r >> 2)) & 1) << 2) | (r & 3); }
+__device__ __forceinline__ int b2_off(int r, int slot) { return r * 128 + ((slot ^ b2_swz(r)) << 4); }
+
+// 32x32x16 operand (8 consecutive pixels k of channel column c0 + ..) from yt
+// (as tr_frag_swz, with b2_swz)
+__device__ __forceinline__ uint4 tr_frag_b2(const unsigned char* yt, int k0, int c0, int lane) {
+  const int gq = lane >> 4, i = lane & 15;
+  const int q = i >> 2, p = i & 3;
+  const int row = k0 + 8 * (gq >> 1) + q;
+  const int colb = (c0 + 16 * (gq & 1) + 4 * p) * 2;
+  const int slot = colb >> 4, inner = colb & 15;
+  const int o0 = b2_off(row, slot) + inner, o1 = b2_off(row + 4, slot) + inner;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(uintptr_t)(const __attribute__((
+          address_space(3))) void*)(yt + o0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(uintptr_t)(const __attribute__((
+          address_space(3))) void*)(yt + o1));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(uint4, v);
+}
 
 // routing stage of the tile at (b, r0, c0): pool outputs (ohb + i, owb + j)
 template <int NT>
@@ -601,194 +666,280 @@ __device__ __forceinline__ uint4 tr_frag_lb(const unsigned char* lb, int k0, int
   return __builtin_bit_cast(uint4, v);
 }
 
-__global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
+// B2 runs as a two-role software pipeline, one 512-thread block per CU:
+// waves 0-3 ("route" waves, VALU) compute dy1 of tile j (phase b) and issue
+// every LDS-DMA, while waves 4-7 ("matrix" waves, MFMA) run the conv of tile
+// j + 1 (phase a) and the weight gradient of tile j - 1 (phase c) in the same
+// barrier interval.  The CU issues wave w and wave w + 4 on one SIMD, so each
+// SIMD pairs a VALU stream with an MFMA stream (MI355X_MICROARCH.md: the two
+// pipes run concurrently) instead of alternating the phases in every wave.
+// Rings: line buffers 5 (issued two intervals ahead, read by phases a and c),
+// routing stages 3, y1 / dy1 images 3.  One barrier per interval.
+constexpr int B3_NLB = 5, B3_NRT = 3, B3_NYT = 3;
+constexpr int B3_LDS = B3_NLB * B2_LB + B3_NRT * B2_RT + B3_NYT * B2_YT;
+static_assert(B3_LDS <= 160 * 1024, "B2 pipeline LDS");
+
+// LDS-DMA instructions issue_route<NT> issues in wave `wave`
+template <int NT>
+__device__ __forceinline__ int route_count(int wave) {
+  int n = 0;
+  for (int j = 0; j < (RT_CHUNKS + NT - 1) / NT; ++j) n += j * NT + wave * 64 < RT_CHUNKS;
+  return n;
+}
+
+template <int PT2, int PL2>
+__global__ __launch_bounds__(512, 2) void stem_bwd_fused_kernel(
     const unsigned char* __restrict__ xp, const unsigned char* __restrict__ ws,
     const uint16_t* __restrict__ dp, const uint8_t* __restrict__ arg,
     const float* __restrict__ coef1, const float* __restrict__ bcoef1, float* __restrict__ slab,
     FGeom g, int tiles_w, int tiles_img, int ntiles) {
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
-  unsigned char* wl = smem;
-  unsigned char* lbuf0 = smem + W_BYTES;
-  unsigned char* rtb0 = smem + W_BYTES + 2 * B2_LB;
-  unsigned char* yt = smem + W_BYTES + 2 * B2_LB + 2 * B2_RT;
-  float* cf = reinterpret_cast<float*>(yt + B2_YT);  // [5][64]: a1, s1, k1, k0, k3
+  unsigned char* lbr = smem;                                   // [5][B2_LB]
+  unsigned char* rtr = lbr + B3_NLB * B2_LB;                   // [3][B2_RT]
+  unsigned char* ytr = rtr + B3_NRT * B2_RT;                   // [3][B2_YT]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r32 = lane & 31, h = lane >> 5;
   const int blk = xcd_linear(blockIdx.x, gridDim.x), nblk = gridDim.x;
+  const int n = blk < ntiles ? (ntiles - 1 - blk) / nblk + 1 : 0;  // this block's tiles
+  const bool route = wave < 4;
 
-  auto tile_pos = [&](int T, int& b, int& r0, int& c0) {
+  auto tile_pos = [&](int j, int& b, int& r0, int& c0) {
+    const int T = blk + j * nblk;
     b = T / tiles_img;
     const int rem = T - b * tiles_img;
     const int th = rem / tiles_w;
     r0 = th * B2_TR;
     c0 = (rem - th * tiles_w) * B2_TC;
   };
-  if (blk < ntiles) {
+  auto issue_lb = [&](int j) {
     int b, r0, c0;
-    tile_pos(blk, b, r0, c0);
-    issue_lbuf<B2_TR, B2_TC, 256>(lbuf0, xp, g, b, r0, c0, tid);
-    issue_route<256>(rtb0, dp, arg, g, b, r0, c0, tid);
-  }
-  load_weights<256>(wl, ws, tid);
-  for (int i = tid; i < 5 * SC; i += 256)
-    cf[i] = i < 2 * SC ? coef1[i] : bcoef1[i - 2 * SC];
-
-  // phase c: wave w owns kernel rows 2w, 2w+1 (wave 3: row 6) for all 64
-  // channels and all 128 pixels of the tile
-  const int kh0 = 2 * wave, nkh = wave < 3 ? 2 : 1;
-  f32x16 accw[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) accw[a][j][r] = 0.f;
-
-  // phase-b thread roles
-  const int cell = tid >> 3, cgp = tid & 7;
-  const int cr = cell >> 3, cc = cell & 7;
-
-  int it = 0;
-  for (int T = blk; T < ntiles; T += nblk, ++it) {
-    const int cur = it & 1;
-    tile_barrier();
+    tile_pos(j, b, r0, c0);
+    issue_lbuf<B2_TR, B2_TC, 256>(lbr + (j % B3_NLB) * B2_LB, xp, g, b, r0, c0, tid);
+  };
+  auto issue_rt = [&](int j) {
     int b, r0, c0;
-    tile_pos(T, b, r0, c0);
-    if (T + nblk < ntiles) {
-      int bn, rn, cn;
-      tile_pos(T + nblk, bn, rn, cn);
-      issue_lbuf<B2_TR, B2_TC, 256>(lbuf0 + (cur ^ 1) * B2_LB, xp, g, bn, rn, cn, tid);
-      issue_route<256>(rtb0 + (cur ^ 1) * B2_RT, dp, arg, g, bn, rn, cn, tid);
+    tile_pos(j, b, r0, c0);
+    issue_route<256>(rtr + (j % B3_NRT) * B2_RT, dp, arg, g, b, r0, c0, tid);
+  };
+
+  // matrix-wave indices (used after the loops too)
+  const int mw = wave & 3, ma = mw & 1, mg0 = 2 * (mw >> 1);
+  const int wa = mw >> 1, kb = 4 * (mw & 1);
+  f32x16 accw[4];
+  if (route) {
+    // ---- route waves: stride cell (cr, cc), channels 8 cgp ..; BN-backward
+    // coefficients in registers (k3 negated)
+    const int cell = tid >> 3, cgp = tid & 7;
+    const int cr = cell >> 3, cc = cell & 7;
+    float ca[8], cs[8], k1[8], k0[8], k3[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = cgp * 8 + k;
+      ca[k] = coef1[c];
+      cs[k] = coef1[SC + c];
+      k1[k] = bcoef1[c];
+      k0[k] = bcoef1[SC + c];
+      k3[k] = -bcoef1[2 * SC + c];
     }
-    // ---- a) conv -> yt
-    {
-      f32x16 acc[2][1];
-      conv_tile<B2_TR, B2_TC, 1>(wl, lbuf0 + cur * B2_LB, 32 * wave, lane, acc);
-      const int m = 32 * wave + r32;
-      const int swz = tr_swz<128>(m);
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int chunk = 4 * a + q;
-          const uint2 v = make_uint2(zk::pack_bf16x2(acc[a][0][4 * q], acc[a][0][4 * q + 1]),
-                                     zk::pack_bf16x2(acc[a][0][4 * q + 2], acc[a][0][4 * q + 3]));
-          *reinterpret_cast<uint2*>(yt + m * 128 + ((chunk ^ swz) << 4) + 8 * h) = v;
-        }
-    }
-    lds_barrier();
-    // ---- b) dy1 in place
-    {
-      const unsigned char* rt = rtb0 + cur * B2_RT;
-      const int ohb = r0 / 2 - 1 + g.pt2, owb = c0 / 2 - 1 + g.pl2;
-      uint32_t aw[2][2][2];
-      uint4 gq[2][2];  // dp of the candidates, packed bf16
-      bool cv[2][2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int o = (cr + i) * RT_OW + cc + j;
-          const int oh = ohb + cr + i, ow = owb + cc + j;
-          cv[i][j] = oh >= 0 && oh < g.H2 && ow >= 0 && ow < g.W2;
-          const uint2 av = *reinterpret_cast<const uint2*>(rt + RT_DP + o * 64 + cgp * 8);
-          aw[i][j][0] = av.x;
-          aw[i][j][1] = av.y;
-          gq[i][j] = *reinterpret_cast<const uint4*>(rt + o * 128 + cgp * 16);
-        }
-      // the four pixels' y1 and the channel coefficients, loads up front
-      uint4 yq[4];
-#pragma unroll
-      for (int pq = 0; pq < 4; ++pq) {
-        const int m = (2 * cr + (pq >> 1)) * B2_TC + 2 * cc + (pq & 1);
-        yq[pq] = *reinterpret_cast<const uint4*>(yt + m * 128 + ((cgp ^ tr_swz<128>(m)) << 4));
+    if (n > 0) issue_lb(0);
+    if (n > 1) issue_lb(1);
+    if (n > 0) issue_rt(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int n_lb = lines_count<LBuf<B2_TR, B2_TC>, 256>(wave);
+    const int n_rt = route_count<256>(wave);
+    for (int i = 0; i < n + 2; ++i) {
+      // DMA two intervals ahead for the conv, one for the routing stage
+      int issued = 0;
+      if (i + 2 < n) {
+        issue_lb(i + 2);
+        issued += n_lb;
       }
-      const float4* c4 = reinterpret_cast<const float4*>(cf + cgp * 8);
-      float ca[8], cs[8], k1[8], k0[8], k3[8];
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const float4 v0 = c4[hf], v1 = c4[SC / 4 + hf], v2 = c4[2 * SC / 4 + hf],
-                     v3 = c4[3 * SC / 4 + hf], v4 = c4[4 * SC / 4 + hf];
-        ca[4 * hf] = v0.x; ca[4 * hf + 1] = v0.y; ca[4 * hf + 2] = v0.z; ca[4 * hf + 3] = v0.w;
-        cs[4 * hf] = v1.x; cs[4 * hf + 1] = v1.y; cs[4 * hf + 2] = v1.z; cs[4 * hf + 3] = v1.w;
-        k1[4 * hf] = v2.x; k1[4 * hf + 1] = v2.y; k1[4 * hf + 2] = v2.z; k1[4 * hf + 3] = v2.w;
-        k0[4 * hf] = v3.x; k0[4 * hf + 1] = v3.y; k0[4 * hf + 2] = v3.z; k0[4 * hf + 3] = v3.w;
-        k3[4 * hf] = v4.x; k3[4 * hf + 1] = v4.y; k3[4 * hf + 2] = v4.z; k3[4 * hf + 3] = v4.w;
+      if (i + 1 < n) {
+        issue_rt(i + 1);
+        issued += n_rt;
       }
-      float gv[2][2][8];
+      // ---- b) dy1 of tile i - 1 in place: du = sum of dp over the candidate
+      // pool outputs whose argmax tap is the pixel; with the pool padding
+      // (PT2, PL2) static, the candidates of each of the cell's 4 pixels and
+      // their taps are compile-time (9 tests per cell).  Candidates outside
+      // the image read the zero page: dp 0 adds nothing whatever the tap.
+      if (i >= 1 && i <= n) {
+        const int j = i - 1;
+        int b, r0, c0;
+        tile_pos(j, b, r0, c0);
+        const unsigned char* rt = rtr + (j % B3_NRT) * B2_RT;
+        unsigned char* yt = ytr + (j % B3_NYT) * B2_YT;
+        uint32_t aw[2][2][2];
+        uint4 gq[2][2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) unpack8(gq[i][j], gv[i][j]);
+          for (int jj = 0; jj < 2; ++jj) {
+            const int o = (cr + ii) * RT_OW + cc + jj;
+            const uint2 av = *reinterpret_cast<const uint2*>(rt + RT_DP + o * 64 + cgp * 8);
+            aw[ii][jj][0] = av.x;
+            aw[ii][jj][1] = av.y;
+            gq[ii][jj] = *reinterpret_cast<const uint4*>(rt + o * 128 + cgp * 16);
+          }
+        uint4 yq[4];
 #pragma unroll
-      for (int pq = 0; pq < 4; ++pq) {
-        const int dy = pq >> 1, dx = pq & 1;
-        const int hh = r0 + 2 * cr + dy, ww = c0 + 2 * cc + dx;
-        float du[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int pq = 0; pq < 4; ++pq) {
+          const int m = (2 * cr + (pq >> 1)) * B2_TC + 2 * cc + (pq & 1);
+          yq[pq] = *reinterpret_cast<const uint4*>(yt + b2_off(m, cgp));
+        }
+        const bool interior = r0 + B2_TR <= g.Ho && c0 + B2_TC <= g.Wo;  // uniform
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int pq = 0; pq < 4; ++pq) {
+          const int dy = pq >> 1, dx = pq & 1;
+          float du[8];
+          bool any = false;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            // tap of this pixel in the window of pool output (ohb+cr+i, owb+cc+j);
-            // the range test is uniform (pt2, pl2), the candidate's validity not
-            const int th = dy + 2 - g.pt2 - 2 * i, tw = dx + 2 - g.pl2 - 2 * j;
-            if (th < 0 || th > 2 || tw < 0 || tw > 2) continue;
-            const uint32_t t = th * 3 + tw;
-            const uint32_t tm = cv[i][j] ? t : 0xFFu;  // 0xFF never matches a tap
+          for (int ii = 0; ii < 2; ++ii) {
+            const int th = dy + 2 - PT2 - 2 * ii;
+            if (th < 0 || th > 2) continue;  // compile-time
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const bool hit = ((aw[i][j][k >> 2] >> (8 * (k & 3))) & 0xff) == tm;
-              du[k] += hit ? gv[i][j][k] : 0.f;
+            for (int jj = 0; jj < 2; ++jj) {
+              const int tw = dx + 2 - PL2 - 2 * jj;
+              if (tw < 0 || tw > 2) continue;  // compile-time
+              const uint32_t t = th * 3 + tw;
+              const uint32_t gw[4] = {gq[ii][jj].x, gq[ii][jj].y, gq[ii][jj].z, gq[ii][jj].w};
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const bool hit = ((aw[ii][jj][k >> 2] >> (8 * (k & 3))) & 0xffu) == t;
+                const uint32_t wv = gw[k >> 1];
+                const float gv = __uint_as_float((k & 1) ? (wv & 0xFFFF0000u) : (wv << 16));
+                const float add = hit ? gv : 0.f;
+                du[k] = any ? du[k] + add : add;
+              }
+              any = true;
             }
           }
-        const int m = (2 * cr + dy) * B2_TC + 2 * cc + dx;
-        float yv[8], o8[8];
-        unpack8(yq[pq], yv);
-        const bool live = hh < g.Ho && ww < g.Wo;
+          float yv[8], o8[8];
+          unpack8(yq[pq], yv);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float u = fmaf(ca[k], yv[k], cs[k]);
-          const float v = k1[k] * (u > 0.f ? du[k] : 0.f) + k0[k] - k3[k] * yv[k];
-          o8[k] = live ? v : 0.f;
+          for (int k = 0; k < 8; ++k) {
+            const float u = fmaf(ca[k], yv[k], cs[k]);
+            o8[k] = fmaf(k1[k], u > 0.f ? du[k] : 0.f, fmaf(k3[k], yv[k], k0[k]));
+          }
+          if (!interior) {
+            const bool live = r0 + 2 * cr + dy < g.Ho && c0 + 2 * cc + dx < g.Wo;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o8[k] = live ? o8[k] : 0.f;
+          }
+          const int m = (2 * cr + dy) * B2_TC + 2 * cc + dx;
+          *reinterpret_cast<uint4*>(yt + b2_off(m, cgp)) = pack8f(o8);
         }
-        *reinterpret_cast<uint4*>(yt + m * 128 + ((cgp ^ tr_swz<128>(m)) << 4)) = pack8f(o8);
       }
+      // the previous interval's DMAs (line buffer i + 1, routing stage i) landed
+      wait_vmcnt_dyn(issued);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // dy1 stores done
+      __builtin_amdgcn_s_barrier();
     }
-    lds_barrier();
-    // ---- c) weight gradient
-    {
-      const unsigned char* lbc = lbuf0 + cur * B2_LB;
-#pragma unroll 2
-      for (int s = 0; s < 8; ++s) {
-        const int k0 = 16 * s;
-        uint4 af[2];
+  } else {
+    // ---- matrix waves: mw computes the conv of channel half ma for pixel
+    // groups mg0, mg0 + 1 with its 32 x 224 weights in VGPRs, and the phase-c
+    // units (wa, rows kb .. kb + 2 all steps; row 3 on steps kb .. kb + 3)
+    uint4 w[SKH][2];
 #pragma unroll
-        for (int a = 0; a < 2; ++a) af[a] = tr_frag_swz<128>(yt, k0, 32 * a, lane);
+    for (int kh = 0; kh < SKH; ++kh)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          if (j < nkh) {  // wave-uniform
-            const uint4 bfr = tr_frag_lb(lbc, k0, kh0 + j, lane);
+      for (int sub = 0; sub < 2; ++sub)
+        w[kh][sub] = *reinterpret_cast<const uint4*>(ws + (kh * SC + 32 * ma + r32) * 64 +
+                                                     (2 * sub + h) * 16);
 #pragma unroll
-            for (int a = 0; a < 2; ++a) accw[a][j] = mfma_bf16(af[a], bfr, accw[a][j]);
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) accw[e][r] = 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int i = 0; i < n + 2; ++i) {
+      // ---- a) conv of tile i -> its y1 image
+      if (i < n) {
+        const unsigned char* lbc = lbr + (i % B3_NLB) * B2_LB;
+        unsigned char* yt = ytr + (i % B3_NYT) * B2_YT;
+        using L = LBuf<B2_TR, B2_TC>;
+        int segb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int px = 32 * (mg0 + u) + r32;  // tile pixel: row px / 16, column px % 16
+          segb[u] = 2 * (px / B2_TC) * L::RB + 16 * (px % B2_TC) + 16 * h;
+        }
+        f32x16 acc[2];
+#pragma unroll
+        for (int kh = 0; kh < SKH; ++kh)
+#pragma unroll
+          for (int sub = 0; sub < 2; ++sub) {
+            uint4 bf[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+              bf[u] = *reinterpret_cast<const uint4*>(lbc + segb[u] + kh * L::RB + 32 * sub);
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+              acc[u] = mfma_bf16(w[kh][sub], bf[u], kh + sub ? acc[u] : f32x16{});
+          }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int m = 32 * (mg0 + u) + r32;
+#pragma unroll
+          for (int pq = 0; pq < 2; ++pq) {
+            uint32_t d[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = 4 * (2 * pq + (e >> 1)) + 2 * (e & 1);
+              d[e] = zk::pack_bf16x2(acc[u][r], acc[u][r + 1]);
+            }
+            const auto s0 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+            const auto s1 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+            *reinterpret_cast<uint4*>(yt + b2_off(m, 4 * ma + 2 * pq + h)) =
+                make_uint4(s0[0], s1[0], s0[1], s1[1]);
           }
         }
       }
+      // ---- c) weight gradient of tile i - 2, 28 MFMAs per wave
+      if (i >= 2) {
+        const int j = i - 2;
+        const unsigned char* lbc = lbr + (j % B3_NLB) * B2_LB;
+        const unsigned char* yt = ytr + (j % B3_NYT) * B2_YT;
+#pragma unroll 2
+        for (int s = 0; s < 8; ++s) {
+          const int k0s = 16 * s;
+          const uint4 af = tr_frag_b2(yt, k0s, 32 * wa, lane);
+#pragma unroll
+          for (int e = 0; e < 3; ++e)
+            accw[e] = mfma_bf16(af, tr_frag_lb(lbc, k0s, kb + e, lane), accw[e]);
+          if ((s >> 2) == (kb >> 2))  // wave-uniform: this wave's half of kernel row 3
+            accw[3] = mfma_bf16(af, tr_frag_lb(lbc, k0s, 3, lane), accw[3]);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // y1 stores done
+      __builtin_amdgcn_s_barrier();
     }
   }
 
-  // one plain-stored dW partial per block: slab[block][co][kh*32 + j]
-  float* sl = slab + (long long)blockIdx.x * B2_NSLAB;
-  constexpr int NR = SKH * 32;
+  // one plain-stored dW partial per block: slab[block][co][kh*32 + j]; the
+  // row-3 halves of waves (2wa, 2wa+1) meet in LDS first
+  __syncthreads();
+  float* cmb = reinterpret_cast<float*>(smem);  // [2 wa][16 r][64 lanes]
+  if (!route && kb) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    if (j >= nkh) continue;
+    for (int r = 0; r < 16; ++r) cmb[(wa * 16 + r) * 64 + lane] = accw[3][r];
+  }
+  __syncthreads();
+  if (!route && !kb) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int r = 0; r < 16; ++r) accw[3][r] += cmb[(wa * 16 + r) * 64 + lane];
+  }
+  if (!route) {
+    float* sl = slab + (long long)blockIdx.x * B2_NSLAB;
+    constexpr int NR = SKH * 32;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = 32 * a + 8 * (r >> 2) + 4 * h + (r & 3);
-        sl[co * NR + (kh0 + j) * 32 + r32] = accw[a][j][r];
-      }
+    for (int r = 0; r < 16; ++r) {
+      const int co = 32 * wa + 8 * (r >> 2) + 4 * h + (r & 3);
+#pragma unroll
+      for (int e = 0; e < 3; ++e) sl[co * NR + (kb + e) * 32 + r32] = accw[e][r];
+      if (!kb) sl[co * NR + 3 * 32 + r32] = accw[3][r];
+    }
   }
 }
 
@@ -868,6 +1019,62 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_sums_ya_kernel(
   }
 }
 
+// BN-2 backward dx and B1 in one pass: dp = bf16(k1 g + k0 - k3 p) (as
+// norm_pool.hip's bn_bwd_dx_bf16), then du = dp [a1 ya + s1 > 0] and the
+// BN-1 sums of du and du (ya - mean1) rstd1 of that rounded dp.  Saves B1's
+// re-read of dp.  bcoef2 [3][64]; coef1 [4][64]; part[block][2][64].
+__global__ __launch_bounds__(256) void stem_bn2_bwd_sums_kernel(
+    const uint16_t* __restrict__ g, const uint16_t* __restrict__ p,
+    const uint16_t* __restrict__ ya, const float* __restrict__ bcoef2,
+    const float* __restrict__ coef, uint16_t* __restrict__ dp, float* __restrict__ part,
+    long long P2) {
+  const int cg = threadIdx.x & 7;
+  float k1[8], k0[8], k3[8], a[8], sh[8], mean[8], rstd[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = cg * 8 + k;
+    k1[k] = bcoef2[c];
+    k0[k] = bcoef2[SC + c];
+    k3[k] = bcoef2[2 * SC + c];
+    a[k] = coef[c];
+    sh[k] = coef[SC + c];
+    mean[k] = coef[2 * SC + c];
+    rstd[k] = coef[3 * SC + c];
+  }
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (long long o = blockIdx.x * 32LL + (threadIdx.x >> 3); o < P2; o += gridDim.x * 32LL) {
+    const long long off = o * SC + cg * 8;
+    float gv[8], pv[8], yv[8], dv[8];
+    unpack8(*reinterpret_cast<const uint4*>(g + off), gv);
+    unpack8(*reinterpret_cast<const uint4*>(p + off), pv);
+    unpack8(*reinterpret_cast<const uint4*>(ya + off), yv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dv[k] = k1[k] * gv[k] + k0[k] - k3[k] * pv[k];
+    const uint4 dq = pack8f(dv);
+    *reinterpret_cast<uint4*>(dp + off) = dq;
+    unpack8(dq, dv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float du = fmaf(a[k], yv[k], sh[k]) > 0.f ? dv[k] : 0.f;
+      s1[k] += du;
+      s2[k] += du * (yv[k] - mean[k]) * rstd[k];
+    }
+  }
+  __shared__ float red[2][256][9];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[0][threadIdx.x][k] = s1[k];
+    red[1][threadIdx.x][k] = s2[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * SC) {
+    const int which = threadIdx.x / SC, ch = threadIdx.x % SC, gq = ch >> 3, k = ch & 7;
+    float t = 0.f;
+    for (int r = gq; r < 256; r += 8) t += red[which][r][k];
+    part[((long long)blockIdx.x * 2 + which) * SC + ch] = t;
+  }
+}
+
 int g_cus = 0;
 int cu_count() {
   if (!g_cus) {
@@ -910,52 +1117,49 @@ int grid_for(long long ntiles, int per_cu) {
 // Number of per-block partial rows / slabs a pass writes (host-side sizing).
 ZK_EXPORT int zk_stem_fused_blocks(int which, int B, int Ho, int Wo, int H2, int W2) {
   long long nt;
-  if (which == 1) {  // F2: pool tiles, one block per CU
-    nt = (long long)B * ((H2 + F2_PR - 1) / F2_PR) * ((W2 + F2_PC - 1) / F2_PC);
+  if (which == 1) {  // F: pool tiles, one pipelined block per CU
+    nt = (long long)B * ((H2 + F_PR - 1) / F_PR) * ((W2 + F_PC - 1) / F_PC);
     return grid_for(nt, 1);
   }
-  nt = (long long)B * ((Ho + 7) / 8) * ((Wo + 15) / 16);  // F1 / B2: conv tiles
-  return grid_for(nt, 2);
+  nt = (long long)B * ((Ho + 7) / 8) * ((Wo + 15) / 16);  // B2: conv tiles, one block per CU
+  return grid_for(nt, 1);
 }
 
 ZK_EXPORT int zk_stem_fused_slab_floats() { return B2_NSLAB; }
 // extra slab rows zk_stem_bwd_fused needs beyond one per block (reduction groups)
 ZK_EXPORT int zk_stem_fused_slab_extra() { return B2_GROUPS; }
 
-ZK_EXPORT int zk_stem_fwd_stats(const void* xp, const void* ws, void* part, int B, int Cin,
-                                int KW, int Ho, int Wo, int Hp, int Wp, int H2, int W2, int pt2,
-                                int pl2, int* nparts, hipStream_t st) {
+// gamma1: BN-1 scale (nullptr: none, all directions +); part: [blocks][2][64]
+// BN-1 partial sums or nullptr; ya (bf16) / arg (u8): [B][H2][W2][64].
+ZK_EXPORT int zk_stem_fwd_fused(const void* xp, const void* ws, const void* gamma1, void* ya,
+                                void* arg, void* part, int B, int Cin, int KW, int Ho, int Wo,
+                                int Hp, int Wp, int H2, int W2, int pt2, int pl2, int* nparts,
+                                hipStream_t st) {
   FGeom g{B, Cin, KW, Ho, Wo, Hp, Wp, H2, W2, pt2, pl2};
   if (!fgeom_ok(g)) return (int)hipErrorInvalidValue;
-  const int tw = (Wo + F1_TC - 1) / F1_TC, th = (Ho + F1_TR - 1) / F1_TR;
-  const long long nt = (long long)B * th * tw;
-  if (nt >= (1LL << 31)) return (int)hipErrorInvalidValue;
-  const int grid = grid_for(nt, 2);
-  if (nparts) *nparts = grid;
-  if (int e = set_lds_once(stem_fwd_stats_kernel, F1_LDS)) return e;
-  hipLaunchKernelGGL(stem_fwd_stats_kernel, dim3(grid), dim3(256), F1_LDS, st,
-                     (const unsigned char*)xp, (const unsigned char*)ws, (float*)part, g, tw,
-                     th * tw, (int)nt);
-  ZK_CHECK_LAUNCH();
-  return 0;
-}
-
-ZK_EXPORT int zk_stem_fwd_pool(const void* xp, const void* ws, const void* coef1, void* p,
-                               void* arg, void* ya, void* part, int B, int Cin, int KW, int Ho,
-                               int Wo, int Hp, int Wp, int H2, int W2, int pt2, int pl2,
-                               int* nparts, hipStream_t st) {
-  FGeom g{B, Cin, KW, Ho, Wo, Hp, Wp, H2, W2, pt2, pl2};
-  if (!fgeom_ok(g)) return (int)hipErrorInvalidValue;
-  const int tw = (W2 + F2_PC - 1) / F2_PC, th = (H2 + F2_PR - 1) / F2_PR;
+  const int tw = (W2 + F_PC - 1) / F_PC, th = (H2 + F_PR - 1) / F_PR;
   const long long nt = (long long)B * th * tw;
   if (nt >= (1LL << 31)) return (int)hipErrorInvalidValue;
   const int grid = grid_for(nt, 1);
   if (nparts) *nparts = grid;
-  if (int e = set_lds_once(stem_fwd_pool_kernel, F2_LDS)) return e;
-  hipLaunchKernelGGL(stem_fwd_pool_kernel, dim3(grid), dim3(F2_NT), F2_LDS, st,
-                     (const unsigned char*)xp, (const unsigned char*)ws, (const float*)coef1,
-                     (uint16_t*)p, (uint8_t*)arg, (uint16_t*)ya, (float*)part, g, tw, th * tw,
-                     (int)nt);
+  if (int e = set_lds_once(stem_fwd_fused_kernel, F_LDS)) return e;
+  hipLaunchKernelGGL(stem_fwd_fused_kernel, dim3(grid), dim3(512), F_LDS, st,
+                     (const unsigned char*)xp, (const unsigned char*)ws, (const float*)gamma1,
+                     (uint16_t*)ya, (uint8_t*)arg, (float*)part, g, tw, th, (int)nt);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
+// p = relu(coef1[0] ya + coef1[1]) (bf16) over P2 x 64; part: [<= 4096][2][64]
+// BN-2 partial sums of p or nullptr.
+ZK_EXPORT int zk_stem_pool_relu(const void* ya, const void* coef1, void* p, void* part,
+                                long long P2, int* nparts, hipStream_t st) {
+  long long grid = (P2 + 31) / 32;
+  if (grid > 4096) grid = 4096;
+  if (grid < 1) grid = 1;
+  if (nparts) *nparts = (int)grid;
+  hipLaunchKernelGGL(stem_pool_relu_kernel, dim3((int)grid), dim3(256), 0, st,
+                     (const uint16_t*)ya, (const float*)coef1, (uint16_t*)p, (float*)part, P2);
   ZK_CHECK_LAUNCH();
   return 0;
 }
@@ -973,6 +1177,22 @@ ZK_EXPORT int zk_stem_pool_bwd_sums_ya(const void* dp, const void* ya, const voi
   return 0;
 }
 
+// dp = BN-2 backward of g (bcoef2 [3][64], p the BN-2 input) and the BN-1
+// partial sums of B1 (coef1 [4][64], ya) in one pass; part: [<= 4096][2][64].
+ZK_EXPORT int zk_stem_bn2_bwd_sums(const void* g, const void* p, const void* ya,
+                                   const void* bcoef2, const void* coef1, void* dp, void* part,
+                                   long long P2, int* nparts, hipStream_t st) {
+  long long grid = (P2 + 31) / 32;
+  if (grid > 4096) grid = 4096;
+  if (grid < 1) grid = 1;
+  if (nparts) *nparts = (int)grid;
+  hipLaunchKernelGGL(stem_bn2_bwd_sums_kernel, dim3((int)grid), dim3(256), 0, st,
+                     (const uint16_t*)g, (const uint16_t*)p, (const uint16_t*)ya,
+                     (const float*)bcoef2, (const float*)coef1, (uint16_t*)dp, (float*)part, P2);
+  ZK_CHECK_LAUNCH();
+  return 0;
+}
+
 // slab: [zk_stem_fused_blocks(0, ...) + zk_stem_fused_slab_extra()]
 // [zk_stem_fused_slab_floats()] fp32 scratch; dw: OHWI fp32 gradient,
 // accumulated.
@@ -985,9 +1205,19 @@ ZK_EXPORT int zk_stem_bwd_fused(const void* xp, const void* ws, const void* dp, 
   const int tw = (Wo + B2_TC - 1) / B2_TC, th = (Ho + B2_TR - 1) / B2_TR;
   const long long nt = (long long)B * th * tw;
   if (nt >= (1LL << 31)) return (int)hipErrorInvalidValue;
-  const int grid = grid_for(nt, 2);
-  if (int e = set_lds_once(stem_bwd_fused_kernel, B2_LDS)) return e;
-  hipLaunchKernelGGL(stem_bwd_fused_kernel, dim3(grid), dim3(256), B2_LDS, st,
+  const int grid = grid_for(nt, 1);  // one pipelined 512-thread block per CU
+  static bool lds_set = false;
+  if (!lds_set) {
+    for (const void* k : {(const void*)stem_bwd_fused_kernel<0, 0>, (const void*)stem_bwd_fused_kernel<0, 1>,
+                          (const void*)stem_bwd_fused_kernel<1, 0>, (const void*)stem_bwd_fused_kernel<1, 1>}) {
+      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, B3_LDS);
+      if (e != hipSuccess) return (int)e;
+    }
+    lds_set = true;
+  }
+  auto kern = g.pt2 ? (g.pl2 ? stem_bwd_fused_kernel<1, 1> : stem_bwd_fused_kernel<1, 0>)
+                    : (g.pl2 ? stem_bwd_fused_kernel<0, 1> : stem_bwd_fused_kernel<0, 0>);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), B3_LDS, st,
                      (const unsigned char*)xp, (const unsigned char*)ws, (const uint16_t*)dp,
                      (const uint8_t*)arg, (const float*)coef1, (const float*)bcoef1,
                      (float*)slab, g, tw, th * tw, (int)nt);

@@ -131,9 +131,10 @@ SIGNATURES = {
     "zk_stem_fused_blocks": (I32, [I32] * 6),
     "zk_stem_fused_slab_floats": (I32, []),
     "zk_stem_fused_slab_extra": (I32, []),
-    "zk_stem_fwd_stats": (I32, [P, P, P] + [I32] * 11 + [IP, P]),
-    "zk_stem_fwd_pool": (I32, [P] * 7 + [I32] * 11 + [IP, P]),
+    "zk_stem_fwd_fused": (I32, [P] * 6 + [I32] * 11 + [IP, P]),
+    "zk_stem_pool_relu": (I32, [P, P, P, P, I64, IP, P]),
     "zk_stem_pool_bwd_sums_ya": (I32, [P, P, P, P, I64, IP, P]),
+    "zk_stem_bn2_bwd_sums": (I32, [P] * 7 + [I64, IP, P]),
     "zk_stem_bwd_fused": (I32, [P] * 8 + [I32] * 11 + [P]),
     "zk_maxpool_fwd": (I32, [P, P, P] + [I32] * 11 + [P]),
     "zk_maxpool_bwd": (I32, [P, P, P] + [I32] * 10 + [P]),

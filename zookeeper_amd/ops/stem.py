@@ -6,13 +6,15 @@ a training step here when the stem runs as library conv + separate
 BN / ReLU / pool passes over the 112×112×64 activation.  The fused version:
 
 forward   pack (zero-padded 4-channel image, bf16 [KH][Cout][32] kernel) →
-          MFMA conv with BN-1 partial sums in the epilogue → BN-1 finalize →
-          BN-1 + ReLU + max-pool (+ argmax tap, BN-2 partial sums) in one
-          pass → BN-2 finalize → BN-2 apply;
-backward  BN-2 backward (bf16 kernels of ``norm_pool``) → BN-1 sums from
-          the pooled side (the pooled value is BN-1's output at the argmax
-          tap: no gather) → dense dy1 in one pass → MFMA weight gradient
-          straight into the flat gradient buffer.
+          (stem_fused.hip, the default) ONE conv pass that takes the BN-1
+          partial sums and max-pools y1 · sign(γ1) (argmax tap + y1 there:
+          BN-1 + ReLU is monotone in y1 in the direction of γ1) → BN-1
+          finalize → p = relu(BN-1(ya)) with BN-2 partial sums → BN-2
+          finalize → BN-2 apply (+ the first binary block's sign images);
+backward  BN-2 backward dx together with the BN-1 sums from the pooled side
+          (the pooled value is BN-1's output at the argmax tap: no gather) →
+          conv recomputed, dense dy1 routed in LDS, MFMA weight gradient
+          straight into the flat gradient buffer.  y1 and dy1 never exist.
 
 The image itself never needs a gradient; the op is only used when it does
 not (``x.requires_grad`` is False).
@@ -32,16 +34,14 @@ from zookeeper_amd.ops._native import (check, direct_grad, grad_ready, lib, slab
                                         stream_ptr, zeroed, zeroed_scratch)
 
 # The recompute-fused kernels of stem_fused.hip are the default
-# (``runtime.stem_fused=False`` selects the materialising kernels of stem.hip): they never write the
-# 112x112x64 conv output or its gradient, E18 at batch 1024 42.95k -> 44.6k
-# img/s.  Round 1 kept them opt-in for a run-to-run gradient difference seen
-# only with them; re-measured in round 2 (tools/grad_determinism.py, hw 64 /
-# batch 4 and hw 224 / batch 32, 6 repeats) the materialising stem shows the
-# same pattern: the fp32-atomic ordering noise of the BN-backward sums
-# (~1e-7) is amplified through the binary blocks, and the stem BN-1 gradient,
-# a near-total cancellation (|g| ~ 4e-3), changes by O(1) relative on some
-# repeats with either stem -- a property of the reductions, not of these
-# kernels (the stem alone is bit-reproducible, tools/one_stem.py --check).
+# (``runtime.stem_fused=False`` selects the materialising kernels of stem.hip):
+# they never write the 112x112x64 conv output or its gradient.  Round-2
+# measurements (tools/grad_determinism.py): the fp32-atomic ordering noise of
+# the BN-backward sums (~1e-7) is amplified through the binary blocks, and the
+# stem BN-1 scale gradient, a near-total cancellation (BN-2 re-normalises the
+# pooled BN-1 output), changes by O(1) relative on some repeats with either
+# stem -- a property of the reductions, not of these kernels (the stem alone
+# is bit-reproducible, tools/one_stem.py --check).
 
 
 def supported(x: torch.Tensor, conv, bn1, pool_k: int, pool_s: int) -> bool:
@@ -194,23 +194,23 @@ class _StemFn(torch.autograd.Function):
         nb2 = ctypes.c_int(0)
         y1 = ya = None
         if fused:
-            # conv recomputed in every pass: y1 never exists (stem_fused.hip)
-            if bn1.training:
-                part = torch.empty((L.zk_stem_fused_blocks(0, B, Ho, Wo, H2, W2), 2, Cout),
-                                   dtype=torch.float32, device=dev)
-                nb = ctypes.c_int(0)
-                check(L.zk_stem_fwd_stats(xp.data_ptr(), ws.data_ptr(), part.data_ptr(), *geo,
-                                          ctypes.byref(nb), st), "zk_stem_fwd_stats")
-                coef1 = finalize1(part, nb.value)
-            else:
-                coef1 = _bn_eval_coef(bn1, Cout, dev)
+            # one conv pass: BN-1 statistics and the pool of y1 * sign(gamma1)
+            # (the direction of relu(BN-1(y)) in y); p once BN-1 is finalised
+            # (stem_fused.hip F / P).  y1 never exists.
             ya = torch.empty_like(p)
-            part2 = torch.empty((L.zk_stem_fused_blocks(1, B, Ho, Wo, H2, W2), 2, Cout),
-                                dtype=torch.float32, device=dev) if want_part2 else None
-            check(L.zk_stem_fwd_pool(xp.data_ptr(), ws.data_ptr(), coef1.data_ptr(),
-                                     p.data_ptr(), arg.data_ptr(), ya.data_ptr(),
-                                     part2.data_ptr() if part2 is not None else None, *geo,
-                                     ctypes.byref(nb2), st), "zk_stem_fwd_pool")
+            part = (torch.empty((L.zk_stem_fused_blocks(1, B, Ho, Wo, H2, W2), 2, Cout),
+                                dtype=torch.float32, device=dev) if bn1.training else None)
+            nb = ctypes.c_int(0)
+            check(L.zk_stem_fwd_fused(xp.data_ptr(), ws.data_ptr(),
+                                      g1.data_ptr() if g1 is not None else None, ya.data_ptr(),
+                                      arg.data_ptr(), part.data_ptr() if part is not None else None,
+                                      *geo, ctypes.byref(nb), st), "zk_stem_fwd_fused")
+            coef1 = finalize1(part, nb.value) if bn1.training else _bn_eval_coef(bn1, Cout, dev)
+            part2 = torch.empty((L.zk_stem_max_pool_parts(), 2, Cout), dtype=torch.float32,
+                                device=dev) if want_part2 else None
+            check(L.zk_stem_pool_relu(ya.data_ptr(), coef1.data_ptr(), p.data_ptr(),
+                                      part2.data_ptr() if part2 is not None else None,
+                                      B * H2 * W2, ctypes.byref(nb2), st), "zk_stem_pool_relu")
         else:
             y1 = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=dev)
             part = torch.empty((L.zk_stem_max_parts(B, Ho, Wo), 2, Cout), dtype=torch.float32,
@@ -324,15 +324,27 @@ class _StemFn(torch.autograd.Function):
                       "zk_bn_bwd_reduce_bf16_parts")
                 bcoef2, dg2, db2 = _bn_bwd_coef(L, st, sums2, coef2, g2p, b2p, P2, Cout, dev,
                                                 stripes=nb2.value, stride=sums2.shape[2])
-            dp = torch.empty_like(g)
-            check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), p.data_ptr(), None, bcoef2.data_ptr(),
-                                      dp.data_ptr(), P2, Cout, st), "zk_bn_bwd_dx_bf16")
-        else:
-            dp = g
         part = torch.empty((L.zk_stem_max_pool_parts(), 2, Cout), dtype=torch.float32,
                            device=dev)
         nb = ctypes.c_int(0)
-        if ctx.fused:
+        b1_done = False
+        if ctx.has_bn2:
+            dp = torch.empty_like(g)
+            if ctx.fused:
+                # BN-2 dx and the BN-1 sums (B1) in one pass over g, p, ya
+                check(L.zk_stem_bn2_bwd_sums(g.data_ptr(), p.data_ptr(), y1.data_ptr(),
+                                             bcoef2.data_ptr(), coef1.data_ptr(), dp.data_ptr(),
+                                             part.data_ptr(), P2, ctypes.byref(nb), st),
+                      "zk_stem_bn2_bwd_sums")
+                b1_done = True
+            else:
+                check(L.zk_bn_bwd_dx_bf16(g.data_ptr(), p.data_ptr(), None, bcoef2.data_ptr(),
+                                          dp.data_ptr(), P2, Cout, st), "zk_bn_bwd_dx_bf16")
+        else:
+            dp = g
+        if b1_done:
+            pass  # the BN-1 sums came with dp
+        elif ctx.fused:
             check(L.zk_stem_pool_bwd_sums_ya(dp.data_ptr(), y1.data_ptr(), coef1.data_ptr(),
                                              part.data_ptr(), P2, ctypes.byref(nb), st),
                   "zk_stem_pool_bwd_sums_ya")
