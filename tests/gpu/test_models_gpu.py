@@ -379,10 +379,12 @@ def test_binary_models_teacher_forced_unit_gradients(name):
     when the whole-network cosine stays positive.  Exempt, and printed:
     parameters whose oracle gradient norm is below 1e-3 of the median
     parameter's -- a gradient that vanishes up to rounding has no direction to
-    compare.  The one such parameter is the stem's BN-1 scale: BN-2 normalises
-    the max-pooled BN-1 output again, so the loss is invariant to it but for
-    the ReLU / pool selection (measured on MI355X: oracle norm 9e-6 against a
-    median of ~1e-2, native cosine 0.02).  Reference: the QuantConv2D /
+    compare.  Such parameters are stem BN parameters that another
+    normalisation follows: E18's BN-1 scale (BN-2 normalises the max-pooled
+    BN-1 output again, so the loss is invariant to it but for the ReLU / pool
+    selection; measured on MI355X: oracle norm 9e-6 against a median of
+    ~1e-2, native cosine 0.02) and QuickNet's stem BN scale / bias (norms
+    5e-6 / 2e-7 against a median of 0.2).  Reference: the QuantConv2D /
     QuantDense stack of /root/reference/examples/larq_experiment.py:59-103."""
     from zookeeper_amd.models.binary_resnet import BinaryResNetE
     from zookeeper_amd.models.quicknet import QuickNetModule
@@ -456,6 +458,7 @@ def test_binary_models_teacher_forced_unit_gradients(name):
     print(f"{name}: {len(rows)} parameters, median oracle grad norm {med:.3g}, worst cosines "
           + ", ".join(f"{n} {c:.4f} (|g| {gn:.2g}{', exempt' if n in exempt else ''})"
                       for n, c, gn in worst))
-    assert len(exempt) <= 1, exempt
+    # only stem BN parameters vanish this way (BN after BN / pool, see above)
+    assert all(n.startswith("stem.") for n in exempt), exempt
     fails = [(n, round(c, 4)) for n, c, _ in rows if n not in exempt and c < 0.99]
     assert not fails, fails

@@ -23,6 +23,8 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--variant", type=int, default=-1)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--no-y", action="store_true",
+                    help="fwd4: statistics only, no int16 y stores (lab option 9)")
     args = ap.parse_args()
     from zookeeper_amd.nn.layers import same_padding
     from zookeeper_amd.ops._native import lib, stream_ptr
@@ -82,6 +84,7 @@ def run_one(args, shape: str) -> None:
                                     args.variant, 32, st)
         assert rc == 0, rc
 
+    L.zk_set_option(9, int(args.no_y))
     run()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -90,7 +93,9 @@ def run_one(args, shape: str) -> None:
     torch.cuda.synchronize()
     us = (time.perf_counter() - t0) / args.reps * 1e6
     flops = 2.0 * B * Ho * Ho * cout * 9 * cin
-    print(f"{args.op} {shape} b{B} v{args.variant}: {us:.1f} us/call "
+    L.zk_set_option(9, 0)
+    print(f"{args.op}{' (no y)' if args.no_y else ''} {shape} b{B} v{args.variant}: "
+          f"{us:.1f} us/call "
           f"({flops / us / 1e9:.3f} PF/s)",
           flush=True)
 

@@ -122,6 +122,8 @@ int g_opt_dgrad_rw = 1;
 // (splits <= cap / |dW|); 0 = no cap (splits from the block target alone).
 // Default 32 MB (ops/options.py has the measurements).
 int g_opt_wgrad_slab_mb = 32;
+// lab only (key 9): the fp4 forward skips its int16 y stores (statistics only)
+int g_opt_lab_fwd_no_y = 0;
 // dgrad_deep (key 6): the phased kernel (deep_gemm.hip, variant 60) for
 // stride-1 3x3 data gradients with Cin % 256 == 0 (igemm_dgrad_impl): 1 for
 // the float convs, 2 also for the binary (STE-mask) ones, 0 never.
@@ -707,7 +709,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv_kernel(ConvArgs ar
           if (!live) t = 0;
           csum[b] += t;
           csq[b] += t * t;  // < 2^32 as unsigned for TM <= 4, K <= 4608
-          if (live) y[mc * g.Cout + n0 + wn * WTN + b * 32 + r32] = (int16_t)t;
+          if (live && y) y[mc * g.Cout + n0 + wn * WTN + b * 32 + r32] = (int16_t)t;
         }
       }
     }
@@ -1045,7 +1047,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_conv3_kernel(ConvArgs a
           if (!live) t = 0;
           csum[b] += t;
           csq[b] += t * t;
-          if (live) y[mc * g.Cout + n0 + wn * WTN + b * 32 + r32] = (int16_t)t;
+          if (live && y) y[mc * g.Cout + n0 + wn * WTN + b * 32 + r32] = (int16_t)t;
         }
       }
     }
@@ -2356,8 +2358,10 @@ ZK_EXPORT int zk_igemm_fwd_fp4(const void* sx4, const void* wf4, void* y, void* 
     else
       variant = Cout % 128 == 0 ? 1 : 8;
   }
-  const int rc =
-      igemm_fwd4_variant(variant, sx4, wf4, y, stats, g, pad_ones, relu, stat_stripes, stream);
+  // lab switch (option 9, tools/one_conv.py --no-y): statistics only, no y
+  // stores -- the cost of the int16 output in the fp4 forward
+  const int rc = igemm_fwd4_variant(variant, sx4, wf4, g_opt_lab_fwd_no_y ? nullptr : y, stats, g,
+                                    pad_ones, relu, stat_stripes, stream);
   if (rc) return rc;
   if (!g_dry_run) ZK_CHECK_LAUNCH();
   return 0;
@@ -2433,6 +2437,7 @@ ZK_EXPORT int zk_set_option(int key, int value) {
     case 6: g_opt_dgrad_deep = value; return 0;
     case 7: g_opt_wgrad_deep = value; return 0;
     case 8: g_opt_epilogue_prefetch = value; return 0;
+    case 9: g_opt_lab_fwd_no_y = value; return 0;
     default: return -1;
   }
 }
@@ -2446,6 +2451,7 @@ ZK_EXPORT int zk_get_option(int key) {
     case 6: return g_opt_dgrad_deep;
     case 7: return g_opt_wgrad_deep;
     case 8: return g_opt_epilogue_prefetch;
+    case 9: return g_opt_lab_fwd_no_y;
     default: return -1;
   }
 }

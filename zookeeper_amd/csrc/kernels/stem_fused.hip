@@ -34,6 +34,8 @@
 // first maximum of y1 * sign(gamma1), which is the first maximum of
 // relu(a1 y1 + s1) up to ties at relu's 0 (which route no gradient); the
 // BN-1 statistics are of the fp32 accumulators.
+#include <utility>
+
 #include "mfma_common.h"
 
 namespace {
@@ -61,30 +63,6 @@ struct LBuf {
   static_assert(RB % 16 == 0, "line-buffer rows must stay 16-B aligned");
 };
 
-// Issue the line buffer of the tile whose first conv output is (b, r0, c0).
-// Rows / pixels outside xp (and the row padding) read the zero page.
-template <class L, int NT>
-__device__ __forceinline__ void issue_lines(unsigned char* lb, const unsigned char* xp,
-                                            const FGeom& g, int b, int r0, int c0, int tid) {
-  const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
-  const int wave = tid >> 6, lane = tid & 63;
-  const long long rowb = (long long)g.Wp * 8;
-  const int yr0 = 2 * r0, xc0 = 2 * c0;
-#pragma unroll
-  for (int j = 0; j < (L::CHUNKS + NT - 1) / NT; ++j) {
-    const int q0 = j * NT + wave * 64;  // wave-uniform
-    if (q0 < L::CHUNKS) {
-      const int off = (q0 + lane) * 16;
-      const int row = off / L::RB, cb = off - row * L::RB;
-      const int yr = yr0 + row, xc = xc0 + (cb >> 3);
-      const unsigned char* src = zp;
-      if (cb < L::BASE && yr >= 0 && yr < g.Hp && xc >= 0 && xc + 1 < g.Wp)
-        src = xp + ((long long)b * g.Hp + yr) * rowb + (long long)xc * 8;
-      glds16(src, lb + q0 * 16);
-    }
-  }
-}
-
 // counted wait on this wave's own vector-memory operations (n <= 15, wave-uniform)
 __device__ __forceinline__ void wait_vmcnt_dyn(int n) {
   switch (n) {
@@ -99,18 +77,90 @@ __device__ __forceinline__ void wait_vmcnt_dyn(int n) {
   }
 }
 
-// LDS-DMA instructions issue_lines<L, NT> issues in wave `wave`
+// LDS-DMA of the line buffer of the tile whose first conv output is (b, r0,
+// c0); rows / pixels outside xp and the row padding read the zero page.  The
+// window row and pixel column of each of a thread's 16-B chunks do not depend
+// on the tile: the plan decodes them once, and a tile's issue costs a few
+// adds, a bounds test and a 32-bit pixel index per chunk (decoding them per
+// tile cost ~2,500 shader cycles per tile in B2's route waves:
+// tools/stem_stamps.cpp).
 template <class L, int NT>
-__device__ __forceinline__ int lines_count(int wave) {
-  int n = 0;
-  for (int j = 0; j < (L::CHUNKS + NT - 1) / NT; ++j) n += j * NT + wave * 64 < L::CHUNKS;
-  return n;
-}
+struct LinePlan {
+  static constexpr int NJ = (L::CHUNKS + NT - 1) / NT;
+  int rc[NJ];  // (window row << 16) | pixel column; -1: row padding (zero page)
+  int n;       // DMA instructions this wave issues
+  __device__ explicit LinePlan(int tid) {
+    const int wave = (tid >> 6) % (NT / 64), lane = tid & 63;
+    n = 0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int q0 = j * NT + wave * 64;
+      const int off = (q0 + lane) * 16;
+      const int row = off / L::RB, cb = off - row * L::RB;
+      rc[j] = cb < L::BASE ? (row << 16) | (cb >> 3) : -1;
+      n += q0 < L::CHUNKS;
+    }
+  }
+  __device__ __forceinline__ void issue(unsigned char* lb, const unsigned char* xp, const FGeom& g,
+                                        int b, int r0, int c0) const {
+    const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
+    const int wave = (threadIdx.x >> 6) % (NT / 64);
+    const int bh = b * g.Hp, yr0 = 2 * r0, xc0 = 2 * c0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int q0 = j * NT + wave * 64;  // wave-uniform
+      if (q0 < L::CHUNKS) {
+        const int yr = yr0 + (rc[j] >> 16), xc = xc0 + (rc[j] & 0xFFFF);
+        const bool v = rc[j] >= 0 && (unsigned)yr < (unsigned)g.Hp && xc >= 0 && xc + 1 < g.Wp;
+        const unsigned pix = (unsigned)((bh + yr) * g.Wp + xc);
+        glds16(v ? xp + (unsigned long long)pix * 8 : zp, lb + q0 * 16);
+      }
+    }
+  }
+};
 
-template <int TR, int TC, int NT>
-__device__ __forceinline__ void issue_lbuf(unsigned char* lb, const unsigned char* xp,
-                                           const FGeom& g, int b, int r0, int c0, int tid) {
-  issue_lines<LBuf<TR, TC>, NT>(lb, xp, g, b, r0, c0, tid);
+// acc[u] = sum over the 14 K-steps (kh, sub) of W[kh][sub] x B(pixel group
+// u), B fragments read from a line buffer with row pitch RB at byte offsets
+// seg0 / seg1.  The fragments stream PF K-steps ahead of their MFMAs: with one
+// matrix wave per SIMD nothing else hides the LDS latency, and the compiler's
+// own schedule kept only one step in flight (the kernels then ran at ~28 % of
+// the MFMA rate).  The read / MFMA interleave is pinned with
+// sched_group_barrier (masks: 0x100 DS read, 0x008 MFMA).
+//   NV > 0: NV independent VALU instructions that follow the call in program
+// order (the previous conv's statistics and keys) are pulled in beside each
+// step's MFMA pair -- an MFMA hides ~5 single-issue VALU of its own wave
+// (MI355X_MICROARCH.md, issue costs).
+template <int RB, int PF, int NV = 0>
+__device__ __forceinline__ void conv2_wreg(const uint4 (&w)[SKH][2], const unsigned char* lbc,
+                                           int seg0, int seg1, f32x16 (&acc)[2]) {
+  constexpr int NS = 2 * SKH;
+  uint4 ring[PF][2];
+#pragma unroll
+  for (int p = 0; p < PF; ++p) {
+    ring[p][0] = *reinterpret_cast<const uint4*>(lbc + seg0 + (p >> 1) * RB + 32 * (p & 1));
+    ring[p][1] = *reinterpret_cast<const uint4*>(lbc + seg1 + (p >> 1) * RB + 32 * (p & 1));
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 2 * PF, 0);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const uint4 b0 = ring[s % PF][0], b1 = ring[s % PF][1];
+    if (s + PF < NS) {
+      const int t = s + PF;
+      ring[s % PF][0] = *reinterpret_cast<const uint4*>(lbc + seg0 + (t >> 1) * RB + 32 * (t & 1));
+      ring[s % PF][1] = *reinterpret_cast<const uint4*>(lbc + seg1 + (t >> 1) * RB + 32 * (t & 1));
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    acc[0] = mfma_bf16(w[s >> 1][s & 1], b0, s ? acc[0] : f32x16{});  // C = 0 first
+    acc[1] = mfma_bf16(w[s >> 1][s & 1], b1, s ? acc[1] : f32x16{});
+    if constexpr (NV > 0) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, NV / 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, NV - NV / 2, 0);
+    } else {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+  }
 }
 
 __device__ __forceinline__ void unpack8(const uint4& q, float (&v)[8]) {
@@ -219,6 +269,44 @@ __device__ __forceinline__ int f_m(int rr, int cc) {
   return rr < F_OR ? (cc < F_OC ? rr * F_OC + cc : F_NOWN + F_TC + rr) : F_NOWN + cc;
 }
 
+// Diagnostic build only (-DZK_STEM_STAMPS, tools/stem_stamps.cpp): per wave,
+// the shader cycles spent working and waiting at the interval barrier of the
+// two-role pipelines (s_memtime), for the role balance.
+#ifdef ZK_STEM_STAMPS
+__device__ unsigned long long g_stem_stamps[2][1024 * 8][3];
+#define ZK_STAMP_BEGIN unsigned long long zs_t = __builtin_readcyclecounter(), zs_work = 0, zs_wait = 0, zs_mem = 0;
+#define ZK_STAMP_WORK                                 \
+  {                                                   \
+    const unsigned long long t_ = __builtin_readcyclecounter(); \
+    zs_work += t_ - zs_t;                             \
+    zs_t = t_;                                        \
+  }
+#define ZK_STAMP_WAIT                                 \
+  {                                                   \
+    const unsigned long long t_ = __builtin_readcyclecounter(); \
+    zs_wait += t_ - zs_t;                             \
+    zs_t = t_;                                        \
+  }
+#define ZK_STAMP_MEM                                  \
+  {                                                   \
+    const unsigned long long t_ = __builtin_readcyclecounter(); \
+    zs_mem += t_ - zs_t;                              \
+    zs_t = t_;                                        \
+  }
+#define ZK_STAMP_STORE(k)                                                  \
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) {                      \
+    g_stem_stamps[k][blockIdx.x * 8 + (threadIdx.x >> 6)][0] = zs_work;    \
+    g_stem_stamps[k][blockIdx.x * 8 + (threadIdx.x >> 6)][1] = zs_wait;    \
+    g_stem_stamps[k][blockIdx.x * 8 + (threadIdx.x >> 6)][2] = zs_mem;     \
+  }
+#else
+#define ZK_STAMP_BEGIN
+#define ZK_STAMP_WORK
+#define ZK_STAMP_WAIT
+#define ZK_STAMP_MEM
+#define ZK_STAMP_STORE(k)
+#endif
+
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 // bf16 pair -> int16 order keys: negative values get their magnitude bits
@@ -228,6 +316,118 @@ __device__ __forceinline__ uint32_t key16x2(uint32_t d) {
   const s16x2 x = __builtin_bit_cast(s16x2, d);
   const s16x2 s = x >> (s16x2){15, 15};
   return d ^ (__builtin_bit_cast(uint32_t, s) & 0x7FFF7FFFu);
+}
+
+// Position (image b, tile row th, tile column tw) of a block's tiles
+// T = T0, T0 + nblk, ...: the divisions happen once per stream, next() is a
+// few scalar adds (three divisions per interval were most of the pipelines'
+// scalar instructions).
+struct TileWalk {
+  int b, th, tw;
+  int db, dh, dw, tiles_w, tiles_h;
+  __device__ TileWalk(int T0, int nblk, int tiles_w_, int tiles_h_)
+      : tiles_w(tiles_w_), tiles_h(tiles_h_) {
+    const int img = tiles_w * tiles_h;
+    b = T0 / img;
+    const int rem = T0 - b * img;
+    th = rem / tiles_w;
+    tw = rem - th * tiles_w;
+    db = nblk / img;
+    const int r2 = nblk - db * img;
+    dh = r2 / tiles_w;
+    dw = r2 - dh * tiles_w;
+  }
+  __device__ __forceinline__ void next() {
+    tw += dw;
+    int c = tw >= tiles_w;
+    tw -= c ? tiles_w : 0;
+    th += dh + c;
+    c = th >= tiles_h;
+    th -= c ? tiles_h : 0;
+    b += db + c;
+  }
+};
+
+struct FTile {
+  const unsigned char* lbc;  // this tile's line buffer
+  unsigned char* yt;         // this tile's key image
+  int hr0, wc0;              // conv coordinates of region (0, 0)
+  bool last_r, last_c;       // last tile of its row / column of tiles
+};
+
+// BN-1 statistics of two 32-pixel groups (first group index G0) and their
+// keys into yt.  FAST: every owned pixel in the image, no halo counted (the
+// 7 owned groups, group 7 skipped); else the per-pixel test.
+template <bool FAST, int G0>
+__device__ __forceinline__ void f_post(const FTile& t, const FGeom& g, const f32x16 (&acc)[2],
+                                       int a, int r32, int h, float (&cs)[16], float (&cq)[16]) {
+  if constexpr (FAST) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (G0 + u >= 7) continue;  // the halo group (compile-time)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const f32x2 v = {acc[u][r], acc[u][r + 1]};
+        f32x2 s2 = {cs[r], cs[r + 1]}, q2 = {cq[r], cq[r + 1]};
+        s2 += v;
+        q2 = __builtin_elementwise_fma(v, v, q2);
+        cs[r] = s2.x;
+        cs[r + 1] = s2.y;
+        cq[r] = q2.x;
+        cq[r + 1] = q2.y;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int m = 32 * (G0 + u) + r32;
+      int rr, cc;
+      f_pix(m, rr, cc);
+      const int hc = t.hr0 + rr, wc = t.wc0 + cc;
+      const bool counted = m < 255 && hc >= 0 && hc < g.Ho && wc >= 0 && wc < g.Wo &&
+                           (rr < F_OR || t.last_r) && (cc < F_OC || t.last_c);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = counted ? acc[u][r] : 0.f;
+        cs[r] += v;
+        cq[r] = fmaf(v, v, cq[r]);
+      }
+    }
+  }
+  // y1 * sign(gamma1) -> LDS keys: per register pair (q, q+1) one permlane32
+  // swap per dword gives each lane a whole 16-B slot (cdna_hip_programming.md T21)
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int m = 32 * (G0 + u) + r32;
+#pragma unroll
+    for (int pq = 0; pq < 2; ++pq) {
+      uint32_t d[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * (2 * pq + (e >> 1)) + 2 * (e & 1);
+        d[e] = key16x2(zk::pack_bf16x2(acc[u][r], acc[u][r + 1]));
+      }
+      const auto s0 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+      *reinterpret_cast<uint4*>(t.yt + f_off(m, 4 * a + 2 * pq + h)) =
+          make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    }
+  }
+}
+
+// One tile of a matrix wave: conv of its 4 pixel groups (channel half a),
+// then the statistics and keys.  HALO: this wave's groups are 4..7.
+template <bool FAST, bool HALO>
+__device__ __forceinline__ void f_matrix_tile(const FTile& t, const FGeom& g,
+                                              const uint4 (&w)[SKH][2], const int (&segb)[4],
+                                              int a, int r32, int h, float (&cs)[16],
+                                              float (&cq)[16]) {
+  constexpr int G0 = HALO ? 4 : 0;
+  f32x16 acc0[2], acc1[2];
+  conv2_wreg<FLB::RB, 3>(w, t.lbc, segb[0], segb[1], acc0);
+  conv2_wreg<FLB::RB, 3, 8>(w, t.lbc, segb[2], segb[3], acc1);
+  f_post<FAST, G0>(t, g, acc0, a, r32, h, cs, cq);
+  f_post<FAST, G0 + 2>(t, g, acc1, a, r32, h, cs, cq);
 }
 
 __device__ __attribute__((aligned(16))) uint4 g_pool_sink[2];
@@ -252,22 +452,12 @@ __global__ __launch_bounds__(512, 2) void stem_fwd_fused_kernel(
   const int r32 = lane & 31, h = lane >> 5;
   const int blk = xcd_linear(blockIdx.x, gridDim.x), nblk = gridDim.x;
   const int n = blk < ntiles ? (ntiles - 1 - blk) / nblk + 1 : 0;  // this block's tiles
-  const int tiles_img = tiles_w * tiles_h;
   const bool pooler = wave < 4;
   const int mw = wave & 3, a = mw & 1, g0 = 4 * (mw >> 1);  // matrix waves: channel half, first group
 
-  auto tile_pos = [&](int j, int& b, int& th, int& tw) {
-    const int T = blk + j * nblk;
-    b = T / tiles_img;
-    const int rem = T - b * tiles_img;
-    th = rem / tiles_w;
-    tw = rem - th * tiles_w;
-  };
-  auto issue_lb = [&](int j) {
-    int b, th, tw;
-    tile_pos(j, b, th, tw);
-    issue_lines<FLB, 256>(lbr + (j % F_NLB) * FLB::BYTES, xp, g, b, 2 * F_PR * th - g.pt2,
-                          2 * F_PC * tw - g.pl2, tid);
+  auto issue_lb = [&](const LinePlan<FLB, 256>& pl, const TileWalk& t, int j) {
+    pl.issue(lbr + (j % F_NLB) * FLB::BYTES, xp, g, t.b, 2 * F_PR * t.th - g.pt2,
+             2 * F_PC * t.tw - g.pl2);
   };
 
   float cs[16], cq[16];  // matrix waves: BN-1 sums / squares of this lane's 16 channels
@@ -297,22 +487,28 @@ __global__ __launch_bounds__(512, 2) void stem_fwd_fused_kernel(
         toff[k][t / 2] = v;
       }
     }
-    if (n > 0) issue_lb(0);
-    if (n > 1) issue_lb(1);
+    const LinePlan<FLB, 256> lplan(tid);
+    TileWalk wdma(blk, nblk, tiles_w, tiles_h), wpool(blk, nblk, tiles_w, tiles_h);
+    if (n > 0) issue_lb(lplan, wdma, 0);
+    wdma.next();
+    if (n > 1) issue_lb(lplan, wdma, 1);
+    wdma.next();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int n_lb = lines_count<FLB, 256>(wave);
+    const int n_lb = lplan.n;
     const int nst = wave < 3 ? 4 : 2;  // ya / arg stores per tile
+    ZK_STAMP_BEGIN
     for (int ii = 0; ii <= n; ++ii) {
       int issued = 0;
       if (ii + 2 < n) {
-        issue_lb(ii + 2);
+        issue_lb(lplan, wdma, ii + 2);
+        wdma.next();
         issued = n_lb;
       }
       if (ii >= 1) {
         const unsigned char* yt = ytr + ((ii - 1) % F_NYT) * F_YT;
-        int b, th, tw;
-        tile_pos(ii - 1, b, th, tw);
+        const int b = wpool.b, th = wpool.th, tw = wpool.tw;
+        wpool.next();
         const int hr0 = 2 * F_PR * th - g.pt2, wc0 = 2 * F_PC * tw - g.pl2;
         // tile inside the image: every tap in the image, every pool output live
         const bool tile_in = hr0 >= 0 && hr0 + F_TR <= g.Ho && wc0 >= 0 && wc0 + F_TC <= g.Wo &&
@@ -375,10 +571,14 @@ __global__ __launch_bounds__(512, 2) void stem_fwd_fused_kernel(
       }
       // everything issued before this interval (line buffer ii + 1, the
       // previous tile's stores) landed
+      ZK_STAMP_WORK
       wait_vmcnt_dyn(issued);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ZK_STAMP_MEM
       __builtin_amdgcn_s_barrier();
+      ZK_STAMP_WAIT
     }
+    ZK_STAMP_STORE(0)
   } else {
     // weights of channel half a, w[kh][sub] = K-chunk 2 sub + h of row
     // co = 32 a + r32, negated where gamma1[co] < 0 (exact in bf16): the MFMA
@@ -403,95 +603,38 @@ __global__ __launch_bounds__(512, 2) void stem_fwd_fused_kernel(
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) cs[r] = cq[r] = 0.f;
+    TileWalk wmat(blk, nblk, tiles_w, tiles_h);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    ZK_STAMP_BEGIN
     for (int ii = 0; ii <= n; ++ii) {
       if (ii < n) {
-        int b, th, tw;
-        tile_pos(ii, b, th, tw);
+        const int th = wmat.th, tw = wmat.tw;
+        wmat.next();
         const int hr0 = 2 * F_PR * th - g.pt2, wc0 = 2 * F_PC * tw - g.pl2;
         const unsigned char* lbc = lbr + (ii % F_NLB) * FLB::BYTES;
         unsigned char* yt = ytr + (ii % F_NYT) * F_YT;
         const bool last_r = th == tiles_h - 1, last_c = tw == tiles_w - 1;
         const bool fast = hr0 >= 0 && hr0 + F_OR <= g.Ho && wc0 >= 0 && wc0 + F_OC <= g.Wo &&
                           !(last_r && hr0 + F_OR < g.Ho) && !(last_c && wc0 + F_OC < g.Wo);
-#pragma unroll
-        for (int hg = 0; hg < 2; ++hg) {
-          // ---- conv: 2 groups x 32 pixels x channel half a
-          f32x16 acc[2];
-#pragma unroll
-          for (int kh = 0; kh < SKH; ++kh)
-#pragma unroll
-            for (int sub = 0; sub < 2; ++sub) {
-              uint4 bf[2];
-#pragma unroll
-              for (int u = 0; u < 2; ++u)
-                bf[u] = *reinterpret_cast<const uint4*>(lbc + segb[2 * hg + u] + kh * FLB::RB +
-                                                        32 * sub);
-#pragma unroll
-              for (int u = 0; u < 2; ++u)  // the first step takes C = 0 (no register zeroing)
-                acc[u] = mfma_bf16(w[kh][sub], bf[u], kh + sub ? acc[u] : f32x16{});
-            }
-          // ---- BN-1 statistics of the fp32 accumulators, each conv output once
-          if (fast) {  // the 7 owned groups, no halo (uniform); packed fp32
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              if (g0 + 2 * hg + u < 7) {
-#pragma unroll
-                for (int r = 0; r < 16; r += 2) {
-                  const f32x2 v = {acc[u][r], acc[u][r + 1]};
-                  f32x2 s2 = {cs[r], cs[r + 1]}, q2 = {cq[r], cq[r + 1]};
-                  s2 += v;
-                  q2 = __builtin_elementwise_fma(v, v, q2);
-                  cs[r] = s2.x;
-                  cs[r + 1] = s2.y;
-                  cq[r] = q2.x;
-                  cq[r + 1] = q2.y;
-                }
-              }
-            }
-          } else {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              const int m = 32 * (g0 + 2 * hg + u) + r32;
-              int rr, cc;
-              f_pix(m, rr, cc);
-              const int hc = hr0 + rr, wc = wc0 + cc;
-              const bool counted = m < 255 && hc >= 0 && hc < g.Ho && wc >= 0 && wc < g.Wo &&
-                                   (rr < F_OR || last_r) && (cc < F_OC || last_c);
-#pragma unroll
-              for (int r = 0; r < 16; ++r) {
-                const float v = counted ? acc[u][r] : 0.f;
-                cs[r] += v;
-                cq[r] = fmaf(v, v, cq[r]);
-              }
-            }
-          }
-          // ---- y1 * sign(gamma1) -> LDS keys: per register pair (q, q+1) one
-          // permlane32 swap per dword gives each lane a whole 16-B slot
-          // (cdna_hip_programming.md T21)
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int m = 32 * (g0 + 2 * hg + u) + r32;
-#pragma unroll
-            for (int pq = 0; pq < 2; ++pq) {
-              uint32_t d[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int r = 4 * (2 * pq + (e >> 1)) + 2 * (e & 1);
-                d[e] = key16x2(zk::pack_bf16x2(acc[u][r], acc[u][r + 1]));
-              }
-              const auto s0 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
-              const auto s1 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
-              *reinterpret_cast<uint4*>(yt + f_off(m, 4 * a + 2 * pq + h)) =
-                  make_uint4(s0[0], s1[0], s0[1], s1[1]);
-            }
-          }
+        // one straight-line body per (statistics path, halo wave): the second
+        // conv's MFMAs and the first pair's statistics / keys share a basic
+        // block, so the scheduler can interleave them
+        const FTile ft{lbc, yt, hr0, wc0, last_r, last_c};
+        if (fast) {
+          if (g0) f_matrix_tile<true, true>(ft, g, w, segb, a, r32, h, cs, cq);
+          else f_matrix_tile<true, false>(ft, g, w, segb, a, r32, h, cs, cq);
+        } else {
+          if (g0) f_matrix_tile<false, true>(ft, g, w, segb, a, r32, h, cs, cq);
+          else f_matrix_tile<false, false>(ft, g, w, segb, a, r32, h, cs, cq);
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // y1 keys stored
+      ZK_STAMP_WORK
       __builtin_amdgcn_s_barrier();
+      ZK_STAMP_WAIT
     }
+    ZK_STAMP_STORE(0)
   }
 
   // statistics: lane r32 of each half ends with the half's total of value r32
@@ -613,39 +756,6 @@ __device__ __forceinline__ uint4 tr_frag_b2(const unsigned char* yt, int k0, int
   return __builtin_bit_cast(uint4, v);
 }
 
-// routing stage of the tile at (b, r0, c0): pool outputs (ohb + i, owb + j)
-template <int NT>
-__device__ __forceinline__ void issue_route(unsigned char* rt, const uint16_t* dp,
-                                            const uint8_t* arg, const FGeom& g, int b, int r0,
-                                            int c0, int tid) {
-  const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
-  const int wave = tid >> 6, lane = tid & 63;
-  const int ohb = r0 / 2 - 1 + g.pt2, owb = c0 / 2 - 1 + g.pl2;
-#pragma unroll
-  for (int j = 0; j < (RT_CHUNKS + NT - 1) / NT; ++j) {
-    const int q0 = j * NT + wave * 64;
-    if (q0 < RT_CHUNKS) {
-      const int q = q0 + lane;
-      const unsigned char* src = zp;
-      if (q < RT_N * 8) {
-        const int o = q >> 3, part = q & 7;
-        const int oh = ohb + o / RT_OW, ow = owb + o % RT_OW;
-        if (oh >= 0 && oh < g.H2 && ow >= 0 && ow < g.W2)
-          src = reinterpret_cast<const unsigned char*>(dp) +
-                (((long long)b * g.H2 + oh) * g.W2 + ow) * 128 + part * 16;
-      } else if (q < RT_CHUNKS) {
-        const int qa = q - RT_N * 8;
-        const int o = qa >> 2, part = qa & 3;
-        const int oh = ohb + o / RT_OW, ow = owb + o % RT_OW;
-        if (oh >= 0 && oh < g.H2 && ow >= 0 && ow < g.W2)
-          src = reinterpret_cast<const unsigned char*>(arg) +
-                (((long long)b * g.H2 + oh) * g.W2 + ow) * 64 + part * 16;
-      }
-      glds16(src, rt + q0 * 16);
-    }
-  }
-}
-
 // 32x32x16 operand: 8 consecutive pixels (k) of column j (0..31) of kernel
 // row kh, read transposed from the line buffer (see tr_frag_swz).
 __device__ __forceinline__ uint4 tr_frag_lb(const unsigned char* lb, int k0, int kh, int lane) {
@@ -676,16 +786,100 @@ __device__ __forceinline__ uint4 tr_frag_lb(const unsigned char* lb, int k0, int
 // Rings: line buffers 5 (issued two intervals ahead, read by phases a and c),
 // routing stages 3, y1 / dy1 images 3.  One barrier per interval.
 constexpr int B3_NLB = 5, B3_NRT = 3, B3_NYT = 3;
-constexpr int B3_LDS = B3_NLB * B2_LB + B3_NRT * B2_RT + B3_NYT * B2_YT;
+constexpr int B3_LDS = B3_NLB * B2_LB + B3_NRT * B2_RT + B3_NYT * B2_YT + 2 * SC * 4;
 static_assert(B3_LDS <= 160 * 1024, "B2 pipeline LDS");
 
-// LDS-DMA instructions issue_route<NT> issues in wave `wave`
-template <int NT>
-__device__ __forceinline__ int route_count(int wave) {
-  int n = 0;
-  for (int j = 0; j < (RT_CHUNKS + NT - 1) / NT; ++j) n += j * NT + wave * 64 < RT_CHUNKS;
-  return n;
+template <int KB, int S>
+__device__ __forceinline__ void b2_wg_load(const unsigned char* yt, const unsigned char* lbc,
+                                           int wa, int lane, uint4& fa, uint4 (&fb)[4]) {
+  fa = tr_frag_b2(yt, 16 * S, 32 * wa, lane);
+#pragma unroll
+  for (int e = 0; e < 3; ++e) fb[e] = tr_frag_lb(lbc, 16 * S, KB + e, lane);
+  if constexpr ((S >> 2) == (KB >> 2)) fb[3] = tr_frag_lb(lbc, 16 * S, 3, lane);
 }
+
+template <int KB, int S>
+__device__ __forceinline__ void b2_wg_step(const unsigned char* yt, const unsigned char* lbc,
+                                           int wa, int lane, uint4 (&fa)[2], uint4 (&fb)[2][4],
+                                           f32x16 (&accw)[4]) {
+  constexpr int K = S & 1;
+  constexpr bool R3 = (S >> 2) == (KB >> 2);
+  if constexpr (S + 1 < 8) {
+    b2_wg_load<KB, S + 1>(yt, lbc, wa, lane, fa[K ^ 1], fb[K ^ 1]);
+  }
+#pragma unroll
+  for (int e = 0; e < 3; ++e) accw[e] = mfma_bf16(fa[K], fb[K][e], accw[e]);
+  if constexpr (R3) accw[3] = mfma_bf16(fa[K], fb[K][3], accw[3]);
+}
+
+template <int KB, int... S>
+__device__ __forceinline__ void b2_wg_steps(const unsigned char* yt, const unsigned char* lbc,
+                                            int wa, int lane, uint4 (&fa)[2], uint4 (&fb)[2][4],
+                                            f32x16 (&accw)[4], std::integer_sequence<int, S...>) {
+  (b2_wg_step<KB, S>(yt, lbc, wa, lane, fa, fb, accw), ...);
+}
+
+// Phase c of one tile for a matrix wave with kernel rows KB .. KB + 2 (all 8
+// pixel steps) and its half of kernel row 3 (steps KB .. KB + 3): the A
+// (dy1^T) and B (X) fragments of step s + 1 are read while step s's MFMAs
+// run (see conv2_wreg; left to the compiler's schedule here: pinning it
+// with sched_group_barrier cost 14 VGPRs of spills).
+template <int KB>
+__device__ __forceinline__ void b2_wgrad_tile(const unsigned char* yt, const unsigned char* lbc,
+                                              int wa, int lane, f32x16 (&accw)[4]) {
+  uint4 fa[2], fb[2][4];
+  b2_wg_load<KB, 0>(yt, lbc, wa, lane, fa[0], fb[0]);
+  b2_wg_steps<KB>(yt, lbc, wa, lane, fa, fb, accw, std::make_integer_sequence<int, 8>{});
+}
+
+// LDS-DMA of the routing stage of the tile at (b, r0, c0): dp rows (128 B)
+// and arg rows (64 B) of its 5 x 9 candidate pool outputs; outside the image
+// the zero page.  Candidate offsets, chunk part and dp / arg kind are decoded
+// once per thread.
+template <int NT>
+struct RoutePlan {
+  static constexpr int NJ = (RT_CHUNKS + NT - 1) / NT;
+  int code[NJ];  // (arg << 24) | (row << 16) | (col << 8) | part; -1: no chunk
+  int n;
+  __device__ explicit RoutePlan(int tid) {
+    const int wave = (tid >> 6) % (NT / 64), lane = tid & 63;
+    n = 0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int q0 = j * NT + wave * 64, q = q0 + lane;
+      n += q0 < RT_CHUNKS;
+      if (q < RT_N * 8) {
+        const int o = q >> 3;
+        code[j] = ((o / RT_OW) << 16) | ((o % RT_OW) << 8) | (q & 7);
+      } else if (q < RT_CHUNKS) {
+        const int qa = q - RT_N * 8, o = qa >> 2;
+        code[j] = (1 << 24) | ((o / RT_OW) << 16) | ((o % RT_OW) << 8) | (qa & 3);
+      } else {
+        code[j] = -1;
+      }
+    }
+  }
+  __device__ __forceinline__ void issue(unsigned char* rt, const uint16_t* dp, const uint8_t* arg,
+                                        const FGeom& g, int b, int r0, int c0) const {
+    const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
+    const int wave = (threadIdx.x >> 6) % (NT / 64);
+    const int ohb = r0 / 2 - 1 + g.pt2, owb = c0 / 2 - 1 + g.pl2, bh = b * g.H2;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int q0 = j * NT + wave * 64;  // wave-uniform
+      if (q0 < RT_CHUNKS) {
+        const int c = code[j];
+        const int oh = ohb + ((c >> 16) & 0xFF), ow = owb + ((c >> 8) & 0xFF);
+        const bool v = c >= 0 && (unsigned)oh < (unsigned)g.H2 && (unsigned)ow < (unsigned)g.W2;
+        const unsigned pix = (unsigned)((bh + oh) * g.W2 + ow);
+        const unsigned char* src =
+            (c >> 24) ? reinterpret_cast<const unsigned char*>(arg) + (unsigned long long)pix * 64
+                      : reinterpret_cast<const unsigned char*>(dp) + (unsigned long long)pix * 128;
+        glds16(v ? src + (c & 0xFF) * 16 : zp, rt + q0 * 16);
+      }
+    }
+  }
+};
 
 template <int PT2, int PL2>
 __global__ __launch_bounds__(512, 2) void stem_bwd_fused_kernel(
@@ -697,29 +891,19 @@ __global__ __launch_bounds__(512, 2) void stem_bwd_fused_kernel(
   unsigned char* lbr = smem;                                   // [5][B2_LB]
   unsigned char* rtr = lbr + B3_NLB * B2_LB;                   // [3][B2_RT]
   unsigned char* ytr = rtr + B3_NRT * B2_RT;                   // [3][B2_YT]
+  float* cf = reinterpret_cast<float*>(ytr + B3_NYT * B2_YT);  // BN-1 a1, s1
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r32 = lane & 31, h = lane >> 5;
   const int blk = xcd_linear(blockIdx.x, gridDim.x), nblk = gridDim.x;
   const int n = blk < ntiles ? (ntiles - 1 - blk) / nblk + 1 : 0;  // this block's tiles
   const bool route = wave < 4;
 
-  auto tile_pos = [&](int j, int& b, int& r0, int& c0) {
-    const int T = blk + j * nblk;
-    b = T / tiles_img;
-    const int rem = T - b * tiles_img;
-    const int th = rem / tiles_w;
-    r0 = th * B2_TR;
-    c0 = (rem - th * tiles_w) * B2_TC;
+  const int tiles_h = tiles_img / tiles_w;
+  auto issue_lb = [&](const LinePlan<LBuf<B2_TR, B2_TC>, 256>& pl, const TileWalk& t, int j) {
+    pl.issue(lbr + (j % B3_NLB) * B2_LB, xp, g, t.b, t.th * B2_TR, t.tw * B2_TC);
   };
-  auto issue_lb = [&](int j) {
-    int b, r0, c0;
-    tile_pos(j, b, r0, c0);
-    issue_lbuf<B2_TR, B2_TC, 256>(lbr + (j % B3_NLB) * B2_LB, xp, g, b, r0, c0, tid);
-  };
-  auto issue_rt = [&](int j) {
-    int b, r0, c0;
-    tile_pos(j, b, r0, c0);
-    issue_route<256>(rtr + (j % B3_NRT) * B2_RT, dp, arg, g, b, r0, c0, tid);
+  auto issue_rt = [&](const RoutePlan<256>& pl, const TileWalk& t, int j) {
+    pl.issue(rtr + (j % B3_NRT) * B2_RT, dp, arg, g, t.b, t.th * B2_TR, t.tw * B2_TC);
   };
 
   // matrix-wave indices (used after the loops too)
@@ -731,33 +915,40 @@ __global__ __launch_bounds__(512, 2) void stem_bwd_fused_kernel(
     // coefficients in registers (k3 negated)
     const int cell = tid >> 3, cgp = tid & 7;
     const int cr = cell >> 3, cc = cell & 7;
-    float ca[8], cs[8], k1[8], k0[8], k3[8];
+    float k1[8], k0[8], k3[8];  // BN-1's a1, s1: in LDS (registers are the limit)
+    for (int i = tid; i < 2 * SC; i += 256) cf[i] = coef1[i];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int c = cgp * 8 + k;
-      ca[k] = coef1[c];
-      cs[k] = coef1[SC + c];
       k1[k] = bcoef1[c];
       k0[k] = bcoef1[SC + c];
       k3[k] = -bcoef1[2 * SC + c];
     }
-    if (n > 0) issue_lb(0);
-    if (n > 1) issue_lb(1);
-    if (n > 0) issue_rt(0);
+    const LinePlan<LBuf<B2_TR, B2_TC>, 256> lplan(tid);
+    const RoutePlan<256> rplan(tid);
+    TileWalk wlb(blk, nblk, tiles_w, tiles_h), wrt(blk, nblk, tiles_w, tiles_h),
+        wb(blk, nblk, tiles_w, tiles_h);
+    if (n > 0) issue_lb(lplan, wlb, 0);
+    wlb.next();
+    if (n > 1) issue_lb(lplan, wlb, 1);
+    wlb.next();
+    if (n > 0) issue_rt(rplan, wrt, 0);
+    wrt.next();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int n_lb = lines_count<LBuf<B2_TR, B2_TC>, 256>(wave);
-    const int n_rt = route_count<256>(wave);
+    ZK_STAMP_BEGIN
     for (int i = 0; i < n + 2; ++i) {
       // DMA two intervals ahead for the conv, one for the routing stage
       int issued = 0;
       if (i + 2 < n) {
-        issue_lb(i + 2);
-        issued += n_lb;
+        issue_lb(lplan, wlb, i + 2);
+        wlb.next();
+        issued += lplan.n;
       }
       if (i + 1 < n) {
-        issue_rt(i + 1);
-        issued += n_rt;
+        issue_rt(rplan, wrt, i + 1);
+        wrt.next();
+        issued += rplan.n;
       }
       // ---- b) dy1 of tile i - 1 in place: du = sum of dp over the candidate
       // pool outputs whose argmax tap is the pixel; with the pool padding
@@ -766,8 +957,8 @@ __global__ __launch_bounds__(512, 2) void stem_bwd_fused_kernel(
       // the image read the zero page: dp 0 adds nothing whatever the tap.
       if (i >= 1 && i <= n) {
         const int j = i - 1;
-        int b, r0, c0;
-        tile_pos(j, b, r0, c0);
+        const int r0 = wb.th * B2_TR, c0 = wb.tw * B2_TC;
+        wb.next();
         const unsigned char* rt = rtr + (j % B3_NRT) * B2_RT;
         unsigned char* yt = ytr + (j % B3_NYT) * B2_YT;
         uint32_t aw[2][2][2];
@@ -787,6 +978,15 @@ __global__ __launch_bounds__(512, 2) void stem_bwd_fused_kernel(
         for (int pq = 0; pq < 4; ++pq) {
           const int m = (2 * cr + (pq >> 1)) * B2_TC + 2 * cc + (pq & 1);
           yq[pq] = *reinterpret_cast<const uint4*>(yt + b2_off(m, cgp));
+        }
+        float ca[8], cs[8];
+        {
+          const float4* c4 = reinterpret_cast<const float4*>(cf + cgp * 8);
+          const float4 a0 = c4[0], a1 = c4[1], s0 = c4[SC / 4], s1 = c4[SC / 4 + 1];
+          ca[0] = a0.x; ca[1] = a0.y; ca[2] = a0.z; ca[3] = a0.w;
+          ca[4] = a1.x; ca[5] = a1.y; ca[6] = a1.z; ca[7] = a1.w;
+          cs[0] = s0.x; cs[1] = s0.y; cs[2] = s0.z; cs[3] = s0.w;
+          cs[4] = s1.x; cs[5] = s1.y; cs[6] = s1.z; cs[7] = s1.w;
         }
         const bool interior = r0 + B2_TR <= g.Ho && c0 + B2_TC <= g.Wo;  // uniform
 #pragma unroll
@@ -831,11 +1031,15 @@ __global__ __launch_bounds__(512, 2) void stem_bwd_fused_kernel(
           *reinterpret_cast<uint4*>(yt + b2_off(m, cgp)) = pack8f(o8);
         }
       }
+      ZK_STAMP_WORK
       // the previous interval's DMAs (line buffer i + 1, routing stage i) landed
       wait_vmcnt_dyn(issued);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // dy1 stores done
+      ZK_STAMP_MEM
       __builtin_amdgcn_s_barrier();
+      ZK_STAMP_WAIT
     }
+    ZK_STAMP_STORE(1)
   } else {
     // ---- matrix waves: mw computes the conv of channel half ma for pixel
     // groups mg0, mg0 + 1 with its 32 x 224 weights in VGPRs, and the phase-c
@@ -853,6 +1057,7 @@ __global__ __launch_bounds__(512, 2) void stem_bwd_fused_kernel(
       for (int r = 0; r < 16; ++r) accw[e][r] = 0.f;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    ZK_STAMP_BEGIN
     for (int i = 0; i < n + 2; ++i) {
       // ---- a) conv of tile i -> its y1 image
       if (i < n) {
@@ -866,18 +1071,7 @@ __global__ __launch_bounds__(512, 2) void stem_bwd_fused_kernel(
           segb[u] = 2 * (px / B2_TC) * L::RB + 16 * (px % B2_TC) + 16 * h;
         }
         f32x16 acc[2];
-#pragma unroll
-        for (int kh = 0; kh < SKH; ++kh)
-#pragma unroll
-          for (int sub = 0; sub < 2; ++sub) {
-            uint4 bf[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-              bf[u] = *reinterpret_cast<const uint4*>(lbc + segb[u] + kh * L::RB + 32 * sub);
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-              acc[u] = mfma_bf16(w[kh][sub], bf[u], kh + sub ? acc[u] : f32x16{});
-          }
+        conv2_wreg<L::RB, 2>(w, lbc, segb[0], segb[1], acc);
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int m = 32 * (mg0 + u) + r32;
@@ -901,20 +1095,17 @@ __global__ __launch_bounds__(512, 2) void stem_bwd_fused_kernel(
         const int j = i - 2;
         const unsigned char* lbc = lbr + (j % B3_NLB) * B2_LB;
         const unsigned char* yt = ytr + (j % B3_NYT) * B2_YT;
-#pragma unroll 2
-        for (int s = 0; s < 8; ++s) {
-          const int k0s = 16 * s;
-          const uint4 af = tr_frag_b2(yt, k0s, 32 * wa, lane);
-#pragma unroll
-          for (int e = 0; e < 3; ++e)
-            accw[e] = mfma_bf16(af, tr_frag_lb(lbc, k0s, kb + e, lane), accw[e]);
-          if ((s >> 2) == (kb >> 2))  // wave-uniform: this wave's half of kernel row 3
-            accw[3] = mfma_bf16(af, tr_frag_lb(lbc, k0s, 3, lane), accw[3]);
-        }
+        if (kb)
+          b2_wgrad_tile<4>(yt, lbc, wa, lane, accw);
+        else
+          b2_wgrad_tile<0>(yt, lbc, wa, lane, accw);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // y1 stores done
+      ZK_STAMP_WORK
       __builtin_amdgcn_s_barrier();
+      ZK_STAMP_WAIT
     }
+    ZK_STAMP_STORE(1)
   }
 
   // one plain-stored dW partial per block: slab[block][co][kh*32 + j]; the
