@@ -214,10 +214,13 @@ __global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
         for (int e = 0; e < 2; ++e) acc[u][e] = mfma_fp4(wv[e], b, t ? acc[u][e] : f32x16{});
       }
     }
-    // ---- epilogue in packed fp32: statistics, int16 16-B slot stores
+    // every wave is done with this tile's stage: it becomes the output staging
+    // area (4 KB per wave), until the DMA of tile it + 2 after the next barrier
+    __syncthreads();
+    unsigned char* ys = smem + (it & 1) * BF_STAGE + wave * (32 * 128);
+    // ---- epilogue in packed fp32: statistics, int16 rows staged through LDS
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int m = m0 + 64 * wave + 32 * u + r32;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         f32x16 c = acc[u][e];
@@ -248,7 +251,9 @@ __global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
           bits[r] = __builtin_bit_cast(uint32_t, c[r] + 12582912.f);
           bits[r + 1] = __builtin_bit_cast(uint32_t, c[r + 1] + 12582912.f);
         }
-        // registers r = 4 q + i hold channels 32 e + 8 q + 4 h + i
+        // registers r = 4 q + i hold channels 32 e + 8 q + 4 h + i; after the
+        // swap lane (p, h) holds 16-B slot 4 e + 2 pq + h of pixel p, staged
+        // at slot ^ (p & 7) (conflict-free 8-lane write groups)
 #pragma unroll
         for (int pq = 0; pq < 2; ++pq) {
           uint32_t d[4];
@@ -259,10 +264,20 @@ __global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
           }
           const auto s0 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
           const auto s1 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
-          if (live[u] && a.y)
-            *reinterpret_cast<uint4*>(a.y + (long long)m * BF_C + (4 * e + 2 * pq + h) * 8) =
-                make_uint4(s0[0], s1[0], s0[1], s1[1]);
+          const int slot = 4 * e + 2 * pq + h;
+          *reinterpret_cast<uint4*>(ys + r32 * 128 + ((slot ^ (r32 & 7)) << 4)) =
+              make_uint4(s0[0], s1[0], s0[1], s1[1]);
         }
+      }
+      // whole 128-B rows: instruction k stores pixels 8 k .. 8 k + 7 of the
+      // group (lane l: pixel 8 k + l / 8, slot l % 8)
+      const int mg = m0 + 64 * wave + 32 * u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = 8 * k + (lane >> 3), sl = lane & 7;
+        const uint4 v = *reinterpret_cast<const uint4*>(ys + p * 128 + ((sl ^ (p & 7)) << 4));
+        if (a.y && mg + p < a.M)
+          *reinterpret_cast<uint4*>(a.y + (long long)(mg + p) * BF_C + sl * 8) = v;
       }
     }
     if ((it + 1) % BF_FLUSH == 0) bf_flush(cs, cq, r32, tsum, tsq);
