@@ -107,12 +107,14 @@ def test_igemm_fwd_fp4_exact(cin, cout, stride, hw, pad_ones, relu):
     assert torch.equal(tot[0], flat.sum(0).cpu()) and torch.equal(tot[1], (flat * flat).sum(0).cpu())
 
 
-@pytest.mark.parametrize("B,hw,pad_ones,relu", [(256, 56, 0, 0), (37, 28, 1, 1), (61, 15, 0, 1)])
+@pytest.mark.parametrize("B,hw,pad_ones,relu",
+                         [(256, 56, 0, 0), (37, 28, 1, 1), (61, 15, 0, 1), (2800, 56, 1, 0)])
 def test_bfwd64_persistent_matches_conv3(B, hw, pad_ones, relu):
     """The persistent 64 -> 64 kernel (variant 40, bfwd.hip) walks many tiles
     per block at these sizes (the float64 test above covers one or two): its
-    int16 outputs and striped int64 statistics equal the conv3 tile's (variant
-    20, itself exact against float64) bit for bit, tail tiles included."""
+    int16 outputs and striped int64 statistics (flushed mid-run at batch 2800)
+    equal the conv3 tile's (variant 20, itself exact against float64) bit for
+    bit, tail tiles included."""
     from zookeeper_amd.ops._native import lib, stream_ptr
 
     torch.manual_seed(11)

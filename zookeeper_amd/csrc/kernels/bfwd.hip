@@ -10,19 +10,20 @@
 // barriered K-steps, 64 two-byte stores per lane and 128 int64 statistics
 // atomics).  Here (MI355X, batch 1536 per GPU):
 //   * persistent blocks (2 per CU, 4 waves) walk 256-pixel tiles (64 pixels
-//     per wave); the three kernel rows' input segments (258 flattened pixels
-//     x 32 B of e2m1 signs each) stream into a two-stage LDS ring by
-//     global_load_lds one tile ahead;
+//     per wave); the union of the three kernel rows' input windows (256 + 2 W
+//     + 2 flattened pixels x 32 B of e2m1 signs) streams into a three-stage
+//     LDS ring by global_load_lds two tiles ahead (one barrier per tile);
 //   * the 18 KB weight image stays in LDS for the whole launch; per tile a
 //     wave reads each of the 18 weight fragments once and issues 36
 //     v_mfma_scale_f32_32x32x64_f8f6f4 (D[co][pixel]: lane = pixel);
 //   * padded taps read a pad row (zeros or e2m1 +1) through a per-lane
 //     address select on scalar edge masks;
-//   * the epilogue stays in packed fp32 (v_pk_add / v_pk_fma): the statistics
+//   * the epilogue stays in fp32 (v_pk_add / v_pk_fma): the statistics
 //     accumulate in fp32 registers (exact: integers below 2^24, flushed to
 //     integers every BF_FLUSH tiles) and the int16 outputs come from the
-//     float bits after adding 1.5 * 2^23, paired by v_perm and exchanged by
-//     v_permlane32_swap into whole 16-B slot stores;
+//     float bits after adding 1.5 * 2^23, paired by v_perm, exchanged by
+//     v_permlane32_swap into 16-B slots and staged through a per-wave LDS
+//     area so every global store writes whole 128-B rows;
 //   * the statistics are reduced once per flush: a reduce-scatter over the
 //     lanes, one LDS pass at the end, 128 int64 atomics per block.
 // Reference: the QuantConv2D -> BatchNorm pairs of
@@ -35,16 +36,17 @@ constexpr int BF_C = 64;        // input and output channels
 constexpr int BF_TM = 256;      // pixels per tile (4 waves x 64)
 constexpr int BF_NT = 256;      // threads per block
 constexpr int BF_ROW = 32;      // bytes per pixel (64 e2m1 nibbles)
-constexpr int BF_SEGR = BF_TM + 2;                  // staged rows per kernel row
-constexpr int BF_SEGCH = BF_SEGR * BF_ROW / 16;     // 16-B chunks per segment (516)
-constexpr int BF_CH = 3 * BF_SEGCH;                 // chunks per stage (1548)
-constexpr int BF_ROUNDS = (BF_CH + BF_NT - 1) / BF_NT;               // DMA rounds (7)
-constexpr int BF_STAGE = ((BF_CH + 63) / 64) * 64 * 16;              // 25 KB
-constexpr int BF_NS = 2;                            // ring: issued one tile ahead
+constexpr int BF_WMAX = 60;     // widest image: the stage holds the union of the
+                                // three kernel rows' windows, BF_TM + 2 W + 2 rows
+constexpr int BF_CHMAX = 2 * (BF_TM + 2 * BF_WMAX + 2);   // 16-B chunks per stage (756)
+constexpr int BF_ROUNDS = (BF_CHMAX + BF_NT - 1) / BF_NT;  // DMA rounds (3)
+constexpr int BF_STAGE = BF_ROUNDS * BF_NT * 16;           // 12 KB
+constexpr int BF_NS = 3;                            // ring: issued two tiles ahead
 constexpr int BF_WBYTES = 9 * BF_C * BF_ROW;        // weight image, 18 KB
 constexpr int BF_WOFF = BF_NS * BF_STAGE;
 constexpr int BF_PADOFF = BF_WOFF + BF_WBYTES;      // 16-B pad fragment
-constexpr int BF_LDS = BF_PADOFF + 16;
+constexpr int BF_YOFF = BF_PADOFF + 16;             // output staging, 4 KB per wave
+constexpr int BF_LDS = BF_YOFF + 4 * 32 * 128;
 constexpr int BF_FLUSH = 24;   // tiles between statistics flushes: 2 pixels per
                                // lane and tile, 24 * 2 * 576^2 < 2^24
 static_assert(2 * BF_LDS <= 160 * 1024, "two blocks per CU");
@@ -76,6 +78,40 @@ __device__ __forceinline__ int rsi32(int (&v)[32], int r32) {
   rsi_step<1>(v, r32);
   return v[0];
 }
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 24]
+__device__ __forceinline__ void bf_wait(int n) {
+  switch (n) {
+#define ZK_BFW(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    ZK_BFW(1) ZK_BFW(2) ZK_BFW(3) ZK_BFW(4) ZK_BFW(5) ZK_BFW(6) ZK_BFW(7) ZK_BFW(8)
+    ZK_BFW(9) ZK_BFW(10) ZK_BFW(11) ZK_BFW(12) ZK_BFW(13) ZK_BFW(14) ZK_BFW(15) ZK_BFW(16)
+    ZK_BFW(17) ZK_BFW(18) ZK_BFW(19) ZK_BFW(20) ZK_BFW(21) ZK_BFW(22) ZK_BFW(23) ZK_BFW(24)
+#undef ZK_BFW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// Diagnostic build only (-DZK_BFWD_STAMPS, tools/bfwd_stamps.cpp): per wave,
+// the shader cycles (s_memtime) of each phase of the tile loop.
+#ifdef ZK_BFWD_STAMPS
+__device__ unsigned long long g_bf_stamps[2048 * 4][6];
+#define BF_ST_BEGIN \
+  unsigned long long zb_t = __builtin_readcyclecounter(), zb[6] = {0, 0, 0, 0, 0, 0};
+#define BF_ST(k)                                                   \
+  {                                                                \
+    const unsigned long long t_ = __builtin_readcyclecounter();    \
+    zb[k] += t_ - zb_t;                                            \
+    zb_t = t_;                                                     \
+  }
+#define BF_ST_STORE                                                        \
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 2048)                        \
+    for (int k_ = 0; k_ < 6; ++k_) g_bf_stamps[blockIdx.x * 4 + (threadIdx.x >> 6)][k_] = zb[k_];
+#else
+#define BF_ST_BEGIN
+#define BF_ST(k)
+#define BF_ST_STORE
+#endif
 
 struct BfArgs {
   const unsigned char* x4;   // [M][32] e2m1 sign image (channel 2j: low nibble of byte j)
@@ -124,60 +160,66 @@ __global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
   if (tid < 4)
     reinterpret_cast<uint32_t*>(smem + BF_PADOFF)[tid] = a.pad_ones ? 0x22222222u : 0u;
 
-  // DMA plan: chunk q = j * 256 + tid of a stage -> byte offset from the
-  // tile's first pixel (LDS slot half c holds source half c ^ swz(row))
+  // DMA plan: stage row r <-> flattened pixel m0 - W - 1 + r (the union of
+  // the three kernel rows' windows); chunk q = j * 256 + tid -> byte offset
+  // from the tile's first pixel (LDS slot half c holds source half c ^ swz)
+  const int nch = 2 * (BF_TM + 2 * a.W + 2);
   int kb[BF_ROUNDS];
+  int nd = 0;  // DMA instructions of this wave per stage
 #pragma unroll
   for (int j = 0; j < BF_ROUNDS; ++j) {
     const int q = j * BF_NT + tid;
-    if (q < BF_CH) {
-      const int th = q / BF_SEGCH, w2 = q - th * BF_SEGCH;
-      const int row = w2 >> 1, c = w2 & 1;
-      kb[j] = ((th - 1) * a.W - 1 + row) * BF_ROW + ((c ^ bf_swz(row)) << 4);
-    } else {
-      kb[j] = -(1 << 30);  // past the stage: the zero page
-    }
+    nd += j * BF_NT + wave * 64 < nch;
+    const int row = q >> 1, c = q & 1;
+    kb[j] = q < nch ? (row - a.W - 1) * BF_ROW + ((c ^ bf_swz(row)) << 4)
+                    : -(1 << 30);  // past the stage: the zero page
   }
   auto issue = [&](int jt) {  // stage of this block's tile jt
     const int m0b = (blk + jt * nblk) * BF_TM * BF_ROW;
-    unsigned char* st = smem + (jt & 1) * BF_STAGE;
+    unsigned char* st = smem + (jt % BF_NS) * BF_STAGE;
 #pragma unroll
     for (int j = 0; j < BF_ROUNDS; ++j) {
       const int q0 = j * BF_NT + wave * 64;  // wave-uniform
-      if (q0 < BF_CH) {
+      if (q0 < nch) {
         const int off = m0b + kb[j];
         glds16((unsigned)off < (unsigned)Mb ? a.x4 + off : zp, st + q0 * 16);
       }
     }
   };
   if (n > 0) issue(0);
+  if (n > 1) issue(1);
 
-  // per-lane constants of the fragment reads: pixel row 64 wave + 32 u + r32
-  // + tw of kernel row th sits at stage + th * segment + 2 KB * wave + 1 KB *
-  // u + lo[tw]
-  int lo[3];
+  // per-lane constants of the fragment reads: tap (th, tw) of pixel 64 wave +
+  // 32 u + r32 is stage row 64 wave + 32 u + (r32 + th W + tw), at byte
+  // 2 KB * wave + 1 KB * u + lo[t]
+  int lo[9];
 #pragma unroll
-  for (int tw = 0; tw < 3; ++tw)
-    lo[tw] = (r32 + tw) * BF_ROW + ((h ^ bf_swz(r32 + tw)) << 4);
+  for (int t = 0; t < 9; ++t) {
+    const int row = r32 + (t / 3) * a.W + t % 3;
+    lo[t] = row * BF_ROW + ((h ^ bf_swz(row)) << 4);
+  }
   const int wlo = (r32 * BF_ROW) + ((h ^ bf_swz(r32)) << 4);  // weight row 32 e + r32
+  unsigned char* ys = smem + BF_YOFF + wave * (32 * 128);     // this wave's output rows
 
   f32x16 cs[2] = {}, cq[2] = {};
   long long tsum = 0;
   unsigned long long tsq = 0;
   const int ns = a.y ? 8 : 0;  // global stores per wave and tile
+  BF_ST_BEGIN
   for (int it = 0; it < n; ++it) {
-    // this tile's stage (DMA issued at the top of tile it - 1) has landed:
-    // only the previous tile's stores were issued after it
-    if (it == 0 || ns == 0)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    // this tile's stage has landed: issued at the top of tile it - 2 (or
+    // before the loop), it is followed by the stores of tiles it - 2 and
+    // it - 1 and the DMA of tile it + 1 (counted in issue order)
+    bf_wait(it == 0 ? (n > 1 ? nd : 0)
+                    : (it == 1 ? ns : 2 * ns) + (it + 1 < n ? nd : 0));
+    BF_ST(0)
     __syncthreads();
-    // every wave is past tile it - 1, whose stage the next DMA reuses
-    if (it + 1 < n) issue(it + 1);
+    BF_ST(1)
+    // every wave is past tile it - 1, whose stage the DMA of tile it + 2 reuses
+    if (it + 2 < n) issue(it + 2);
     const int m0 = (blk + it * nblk) * BF_TM;
     const bool full = m0 + BF_TM <= a.M;
-    const int sb = (it & 1) * BF_STAGE + wave * (64 * BF_ROW);
+    const int sb = (it % BF_NS) * BF_STAGE + wave * (64 * BF_ROW);
     // this lane's two pixels and their edge flags
     bool top[2], bot[2], lft[2], rgt[2], live[2];
 #pragma unroll
@@ -192,6 +234,7 @@ __global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
       lft[u] = ww > 0;
       rgt[u] = ww < a.W - 1;
     }
+    BF_ST(2)
     // ---- 9 taps x 2 channel halves x 2 pixel groups
     f32x16 acc[2][2];
 #pragma unroll
@@ -208,16 +251,13 @@ __global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
         if (th == 2) ok = ok && bot[u];
         if (tw == 0) ok = ok && lft[u];
         if (tw == 2) ok = ok && rgt[u];
-        const int off = ok ? sb + th * (BF_SEGCH * 16) + u * (32 * BF_ROW) + lo[tw] : BF_PADOFF;
+        const int off = ok ? sb + u * (32 * BF_ROW) + lo[t] : BF_PADOFF;
         const uint4 b = *reinterpret_cast<const uint4*>(smem + off);
 #pragma unroll
         for (int e = 0; e < 2; ++e) acc[u][e] = mfma_fp4(wv[e], b, t ? acc[u][e] : f32x16{});
       }
     }
-    // every wave is done with this tile's stage: it becomes the output staging
-    // area (4 KB per wave), until the DMA of tile it + 2 after the next barrier
-    __syncthreads();
-    unsigned char* ys = smem + (it & 1) * BF_STAGE + wave * (32 * 128);
+    BF_ST(3)
     // ---- epilogue in packed fp32: statistics, int16 rows staged through LDS
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -280,8 +320,11 @@ __global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
           *reinterpret_cast<uint4*>(a.y + (long long)(mg + p) * BF_C + sl * 8) = v;
       }
     }
+    BF_ST(4)
     if ((it + 1) % BF_FLUSH == 0) bf_flush(cs, cq, r32, tsum, tsq);
+    BF_ST(5)
   }
+  BF_ST_STORE
   bf_flush(cs, cq, r32, tsum, tsq);
 
   // ---- statistics: lane r32 of each half holds value r32 of the half
@@ -315,8 +358,9 @@ int bf_cus() {
 
 }  // namespace
 
-// Shape check of zk_bfwd64_fp4: 3x3 stride 1 'same', 64 -> 64 channels and
-// the flattened pixel count inside the float-reciprocal division range (the
+// Shape check of zk_bfwd64_fp4: 3x3 stride 1 'same', 64 -> 64 channels, the
+// image at most BF_WMAX wide (the stage holds 256 + 2 W + 2 rows) and the
+// flattened pixel count inside the float-reciprocal division range (the
 // statistics are exact at any size: fp32 below 2^24 between flushes, 32-bit
 // lane reductions below 2^32, 64-bit totals).
 ZK_EXPORT int zk_bfwd64_supported(int B, int H, int W, int Cin, int Cout, int kh, int kw,
@@ -324,7 +368,7 @@ ZK_EXPORT int zk_bfwd64_supported(int B, int H, int W, int Cin, int Cout, int kh
   const long long M = (long long)B * H * W;
   if (Cin != BF_C || Cout != BF_C || kh != 3 || kw != 3 || stride != 1 || pt != 1 || pl != 1)
     return 0;
-  return M > 0 && M < (1LL << 24) ? 1 : 0;
+  return M > 0 && M < (1LL << 24) && W <= BF_WMAX ? 1 : 0;
 }
 
 // y int16 [B][H][W][64] = 3x3 'same' binary conv of the e2m1 sign image x4
