@@ -285,9 +285,9 @@ __global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
           cq[e][r] = q2[0];
           cq[e][r + 1] = q2[1];
           // + 1.5 * 2^23: the low 16 bits of the float are the integer.  Scalar
-          // adds on purpose (the compiler pairs them into v_pk_add_f32 itself):
-          // spelled as one f32x2 add, hipcc (ROCm 7.2) packs the wrong halves
-          // below -- it reused element 0's bits for element 1.
+          // adds on purpose: spelled as one f32x2 add, hipcc (ROCm 7.2) packs
+          // the wrong halves below -- it reused element 0's bits for element 1
+          // (profiles/r6/bfwd.md).
           bits[r] = __builtin_bit_cast(uint32_t, c[r] + 12582912.f);
           bits[r + 1] = __builtin_bit_cast(uint32_t, c[r + 1] + 12582912.f);
         }

@@ -31,6 +31,7 @@
 // Reference anchor: the QuantConv2D stack whose backward this is
 // (/root/reference/examples/larq_experiment.py:62-99).
 #include "mfma_common.h"
+#include "splitk_tree.h"
 
 namespace {
 
@@ -283,8 +284,9 @@ __global__ __launch_bounds__(DP_NT, 1) void dgrad_deep_kernel(DeepDgradArgs a) {
 // (each 32-lane group reads 8 rows x 32 B).  sx rows of taps outside the
 // image read a 512-B pad row (zeros, or bf16 +1 for pad_values=1); dY rows
 // past the split read zeros.  Epilogue: the kernel STE mask and fp32 atomics
-// into dW, or plain stores of this split's partial into a slab (reduced in a
-// fixed order by igemm.hip's wgrad_reduce_kernel: deterministic mode).
+// into dW, or this split's partial into the level-0 slab of the in-launch
+// fixed-order split-K tree (splitk_tree.h; the default), or plain stores into
+// a slab reduced by igemm.hip's wgrad_reduce_kernel (tree off).
 // ===========================================================================
 __device__ __attribute__((aligned(512))) uint4 g_dz_page[32];  // 512 B of zeros
 
@@ -298,6 +300,7 @@ struct DeepWgradArgs {
   float clip;
   int kps;             // pixels per split (multiple of 64)
   int co_tiles, ci_tiles;
+  SkTree tree;         // tree mode (tree.dwn > 0): in-launch split-K combine
 };
 
 __device__ __forceinline__ uint4 wp_frag(const unsigned char* piece, int c0, int lane) {
@@ -448,6 +451,7 @@ __global__ __launch_bounds__(DP_NT, 1) void wgrad_deep_kernel(DeepWgradArgs a) {
   // ---- epilogue: acc[i][j] reg e = D[co][ci], co = co0 + arow0 + 16 i +
   // 4 (lane >> 4) + e, ci = ci0 + brow0 + 16 j + (lane & 15)
   const long long NTOT = 9LL * a.Cin;
+  const bool treed = a.tree.dwn > 0;
   float* sl = a.slab ? a.slab + (long long)split * a.Cout * NTOT : nullptr;
   const int ci = ci0 + brow0 + (lane & 15);
 #pragma unroll
@@ -459,12 +463,21 @@ __global__ __launch_bounds__(DP_NT, 1) void wgrad_deep_kernel(DeepWgradArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const long long idx = row + 16 * j;
-        if (sl)
+        if (treed) {
+          if (a.tree.levels > 0)
+            skt_store(a.tree, split, idx, acc[i][j][e]);
+          else if (fabsf(a.w[idx]) <= a.clip)
+            a.dw[idx] += acc[i][j][e];  // one split: this block owns the element
+        } else if (sl) {
           sl[idx] = acc[i][j][e];
-        else if (fabsf(a.w[idx]) <= a.clip)
+        } else if (fabsf(a.w[idx]) <= a.clip) {
           atomicAdd(a.dw + idx, acc[i][j][e]);
+        }
       }
     }
+  if (treed && a.tree.levels > 0)
+    skt_combine<DP_NT, 256, 256>(a.tree, tile, split, co0, (long long)tap * a.Cin + ci0, NTOT,
+                                 a.dw, a.w, a.clip, reinterpret_cast<int*>(smem));
 }
 
 bool g_dp_attr = false;
@@ -494,7 +507,7 @@ static void wgrad_deep_plan(long long P, int tiles, int target_blocks, long long
 int zk_wgrad_deep_impl(const void* dy, const void* sx, const void* w, void* dw, int B, int H,
                        int W, int Cin, int Cout, int pad_ones, float clip, int target_blocks,
                        void* slab, long long slab_bytes, long long* need, int* splits, bool dry,
-                       hipStream_t st) {
+                       bool tree, hipStream_t st) {
   if (Cin % 256 || Cout % 256 || B < 1 || H < 1 || W < 1) return (int)hipErrorInvalidValue;
   const long long P = (long long)B * H * W;
   if (P >= (1 << 24)) return (int)hipErrorInvalidValue;  // fdiv range
@@ -502,14 +515,29 @@ int zk_wgrad_deep_impl(const void* dy, const void* sx, const void* w, void* dw, 
   long long kps = 0;
   int ns = 0;
   wgrad_deep_plan(P, tiles, target_blocks, kps, ns);
-  const long long sb = (long long)ns * Cout * 9 * Cin * 4;
+  const long long dwn = (long long)Cout * 9 * Cin;
+  long long sb = (long long)ns * dwn * 4;
+  SkTree t{};
+  long long tf = 0, tc = 0;
+  const bool tree_plan = tree && skt_plan(ns, tiles, dwn, t, tf, tc);
+  if (tree_plan) sb = tf * 4;
   if (need) {
     *need = sb;
     return 0;
   }
-  if (slab && slab_bytes < sb) slab = nullptr;
-  if (splits) *splits = slab ? ns : 0;
+  int* cnt = nullptr;
+  const bool treed = tree_plan && (t.levels == 0 || (slab && slab_bytes >= sb)) &&
+                     (dry || (cnt = skt_counters(st)) != nullptr);
+  if (!treed && slab && slab_bytes < (long long)ns * dwn * 4) slab = nullptr;
+  if (splits) *splits = (!treed && slab) ? ns : 0;  // > 0: the caller reduces the slab
   if (dry) return 0;
+  if (treed) {
+    t.slab = t.levels > 0 ? (float*)slab : nullptr;
+    t.cnt = cnt;
+    slab = nullptr;
+  } else {
+    t = SkTree{};
+  }
   if (!g_wp_attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)wgrad_deep_kernel,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, DP_LDS);
@@ -518,7 +546,7 @@ int zk_wgrad_deep_impl(const void* dy, const void* sx, const void* w, void* dw, 
   }
   DeepWgradArgs a{(const uint16_t*)dy, (const uint16_t*)sx, (const float*)w, (float*)dw,
                   (float*)slab, B, H, W, Cin, Cout, pad_ones, clip, (int)kps, Cout / 256,
-                  Cin / 256};
+                  Cin / 256, t};
   (void)hipGetLastError();
   hipLaunchKernelGGL(wgrad_deep_kernel, dim3((unsigned)(tiles * ns)), dim3(DP_NT), DP_LDS, st, a);
   return (int)hipGetLastError();

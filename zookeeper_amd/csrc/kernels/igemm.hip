@@ -27,6 +27,7 @@
 //     per register group: the epilogue moves 8 B per access;
 //   * XCD-aware tile order: consecutive M tiles of one N tile share an XCD.
 #include "mfma_common.h"
+#include "splitk_tree.h"
 
 // bfwd.hip: the persistent 64 -> 64-channel 3x3 binary forward
 extern "C" int zk_bfwd64_supported(int B, int H, int W, int Cin, int Cout, int kh, int kw,
@@ -39,7 +40,7 @@ extern "C" int zk_bfwd64_fp4(const void* x4, const void* w4, void* y, void* stat
 int zk_wgrad_deep_impl(const void* dy, const void* sx, const void* w, void* dw, int B, int H,
                        int W, int Cin, int Cout, int pad_ones, float clip, int target_blocks,
                        void* slab, long long slab_bytes, long long* need, int* splits, bool dry,
-                       hipStream_t st);
+                       bool tree, hipStream_t st);
 
 namespace {
 
@@ -140,6 +141,10 @@ int g_opt_wgrad_deep = 1;
 // epilogue_prefetch (key 8): the LDS-epilogue dgrad prefetches its residual /
 // BN-input loads in groups of 4 chunks before they are needed.
 int g_opt_epilogue_prefetch = 1;
+// wgrad_tree (key 10): split-K weight gradients combined inside the launch
+// by the fixed-order tree (splitk_tree.h) instead of slab + wgrad_reduce_kernel
+// (off by default: ~1 % slower in the E18 step, profiles/r6/wgrad_tree.md).
+int g_opt_wgrad_tree = 0;
 
 // splits limited by the slab cap (plan_wgrad / plan_wgrad3)
 inline long long cap_splits(long long splits, long long dw_bytes) {
@@ -1461,7 +1466,7 @@ template <int BM, int BN, int WM, int WN, int BK, int NS>
 __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ sx,
     const float* __restrict__ w, float* __restrict__ dw, float* __restrict__ slab, IGeom g,
-    int pad_ones, float clip, int k_per_split, int m_tiles, int n_tiles) {
+    int pad_ones, float clip, int k_per_split, int m_tiles, int n_tiles, SkTree tree) {
   constexpr int NWAVES = WM * WN;
   constexpr int RA = BM * 2, RBB = BN * 2;      // bytes per pixel row of A / B
   constexpr int SA = BK * RA, SB = BK * RBB;    // bytes per stage
@@ -1595,12 +1600,14 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
     }
   }
 
-  // epilogue.  slab mode: plain stores of this split's partial dW into
-  // slab[split][Cout][T*Cin] (summed + masked by wgrad_reduce_kernel: plain
-  // stores run at ~6 TB/s, fp32 atomics at ~1.3 TB/s of added bytes).
-  // Otherwise: kernel STE mask and fp32 atomics straight into dW.
+  // epilogue.  Tree mode (tree.slab): this split's partial into the level-0
+  // slab, then the in-launch fixed-order combine (splitk_tree.h); a single
+  // split adds straight into dW.  Slab mode: plain stores into
+  // slab[split][Cout][T*Cin] for wgrad_reduce_kernel.  Otherwise: kernel STE
+  // mask and fp32 atomics straight into dW.
   const int h = lane >> 5, r32 = lane & 31;
   const int NTOT = g.kh * g.kw * g.Cin;
+  const bool treed = tree.slab != nullptr || (tree.levels == 0 && tree.dwn > 0);
   float* sl = slab ? slab + (long long)split * g.Cout * NTOT : nullptr;
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
@@ -1611,52 +1618,63 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void igemm_wgrad_kernel(
       for (int b = 0; b < TN; ++b) {
         const int n = n0 + wn * WTN + b * 32 + r32;
         const long long idx = (long long)co * NTOT + n;
-        if (sl)
+        if (treed) {
+          if (tree.levels > 0)
+            skt_store(tree, split, idx, acc[a][b][r]);
+          else if (!w || fabsf(w[idx]) <= clip)
+            dw[idx] += acc[a][b][r];  // one split: this block owns the element
+        } else if (sl) {
           sl[idx] = acc[a][b][r];
-        else if (fabsf(w[idx]) <= clip)
+        } else if (fabsf(w[idx]) <= clip) {
           atomicAdd(dw + idx, acc[a][b][r]);
+        }
       }
     }
   }
+  if (treed && tree.levels > 0)
+    skt_combine<NWAVES * 64, BM, BN>(tree, tile, split, m0, n0, NTOT, dw, w, clip,
+                                     reinterpret_cast<int*>(smem));
 }
 
-// dW[i] += [|w[i]| <= clip] * sum_s slab[s][i].  Block = 16 float4 columns
-// x 16 split lanes (each lane sums every 16th split), then an LDS reduction:
-// many splits (small dW, long K) still spread over many threads.
+// dW[i] += [|w[i]| <= clip] * sum_s slab[s][i], the splits summed in index
+// order.  One float4 column per thread, the split loads 8 at a time (the sum
+// stays sequential): a streaming pass over the slabs at HBM rate.  (Round 5's
+// form -- 16 columns x 16 split lanes per block and an LDS reduction, ~37k
+// blocks for a 2.4 M-float dW -- ran at ~0.5 TB/s: ~70 us per layer.)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float4* __restrict__ slab,
                                                            int splits, long long n4,
                                                            const float4* __restrict__ w,
                                                            float clip, float4* __restrict__ dw) {
-  const int c = threadIdx.x & 15, sl = threadIdx.x >> 4;
-  const long long i = (long long)blockIdx.x * 16 + c;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
   float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (i < n4)
-    for (int sp = sl; sp < splits; sp += 16) {
-      const float4 v = slab[(long long)sp * n4 + i];
-      t.x += v.x;
-      t.y += v.y;
-      t.z += v.z;
-      t.w += v.w;
+  int sp = 0;
+  for (; sp + 8 <= splits; sp += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = slab[(long long)(sp + u) * n4 + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      t.x += v[u].x;
+      t.y += v[u].y;
+      t.z += v[u].z;
+      t.w += v[u].w;
     }
-  __shared__ float4 red[16][17];
-  red[sl][c] = t;
-  __syncthreads();
-  if (sl == 0 && i < n4) {
-    for (int k = 1; k < 16; ++k) {
-      const float4 v = red[k][c];
-      t.x += v.x;
-      t.y += v.y;
-      t.z += v.z;
-      t.w += v.w;
-    }
-    const float4 wv = w ? w[i] : make_float4(0.f, 0.f, 0.f, 0.f);  // no w: no mask
-    float4 d = dw[i];
-    d.x += fabsf(wv.x) <= clip ? t.x : 0.f;
-    d.y += fabsf(wv.y) <= clip ? t.y : 0.f;
-    d.z += fabsf(wv.z) <= clip ? t.z : 0.f;
-    d.w += fabsf(wv.w) <= clip ? t.w : 0.f;
-    dw[i] = d;
   }
+  for (; sp < splits; ++sp) {
+    const float4 v = slab[(long long)sp * n4 + i];
+    t.x += v.x;
+    t.y += v.y;
+    t.z += v.z;
+    t.w += v.w;
+  }
+  const float4 wv = w ? w[i] : make_float4(0.f, 0.f, 0.f, 0.f);  // no w: no mask
+  float4 d = dw[i];
+  d.x += fabsf(wv.x) <= clip ? t.x : 0.f;
+  d.y += fabsf(wv.y) <= clip ? t.y : 0.f;
+  d.z += fabsf(wv.z) <= clip ? t.z : 0.f;
+  d.w += fabsf(wv.w) <= clip ? t.w : 0.f;
+  dw[i] = d;
 }
 
 struct WgradPlan {
@@ -1695,8 +1713,14 @@ int launch_igemm_wgrad(const void* dy, const void* sx, const void* w, void* dw, 
     return (int)hipErrorInvalidValue;
   const int NTOT = g.kh * g.kw * g.Cin;
   const long long slab_bytes = (long long)p.splits * g.Cout * NTOT * 4;
-  if (ws_needed) {  // size query only
-    *ws_needed = slab_bytes;
+  if (ws_needed) {  // size query only: the tree's levels when it applies
+    SkTree t;
+    long long tf = 0, tc = 0;
+    const long long tiles = (long long)p.m_tiles * p.n_tiles;
+    *ws_needed = (g_opt_wgrad_tree && skt_plan(p.splits, (int)tiles, (long long)g.Cout * NTOT, t,
+                                               tf, tc))
+                     ? tf * 4
+                     : slab_bytes;
     return 0;
   }
   constexpr int LDS = NS * BK * (BM + BN) * 2;
@@ -1709,14 +1733,30 @@ int launch_igemm_wgrad(const void* dy, const void* sx, const void* w, void* dw, 
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  float* slab = (ws && ws_bytes >= slab_bytes && NTOT % 4 == 0) ? (float*)ws : nullptr;
   const long long tiles = (long long)p.m_tiles * p.n_tiles;
+  // the in-launch tree when its slab and counters are available, else the
+  // slab + wgrad_reduce_kernel pair
+  SkTree tree{};
+  long long tree_floats = 0, tree_cnt = 0;
+  int* cnt = nullptr;
+  const bool tree_ok = g_opt_wgrad_tree && ws && NTOT % 4 == 0 &&
+                       skt_plan(p.splits, (int)tiles, (long long)g.Cout * NTOT, tree,
+                                tree_floats, tree_cnt) &&
+                       ws_bytes >= tree_floats * 4 && (cnt = skt_counters(stream)) != nullptr;
+  float* slab = nullptr;
+  if (tree_ok) {
+    tree.slab = tree.levels > 0 ? (float*)ws : nullptr;
+    tree.cnt = cnt;
+  } else {
+    tree = SkTree{};
+    slab = (ws && ws_bytes >= slab_bytes && NTOT % 4 == 0) ? (float*)ws : nullptr;
+  }
   hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * p.splits)), dim3(WM * WN * 64), LDS, stream,
                      (const uint16_t*)dy, (const uint16_t*)sx, (const float*)w, (float*)dw, slab,
-                     g, pad_ones, clip, p.kps, p.m_tiles, p.n_tiles);
+                     g, pad_ones, clip, p.kps, p.m_tiles, p.n_tiles, tree);
   if (slab) {
     const long long n4 = (long long)g.Cout * NTOT / 4;
-    const long long blocks = (n4 + 15) / 16;
+    const long long blocks = (n4 + 255) / 256;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
                        (const float4*)slab, p.splits, n4, (const float4*)w, clip, (float4*)dw);
   }
@@ -1956,7 +1996,7 @@ int launch_igemm_wgrad3(const void* dy, const void* sx, const void* w, void* dw,
                      g, pad_ones, clip, p.kps, p.m_tiles, p.n_tiles);
   if (slab) {
     const long long n4 = (long long)g.Cout * NTOT / 4;
-    const long long blocks = (n4 + 15) / 16;
+    const long long blocks = (n4 + 255) / 256;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
                        (const float4*)slab, p.splits, n4, (const float4*)w, clip, (float4*)dw);
   }
@@ -1970,14 +2010,15 @@ int igemm_wgrad_variant(int v, const void* dy, const void* sx, const void* w, vo
   return launch_igemm_wgrad<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, ws, wsb, need, st)
 #define ZK_IGW3(...) \
   return launch_igemm_wgrad3<__VA_ARGS__>(dy, sx, w, dw, g, po, clip, tb, ws, wsb, need, st)
-  if (v == 60) {  // deep_gemm.hip phased 256x256 kernel + the fixed-order slab reduce
+  if (v == 60) {  // deep_gemm.hip phased 256x256 kernel + its fixed-order split-K combine
     if (!conv3_ok(g, 0)) return (int)hipErrorInvalidValue;
     int splits = 0;
     const int rc = zk_wgrad_deep_impl(dy, sx, w, dw, g.B, g.H, g.W, g.Cin, g.Cout, po, clip, tb,
-                                      ws, wsb, need, &splits, need != nullptr || g_dry_run, st);
-    if (rc || need || g_dry_run || splits == 0) return rc;
+                                      ws, wsb, need, &splits, need != nullptr || g_dry_run,
+                                      g_opt_wgrad_tree != 0, st);
+    if (rc || need || g_dry_run || splits == 0) return rc;  // splits 0: combined in-launch
     const long long n4 = (long long)g.Cout * 9 * g.Cin / 4;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st,
                        (const float4*)ws, splits, n4, (const float4*)w, clip, (float4*)dw);
     return 0;
   }
@@ -2281,7 +2322,7 @@ ZK_EXPORT int zk_wgrad_slab_reduce(const void* slab, int splits, long long n, co
                                    float clip, void* dw, hipStream_t stream) {
   if (n % 4 || splits < 1) return (int)hipErrorInvalidValue;
   const long long n4 = n / 4;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, stream,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream,
                      (const float4*)slab, splits, n4, (const float4*)w, clip, (float4*)dw);
   ZK_CHECK_LAUNCH();
   return 0;
@@ -2454,6 +2495,7 @@ ZK_EXPORT int zk_set_option(int key, int value) {
     case 7: g_opt_wgrad_deep = value; return 0;
     case 8: g_opt_epilogue_prefetch = value; return 0;
     case 9: g_opt_lab_fwd_no_y = value; return 0;
+    case 10: g_opt_wgrad_tree = value; return 0;
     default: return -1;
   }
 }
@@ -2468,6 +2510,7 @@ ZK_EXPORT int zk_get_option(int key) {
     case 7: return g_opt_wgrad_deep;
     case 8: return g_opt_epilogue_prefetch;
     case 9: return g_opt_lab_fwd_no_y;
+    case 10: return g_opt_wgrad_tree;
     default: return -1;
   }
 }

@@ -79,6 +79,12 @@ class KernelOptions:
     # half the CUs).  Peak slab at batch 1536: ~134 MB (14x14x256, 57 x
     # 2.36 MB) and ~141 MB (7x7x512, 15 x 9.4 MB), freed after the layer.
     wgrad_deep: bool = True
+    # Split-K of the igemm / deep weight gradients combined inside the launch
+    # by a fixed-order tree (splitk_tree.h) instead of per-split slabs and a
+    # streaming reduce launch.  Both are bit-reproducible.  Off: same-box E18
+    # b1536 pairs 54.05k / 54.30k (reduce launch) vs 53.55k / 53.66k img/s
+    # (tree) -- profiles/r6/wgrad_tree.md.
+    wgrad_tree: bool = False
     # Float BatchNorm backward sums (sum g, sum g*xhat) added up in the data-
     # gradient epilogue of the 1x1 conv that consumes the BN output (when that
     # epilogue writes the BN output's whole gradient) instead of a separate
@@ -104,7 +110,7 @@ OPTS = KernelOptions()
 
 # keys the native library reads (zk_set_option); values are ints
 _NATIVE_KEYS = {"tile_huge": 0, "deterministic": 2, "dgrad_rw": 3, "wgrad_slab_mb": 5,
-                "dgrad_deep": 6, "wgrad_deep": 7, "epilogue_prefetch": 8}
+                "dgrad_deep": 6, "wgrad_deep": 7, "epilogue_prefetch": 8, "wgrad_tree": 10}
 
 
 def _push_native() -> None:

@@ -47,6 +47,7 @@ class Runtime:
     wgrad_fp4: bool = Field(True)
     dgrad_deep: int = Field(1)
     wgrad_deep: bool = Field(True)
+    wgrad_tree: bool = Field(False)
     weight_images: bool = Field(True)
     bn_bwd_fuse: bool = Field(True)
     bn_masked_handoff: bool = Field(True)
