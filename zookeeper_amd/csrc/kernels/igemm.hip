@@ -2395,7 +2395,7 @@ ZK_EXPORT int zk_igemm_fwd_fp4(const void* sx4, const void* wf4, void* y, void* 
     const bool wide = Cin % 256 == 0 && Cout % 256 == 0 && Po >= 25088;
     if (c3 && Cin == 64 && Cout == 64 && Ho == H && Wo == W &&
         zk_bfwd64_supported(B, H, W, Cin, Cout, kh, kw, stride, pt, pl))
-      variant = 40;  // persistent, weights in registers (bfwd.hip): 285 -> see profiles/r6
+      variant = 40;  // persistent, LDS-resident weights (bfwd.hip, profiles/r6/bfwd.md)
     else if (c3 && Cin == 64)
       variant = 20;
     else if (c3 && Cin == 256 && Cout % 256 == 0)
