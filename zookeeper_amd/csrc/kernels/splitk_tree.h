@@ -19,6 +19,14 @@
 
 #include "mfma_common.h"
 
+// The publish protocol (relaxed agent-scope stores, vmcnt(0), relaxed counter
+// atomic; the reader's sc1 loads, no acquire fence) relies on gfx950's sc1
+// write-through behaviour, not on the HIP memory model alone: refuse other
+// targets rather than produce silently wrong gradients.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "splitk_tree.h: the fence-free publish protocol is specific to gfx950"
+#endif
+
 namespace {
 
 constexpr int SKT_G = 8;          // fan-in

@@ -49,6 +49,13 @@
 
 #include "mfma_common.h"
 
+// The in-launch tree's fence-free publish (relaxed agent-scope stores,
+// vmcnt(0), relaxed counter atomic, sc1 loads without an acquire) relies on
+// gfx950's sc1 write-through behaviour: refuse other targets.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "wgrad_rows.hip: the fence-free split-K publish protocol is specific to gfx950"
+#endif
+
 namespace {
 
 constexpr int WR_NT = 256;     // 4 waves
