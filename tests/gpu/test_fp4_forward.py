@@ -107,32 +107,36 @@ def test_igemm_fwd_fp4_exact(cin, cout, stride, hw, pad_ones, relu):
     assert torch.equal(tot[0], flat.sum(0).cpu()) and torch.equal(tot[1], (flat * flat).sum(0).cpu())
 
 
-@pytest.mark.parametrize("B,hw,pad_ones,relu",
-                         [(256, 56, 0, 0), (37, 28, 1, 1), (61, 15, 0, 1), (2800, 56, 1, 0)])
-def test_bfwd64_persistent_matches_conv3(B, hw, pad_ones, relu):
-    """The persistent 64 -> 64 kernel (variant 40, bfwd.hip) walks many tiles
-    per block at these sizes (the float64 test above covers one or two): its
-    int16 outputs and striped int64 statistics (flushed mid-run at batch 2800)
-    equal the conv3 tile's (variant 20, itself exact against float64) bit for
-    bit, tail tiles included."""
+@pytest.mark.parametrize("cin,B,hw,pad_ones,relu", [
+    (64, 256, 56, 0, 0), (64, 37, 28, 1, 1), (64, 61, 15, 0, 1), (64, 2800, 56, 1, 0),
+    (128, 256, 28, 0, 0), (128, 37, 28, 1, 1), (128, 61, 15, 0, 1), (128, 900, 28, 1, 0),
+])
+def test_bfwd_persistent_matches_conv3(cin, B, hw, pad_ones, relu):
+    """The persistent kernel (variant 40, bfwd.hip; Cin 64: 256-pixel tiles,
+    Cin 128: 512-pixel tiles and one 64-channel output slice per block) walks
+    many tiles per block at these sizes (the float64 test above covers one or
+    two): its int16 outputs and striped int64 statistics (flushed mid-run at
+    batch 2800 / 900) equal the conv3 tile's (variant 20, itself exact
+    against float64) bit for bit, tail tiles included."""
     from zookeeper_amd.ops._native import lib, stream_ptr
 
     torch.manual_seed(11)
     L, st = lib(), stream_ptr()
-    x = torch.randn(B, hw, hw, 64, device="cuda").to(torch.bfloat16)
-    w = torch.randn(64, 3, 3, 64, device="cuda")
-    sx4 = torch.empty(B, hw, hw, 32, dtype=torch.uint8, device="cuda")
+    cout = cin
+    x = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
+    w = torch.randn(cout, 3, 3, cin, device="cuda")
+    sx4 = torch.empty(B, hw, hw, cin // 2, dtype=torch.uint8, device="cuda")
     assert L.zk_sign_pack(x.data_ptr(), None, None, None, sx4.data_ptr(), x.numel() // 32, 1.0,
                           st) == 0
-    wf4 = torch.empty(9, 64, 32, dtype=torch.uint8, device="cuda")
-    assert L.zk_weight_pack(w.data_ptr(), None, None, None, None, wf4.data_ptr(), 64, 9, 64,
+    wf4 = torch.empty(9, cout, cin // 2, dtype=torch.uint8, device="cuda")
+    assert L.zk_weight_pack(w.data_ptr(), None, None, None, None, wf4.data_ptr(), cout, 9, cin,
                             st) == 0
     out = {}
     for v, stripes in ((20, 1), (40, 1), (40, 32)):
-        y = torch.full((B, hw, hw, 64), -12345, dtype=torch.int16, device="cuda")
-        stats = torch.zeros(stripes, 2, 64, dtype=torch.int64, device="cuda")
+        y = torch.full((B, hw, hw, cout), -12345, dtype=torch.int16, device="cuda")
+        stats = torch.zeros(stripes, 2, cout, dtype=torch.int64, device="cuda")
         assert L.zk_igemm_fwd_fp4(sx4.data_ptr(), wf4.data_ptr(), y.data_ptr(), stats.data_ptr(),
-                                  B, hw, hw, 64, 64, 3, 3, 1, 1, 1, hw, hw, pad_ones, relu, v,
+                                  B, hw, hw, cin, cout, 3, 3, 1, 1, 1, hw, hw, pad_ones, relu, v,
                                   stripes, st) == 0
         torch.cuda.synchronize()
         out[(v, stripes)] = (y, stats.sum(0))

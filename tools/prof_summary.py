@@ -32,7 +32,7 @@ FAMILY_RULES = [
     ("conv3rw_dgrad", "data gradient (MFMA)"),
     ("bconv_dgrad", "data gradient (MFMA)"),
     ("igemm_conv3_kernel<true", "conv forward (MFMA; binary ±1 or float)"),
-    ("bfwd64_kernel", "conv forward (MFMA; binary ±1 or float)"),
+    ("bfwd", "conv forward (MFMA; binary ±1 or float)"),
     ("igemm_conv_kernel<true", "conv forward (MFMA; binary ±1 or float)"),
     ("bconv_fwd", "conv forward (MFMA; binary ±1 or float)"),
     # FWD=false: the data gradients and the float 1x1 forward GEMMs

@@ -1,9 +1,9 @@
-// Persistent binary forward for the 64 -> 64-channel 3x3 stride-1 'same'
-// convolutions (BinaryResNet-E18 stage 1, QuickNet's first section) on MX-FP4
-// MFMA, for gfx950.
+// Persistent binary forward for the 3x3 stride-1 'same' convolutions with 64
+// or 128 input channels (BinaryResNet-E18 stages 1-2, QuickNet's first
+// sections) on MX-FP4 MFMA, for gfx950.
 //
-// y[m][co] = sum over the 9 taps and 64 input channels of sign(x) * sign(W)
-// (exact integers, |y| <= 576) as int16, plus the per-channel sum and sum of
+// y[m][co] = sum over the 9 taps and Cin input channels of sign(x) * sign(W)
+// (exact integers, |y| <= 9 Cin) as int16, plus the per-channel sum and sum of
 // squares for the following BatchNorm -- the same outputs, bit for bit, as
 // igemm.hip's conv3 forward (igemm_conv3_kernel<true, ..., F4>, 285-317 us
 // at batch 1536: 37.6k short-lived blocks, each with its own prologue, three
@@ -26,37 +26,49 @@
 //     area so every global store writes whole 128-B rows;
 //   * the statistics are reduced once per flush: a reduce-scatter over the
 //     lanes, one LDS pass at the end, 128 int64 atomics per block.
+// Cin = 128 (BfCfg<128, 8, 2, 32>): one 8-wave block per CU, 512-pixel
+// tiles, two-stage ring; each block owns one 64-channel slice of the output
+// (its 36 KB weight image in LDS), so the input is read once per slice.
 // Reference: the QuantConv2D -> BatchNorm pairs of
 // /root/reference/examples/larq_experiment.py:71-91.
 #include "mfma_common.h"
 
 namespace {
 
-constexpr int BF_C = 64;        // input and output channels
-constexpr int BF_TM = 256;      // pixels per tile (4 waves x 64)
-constexpr int BF_NT = 256;      // threads per block
-constexpr int BF_ROW = 32;      // bytes per pixel (64 e2m1 nibbles)
-constexpr int BF_WMAX = 60;     // widest image: the stage holds the union of the
-                                // three kernel rows' windows, BF_TM + 2 W + 2 rows
-constexpr int BF_CHMAX = 2 * (BF_TM + 2 * BF_WMAX + 2);   // 16-B chunks per stage (756)
-constexpr int BF_ROUNDS = (BF_CHMAX + BF_NT - 1) / BF_NT;  // DMA rounds (3)
-constexpr int BF_STAGE = BF_ROUNDS * BF_NT * 16;           // 12 KB
-constexpr int BF_NS = 3;                            // ring: issued two tiles ahead
-constexpr int BF_WBYTES = 9 * BF_C * BF_ROW;        // weight image, 18 KB
-constexpr int BF_WOFF = BF_NS * BF_STAGE;
-constexpr int BF_PADOFF = BF_WOFF + BF_WBYTES;      // 16-B pad fragment
-constexpr int BF_YOFF = BF_PADOFF + 16;             // output staging, 4 KB per wave
-constexpr int BF_LDS = BF_YOFF + 4 * 32 * 128;
-constexpr int BF_FLUSH = 24;   // tiles between statistics flushes: 2 pixels per
-                               // lane and tile, 24 * 2 * 576^2 < 2^24
-static_assert(2 * BF_LDS <= 160 * 1024, "two blocks per CU");
-
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// Swizzle of the two 16-B halves of a staged pixel row: rows 8..15 of every
-// 16 swap them, so the fragment reads of 16 consecutive rows (same half) hit
-// 16 distinct 16-B bank slots.
-__device__ __forceinline__ int bf_swz(int row) { return (row >> 3) & 1; }
+// Tile / LDS plan of one instantiation: CIN input channels (64 or 128), NW
+// waves per block (64 pixels each), NS-stage input ring, images at most WMAX
+// wide.  Each block computes one 64-channel slice of the output.
+template <int CIN_, int NW_, int NS_, int WMAX_>
+struct BfCfg {
+  static constexpr int CIN = CIN_, NW = NW_, NS = NS_, WMAX = WMAX_;
+  static constexpr int NT = NW * 64;                 // threads per block
+  static constexpr int TM = NW * 64;                 // pixels per tile
+  static constexpr int ROW = CIN / 2;                // bytes per pixel row (e2m1)
+  static constexpr int CH = ROW / 16;                // 16-B chunks per row
+  static constexpr int KC = CIN / 64;                // MFMA K-chunks per tap
+  static constexpr int RPB = 256 / ROW;              // rows per 256-B bank window
+  static constexpr int CHMAX = CH * (TM + 2 * WMAX + 2);   // chunks of the widest stage
+  static constexpr int ROUNDS = (CHMAX + NT - 1) / NT;     // DMA rounds per stage
+  static constexpr int STAGE = ROUNDS * NT * 16;
+  static constexpr int WBYTES = 9 * 64 * ROW;        // weight image of one output slice
+  static constexpr int WOFF = NS * STAGE;
+  static constexpr int PADOFF = WOFF + WBYTES;       // 16-B pad fragment
+  static constexpr int YOFF = PADOFF + 16;           // output staging, 4 KB per wave
+  static constexpr int LDS = YOFF + NW * 32 * 128;
+  static constexpr int OCC = (2 * LDS <= 160 * 1024) ? 2 : 1;  // blocks per CU
+  // tiles between statistics flushes: 2 pixels per lane and tile, the fp32
+  // sums of squares exact below 2^24
+  static constexpr int FLUSH = (1 << 24) / (2 * (9 * CIN) * (9 * CIN));
+  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(FLUSH >= 1, "flush interval");
+  // Swizzle of a staged row's 16-B chunks: the fragment reads of 16
+  // consecutive rows (same chunk) hit 16 distinct 16-B bank slots.
+  __device__ static __forceinline__ int swz(int row) { return (row / RPB) % CH; }
+};
+using Bf64 = BfCfg<64, 4, 3, 60>;    // 2 blocks per CU, 256-pixel tiles, 3-stage ring
+using Bf128 = BfCfg<128, 8, 2, 32>;  // 1 block per CU, 512-pixel tiles, 2-stage ring
 
 // Reduce-scatter of 32 ints over the 32 lanes of a wave half (lane r ends
 // with the half's total of value r).
@@ -95,7 +107,7 @@ __device__ __forceinline__ void bf_wait(int n) {
 // Diagnostic build only (-DZK_BFWD_STAMPS, tools/bfwd_stamps.cpp): per wave,
 // the shader cycles (s_memtime) of each phase of the tile loop.
 #ifdef ZK_BFWD_STAMPS
-__device__ unsigned long long g_bf_stamps[2048 * 4][6];
+__device__ unsigned long long g_bf_stamps[2048 * 8][6];
 #define BF_ST_BEGIN \
   unsigned long long zb_t = __builtin_readcyclecounter(), zb[6] = {0, 0, 0, 0, 0, 0};
 #define BF_ST(k)                                                   \
@@ -106,7 +118,8 @@ __device__ unsigned long long g_bf_stamps[2048 * 4][6];
   }
 #define BF_ST_STORE                                                        \
   if ((threadIdx.x & 63) == 0 && blockIdx.x < 2048)                        \
-    for (int k_ = 0; k_ < 6; ++k_) g_bf_stamps[blockIdx.x * 4 + (threadIdx.x >> 6)][k_] = zb[k_];
+    for (int k_ = 0; k_ < 6; ++k_)                                         \
+      g_bf_stamps[blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)][k_] = zb[k_];
 #else
 #define BF_ST_BEGIN
 #define BF_ST(k)
@@ -114,11 +127,11 @@ __device__ unsigned long long g_bf_stamps[2048 * 4][6];
 #endif
 
 struct BfArgs {
-  const unsigned char* x4;   // [M][32] e2m1 sign image (channel 2j: low nibble of byte j)
-  const unsigned char* w4;   // [9][64][32] e2m1 weight signs
-  short* y;                  // [M][64] int16
-  unsigned long long* stats;  // [stripes][2][64] int64 (sum; sum of squares)
-  int M, H, W, stripes, ntiles;
+  const unsigned char* x4;   // [M][Cin/2] e2m1 sign image (channel 2j: low nibble of byte j)
+  const unsigned char* w4;   // [9][Cout][Cin/2] e2m1 weight signs
+  short* y;                  // [M][Cout] int16
+  unsigned long long* stats;  // [stripes][2][Cout] int64 (sum; sum of squares)
+  int M, H, W, Cout, nsl, stripes, ntiles;
   int pad_ones;
   float inv_w, inv_h;
 };
@@ -138,68 +151,100 @@ __device__ __forceinline__ void bf_flush(f32x16 (&cs)[2], f32x16 (&cq)[2], int r
   for (int e = 0; e < 2; ++e) cs[e] = cq[e] = f32x16{};
 }
 
-template <bool RELU>
-__global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
+// vm ops a wave issued after the DMA of its tile `it` (issue order: the
+// prologue's LA stages, then per tile the DMA of tile + LA after the barrier
+// and the tile's ns stores; nd DMA instructions per stage)
+template <int LA>
+__device__ __forceinline__ int bf_after(int it, int n, int nd, int ns) {
+  int after = 0;
+  if (it < LA) {
+#pragma unroll
+    for (int j = 1; j < LA; ++j) after += (it + j < LA && it + j < n) ? nd : 0;
+    for (int k = 0; k < it; ++k) after += (k + LA < n ? nd : 0) + ns;
+  } else {
+    after += ns;
+#pragma unroll
+    for (int d = 1; d < LA; ++d) {
+      const int k = it - LA + d;
+      after += (k + LA < n ? nd : 0) + ns;
+    }
+  }
+  return after;
+}
+
+template <class C, bool RELU>
+__global__ __launch_bounds__(C::NT, C::OCC) void bfwd_kernel(BfArgs a) {
+  constexpr int NT = C::NT, TM = C::TM, ROW = C::ROW, CH = C::CH, KC = C::KC;
+  constexpr int LA = C::NS - 1;  // tiles of DMA lookahead
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, h = lane >> 5;
-  const int blk = xcd_linear(blockIdx.x, gridDim.x), nblk = gridDim.x;
+  // logical block: output slice L % nsl, tile stream L / nsl
+  const int L = xcd_linear(blockIdx.x, gridDim.x);
+  const int slice = L % a.nsl, blk = L / a.nsl, nblk = gridDim.x / a.nsl;
   const int n = blk < a.ntiles ? (a.ntiles - 1 - blk) / nblk + 1 : 0;
   const unsigned char* zp = reinterpret_cast<const unsigned char*>(g_zero_page);
-  const int Mb = a.M * BF_ROW;
+  const int Mb = a.M * ROW;
 
-  // weight image [t][co][32 B] -> LDS (halves swizzled like the pixel rows),
-  // plus the pad fragment
-  unsigned char* wl = smem + BF_WOFF;
-  for (int q = tid; q < BF_WBYTES / 16; q += BF_NT) {
-    const int row = q >> 1, c = q & 1;
-    *reinterpret_cast<uint4*>(wl + row * BF_ROW + ((c ^ bf_swz(row)) << 4)) =
-        *reinterpret_cast<const uint4*>(a.w4 + q * 16);
+  // this slice's weight image [t][64 co][ROW] -> LDS (chunks swizzled like
+  // the pixel rows), plus the pad fragment
+  unsigned char* wl = smem + C::WOFF;
+  for (int q = tid; q < C::WBYTES / 16; q += NT) {
+    const int row = q / CH, c = q % CH;  // row = t * 64 + co
+    const int t = row >> 6, co = row & 63;
+    *reinterpret_cast<uint4*>(wl + row * ROW + ((c ^ C::swz(row)) << 4)) =
+        *reinterpret_cast<const uint4*>(a.w4 + ((long long)t * a.Cout + slice * 64 + co) * ROW +
+                                        c * 16);
   }
   if (tid < 4)
-    reinterpret_cast<uint32_t*>(smem + BF_PADOFF)[tid] = a.pad_ones ? 0x22222222u : 0u;
+    reinterpret_cast<uint32_t*>(smem + C::PADOFF)[tid] = a.pad_ones ? 0x22222222u : 0u;
 
   // DMA plan: stage row r <-> flattened pixel m0 - W - 1 + r (the union of
-  // the three kernel rows' windows); chunk q = j * 256 + tid -> byte offset
-  // from the tile's first pixel (LDS slot half c holds source half c ^ swz)
-  const int nch = 2 * (BF_TM + 2 * a.W + 2);
-  int kb[BF_ROUNDS];
+  // the three kernel rows' windows); chunk q = j * NT + tid -> byte offset
+  // from the tile's first pixel (LDS slot c holds source chunk c ^ swz(row))
+  const int nch = CH * (TM + 2 * a.W + 2);
+  int kb[C::ROUNDS];
   int nd = 0;  // DMA instructions of this wave per stage
 #pragma unroll
-  for (int j = 0; j < BF_ROUNDS; ++j) {
-    const int q = j * BF_NT + tid;
-    nd += j * BF_NT + wave * 64 < nch;
-    const int row = q >> 1, c = q & 1;
-    kb[j] = q < nch ? (row - a.W - 1) * BF_ROW + ((c ^ bf_swz(row)) << 4)
+  for (int j = 0; j < C::ROUNDS; ++j) {
+    const int q = j * NT + tid;
+    nd += j * NT + wave * 64 < nch;
+    const int row = q / CH, c = q % CH;
+    kb[j] = q < nch ? (row - a.W - 1) * ROW + ((c ^ C::swz(row)) << 4)
                     : -(1 << 30);  // past the stage: the zero page
   }
   auto issue = [&](int jt) {  // stage of this block's tile jt
-    const int m0b = (blk + jt * nblk) * BF_TM * BF_ROW;
-    unsigned char* st = smem + (jt % BF_NS) * BF_STAGE;
+    const int m0b = (blk + jt * nblk) * TM * ROW;
+    unsigned char* st = smem + (jt % C::NS) * C::STAGE;
 #pragma unroll
-    for (int j = 0; j < BF_ROUNDS; ++j) {
-      const int q0 = j * BF_NT + wave * 64;  // wave-uniform
+    for (int j = 0; j < C::ROUNDS; ++j) {
+      const int q0 = j * NT + wave * 64;  // wave-uniform
       if (q0 < nch) {
         const int off = m0b + kb[j];
         glds16((unsigned)off < (unsigned)Mb ? a.x4 + off : zp, st + q0 * 16);
       }
     }
   };
-  if (n > 0) issue(0);
-  if (n > 1) issue(1);
+#pragma unroll
+  for (int j = 0; j < LA; ++j)
+    if (j < n) issue(j);
 
-  // per-lane constants of the fragment reads: tap (th, tw) of pixel 64 wave +
-  // 32 u + r32 is stage row 64 wave + 32 u + (r32 + th W + tw), at byte
-  // 2 KB * wave + 1 KB * u + lo[t]
-  int lo[9];
+  // per-lane constants of the fragment reads: chunk 2 kc + h of tap (th, tw)
+  // of pixel 64 wave + 32 u + r32 is stage row 64 wave + 32 u + (r32 + th W +
+  // tw), at byte 64 ROW * wave + 32 ROW * u + lo[t][kc]
+  int lo[9][KC];
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     const int row = r32 + (t / 3) * a.W + t % 3;
-    lo[t] = row * BF_ROW + ((h ^ bf_swz(row)) << 4);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) lo[t][kc] = row * ROW + (((2 * kc + h) ^ C::swz(row)) << 4);
   }
-  const int wlo = (r32 * BF_ROW) + ((h ^ bf_swz(r32)) << 4);  // weight row 32 e + r32
-  unsigned char* ys = smem + BF_YOFF + wave * (32 * 128);     // this wave's output rows
+  int wlo[KC];  // weight row 32 e + r32 (t * 64 + 32 e: the same swizzle)
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) wlo[kc] = r32 * ROW + (((2 * kc + h) ^ C::swz(r32)) << 4);
+  unsigned char* ys = smem + C::YOFF + wave * (32 * 128);  // this wave's output rows
+  short* ybase = a.y ? a.y + slice * 64 : nullptr;
 
   f32x16 cs[2] = {}, cq[2] = {};
   long long tsum = 0;
@@ -207,19 +252,16 @@ __global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
   const int ns = a.y ? 8 : 0;  // global stores per wave and tile
   BF_ST_BEGIN
   for (int it = 0; it < n; ++it) {
-    // this tile's stage has landed: issued at the top of tile it - 2 (or
-    // before the loop), it is followed by the stores of tiles it - 2 and
-    // it - 1 and the DMA of tile it + 1 (counted in issue order)
-    bf_wait(it == 0 ? (n > 1 ? nd : 0)
-                    : (it == 1 ? ns : 2 * ns) + (it + 1 < n ? nd : 0));
+    // this tile's stage has landed
+    bf_wait(bf_after<LA>(it, n, nd, ns));
     BF_ST(0)
     __syncthreads();
     BF_ST(1)
-    // every wave is past tile it - 1, whose stage the DMA of tile it + 2 reuses
-    if (it + 2 < n) issue(it + 2);
-    const int m0 = (blk + it * nblk) * BF_TM;
-    const bool full = m0 + BF_TM <= a.M;
-    const int sb = (it % BF_NS) * BF_STAGE + wave * (64 * BF_ROW);
+    // every wave is past tile it - 1, whose stage the DMA of tile it + LA reuses
+    if (it + LA < n) issue(it + LA);
+    const int m0 = (blk + it * nblk) * TM;
+    const bool full = m0 + TM <= a.M;
+    const int sb = (it % C::NS) * C::STAGE + wave * (64 * ROW);
     // this lane's two pixels and their edge flags
     bool top[2], bot[2], lft[2], rgt[2], live[2];
 #pragma unroll
@@ -235,26 +277,30 @@ __global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
       rgt[u] = ww < a.W - 1;
     }
     BF_ST(2)
-    // ---- 9 taps x 2 channel halves x 2 pixel groups
+    // ---- 9 taps x KC K-chunks x 2 channel halves x 2 pixel groups
     f32x16 acc[2][2];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int th = t / 3, tw = t % 3;
-      uint4 wv[2];
 #pragma unroll
-      for (int e = 0; e < 2; ++e)
-        wv[e] = *reinterpret_cast<const uint4*>(wl + (t * BF_C + 32 * e) * BF_ROW + wlo);
+      for (int kc = 0; kc < KC; ++kc) {
+        uint4 wv[2];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        bool ok = live[u];
-        if (th == 0) ok = ok && top[u];
-        if (th == 2) ok = ok && bot[u];
-        if (tw == 0) ok = ok && lft[u];
-        if (tw == 2) ok = ok && rgt[u];
-        const int off = ok ? sb + u * (32 * BF_ROW) + lo[t] : BF_PADOFF;
-        const uint4 b = *reinterpret_cast<const uint4*>(smem + off);
+        for (int e = 0; e < 2; ++e)
+          wv[e] = *reinterpret_cast<const uint4*>(wl + (t * 64 + 32 * e) * ROW + wlo[kc]);
 #pragma unroll
-        for (int e = 0; e < 2; ++e) acc[u][e] = mfma_fp4(wv[e], b, t ? acc[u][e] : f32x16{});
+        for (int u = 0; u < 2; ++u) {
+          bool ok = live[u];
+          if (th == 0) ok = ok && top[u];
+          if (th == 2) ok = ok && bot[u];
+          if (tw == 0) ok = ok && lft[u];
+          if (tw == 2) ok = ok && rgt[u];
+          const int off = ok ? sb + u * (32 * ROW) + lo[t][kc] : C::PADOFF;
+          const uint4 b = *reinterpret_cast<const uint4*>(smem + off);
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            acc[u][e] = mfma_fp4(wv[e], b, (t || kc) ? acc[u][e] : f32x16{});
+        }
       }
     }
     BF_ST(3)
@@ -309,19 +355,19 @@ __global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
               make_uint4(s0[0], s1[0], s0[1], s1[1]);
         }
       }
-      // whole 128-B rows: instruction k stores pixels 8 k .. 8 k + 7 of the
-      // group (lane l: pixel 8 k + l / 8, slot l % 8)
+      // whole 128-B slice rows: instruction k stores pixels 8 k .. 8 k + 7 of
+      // the group (lane l: pixel 8 k + l / 8, slot l % 8)
       const int mg = m0 + 64 * wave + 32 * u;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int p = 8 * k + (lane >> 3), sl = lane & 7;
         const uint4 v = *reinterpret_cast<const uint4*>(ys + p * 128 + ((sl ^ (p & 7)) << 4));
-        if (a.y && mg + p < a.M)
-          *reinterpret_cast<uint4*>(a.y + (long long)(mg + p) * BF_C + sl * 8) = v;
+        if (ybase && mg + p < a.M)
+          *reinterpret_cast<uint4*>(ybase + (long long)(mg + p) * a.Cout + sl * 8) = v;
       }
     }
     BF_ST(4)
-    if ((it + 1) % BF_FLUSH == 0) bf_flush(cs, cq, r32, tsum, tsq);
+    if ((it + 1) % C::FLUSH == 0) bf_flush(cs, cq, r32, tsum, tsq);
     BF_ST(5)
   }
   BF_ST_STORE
@@ -331,19 +377,21 @@ __global__ __launch_bounds__(BF_NT, 2) void bfwd64_kernel(BfArgs a) {
   const int e = r32 >> 4, r = r32 & 15;
   const int co = 32 * e + 8 * (r >> 2) + 4 * h + (r & 3);
   __syncthreads();
-  long long* red = reinterpret_cast<long long*>(smem);  // [4 waves][2][64]
-  red[(wave * 2 + 0) * BF_C + co] = tsum;
-  red[(wave * 2 + 1) * BF_C + co] = (long long)tsq;
+  long long* red = reinterpret_cast<long long*>(smem);  // [NW waves][2][64]
+  red[(wave * 2 + 0) * 64 + co] = tsum;
+  red[(wave * 2 + 1) * 64 + co] = (long long)tsq;
   __syncthreads();
-  if (tid < 2 * BF_C) {
-    const int which = tid / BF_C, c = tid % BF_C;
+  if (tid < 128) {
+    const int which = tid / 64, c = tid % 64;
     long long tot = 0;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) tot += red[(w * 2 + which) * BF_C + c];
+    for (int w = 0; w < C::NW; ++w) tot += red[(w * 2 + which) * 64 + c];
     const int stripe = a.stripes > 1 ? (int)(blockIdx.x % a.stripes) : 0;
-    atomicAdd(a.stats + ((long long)stripe * 2 + which) * BF_C + c, (unsigned long long)tot);
+    atomicAdd(a.stats + ((long long)stripe * 2 + which) * a.Cout + slice * 64 + c,
+              (unsigned long long)tot);
   }
 }
+
 int bf_cus() {
   static int cus = 0;
   if (!cus) {
@@ -356,28 +404,60 @@ int bf_cus() {
   return cus;
 }
 
-}  // namespace
-
-// Shape check of zk_bfwd64_fp4: 3x3 stride 1 'same', 64 -> 64 channels, the
-// image at most BF_WMAX wide (the stage holds 256 + 2 W + 2 rows) and the
-// flattened pixel count inside the float-reciprocal division range (the
-// statistics are exact at any size: fp32 below 2^24 between flushes, 32-bit
-// lane reductions below 2^32, 64-bit totals).
-ZK_EXPORT int zk_bfwd64_supported(int B, int H, int W, int Cin, int Cout, int kh, int kw,
-                                  int stride, int pt, int pl) {
-  const long long M = (long long)B * H * W;
-  if (Cin != BF_C || Cout != BF_C || kh != 3 || kw != 3 || stride != 1 || pt != 1 || pl != 1)
-    return 0;
-  return M > 0 && M < (1LL << 24) && W <= BF_WMAX ? 1 : 0;
+template <class C>
+int bf_launch(const BfArgs& a0, int relu, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    for (const void* f : {(const void*)bfwd_kernel<C, false>, (const void*)bfwd_kernel<C, true>}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               C::LDS);
+      if (e != hipSuccess) return (int)e;
+    }
+    attr = true;
+  }
+  BfArgs a = a0;
+  a.ntiles = (a.M + C::TM - 1) / C::TM;
+  // blocks per slice: the resident count split over the slices, at most one
+  // per tile
+  int bps = C::OCC * bf_cus() / a.nsl;
+  if (bps < 1) bps = 1;
+  if (bps > a.ntiles) bps = a.ntiles;
+  const dim3 grid(bps * a.nsl);
+  if (relu)
+    hipLaunchKernelGGL((bfwd_kernel<C, true>), grid, dim3(C::NT), C::LDS, st, a);
+  else
+    hipLaunchKernelGGL((bfwd_kernel<C, false>), grid, dim3(C::NT), C::LDS, st, a);
+  return 0;
 }
 
-// y int16 [B][H][W][64] = 3x3 'same' binary conv of the e2m1 sign image x4
-// [B][H][W][32 B] with the e2m1 weights w4 [9][64][32 B] (+ReLU), padding
-// +1 (pad_ones) or 0; stats [stripes][2][64] int64 += per-channel sum and sum
-// of squares of y (block b adds into copy b % stripes).
-ZK_EXPORT int zk_bfwd64_fp4(const void* x4, const void* w4, void* y, void* stats, int B, int H,
-                            int W, int pad_ones, int relu, int stripes, hipStream_t st) {
-  if (!zk_bfwd64_supported(B, H, W, BF_C, BF_C, 3, 3, 1, 1, 1)) return (int)hipErrorInvalidValue;
+}  // namespace
+
+// Shape check of zk_bfwd_fp4: 3x3 stride 1 'same', Cin 64 (W <= 60) or 128
+// (W <= 32; the stage holds TM + 2 W + 2 rows), Cout a multiple of 64 (one
+// 64-channel slice per block), and the flattened pixel count inside the
+// float-reciprocal division range (the statistics are exact at any size:
+// fp32 below 2^24 between flushes, 32-bit lane reductions below 2^32, 64-bit
+// totals).
+ZK_EXPORT int zk_bfwd_supported(int B, int H, int W, int Cin, int Cout, int kh, int kw,
+                                int stride, int pt, int pl) {
+  const long long M = (long long)B * H * W;
+  if (kh != 3 || kw != 3 || stride != 1 || pt != 1 || pl != 1) return 0;
+  if (Cout <= 0 || Cout % 64 || Cout > 1024) return 0;
+  if (M <= 0 || M >= (1LL << 24)) return 0;
+  if (Cin == 64) return W <= Bf64::WMAX ? 1 : 0;
+  if (Cin == 128) return W <= Bf128::WMAX ? 1 : 0;
+  return 0;
+}
+
+// y int16 [B][H][W][Cout] = 3x3 'same' binary conv of the e2m1 sign image x4
+// [B][H][W][Cin/2 B] with the e2m1 weights w4 [9][Cout][Cin/2 B] (+ReLU),
+// padding +1 (pad_ones) or 0; stats [stripes][2][Cout] int64 += per-channel
+// sum and sum of squares of y (block b adds into copy b % stripes).  y null:
+// statistics only.
+ZK_EXPORT int zk_bfwd_fp4(const void* x4, const void* w4, void* y, void* stats, int B, int H,
+                          int W, int Cin, int Cout, int pad_ones, int relu, int stripes,
+                          hipStream_t st) {
+  if (!zk_bfwd_supported(B, H, W, Cin, Cout, 3, 3, 1, 1, 1)) return (int)hipErrorInvalidValue;
   BfArgs a{};
   a.x4 = (const unsigned char*)x4;
   a.w4 = (const unsigned char*)w4;
@@ -386,26 +466,14 @@ ZK_EXPORT int zk_bfwd64_fp4(const void* x4, const void* w4, void* y, void* stats
   a.M = B * H * W;
   a.H = H;
   a.W = W;
+  a.Cout = Cout;
+  a.nsl = Cout / 64;
   a.stripes = stripes;
-  a.ntiles = (a.M + BF_TM - 1) / BF_TM;
   a.pad_ones = pad_ones;
   a.inv_w = 1.f / (float)W;
   a.inv_h = 1.f / (float)H;
-  static bool attr = false;
-  if (!attr) {
-    for (const void* f : {(const void*)bfwd64_kernel<false>, (const void*)bfwd64_kernel<true>}) {
-      const hipError_t e =
-          hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, BF_LDS);
-      if (e != hipSuccess) return (int)e;
-    }
-    attr = true;
-  }
-  int grid = 2 * bf_cus();
-  if (grid > a.ntiles) grid = a.ntiles;
-  if (relu)
-    hipLaunchKernelGGL(bfwd64_kernel<true>, dim3(grid), dim3(BF_NT), BF_LDS, st, a);
-  else
-    hipLaunchKernelGGL(bfwd64_kernel<false>, dim3(grid), dim3(BF_NT), BF_LDS, st, a);
+  const int rc = Cin == 64 ? bf_launch<Bf64>(a, relu, st) : bf_launch<Bf128>(a, relu, st);
+  if (rc) return rc;
   ZK_CHECK_LAUNCH();
   return 0;
 }

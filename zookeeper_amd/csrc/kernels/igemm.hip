@@ -29,11 +29,12 @@
 #include "mfma_common.h"
 #include "splitk_tree.h"
 
-// bfwd.hip: the persistent 64 -> 64-channel 3x3 binary forward
-extern "C" int zk_bfwd64_supported(int B, int H, int W, int Cin, int Cout, int kh, int kw,
-                                   int stride, int pt, int pl);
-extern "C" int zk_bfwd64_fp4(const void* x4, const void* w4, void* y, void* stats, int B, int H,
-                             int W, int pad_ones, int relu, int stripes, hipStream_t st);
+// bfwd.hip: the persistent 3x3 binary forward (Cin 64 / 128)
+extern "C" int zk_bfwd_supported(int B, int H, int W, int Cin, int Cout, int kh, int kw,
+                                 int stride, int pt, int pl);
+extern "C" int zk_bfwd_fp4(const void* x4, const void* w4, void* y, void* stats, int B, int H,
+                           int W, int Cin, int Cout, int pad_ones, int relu, int stripes,
+                           hipStream_t st);
 
 // deep_gemm.hip: phased 256x256 wgrad of the stride-1 3x3 convs with Cin and
 // Cout % 256 == 0 (variant 60 of the wgrad dispatch)
@@ -1346,12 +1347,12 @@ int igemm_fwd_variant(int v, const void* sx, const void* wf, void* y, void* stat
 // one tap, 4x the K of a bf16 K-step over the same LDS bytes.
 int igemm_fwd4_variant(int v, const void* sx, const void* wf, void* y, void* stats,
                        const IGeom& g, int po, int relu, int ns, hipStream_t st) {
-  if (v == 40) {  // persistent 64 -> 64 3x3 kernel (bfwd.hip)
-    if (!zk_bfwd64_supported(g.B, g.H, g.W, g.Cin, g.Cout, g.kh, g.kw, g.s, g.pt, g.pl) ||
+  if (v == 40) {  // persistent 3x3 kernel (bfwd.hip)
+    if (!zk_bfwd_supported(g.B, g.H, g.W, g.Cin, g.Cout, g.kh, g.kw, g.s, g.pt, g.pl) ||
         g.Ho != g.H || g.Wo != g.W)
       return (int)hipErrorInvalidValue;
     if (g_dry_run) return 0;
-    return zk_bfwd64_fp4(sx, wf, y, stats, g.B, g.H, g.W, po, relu, ns, st);
+    return zk_bfwd_fp4(sx, wf, y, stats, g.B, g.H, g.W, g.Cin, g.Cout, po, relu, ns, st);
   }
 #define ZK_IGF4(BM, BN, WM, WN, NS, CB) \
   return launch_igemm_fwd<BM, BN, WM, WN, NS, CB, true>(sx, wf, y, stats, g, po, relu, ns, st)
@@ -2393,9 +2394,11 @@ ZK_EXPORT int zk_igemm_fwd_fp4(const void* sx4, const void* wf4, void* y, void* 
     // 37 -> 27 us; profiles/r1av_bconv_tuning_b512.md).
     const long long Po = (long long)g.B * g.Ho * g.Wo;
     const bool wide = Cin % 256 == 0 && Cout % 256 == 0 && Po >= 25088;
-    if (c3 && Cin == 64 && Cout == 64 && Ho == H && Wo == W &&
-        zk_bfwd64_supported(B, H, W, Cin, Cout, kh, kw, stride, pt, pl))
-      variant = 40;  // persistent, LDS-resident weights (bfwd.hip, profiles/r6/bfwd.md)
+    if (c3 && (Cin == 64 || Cin == 128) && Cout == Cin && Ho == H && Wo == W &&
+        zk_bfwd_supported(B, H, W, Cin, Cout, kh, kw, stride, pt, pl))
+      // persistent, LDS-resident weights (bfwd.hip, profiles/r6/bfwd.md): batch
+      // 1536, 56x56x64 285 -> 151 us, 28x28x128 204 -> 109 us
+      variant = 40;
     else if (c3 && Cin == 64)
       variant = 20;
     else if (c3 && Cin == 256 && Cout % 256 == 0)

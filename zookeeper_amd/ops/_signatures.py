@@ -48,8 +48,8 @@ SIGNATURES = {
     "zk_bn_bwd_tiles_reduce": (I32, [P, I32, I32, P, P]),
     "zk_igemm_fwd": (I32, [P, P, P, P] + [I32] * 16 + [P]),
     "zk_igemm_fwd_fp4": (I32, [P, P, P, P] + [I32] * 16 + [P]),
-    "zk_bfwd64_supported": (I32, [I32] * 10),
-    "zk_bfwd64_fp4": (I32, [P, P, P, P] + [I32] * 6 + [P]),
+    "zk_bfwd_supported": (I32, [I32] * 10),
+    "zk_bfwd_fp4": (I32, [P, P, P, P] + [I32] * 8 + [P]),
     "zk_igemm_wgrad": (I32, [P, P, P, P] + [I32] * 13 + [F32, I32, I32, P, I64, P]),
     "zk_igemm_wgrad_ws_bytes": (I64, [I32] * 14),
     "zk_wgrad_slab_reduce": (I32, [P, I32, I64, P, F32, P, P]),
