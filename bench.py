@@ -47,6 +47,13 @@ from typing import Tuple
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+# hardware queues for the step's streams, before anything initialises HIP
+# (zookeeper_amd/parallel/devices.py: with HIP's default 4 the gradient
+# all-reduce's stream waits stalled the input copies, ~15 % under DP)
+from zookeeper_amd.parallel.devices import configure_hw_queues  # noqa: E402
+
+configure_hw_queues()
+
 METRIC = "images/sec (whole node) BinaryResNet-E18 ImageNet at 1/2/4/8 MI355X"
 OTHER_METRIC = "images/sec (whole node) {model} ImageNet-shape training"
 
@@ -311,7 +318,8 @@ def main() -> int:
                      "bucket_mb": args.bucket_mb,
                      "bucket_sizes_mb": [round((hi - lo) * 4 / 2**20, 2)
                                          for lo, hi in trainer.bucketer.ranges],
-                     "bucket_order_checks": trainer.bucketer.order_checks},
+                     "bucket_order_checks": trainer.bucketer.order_checks,
+                     "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")},
             "runtime": runtime.as_dict(),
             "final_loss": round(final_loss, 4),
         },

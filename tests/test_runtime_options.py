@@ -112,3 +112,15 @@ def test_visible_gpu_count_from_env_and_sysfs(tmp_path):
     fake = {"HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7"}
     assert visible_gpu_count(fake, str(tmp_path / "none")) == 8
     assert visible_gpu_ids(fake, root) == [str(i) for i in range(8)]
+
+
+def test_hw_queues_default_and_user_override(monkeypatch):
+    """bench.py / dist.init give the process 16 hardware queues (HIP's
+    default 4 serialised the comm stream's waits with the input copies)
+    unless the user chose a value."""
+    from zookeeper_amd.parallel.devices import HW_QUEUES, configure_hw_queues
+
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
+    assert configure_hw_queues() == str(HW_QUEUES) == "16"
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "6")
+    assert configure_hw_queues() == "6"

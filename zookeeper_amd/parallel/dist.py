@@ -125,6 +125,11 @@ def init(backend: str = "auto", timeout_s: float = 600.0, single_group: bool = F
     down (failure detection)."""
     timeout_s = float(os.environ.get("ZK_DIST_TIMEOUT_S", timeout_s))
     comm = comm or CommConfig()
+    # enough hardware queues for the step's streams (devices.py: effective
+    # when this runs before the first GPU use, as in bench.py / Experiment)
+    from zookeeper_amd.parallel.devices import configure_hw_queues
+
+    configure_hw_queues()
     global _INFO
     if _INFO.backend != "none" or (dist.is_available() and dist.is_initialized()):
         return _INFO
