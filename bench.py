@@ -47,7 +47,7 @@ from typing import Tuple
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-# hardware queues for the step's streams, before anything initialises HIP
+# hardware queues for the step's streams (at least 16), before anything initialises HIP
 # (zookeeper_amd/parallel/devices.py: with HIP's default 4 the gradient
 # all-reduce's stream waits stalled the input copies, ~15 % under DP)
 from zookeeper_amd.parallel.devices import configure_hw_queues  # noqa: E402

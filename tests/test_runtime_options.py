@@ -115,12 +115,18 @@ def test_visible_gpu_count_from_env_and_sysfs(tmp_path):
 
 
 def test_hw_queues_default_and_user_override(monkeypatch):
-    """bench.py / dist.init give the process 16 hardware queues (HIP's
-    default 4 serialised the comm stream's waits with the input copies)
-    unless the user chose a value."""
+    """bench.py / dist.init raise the process to 16 hardware queues (HIP's
+    default 4, which the boxes export explicitly, serialised the comm
+    stream's waits with the input copies); ZK_HW_QUEUES picks a value, and a
+    larger user setting stays."""
     from zookeeper_amd.parallel.devices import HW_QUEUES, configure_hw_queues
 
+    monkeypatch.delenv("ZK_HW_QUEUES", raising=False)
     monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
     assert configure_hw_queues() == str(HW_QUEUES) == "16"
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "6")
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    assert configure_hw_queues() == "16"
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "24")
+    assert configure_hw_queues() == "24"
+    monkeypatch.setenv("ZK_HW_QUEUES", "6")
     assert configure_hw_queues() == "6"

@@ -76,7 +76,15 @@ HW_QUEUES = 16
 
 
 def configure_hw_queues(n: int = HW_QUEUES) -> str:
-    """Set ``GPU_MAX_HW_QUEUES`` for this process unless the user set it.
-    Effective only before the HIP runtime initialises (call before the first
-    GPU use; rank processes inherit it).  Returns the value in effect."""
-    return os.environ.setdefault("GPU_MAX_HW_QUEUES", str(int(n)))
+    """Raise ``GPU_MAX_HW_QUEUES`` to at least ``n`` for this process (the
+    MI355X boxes export HIP's default, 4, explicitly); ``ZK_HW_QUEUES`` picks
+    an exact value instead.  Effective only before the HIP runtime
+    initialises (call before the first GPU use; rank processes inherit it).
+    Returns the value in effect."""
+    want = os.environ.get("ZK_HW_QUEUES")
+    cur = os.environ.get("GPU_MAX_HW_QUEUES")
+    if want:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(int(want))
+    elif cur is None or not cur.strip().isdigit() or int(cur) < n:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(int(n))
+    return os.environ["GPU_MAX_HW_QUEUES"]
