@@ -80,6 +80,15 @@ def main() -> None:
             y.data_ptr(), sc.data_ptr(), sh.data_ptr(), res.data_ptr(), out.data_ptr(), None,
             mask.data_ptr(), sx4.data_ptr(), 1.0, P, C, st), "apply"), args.reps)
         report("bn_apply_sign (+res, sx4)", P, C, us, n * (2 + 2 + 2 + 0.5 + 0.125))
+        hw = {64: 56, 128: 28, 256: 14, 512: 7}[C]
+        if hw % 2 == 0:
+            pooled = torch.empty(P // 4, C, dtype=torch.bfloat16, device=dev)
+            us = timed(lambda: check(L.zk_bn_apply_sign_pool(
+                y.data_ptr(), sc.data_ptr(), sh.data_ptr(), res.data_ptr(), out.data_ptr(), None,
+                mask.data_ptr(), sx4.data_ptr(), 1.0, pooled.data_ptr(), P // (hw * hw), hw, hw,
+                C, st), "apply_pool"), args.reps)
+            report("bn_apply_sign_pool", P, C, us, n * (2 + 2 + 2 + 0.5 + 0.125 + 0.5))
+            del pooled
         del g, y, res, out, dy, mask, sx4
     for P, C in R50:
         g = torch.randn(P, C, device=dev).to(torch.bfloat16)

@@ -504,12 +504,18 @@ __global__ __launch_bounds__(256) void bn_bwd_tiles_reduce_kernel(float* __restr
   }
 }
 
-int rows_grid(long long P, int C) {
+int rows_grid(long long P, int C, long long cap = 2048) {
   const long long rb = 256 / (C / 8);
   long long b = (P + rb - 1) / rb;
-  if (b > 2048) b = 2048;
+  if (b > cap) b = cap;
   return b < 1 ? 1 : (int)b;
 }
+
+// The apply kernels take up to 65536 blocks (a few rows per thread: 5-9 %
+// faster at the large ResNet-50 shapes); the dx kernels stay at 2048, where
+// larger grids were up to 3x slower at every shape with C >= 128
+// (tools/bn_lab.py, profiles/r6/bn_grid.md).
+int apply_grid(long long P, int C) { return rows_grid(P, C, 65536); }
 
 // reductions: fewer blocks (each with 4 rows in flight per thread) so the
 // per-block atomics into the 2*C accumulators do not serialise
@@ -634,7 +640,7 @@ ZK_EXPORT int zk_bn_apply_bf16(const void* x, const void* coef, void* y, long lo
   if (C % 8) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                           \
   case cg:                                                                                 \
-    hipLaunchKernelGGL(bn_apply_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,  \
+    hipLaunchKernelGGL(bn_apply_bf16_kernel<cg>, dim3(apply_grid(P, C)), dim3(256), 0, st,  \
                        (const uint16_t*)x, (const float*)coef, (uint16_t*)y, P, relu);     \
     break;
   ZK_CG_CASES(C, CASE)
@@ -651,7 +657,7 @@ ZK_EXPORT int zk_bn_apply_bf16_sign(const void* x, const void* coef, void* y, vo
   if (C % 32) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                           \
   case cg:                                                                                 \
-    hipLaunchKernelGGL(bn_apply_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,  \
+    hipLaunchKernelGGL(bn_apply_bf16_kernel<cg>, dim3(apply_grid(P, C)), dim3(256), 0, st,  \
                        (const uint16_t*)x, (const float*)coef, (uint16_t*)y, P, relu,      \
                        (uint16_t*)sx, (uint8_t*)mask, clip, (uint32_t*)sx4);               \
     break;
@@ -768,7 +774,7 @@ ZK_EXPORT int zk_bn_apply_res_bf16(const void* x, const void* coef, const void* 
   if (C % 8) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                           \
   case cg:                                                                                 \
-    hipLaunchKernelGGL(bn_apply_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,  \
+    hipLaunchKernelGGL(bn_apply_bf16_kernel<cg>, dim3(apply_grid(P, C)), dim3(256), 0, st,  \
                        (const uint16_t*)x, (const float*)coef, (uint16_t*)y, P, relu,      \
                        nullptr, nullptr, 1.f, nullptr, (const uint16_t*)res,               \
                        (uint8_t*)omask);                                                   \
