@@ -6,6 +6,7 @@ per-call us and the effective HBM rate of the bytes each call must move.
 """
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -80,6 +81,13 @@ def main() -> None:
             y.data_ptr(), sc.data_ptr(), sh.data_ptr(), res.data_ptr(), out.data_ptr(), None,
             mask.data_ptr(), sx4.data_ptr(), 1.0, P, C, st), "apply"), args.reps)
         report("bn_apply_sign (+res, sx4)", P, C, us, n * (2 + 2 + 2 + 0.5 + 0.125))
+        mean = torch.rand(C, device=dev)
+        rstd = torch.rand(C, device=dev)
+        sums = torch.zeros(2 * C * 512, device=dev)
+        us = timed(lambda: check(L.zk_bn_bwd_reduce(g.data_ptr(), y.data_ptr(), mean.data_ptr(),
+                                                    rstd.data_ptr(), sums.data_ptr(), P, C, 512,
+                                                    st), "reduce"), args.reps)
+        report("bn_bwd_reduce (int16 y)", P, C, us, 4 * n)
         hw = {64: 56, 128: 28, 256: 14, 512: 7}[C]
         if hw % 2 == 0:
             pooled = torch.empty(P // 4, C, dtype=torch.bfloat16, device=dev)
@@ -106,6 +114,12 @@ def main() -> None:
             g.data_ptr(), x.data_ptr(), fcoef.data_ptr(), bcoef.data_ptr(), dx.data_ptr(), P, C,
             st), "dxrelu"), args.reps)
         report("bn_bwd_dx_relu_bf16", P, C, us, n * 6)
+        parts = torch.zeros(2 * C * 512, device=dev)
+        npart = ctypes.c_int(0)
+        us = timed(lambda: check(L.zk_bn_bwd_reduce_bf16_parts(
+            g.data_ptr(), x.data_ptr(), m.data_ptr(), fcoef.data_ptr(), parts.data_ptr(), P, C,
+            ctypes.byref(npart), st), "reduce_bf16"), args.reps)
+        report("bn_bwd_reduce_bf16_parts", P, C, us, n * (4 + 0.125))
         us = timed(lambda: check(L.zk_bn_apply_bf16(x.data_ptr(), fcoef.data_ptr(),
                                                     dx.data_ptr(), P, C, 1, st), "apbf"),
                    args.reps)

@@ -516,6 +516,11 @@ int rows_grid(long long P, int C, long long cap = 2048) {
 // larger grids were up to 3x slower at every shape with C >= 128
 // (tools/bn_lab.py, profiles/r6/bn_grid.md).
 int apply_grid(long long P, int C) { return rows_grid(P, C, 65536); }
+// The dx kernels: 1024 blocks with the stored ReLU mask (or none), 512 with
+// the mask recomputed from x (RC) -- 10-30 % faster than 2048 at most
+// ResNet-50 shapes, and larger grids were slower still (profiles/r6/bn_grid.md).
+int dx_grid(long long P, int C) { return rows_grid(P, C, 1024); }
+int dx_rc_grid(long long P, int C) { return rows_grid(P, C, 512); }
 
 // reductions: fewer blocks (each with 4 rows in flight per thread) so the
 // per-block atomics into the 2*C accumulators do not serialise
@@ -723,7 +728,7 @@ ZK_EXPORT int zk_bn_bwd_dx_bf16(const void* g, const void* x, const void* m, con
   if (C % 8) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                             \
   case cg:                                                                                   \
-    hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,   \
+    hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(dx_grid(P, C)), dim3(256), 0, st,     \
                        (const uint16_t*)g, (const uint16_t*)x, (const uint8_t*)m,            \
                        (const float*)bcoef, (uint16_t*)dx, P);                               \
     break;
@@ -756,7 +761,7 @@ ZK_EXPORT int zk_bn_bwd_dx_relu_bf16(const void* g, const void* x, const void* c
   if (C % 8) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                             \
   case cg:                                                                                   \
-    hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,   \
+    hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(dx_rc_grid(P, C)), dim3(256), 0, st,  \
                        (const uint16_t*)g, (const uint16_t*)x, nullptr, (const float*)bcoef, \
                        (uint16_t*)dx, P, nullptr, (const float*)coef);                       \
     break;
@@ -793,7 +798,7 @@ ZK_EXPORT int zk_bn_bwd_dx_res_bf16(const void* g, const void* x, const void* m,
   if (C % 8) return (int)hipErrorInvalidValue;
 #define CASE(cg)                                                                             \
   case cg:                                                                                   \
-    hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(rows_grid(P, C)), dim3(256), 0, st,   \
+    hipLaunchKernelGGL(bn_bwd_dx_bf16_kernel<cg>, dim3(dx_grid(P, C)), dim3(256), 0, st,     \
                        (const uint16_t*)g, (const uint16_t*)x, (const uint8_t*)m,            \
                        (const float*)bcoef, (uint16_t*)dx, P, (uint16_t*)dres);              \
     break;
