@@ -148,3 +148,25 @@ def test_avgpool2():
     yh.backward(g)
     yr.backward(g.float())
     torch.testing.assert_close(xh.grad.float(), xr.grad, atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("tiles,C", [(1, 64), (300, 200), (1568, 64), (5000, 1024), (513, 8)])
+def test_bn_bwd_tiles_reduce_fixed_order(tiles, C):
+    """zk_bn_bwd_tiles_reduce: copy b of value c = rows b, b + 512, ... of
+    column c summed in that order (fp32, bit-exact against the same order in
+    torch), written channel-major [2C][512]; every row re-zeroed."""
+    from zookeeper_amd.ops._native import check, lib, stream_ptr
+
+    L = lib()
+    nparts = L.zk_bn_bwd_parts_max()
+    rows = torch.randn(tiles, 2 * C, device="cuda")
+    ref = torch.zeros(nparts, 2 * C, device="cuda")
+    for k in range(0, tiles, nparts):
+        blk = rows[k:k + nparts]
+        ref[:blk.shape[0]] = ref[:blk.shape[0]] + blk
+    out = torch.full((2 * C, nparts), float("nan"), device="cuda")
+    check(L.zk_bn_bwd_tiles_reduce(rows.data_ptr(), tiles, C, out.data_ptr(), stream_ptr()),
+          "zk_bn_bwd_tiles_reduce")
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref.t().contiguous())
+    assert torch.count_nonzero(rows).item() == 0

@@ -124,7 +124,13 @@ def main() -> None:
                                                     dx.data_ptr(), P, C, 1, st), "apbf"),
                    args.reps)
         report("bn_apply_bf16 (relu)", P, C, us, n * 4)
-        del g, x, dx, m
+        tiles = (P + 255) // 256  # a 256-row GEMM tile's epilogue rows
+        rows_t = torch.zeros(tiles, 2 * C, device=dev)
+        us = timed(lambda: check(L.zk_bn_bwd_tiles_reduce(rows_t.data_ptr(), tiles, C,
+                                                          parts.data_ptr(), st), "tiles"),
+                   args.reps)
+        report("bn_bwd_tiles_reduce", tiles, C, us, tiles * 2 * C * 8 + 2 * C * 512 * 4)
+        del g, x, dx, m, rows_t
     if args.json:
         os.makedirs(os.path.dirname(args.json) or ".", exist_ok=True)
         with open(args.json, "a") as f:

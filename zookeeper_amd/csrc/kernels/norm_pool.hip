@@ -488,20 +488,44 @@ __global__ __launch_bounds__(256) void avgpool2_bwd_kernel(const uint16_t* __res
 // Per-tile BN-backward partials [tiles][2][C] (a GEMM epilogue's rows,
 // zk_igemm_dgrad_bsums) -> the channel-major copies [2][C][kBnBwdParts] that
 // zk_bn_bwd_coef sums: copy b = rows b, b + kBnBwdParts, ... in that order
-// (fixed: bit-reproducible), each row read once by one block and re-zeroed.
+// (fixed: bit-reproducible), each row read once and re-zeroed.  A block owns
+// TR_C consecutive values of the 2C and TR_B consecutive copies, one (value,
+// copy) per thread; a thread's rows are loaded TR_U at a time (independent
+// loads) and added in row order.  The block's [TR_C][TR_B] tile goes through
+// LDS so that every output row is written as TR_B contiguous floats.  (One
+// block per copy with a thread per value wrote each float 2 KB from its
+// neighbour: ~21 us per call at ResNet-50 shapes, profiles/r6/bn_grid.md.)
+constexpr int TR_C = 16, TR_B = 16, TR_U = 8;
 __global__ __launch_bounds__(256) void bn_bwd_tiles_reduce_kernel(float* __restrict__ rows,
                                                                   int tiles, int C,
                                                                   float* __restrict__ out) {
-  const int b = blockIdx.x;
-  for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
-    float t = 0.f;
-    for (int r = b; r < tiles; r += kBnBwdParts) {
-      float* p = rows + (long long)r * 2 * C + c;
-      t += *p;
-      *p = 0.f;
+  __shared__ float tile[TR_C][TR_B + 1];
+  const int c0 = blockIdx.x * TR_C, b0 = blockIdx.y * TR_B;
+  const int cl = threadIdx.x % TR_C, bl = threadIdx.x / TR_C;
+  const int c = c0 + cl, b = b0 + bl;
+  float t = 0.f;
+  if (c < 2 * C) {
+    for (int r = b; r < tiles; r += TR_U * kBnBwdParts) {
+      float v[TR_U];
+#pragma unroll
+      for (int u = 0; u < TR_U; ++u) {
+        const int ru = r + u * kBnBwdParts;
+        v[u] = ru < tiles ? rows[(long long)ru * 2 * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < TR_U; ++u) {
+        const int ru = r + u * kBnBwdParts;
+        if (ru < tiles) {
+          t += v[u];
+          rows[(long long)ru * 2 * C + c] = 0.f;
+        }
+      }
     }
-    out[(long long)c * kBnBwdParts + b] = t;
   }
+  tile[cl][bl] = t;
+  __syncthreads();
+  const int cc = threadIdx.x / TR_B, bb = threadIdx.x % TR_B;
+  if (c0 + cc < 2 * C) out[(long long)(c0 + cc) * kBnBwdParts + b0 + bb] = tile[cc][bb];
 }
 
 int rows_grid(long long P, int C, long long cap = 2048) {
@@ -699,8 +723,9 @@ ZK_EXPORT int zk_bn_bwd_parts_max() { return kBnBwdParts; }
 // zk_bn_bwd_coef.
 ZK_EXPORT int zk_bn_bwd_tiles_reduce(void* rows, int tiles, int C, void* parts, hipStream_t st) {
   if (tiles < 1 || C < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_bwd_tiles_reduce_kernel, dim3(kBnBwdParts), dim3(256), 0, st,
-                     (float*)rows, tiles, C, (float*)parts);
+  static_assert(kBnBwdParts % TR_B == 0, "copies tile by TR_B");
+  hipLaunchKernelGGL(bn_bwd_tiles_reduce_kernel, dim3((2 * C + TR_C - 1) / TR_C, kBnBwdParts / TR_B),
+                     dim3(256), 0, st, (float*)rows, tiles, C, (float*)parts);
   ZK_CHECK_LAUNCH();
   return 0;
 }
