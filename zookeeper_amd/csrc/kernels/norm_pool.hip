@@ -88,29 +88,36 @@ __global__ __launch_bounds__(256) void bn_stats_bf16_kernel(const uint16_t* __re
 }
 
 // sums: [nparts][2][C] (nparts = 1: the atomically accumulated row, re-zeroed
-// here for the next use; > 1: per-block partials summed in block order).
-__global__ void bn_finalize_f64_kernel(double* __restrict__ sums, int C, double P,
-                                       const float* __restrict__ gamma,
-                                       const float* __restrict__ beta, float eps, float momentum,
-                                       float* __restrict__ rmean, float* __restrict__ rvar,
-                                       float* __restrict__ coef, int nparts,
-                                       int rezero) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// here for the next use; > 1: per-block partials summed in a fixed order).
+// A group of 32 lanes owns one channel: lane k sums parts k, k + 32, ... and
+// the group reduces with cross-lane shuffles (one thread per channel walking
+// all parts ran ~12 us per call at nparts = 512, 52 calls per ResNet-50 step,
+// profiles/r6/bn_grid.md).
+__global__ __launch_bounds__(256) void bn_finalize_f64_kernel(
+    double* __restrict__ sums, int C, double P, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float momentum, float* __restrict__ rmean,
+    float* __restrict__ rvar, float* __restrict__ coef, int nparts, int rezero) {
+  const int k = threadIdx.x & 31;
+  const int c = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (c >= C) return;  // uniform over the 32-lane group
+  const bool zero = nparts == 1 || rezero;  // re-zeroed for the next use (persistent buffer)
   double s1 = 0.0, s2 = 0.0;
-  for (int j = 0; j < nparts; ++j) {
+  for (int j = k; j < nparts; j += 32) {
     s1 += sums[(2LL * j) * C + c];
     s2 += sums[(2LL * j + 1) * C + c];
-  }
-  const double mean = s1 / P;
-  double var = s2 / P - mean * mean;
-  if (nparts == 1 || rezero) {
-    // re-zeroed for the next use (persistent per-layer buffer)
-    for (int j = 0; j < nparts; ++j) {
+    if (zero) {
       sums[(2LL * j) * C + c] = 0.0;
       sums[(2LL * j + 1) * C + c] = 0.0;
     }
   }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, 32);
+    s2 += __shfl_xor(s2, o, 32);
+  }
+  if (k != 0) return;
+  const double mean = s1 / P;
+  double var = s2 / P - mean * mean;
   if (var < 0) var = 0;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
   const float g = gamma ? gamma[c] : 1.f;
@@ -594,7 +601,7 @@ ZK_EXPORT int zk_bn_stats_bf16(const void* x, void* sums, long long P, int C, hi
 ZK_EXPORT int zk_bn_finalize_f64(const void* sums, int C, double P, const void* gamma,
                                  const void* beta, float eps, float momentum, void* rmean,
                                  void* rvar, void* coef, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
+  hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 7) / 8), dim3(256), 0, st,
                      (double*)sums, C, P, (const float*)gamma, (const float*)beta, eps,
                      momentum, (float*)rmean, (float*)rvar, (float*)coef, 1, 0);
   ZK_CHECK_LAUNCH();
@@ -624,7 +631,7 @@ ZK_EXPORT int zk_bn_finalize_f64_parts(const void* parts, int nparts, int C, dou
                                        const void* gamma, const void* beta, float eps,
                                        float momentum, void* rmean, void* rvar, void* coef,
                                        hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
+  hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 7) / 8), dim3(256), 0, st,
                      (double*)parts, C, P, (const float*)gamma, (const float*)beta, eps,
                      momentum, (float*)rmean, (float*)rvar, (float*)coef, nparts < 1 ? 1 : nparts, 0);
   ZK_CHECK_LAUNCH();
@@ -638,7 +645,7 @@ ZK_EXPORT int zk_bn_finalize_f64_stripes(void* parts, int nparts, int C, double 
                                          const void* gamma, const void* beta, float eps,
                                          float momentum, void* rmean, void* rvar, void* coef,
                                          hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
+  hipLaunchKernelGGL(bn_finalize_f64_kernel, dim3((C + 7) / 8), dim3(256), 0, st,
                      (double*)parts, C, P, (const float*)gamma, (const float*)beta, eps,
                      momentum, (float*)rmean, (float*)rvar, (float*)coef, nparts < 1 ? 1 : nparts,
                      1);
