@@ -2113,7 +2113,11 @@ int igemm_dgrad_impl(const void* dy, const void* wt, const void* mask, const voi
       // do not (E18 with it off 51.6k vs 51.3k)
       variant = 60;
     else if (le && g.kh == 1 && g.kw == 1 && stride == 1 && Cin % 64 == 0)
-      variant = Cin % 256 == 0 ? 45 : Cin % 128 == 0 ? 41 : 43;
+      // 256x256 only for deep K: with K < 1024 the 128x128 4-stage ring (41)
+      // is 12-25 % faster at batch 512 and 1024, with and without a residual
+      // (tools/tune_pw.py, profiles/r6/pw_tiles.md: 56x56 N256 K64 b1024
+      // 1033 -> 832 us, 14x14 N1024 K256 345 -> 331, 7x7 N2048 K512 232 -> 203)
+      variant = Cin % 256 == 0 ? (g.Cout >= 1024 ? 45 : 41) : Cin % 128 == 0 ? 41 : 43;
     else if (Cin == 256 && stride == 1)
       variant = v256;
     else if (Cin >= 256 && Cin % 256 == 0 && g.B >= 512)
