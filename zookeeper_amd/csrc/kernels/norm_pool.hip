@@ -543,9 +543,9 @@ int rows_grid(long long P, int C, long long cap = 2048) {
 }
 
 // The apply kernels take up to 65536 blocks (a few rows per thread: 5-9 %
-// faster at the large ResNet-50 shapes); the dx kernels stay at 2048, where
-// larger grids were up to 3x slower at every shape with C >= 128
-// (tools/bn_lab.py, profiles/r6/bn_grid.md).
+// faster at the large ResNet-50 shapes); for the dx kernels larger grids were
+// up to 3x slower at every shape with C >= 128 (tools/bn_lab.py,
+// profiles/r6/bn_grid.md).
 int apply_grid(long long P, int C) { return rows_grid(P, C, 65536); }
 // The dx kernels: 1024 blocks with the stored ReLU mask (or none), 512 with
 // the mask recomputed from x (RC) -- 10-30 % faster than 2048 at most
