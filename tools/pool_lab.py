@@ -1,4 +1,4 @@
-"""Standalone timings of the max-pool forward (norm_pool.hip) at the
+"""Standalone timings of the max-pool forward and backward (norm_pool.hip) at the
 QuickNet-Large transition shapes (2x2 stride 1, valid, batch 1024) and at
 ResNet's 3x3 stride 2: us per call and the HBM rate of input + output +
 argmax bytes.
@@ -49,7 +49,23 @@ def main() -> None:
         nbytes = x.numel() * 2 + y.numel() * 3
         print(f"{args.tag:6s} maxpool {k}x{k}/{s} B={B} {H}x{H}x{C}: {us:8.1f} us "
               f"{nbytes / us / 1e6:5.2f} TB/s", flush=True)
-        del x, y, arg
+        dx = torch.empty_like(x)
+
+        def run_bwd():
+            check(L.zk_maxpool_bwd(y.data_ptr(), arg.data_ptr(), dx.data_ptr(), B, H, H, C, Ho,
+                                   Ho, k, s, p, p, st), "maxpool_bwd")
+
+        for _ in range(3):
+            run_bwd()
+        e0.record()
+        for _ in range(args.reps):
+            run_bwd()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / args.reps
+        print(f"{args.tag:6s} maxpool_bwd {k}x{k}/{s} B={B} {H}x{H}x{C}: {us:8.1f} us "
+              f"{nbytes / us / 1e6:5.2f} TB/s", flush=True)
+        del x, y, arg, dx
 
 
 if __name__ == "__main__":

@@ -430,11 +430,17 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
 
 // Gather form (deterministic, no atomics): each input pixel sums the
 // gradients of the output windows whose argmax it was.
+// KT, ST > 0: window and stride at compile time -- the (at most
+// ceil(k/s)^2) candidate outputs' dy / argmax chunks are all loaded before the
+// first is added, in the same (ho, wo) order as the runtime loops, so the sums
+// are bit-identical.  KT = 0: k and s at run time.
+template <int KT, int ST>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy,
                                                           const uint8_t* __restrict__ arg,
                                                           uint16_t* __restrict__ dx, int B,
                                                           int H, int W, int C, int Ho, int Wo,
-                                                          int k, int s, int pt, int pl) {
+                                                          int k_rt, int s_rt, int pt, int pl) {
+  const int k = KT > 0 ? KT : k_rt, s = KT > 0 ? ST : s_rt;
   const int CG = C / 8;
   const long long total = (long long)B * H * W * CG;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -448,21 +454,43 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __rest
     // outputs whose window covers (hi, wi): ho*s - pt <= hi <= ho*s - pt + k - 1
     const int ho_lo = max(0, (hi + pt - k + s) / s), ho_hi = min(Ho - 1, (hi + pt) / s);
     const int wo_lo = max(0, (wi + pl - k + s) / s), wo_hi = min(Wo - 1, (wi + pl) / s);
-    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
-      const int dh = hi - (ho * s - pt);
-      if (dh < 0 || dh >= k) continue;
-      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
-        const int dw = wi - (wo * s - pl);
-        if (dw < 0 || dw >= k) continue;
-        const long long o = (((long long)b * Ho + ho) * Wo + wo) * C + cg * 8;
-        const uint2 a = *reinterpret_cast<const uint2*>(arg + o);
-        const uint8_t* ab = reinterpret_cast<const uint8_t*>(&a);
-        float g[8];
-        load8_bf16(dy + o, g);
-        const uint8_t tap = (uint8_t)(dh * k + dw);
+    auto add = [&](const uint4& gq, const uint2& a, int tap) {
+      const uint8_t* ab = reinterpret_cast<const uint8_t*>(&a);
+      float g[8];
+      unpack8_bf16(gq, g);
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (ab[q] == tap) acc[q] += g[q];
+      for (int q = 0; q < 8; ++q)
+        if (ab[q] == (uint8_t)tap) acc[q] += g[q];
+    };
+    if constexpr (KT > 0) {
+      constexpr int N = (KT + ST - 1) / ST;  // candidates per dimension
+      uint4 gq[N * N];
+      uint2 aq[N * N];
+      int tap[N * N];
+#pragma unroll
+      for (int t = 0; t < N * N; ++t) {
+        const int ho = ho_lo + t / N, wo = wo_lo + t % N;
+        const int dh = hi - (ho * ST - pt), dw = wi - (wo * ST - pl);
+        const bool ok = ho <= ho_hi && wo <= wo_hi && dh >= 0 && dh < KT && dw >= 0 && dw < KT;
+        tap[t] = ok ? dh * KT + dw : -1;
+        const long long o = (((long long)b * Ho + ho) * Wo + wo) * C + cg * 8;
+        gq[t] = ok ? *reinterpret_cast<const uint4*>(dy + o) : make_uint4(0, 0, 0, 0);
+        aq[t] = ok ? *reinterpret_cast<const uint2*>(arg + o) : make_uint2(0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < N * N; ++t)
+        if (tap[t] >= 0) add(gq[t], aq[t], tap[t]);
+    } else {
+      for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+        const int dh = hi - (ho * s - pt);
+        if (dh < 0 || dh >= k) continue;
+        for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+          const int dw = wi - (wo * s - pl);
+          if (dw < 0 || dw >= k) continue;
+          const long long o = (((long long)b * Ho + ho) * Wo + wo) * C + cg * 8;
+          add(*reinterpret_cast<const uint4*>(dy + o), *reinterpret_cast<const uint2*>(arg + o),
+              dh * k + dw);
+        }
       }
     }
     store8_bf16(dx + pix * C + cg * 8, acc);
@@ -897,9 +925,13 @@ ZK_EXPORT int zk_maxpool_bwd(const void* dy, const void* arg, void* dx, int B, i
                              hipStream_t st) {
   if (C % 8) return (int)hipErrorInvalidValue;
   const long long work = (long long)B * H * W * (C / 8);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(flat_grid(work)), dim3(256), 0, st,
-                     (const uint16_t*)dy, (const uint8_t*)arg, (uint16_t*)dx, B, H, W, C, Ho,
-                     Wo, k, s, pt, pl);
+  // QuickNet's 2x2/1 and ResNet's 3x3/2 at compile time: 15-20 % faster at
+  // batch 1024 (profiles/r6/maxpool.md)
+  auto kern = (k == 2 && s == 1) ? maxpool_bwd_kernel<2, 1>
+              : (k == 3 && s == 2) ? maxpool_bwd_kernel<3, 2>
+                                   : maxpool_bwd_kernel<0, 0>;
+  hipLaunchKernelGGL(kern, dim3(flat_grid(work)), dim3(256), 0, st, (const uint16_t*)dy,
+                     (const uint8_t*)arg, (uint16_t*)dx, B, H, W, C, Ho, Wo, k, s, pt, pl);
   ZK_CHECK_LAUNCH();
   return 0;
 }
